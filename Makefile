@@ -1,0 +1,23 @@
+# Builds libliteasr_hip.so (gfx950) from liteasr_amd/csrc/*.hip and the C oracle.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH  ?= gfx950
+SRC   := $(wildcard liteasr_amd/csrc/*.hip)
+OBJ   := $(patsubst liteasr_amd/csrc/%.hip,build/obj/%.o,$(SRC))
+LIB   := liteasr_amd/lib/libliteasr_hip.so
+HDRS  := liteasr_amd/csrc/common.h include/liteasr_hip.h
+FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC
+
+all: $(LIB)
+
+build/obj/%.o: liteasr_amd/csrc/%.hip $(HDRS)
+	@mkdir -p build/obj
+	$(HIPCC) $(FLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	@mkdir -p liteasr_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

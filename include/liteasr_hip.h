@@ -1,0 +1,273 @@
+/*
+ * liteasr_hip.h — C ABI of libliteasr_hip.so, the MI355X (gfx950) kernels behind
+ * the U2 / Conformer + hybrid CTC-attention training step.
+ *
+ * The reference (Nazukixv/LiteASR) is pure PyTorch: every op on its hot path is an
+ * aten kernel reached from a liteasr.nets module.  Each entry point below replaces
+ * one of those aten call sites; the citation names the reference file:line whose
+ * behaviour it reproduces (paths relative to the reference repo root).
+ *
+ * Conventions
+ *   - Plain pointers + sizes; no framework types.  Caller owns every buffer; the
+ *     library keeps no device allocations (scratch is caller-provided workspace).
+ *   - dtype codes: LASR_F32 / LASR_BF16 for activation storage; arithmetic is fp32.
+ *   - Every call is stream-ordered on `stream` (a hipStream_t passed as void*),
+ *     never synchronises, and is safe to capture into a hipGraph.
+ *   - Return 0 on success, a negative LASR_ERR_* on failure; lasr_last_error()
+ *     returns a thread-local message for the last failure.
+ *   - Dropout: (p, seed) pairs.  The keep-mask is a pure function of
+ *     (seed, logical element index) so backward regenerates it.
+ *   - Reductions use fixed orders (no float atomics) => bitwise deterministic.
+ */
+#ifndef LITEASR_HIP_H
+#define LITEASR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { LASR_F32 = 0, LASR_BF16 = 1, LASR_I32 = 2, LASR_I64 = 3, LASR_U8 = 4 };
+enum { LASR_OK = 0, LASR_ERR_INVALID = -1, LASR_ERR_LAUNCH = -2 };
+enum { LASR_ACT_NONE = 0, LASR_ACT_RELU = 1, LASR_ACT_SWISH = 2 };
+
+const char* lasr_last_error(void);
+int lasr_version(void);
+
+/* ------------------------------------------------------------------------
+ * Batched GEMM with fused epilogue.
+ *   C[z][m,n] = epilogue( alpha * sum_k A[z][m,k] * B[z][k,n] )
+ * Replaces the aten addmm/mm/bmm behind nn.Linear and the attention matmuls:
+ *   liteasr/nets/feed_forward.py:18-19, liteasr/nets/attention.py:35-37,58,69,145,149,
+ *   liteasr/nets/subsampling.py:34,47, liteasr/nets/conformer_convolution.py:48,55,
+ *   liteasr/nets/ctc.py:29, liteasr/nets/transformer_decoder.py:91.
+ * Element strides are free (one of lda_m/lda_k must be 1, same for B).
+ * z in [0,batch): z1 = z / batch_div, z2 = z % batch_div; operand offset
+ *   = z1*s?1 + z2*s?2.
+ * Epilogue order: v = alpha*acc (* *alpha_dev); v += bias[n]; zout = v; v = act(v);
+ *   v *= act'(aux[m,n]); v *= dropmask(z*M*N + m*N + n); v = res[m,n] + res_scale*v;
+ *   C = beta*C + v.
+ * split_k > 1 (dW GEMMs): partial sums go to `workspace` (split_k*batch*M*N fp32),
+ *   then are reduced; only alpha/alpha_dev/beta/bias are honoured in that mode.
+ * ---------------------------------------------------------------------- */
+typedef struct lasr_gemm_args {
+  int M, N, K;
+  int batch, batch_div;
+  const void* A; int64_t lda_m, lda_k, sa1, sa2;
+  const void* B; int64_t ldb_n, ldb_k, sb1, sb2;
+  void* C; int64_t ldc, sc1, sc2;
+  int in_dtype;  /* dtype of A and B */
+  int c_dtype;
+  float alpha; const float* alpha_dev;
+  float beta;
+  const float* bias;
+  int act;
+  void* zout;  /* pre-activation copy (c_dtype, ld = ldc), optional */
+  const void* aux; int aux_dtype; int64_t ldaux; int aux_act;
+  float drop_p; uint64_t drop_seed;
+  const void* res; int res_dtype; int64_t ldres; float res_scale;
+  int split_k; void* workspace; int64_t workspace_bytes;
+} lasr_gemm_args;
+int lasr_gemm(const lasr_gemm_args* args, void* stream);
+
+/* Column sums: out[n] (+)= sum_m X[m,n]  (bias gradients; fp32 out).
+ * Two-pass deterministic; workspace >= ceil(M/rows_per_block)*N floats (see impl). */
+int lasr_colsum(const void* X, int dtype, int64_t M, int64_t N, int64_t ldx,
+                float* out, int accumulate, float* workspace, int64_t ws_floats, void* stream);
+
+/* ------------------------------------------------------------------------
+ * LayerNorm over the last dim, eps from caller (1e-12 in LiteASR:
+ * liteasr/nets/layer_norm.py:10-21).  Row-major [rows, D].
+ * fwd: y (y_dtype) = (x-mean)*rstd*gamma + beta; saves mean/rstd (fp32, [rows]).
+ *      y2 (optional, y2_dtype): a second copy, with dropout (p2,seed2) applied
+ *      (used for CTC's input dropout, liteasr/nets/ctc.py:29).
+ * bwd: dx = LN'(dy) (+ dres if given); dgamma/dbeta accumulated into fp32 outs.
+ *      Optional branch-grad output: gb = bscale * dropmask(bseed) * dx (gb_dtype),
+ *      the gradient entering the preceding residual branch
+ *      (liteasr/nets/conformer_layer.py:42,54,63; transformer_layer.py:48,58,173).
+ * ---------------------------------------------------------------------- */
+int lasr_layernorm_fwd(const void* x, int x_dtype, int64_t rows, int D, const float* gamma,
+                       const float* beta, float eps, void* y, int y_dtype, float* mean,
+                       float* rstd, void* y2, int y2_dtype, float p2, uint64_t seed2,
+                       void* stream);
+int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype, int64_t rows,
+                       int D, const float* gamma, const float* mean, const float* rstd,
+                       const void* dres, int dres_dtype, void* dx, int dx_dtype,
+                       float* dgamma, float* dbeta, float* workspace, int64_t ws_floats,
+                       void* gb, int gb_dtype, float bscale, float bp, uint64_t bseed,
+                       void* stream);
+/* gb = scale * dropmask(seed) * dx  (residual-branch gradient, standalone form). */
+int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_dtype,
+                     float scale, float p, uint64_t seed, void* stream);
+
+/* ------------------------------------------------------------------------
+ * CTC (blank=0, reduction=sum) fused with log_softmax over the vocab.
+ * Replaces liteasr/criterions/hybrid_ctc_attn.py:67-75 (h_ctc.transpose(0,1)
+ * .log_softmax(-1) -> nn.CTCLoss) and aten's ctc_loss / _ctc_loss_backward.
+ * logits: [B, T, V] (batch-major, ld = V), dtype `ldt`.
+ * targets: [B, Lmax] int32, padded; tlen/ilen: [B] int32.
+ * fwd: writes nll[B] (fp32; +inf when infeasible), and saves lse[B*T], lp[B*T*(Lmax+1)]
+ *      (log-probs of blank and each target position) and alpha[B*T*(2*Lmax+1)].
+ * bwd: grad[b,t,:] = g * (softmax - gamma_t) for t < ilen[b], 0 otherwise, where
+ *      g = gscale * (*gdev if gdev).  Uses beta[B*T*(2*Lmax+1)] scratch.
+ * ---------------------------------------------------------------------- */
+int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, const int32_t* targets,
+                 int Lmax, const int32_t* ilen, const int32_t* tlen, float* lse, float* lp,
+                 float* alpha, float* nll, void* stream);
+int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, const int32_t* targets,
+                 int Lmax, const int32_t* ilen, const int32_t* tlen, const float* lse,
+                 const float* lp, const float* alpha, const float* nll, float* beta,
+                 void* grad, int gdt, float gscale, const float* gdev, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Label-smoothed KL (liteasr/criterions/hybrid_ctc_attn.py:49-64):
+ *   row loss = sum_c td_c (log td_c - log_softmax(h)_c), td = s/(V-1), 1-s at target;
+ *   rows with target == ignore contribute 0.
+ * fwd: loss_rows[R] fp32, lse[R]. bwd: grad = g*(softmax - td) (0 on ignored rows).
+ * ---------------------------------------------------------------------- */
+int lasr_lsm_kl_fwd(const void* logits, int ldt, int R, int V, const int32_t* target,
+                    int ignore, float smoothing, float* lse, float* loss_rows, void* stream);
+int lasr_lsm_kl_bwd(const void* logits, int ldt, int R, int V, const int32_t* target,
+                    int ignore, float smoothing, const float* lse, void* grad, int gdt,
+                    float gscale, const float* gdev, void* stream);
+/* out[0] = wa * sum(a[0:na]) + wb * sum(b[0:nb])   (hybrid loss combine,
+ * liteasr/criterions/hybrid_ctc_attn.py:63-64,75,78). */
+int lasr_loss_combine(const float* a, int na, float wa, const float* b, int nb, float wb,
+                      float* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Attention pieces (materialised-score form).
+ * Relative-position MHA (liteasr/nets/attention.py:120-154, rel_shift :99-118):
+ *   qu = q + pos_bias_u, qv = q + pos_bias_v       (lasr_qbias_fwd)
+ *   S = scale*(qu k^T + rel_shift(qv p^T)), masked_fill(mask,-1e38), softmax, dropout
+ *                                                  (lasr_attn_softmax_fwd, relpos=1)
+ * Scores/probs are [Z=B*H, Tq, ldS] with ldS >= Tk (padding columns written 0).
+ * mask: uint8 (1 = masked) addressed mask[b*mask_sb + i*mask_sq + j], may be NULL.
+ * ---------------------------------------------------------------------- */
+int lasr_qbias_fwd(const void* qkv, int dt, int B, int T, int H, int dk, int64_t ld_qkv,
+                   const float* bias_u, const float* bias_v, void* qu, void* qv, void* stream);
+int lasr_qbias_bwd(const void* dqu, const void* dqv, int dt, int B, int T, int H, int dk,
+                   void* dqkv, int64_t ld_dqkv, float* dbias_u, float* dbias_v,
+                   float* workspace, int64_t ws_floats, void* stream);
+int lasr_attn_softmax_fwd(const float* s_ac, const float* s_bd, int relpos, int B, int H,
+                          int Tq, int Tk, int ldS, const uint8_t* mask, int64_t mask_sb,
+                          int64_t mask_sq, void* P, int pdt, float drop_p, uint64_t seed,
+                          void* Praw, void* stream);
+/* P: probabilities after dropout (the P.V operand); Praw (optional, needed only when
+ * drop_p > 0): probabilities before dropout, for the backward.
+ * bwd: dS = Praw * (dPd*dropmask - rowsum(Praw*dPd*dropmask)), zeroed where masked
+ * (masked_fill backward); dPd = dO V^T (fp32 [Z,Tq,ldS]). */
+int lasr_attn_softmax_bwd(const void* P, int pdt, const float* dPd, int B, int H, int Tq, int Tk,
+                          int ldS, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq,
+                          float drop_p, uint64_t seed, void* dS, int dsdt, void* stream);
+/* Inverse of rel_shift: dBD[z,r,c] = dS[z,i,j] for the unique (i,j) that reads
+ * BD[r,c] in attention.py:99-118, else 0. */
+int lasr_relshift_bwd(const void* dS, int dt, int Z, int T, int ldS, void* dBD, void* stream);
+/* dst[t, h*dk + c] = sum_b src[b,h,t,c]  (pos-projection grad reduced over batch). */
+int lasr_reduce_batch(const float* src, int B, int H, int T, int dk, void* dst, int dt,
+                      void* stream);
+
+/* ------------------------------------------------------------------------
+ * Conv2d subsampling (liteasr/nets/subsampling.py:31-47), channels-last layout.
+ * conv1: x [B,T,F] fp32 -> y1 [B,T1,F1,C] = relu(conv3x3s2(x) + b)   (W1: [C,9])
+ * conv1 bwd: dW1[C,9], db1[C] from dy1 (pre-masked by relu').
+ * im2col: y1 -> col [B*T2*F2, 9*C] (k = (kh*3+kw)*C + cin).
+ * col2im: dcol -> dy1 (sum of the <=4 taps), multiplied by relu'(y1).
+ * ---------------------------------------------------------------------- */
+int lasr_conv1_fwd(const float* x, int B, int T, int F, int C, const float* w,
+                   const float* bias, void* y1, int dt, void* stream);
+int lasr_conv1_bwd(const float* x, int B, int T, int F, int C, const void* dy1, int dt,
+                   float* dw, float* db, float* workspace, int64_t ws_floats, void* stream);
+int lasr_im2col3x3s2(const void* y1, int dt, int B, int T1, int F1, int C, void* col,
+                     void* stream);
+int lasr_col2im3x3s2(const void* dcol, int dt, int B, int T1, int F1, int C,
+                     const void* y1, void* dy1, void* stream);
+/* Transpose the last two dims of [N][A][Bd] into [N][Bd][A] (fp32 -> dst dtype), or
+ * (reverse=1) [N][Bd][A] -> [N][A][Bd] with optional accumulate into fp32. */
+int lasr_permute_last2(const void* src, int sdt, int64_t N, int64_t A, int64_t Bd, void* dst,
+                       int ddt, int reverse, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Conformer convolution module (liteasr/nets/conformer_convolution.py:44-57),
+ * channels-last [B,T,C]:  glu(pw1) -> depthwise conv (K taps, pad (K-1)/2) -> BN(train)
+ * -> swish -> pw2.  pw1/pw2 are lasr_gemm calls.
+ * ---------------------------------------------------------------------- */
+int lasr_glu_dwconv_fwd(const void* z1, int dt, int B, int T, int C, int K, const float* w,
+                        const float* bias, void* y, int ydt, float* stats_ws, void* stream);
+/* number of stats partials written by lasr_glu_dwconv_fwd (3*C floats each) */
+int lasr_dwconv_nparts(int B, int T);
+int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float eps, float momentum,
+                     const float* gamma, const float* beta, float* running_mean,
+                     float* running_var, int64_t* num_batches, float* mean, float* rstd,
+                     float* scale, float* shift, int update_running, void* stream);
+int lasr_bn_swish_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
+                      const float* shift, void* h, int hdt, void* stream);
+/* BN(train)+Swish backward: dgamma/dbeta accumulated, dy = BN'(dh * swish'(u)).
+ * ws >= (ceil(rows/64)+1)*2*C floats. */
+int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt, int64_t rows, int C,
+                      const float* scale, const float* shift, const float* mean,
+                      const float* rstd, const float* gamma, float* dgamma, float* dbeta,
+                      void* dy, int dydt, float* ws, int64_t ws_floats, void* stream);
+int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int dydt, int B, int T, int C,
+                        int K, const float* w, void* dz1, float* dw, float* db, float* ws,
+                        int64_t ws_floats, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Elementwise / embedding / positional encoding
+ * ---------------------------------------------------------------------- */
+int lasr_cast(const void* src, int sdt, void* dst, int ddt, int64_t n, void* stream);
+int lasr_scale_add(const void* a, int adt, const void* b, int bdt, float sa, float sb,
+                   void* out, int odt, int64_t n, void* stream); /* out = sa*a + sb*b */
+/* Decoder embedding + absolute PE (liteasr/nets/transformer_decoder.py:77-78,
+ * positional_encoding.py:49-56): y[r,:] = E[ids[r],:]*xscale + pe[r % L,:], dropout. */
+int lasr_embed_pe_fwd(const int32_t* ids, int R, int L, int D, const float* E,
+                      const float* pe, float xscale, float p, uint64_t seed, void* y, int ydt,
+                      void* stream);
+int lasr_embed_bwd(const int32_t* ids, int R, int D, const void* dy, int dydt, float xscale,
+                   float p, uint64_t seed, float* dE, void* stream);
+/* y = x*xscale (+ pe[t]) with dropout; rows = B*T, row r uses pe row r % T. */
+int lasr_pe_fwd(const void* x, int xdt, int64_t rows, int T, int D, const float* pe,
+                float xscale, float p, uint64_t seed, void* y, int ydt, void* stream);
+
+/* ------------------------------------------------------------------------
+ * U2 bookkeeping (liteasr/models/u2.py:319-358, liteasr/utils/mask.py:8-90,
+ * transformer_encoder.py:117-120): int64 in -> int32/uint8 out, bit-exact.
+ *   ys_in [B, L+1]  = [sos | ys(-1 -> eos)]
+ *   tgt   [B, L+1]  = [ys | -1] with tgt[b, ylen[b]] = eos
+ *   tgt_ctc [B, L]  = ys (int32)
+ *   dec_mask [B, L+1, L+1] = (j >= ylen[b]+1) | (j > i)
+ *   enc_mask [B, T'] = key padding after the two stride-2 slicings
+ *   pred_len [B]    = ((xlen-1)//2-1)//2
+ *   ylen32 [B]
+ * ---------------------------------------------------------------------- */
+int lasr_u2_prep(const int64_t* xlens, const int64_t* ys, const int64_t* ylens, int B, int Tx,
+                 int L, int Tsub, int sos, int eos, int chunk, int32_t* ys_in, int32_t* tgt,
+                 int32_t* tgt_ctc, uint8_t* dec_mask, uint8_t* enc_mask, int32_t* pred_len,
+                 int32_t* ylen32, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Optimizer: clip_grad_norm_ + NaN-skip + Noam/Adam over flat fp32 buffers
+ * (liteasr/trainer.py:152-171, liteasr/optims/noam.py:33-46, optims/adam.py:27-34,
+ *  torch.optim.Adam semantics).  State lives on the device:
+ *   state[0] = successful step count (float), state[1] = last lr, state[2] = last norm,
+ *   state[3] = skipped flag of the last call.
+ * lr_mode 0: constant lr; 1: Noam (factor, model_dim, warmup).
+ * ---------------------------------------------------------------------- */
+int lasr_sumsq_nparts(int64_t n);
+int lasr_sumsq_partial(const float* g, int64_t n, float* ws, int64_t ws_floats, void* stream);
+/* state[5]: [0] taken steps, [1] lr of the last step, [2] grad norm, [3] skipped flag,
+ * [4] clip coefficient.  ws/nparts: the lasr_sumsq_partial output (may cover several
+ * gradient buffers concatenated). param_lp: optional low-precision working copy that is
+ * refreshed in the same pass. */
+int lasr_adam_step(float* param, void* param_lp, int lp_dtype, const float* grad, float* m,
+                   float* v, int64_t n, const float* ws, int nparts, float* state,
+                   float max_norm, int lr_mode, float lr, float factor, float model_dim,
+                   float warmup, float beta1, float beta2, float eps, float weight_decay,
+                   void* stream);
+int lasr_fill(void* dst, int dt, int64_t n, float value, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LITEASR_HIP_H */

@@ -1,0 +1,134 @@
+"""ctypes binding of libliteasr_hip.so (C ABI declared in include/liteasr_hip.h).
+
+The library is the product path: there is no fallback.  If it cannot be loaded the
+import of any op raises, loudly.  Build it with ``make`` (or ``__graft_entry__.build()``).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "LITEASR_HIP_LIB", os.path.join(_HERE, "lib", "libliteasr_hip.so")
+)
+
+F32, BF16, I32, I64, U8 = 0, 1, 2, 3, 4
+ACT_NONE, ACT_RELU, ACT_SWISH = 0, 1, 2
+
+_p = C.c_void_p
+_i = C.c_int
+_l = C.c_int64
+_f = C.c_float
+_u = C.c_uint64
+
+
+class GemmArgs(C.Structure):
+    """Mirror of ``lasr_gemm_args``."""
+
+    _fields_ = [
+        ("M", _i), ("N", _i), ("K", _i),
+        ("batch", _i), ("batch_div", _i),
+        ("A", _p), ("lda_m", _l), ("lda_k", _l), ("sa1", _l), ("sa2", _l),
+        ("B", _p), ("ldb_n", _l), ("ldb_k", _l), ("sb1", _l), ("sb2", _l),
+        ("C", _p), ("ldc", _l), ("sc1", _l), ("sc2", _l),
+        ("in_dtype", _i), ("c_dtype", _i),
+        ("alpha", _f), ("alpha_dev", _p),
+        ("beta", _f),
+        ("bias", _p),
+        ("act", _i),
+        ("zout", _p),
+        ("aux", _p), ("aux_dtype", _i), ("ldaux", _l), ("aux_act", _i),
+        ("drop_p", _f), ("drop_seed", _u),
+        ("res", _p), ("res_dtype", _i), ("ldres", _l), ("res_scale", _f),
+        ("split_k", _i), ("workspace", _p), ("workspace_bytes", _l),
+    ]
+
+
+# name -> argtypes (all return int unless listed in _RESTYPES)
+SIGNATURES = {
+    "lasr_version": [],
+    "lasr_last_error": [],
+    "lasr_gemm": [C.POINTER(GemmArgs), _p],
+    "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
+    "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],
+    "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,
+                           _p, _i, _f, _f, _u, _p],
+    "lasr_branch_grad": [_p, _i, _l, _p, _i, _f, _f, _u, _p],
+    "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _p, _p],
+    "lasr_ctc_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p],
+    "lasr_lsm_kl_fwd": [_p, _i, _i, _i, _p, _i, _f, _p, _p, _p],
+    "lasr_lsm_kl_bwd": [_p, _i, _i, _i, _p, _i, _f, _p, _p, _i, _f, _p, _p],
+    "lasr_loss_combine": [_p, _i, _f, _p, _i, _f, _p, _p],
+    "lasr_qbias_fwd": [_p, _i, _i, _i, _i, _i, _l, _p, _p, _p, _p, _p],
+    "lasr_qbias_bwd": [_p, _p, _i, _i, _i, _i, _i, _p, _l, _p, _p, _p, _l, _p],
+    "lasr_attn_softmax_fwd": [_p, _p, _i, _i, _i, _i, _i, _i, _p, _l, _l, _p, _i, _f, _u, _p, _p],
+    "lasr_attn_softmax_bwd": [_p, _i, _p, _i, _i, _i, _i, _i, _p, _l, _l, _f, _u, _p, _i, _p],
+    "lasr_relshift_bwd": [_p, _i, _i, _i, _i, _p, _p],
+    "lasr_reduce_batch": [_p, _i, _i, _i, _i, _p, _i, _p],
+    "lasr_conv1_fwd": [_p, _i, _i, _i, _i, _p, _p, _p, _i, _p],
+    "lasr_conv1_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _l, _p],
+    "lasr_im2col3x3s2": [_p, _i, _i, _i, _i, _i, _p, _p],
+    "lasr_col2im3x3s2": [_p, _i, _i, _i, _i, _i, _p, _p, _p],
+    "lasr_permute_last2": [_p, _i, _l, _l, _l, _p, _i, _i, _i, _p],
+    "lasr_glu_dwconv_fwd": [_p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _p],
+    "lasr_dwconv_nparts": [_i, _i],
+    "lasr_bn_finalize": [_p, _i, _i, _f, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p],
+    "lasr_bn_swish_fwd": [_p, _i, _l, _i, _p, _p, _p, _i, _p],
+    "lasr_bn_swish_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _l, _p],
+    "lasr_glu_dwconv_bwd": [_p, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _l, _p],
+    "lasr_cast": [_p, _i, _p, _i, _l, _p],
+    "lasr_scale_add": [_p, _i, _p, _i, _f, _f, _p, _i, _l, _p],
+    "lasr_embed_pe_fwd": [_p, _i, _i, _i, _p, _p, _f, _f, _u, _p, _i, _p],
+    "lasr_embed_bwd": [_p, _i, _i, _p, _i, _f, _f, _u, _p, _p],
+    "lasr_pe_fwd": [_p, _i, _l, _i, _i, _p, _f, _f, _u, _p, _i, _p],
+    "lasr_u2_prep": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
+    "lasr_sumsq_nparts": [_l],
+    "lasr_sumsq_partial": [_p, _l, _p, _l, _p],
+    "lasr_adam_step": [_p, _p, _i, _p, _p, _p, _l, _p, _i, _p, _f, _i, _f, _f, _f, _f, _f, _f,
+                       _f, _f, _p],
+    "lasr_fill": [_p, _i, _l, _f, _p],
+}
+_RESTYPES = {"lasr_last_error": C.c_char_p}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the native library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"libliteasr_hip.so not found at {LIB_PATH}; build it with `make` "
+            "(the HIP path has no fallback)"
+        )
+    lib = C.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPES.get(name, C.c_int)
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Call ``name`` and raise NativeError on a non-zero status."""
+    lib = _lib if _lib is not None else load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.lasr_last_error().decode(errors="replace")
+        raise NativeError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def exported_symbols():
+    """Names of all lasr_* functions bound here."""
+    return sorted(SIGNATURES)

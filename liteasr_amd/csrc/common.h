@@ -1,0 +1,108 @@
+// Shared device helpers for the liteasr_amd HIP kernels (gfx950 / CDNA4).
+// Storage types: fp32 (`float`) and bf16 (`bf16_t`, raw 16-bit); all arithmetic
+// is done in fp32.  Wave = 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/liteasr_hip.h"
+
+typedef uint16_t bf16_t;
+
+#define LASR_DEV __device__ __forceinline__
+
+LASR_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+LASR_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+LASR_DEV float to_f(float x) { return x; }
+LASR_DEV float to_f(bf16_t x) { return bf2f(x); }
+template <typename T> LASR_DEV T from_f(float x);
+template <> LASR_DEV float from_f<float>(float x) { return x; }
+template <> LASR_DEV bf16_t from_f<bf16_t>(float x) { return f2bf(x); }
+
+template <typename T> LASR_DEV float ldf(const T* p, int64_t i) { return to_f(p[i]); }
+template <typename T> LASR_DEV void stf(T* p, int64_t i, float v) { p[i] = from_f<T>(v); }
+
+// ---- wave (64-lane) reductions ------------------------------------------------
+LASR_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+LASR_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+LASR_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block reduction (blockDim.x multiple of 64, <= 1024). `red` holds >= 16 floats.
+LASR_DEV float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += red[i];  // fixed order -> deterministic
+  return r;
+}
+LASR_DEV float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
+// ---- counter-based dropout RNG -----------------------------------------------
+// keep(seed, idx) is a pure function of (seed, logical element index), so the
+// backward pass regenerates the forward mask instead of storing it.
+LASR_DEV uint32_t lasr_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+struct DropCfg {
+  float p;        // drop probability (0 = off)
+  uint64_t seed;  // per-site, per-step seed
+};
+// Returns the multiplier for element idx: 0 or 1/(1-p); 1 when dropout is off.
+LASR_DEV float drop_mul(const DropCfg& d, uint64_t idx) {
+  if (d.p <= 0.f) return 1.f;
+  const uint32_t thr = (uint32_t)fminf(d.p * 4294967296.0f, 4294967295.0f);
+  return lasr_hash(d.seed, idx) >= thr ? 1.f / (1.f - d.p) : 0.f;
+}
+
+LASR_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+LASR_DEV float swishf(float x) { return x * sigmoidf_(x); }
+LASR_DEV float swish_grad(float z) {
+  const float s = sigmoidf_(z);
+  return s * (1.f + z * (1.f - s));
+}
+
+// ---- error plumbing (defined in capi.cpp) ------------------------------------
+void lasr_set_error(const char* fmt, ...);
+int lasr_check_launch(const char* what);
+
+#define LASR_CHECK_ARG(cond, ...)          \
+  do {                                     \
+    if (!(cond)) {                         \
+      lasr_set_error(__VA_ARGS__);         \
+      return LASR_ERR_INVALID;             \
+    }                                      \
+  } while (0)
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -1,0 +1,257 @@
+// CTC loss (blank = 0, reduction = sum) fused with log_softmax over the vocabulary.
+//
+// Reference call site: liteasr/criterions/hybrid_ctc_attn.py:67-75
+//   h_ctc.transpose(0,1).log_softmax(-1) -> nn.CTCLoss(reduction="sum")(..., get_pred_len(xlens), ylens)
+// whose arithmetic lives in PyTorch aten (ctc_loss / _ctc_loss_backward).  The
+// composed gradient w.r.t. the *logits* is softmax - gamma (gamma = posterior of the
+// extended-label lattice), which is what lasr_ctc_bwd writes directly.
+//
+// Work split (per utterance b, lattice S_b = 2*L_b + 1 states):
+//   ctc_lse_gather_kernel : one workgroup per (b,t) row: online max/sum-exp over V
+//                           (one HBM read of the row) + gather of the L_b+1 label
+//                           log-probs the lattice needs.
+//   ctc_alpha_kernel      : one workgroup per utterance, threads over states, LDS
+//                           ping-pong across the serial t recursion.
+//   ctc_beta_kernel       : same, backward in t.
+//   ctc_grad_kernel       : one workgroup per (b,t) row: gamma from alpha+beta, then a
+//                           single coalesced write of g*(softmax - gamma) over V.
+#include "common.h"
+
+template <typename T>
+__global__ __launch_bounds__(256) void ctc_lse_gather_kernel(const T* __restrict__ logits, int B,
+                                                             int T_, int V,
+                                                             const int32_t* __restrict__ targets,
+                                                             int Lmax, const int32_t* ilen,
+                                                             const int32_t* tlen, float* lse,
+                                                             float* lp) {
+  __shared__ float red[32];
+  const int row = blockIdx.x;
+  const int b = row / T_, t = row - b * T_;
+  float* lprow = lp + (int64_t)row * (Lmax + 1);
+  const int Tb = ilen[b];
+  if (t >= Tb) {  // rows past the input length never enter the lattice
+    if (threadIdx.x == 0) lse[row] = 0.f;
+    for (int j = threadIdx.x; j <= Lmax; j += blockDim.x) lprow[j] = 0.f;
+    return;
+  }
+  const T* x = logits + (int64_t)row * V;
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+    const float v = to_f(x[c]);
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+    else s += __expf(v - m);
+  }
+  const float M = block_max(m, red);
+  const float S = block_sum(m == -INFINITY ? 0.f : s * __expf(m - M), red + 16);
+  const float l = M + __logf(S);
+  if (threadIdx.x == 0) lse[row] = l;
+  const int Lb = tlen[b];
+  for (int j = threadIdx.x; j <= Lmax; j += blockDim.x) {
+    float v = 0.f;
+    if (j == 0) v = to_f(x[0]) - l;
+    else if (j <= Lb) v = to_f(x[targets[(int64_t)b * Lmax + (j - 1)]]) - l;
+    lprow[j] = v;
+  }
+}
+
+LASR_DEV float lse3(float a, float b, float c) {
+  const float m = fmaxf(a, fmaxf(b, c));
+  if (m == -INFINITY) return -INFINITY;
+  return m + __logf(__expf(a - m) + __expf(b - m) + __expf(c - m));
+}
+LASR_DEV float lse2(float a, float b) {
+  const float m = fmaxf(a, b);
+  if (m == -INFINITY) return -INFINITY;
+  return m + __logf(__expf(a - m) + __expf(b - m));
+}
+
+// label id of extended state s (blank for even s)
+LASR_DEV int ext_label(const int32_t* tg, int s) { return (s & 1) ? tg[s >> 1] : 0; }
+
+__global__ void ctc_alpha_kernel(int T_, int Lmax, const int32_t* __restrict__ targets,
+                                 const int32_t* ilen, const int32_t* tlen, const float* lp,
+                                 float* alpha, float* nll) {
+  extern __shared__ float sh[];
+  const int b = blockIdx.x;
+  const int Tb = ilen[b], Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
+  const int32_t* tg = targets + (int64_t)b * Lmax;
+  float* buf0 = sh;
+  float* buf1 = sh + Smax;
+  if (Tb <= 0) {
+    if (threadIdx.x == 0) nll[b] = (Lb == 0) ? 0.f : INFINITY;
+    return;
+  }
+  const float* lpb = lp + (int64_t)b * T_ * (Lmax + 1);
+  float* al = alpha + (int64_t)b * T_ * Smax;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    const float v = (s == 0) ? lpb[0] : (s == 1) ? lpb[1] : -INFINITY;
+    buf0[s] = v;
+    al[s] = v;
+  }
+  __syncthreads();
+  float* prev = buf0;
+  float* cur = buf1;
+  for (int t = 1; t < Tb; ++t) {
+    const float* lpt = lpb + (int64_t)t * (Lmax + 1);
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const float a0 = prev[s];
+      const float a1 = s >= 1 ? prev[s - 1] : -INFINITY;
+      float a2 = -INFINITY;
+      if (s >= 2 && (s & 1) && ext_label(tg, s) != ext_label(tg, s - 2)) a2 = prev[s - 2];
+      const float e = (s & 1) ? lpt[1 + (s >> 1)] : lpt[0];
+      const float v = lse3(a0, a1, a2) + e;
+      cur[s] = v;
+      al[(int64_t)t * Smax + s] = v;
+    }
+    __syncthreads();
+    float* tmp = prev; prev = cur; cur = tmp;
+  }
+  if (threadIdx.x == 0) {
+    const float ll = (S >= 2) ? lse2(prev[S - 1], prev[S - 2]) : prev[0];
+    nll[b] = -ll;
+  }
+}
+
+__global__ void ctc_beta_kernel(int T_, int Lmax, const int32_t* __restrict__ targets,
+                                const int32_t* ilen, const int32_t* tlen, const float* lp,
+                                float* beta) {
+  extern __shared__ float sh[];
+  const int b = blockIdx.x;
+  const int Tb = ilen[b], Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
+  if (Tb <= 0) return;
+  const int32_t* tg = targets + (int64_t)b * Lmax;
+  float* buf0 = sh;
+  float* buf1 = sh + Smax;
+  const float* lpb = lp + (int64_t)b * T_ * (Lmax + 1);
+  float* be = beta + (int64_t)b * T_ * Smax;
+  {
+    const float* lpt = lpb + (int64_t)(Tb - 1) * (Lmax + 1);
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const float e = (s & 1) ? lpt[1 + (s >> 1)] : lpt[0];
+      const float v = (s >= S - 2) ? e : -INFINITY;
+      buf0[s] = v;
+      be[(int64_t)(Tb - 1) * Smax + s] = v;
+    }
+  }
+  __syncthreads();
+  float* nxt = buf0;
+  float* cur = buf1;
+  for (int t = Tb - 2; t >= 0; --t) {
+    const float* lpt = lpb + (int64_t)t * (Lmax + 1);
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const float b0 = nxt[s];
+      const float b1 = (s + 1 < S) ? nxt[s + 1] : -INFINITY;
+      float b2 = -INFINITY;
+      if (s + 2 < S && (s & 1) && ext_label(tg, s) != ext_label(tg, s + 2)) b2 = nxt[s + 2];
+      const float e = (s & 1) ? lpt[1 + (s >> 1)] : lpt[0];
+      const float v = lse3(b0, b1, b2) + e;
+      cur[s] = v;
+      be[(int64_t)t * Smax + s] = v;
+    }
+    __syncthreads();
+    float* tmp = nxt; nxt = cur; cur = tmp;
+  }
+}
+
+template <typename T, typename TG>
+__global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ logits, int B, int T_,
+                                                       int V, const int32_t* __restrict__ targets,
+                                                       int Lmax, const int32_t* ilen,
+                                                       const int32_t* tlen, const float* lse,
+                                                       const float* lp, const float* alpha,
+                                                       const float* beta, const float* nll,
+                                                       TG* grad, float gscale, const float* gdev) {
+  // dynamic LDS: [Lmax] gamma per label position, [Lmax] labels, [(V+31)/32] label bitmap
+  extern __shared__ float sh[];
+  __shared__ float red[32];
+  float* glab = sh;
+  int* lab = (int*)(sh + Lmax);
+  uint32_t* bits = (uint32_t*)(sh + 2 * Lmax);
+  const int row = blockIdx.x;
+  const int b = row / T_, t = row - b * T_;
+  TG* g = grad + (int64_t)row * V;
+  const int Tb = ilen[b];
+  if (t >= Tb) {
+    for (int c = threadIdx.x; c < V; c += blockDim.x) g[c] = from_f<TG>(0.f);
+    return;
+  }
+  const int Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
+  const float nl = nll[b];
+  const float* a = alpha + ((int64_t)b * T_ + t) * Smax;
+  const float* be = beta + ((int64_t)b * T_ + t) * Smax;
+  const float* lpt = lp + (int64_t)row * (Lmax + 1);
+  const int32_t* tg = targets + (int64_t)b * Lmax;
+  // blank posterior: sum over even states
+  float gb = 0.f;
+  for (int s = threadIdx.x * 2; s < S; s += blockDim.x * 2) gb += __expf(a[s] + be[s] + nl - lpt[0]);
+  gb = block_sum(gb, red);
+  for (int w = threadIdx.x; w < (V + 31) / 32; w += blockDim.x) bits[w] = 0u;
+  __syncthreads();
+  for (int j = threadIdx.x; j < Lb; j += blockDim.x) {
+    const int s = 2 * j + 1;
+    glab[j] = __expf(a[s] + be[s] + nl - lpt[1 + j]);
+    lab[j] = tg[j];
+    atomicOr(&bits[tg[j] >> 5], 1u << (tg[j] & 31));
+  }
+  __syncthreads();
+  const float gs = gscale * (gdev ? gdev[0] : 1.f);
+  const T* x = logits + (int64_t)row * V;
+  const float l = lse[row];
+  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+    float sub = (c == 0) ? gb : 0.f;
+    if (c != 0 && ((bits[c >> 5] >> (c & 31)) & 1u)) {
+      for (int j = 0; j < Lb; ++j)
+        if (lab[j] == c) sub += glab[j];
+    }
+    g[c] = from_f<TG>(gs * (__expf(to_f(x[c]) - l) - sub));
+  }
+}
+
+static int ctc_block(int S) {
+  int nt = ((S + 63) / 64) * 64;
+  return nt < 64 ? 64 : (nt > 1024 ? 1024 : nt);
+}
+
+extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V,
+                            const int32_t* targets, int Lmax, const int32_t* ilen,
+                            const int32_t* tlen, float* lse, float* lp, float* alpha, float* nll,
+                            void* stream) {
+  LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0, "lasr_ctc_fwd: bad sizes");
+  LASR_CHECK_ARG(ldt == LASR_F32 || ldt == LASR_BF16, "lasr_ctc_fwd: bad dtype");
+  LASR_CHECK_ARG(2 * (2 * Lmax + 1) * 4 <= 160 * 1024, "lasr_ctc_fwd: Lmax too large");
+  hipStream_t st = (hipStream_t)stream;
+  if (ldt == LASR_F32)
+    ctc_lse_gather_kernel<float><<<B * T, 256, 0, st>>>((const float*)logits, B, T, V, targets, Lmax, ilen, tlen, lse, lp);
+  else
+    ctc_lse_gather_kernel<bf16_t><<<B * T, 256, 0, st>>>((const bf16_t*)logits, B, T, V, targets, Lmax, ilen, tlen, lse, lp);
+  int rc = lasr_check_launch("ctc_lse_gather");
+  if (rc) return rc;
+  const int Smax = 2 * Lmax + 1;
+  ctc_alpha_kernel<<<B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(T, Lmax, targets, ilen, tlen, lp, alpha, nll);
+  return lasr_check_launch("ctc_alpha");
+}
+
+extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V,
+                            const int32_t* targets, int Lmax, const int32_t* ilen,
+                            const int32_t* tlen, const float* lse, const float* lp,
+                            const float* alpha, const float* nll, float* beta, void* grad, int gdt,
+                            float gscale, const float* gdev, void* stream) {
+  LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0, "lasr_ctc_bwd: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  const int Smax = 2 * Lmax + 1;
+  ctc_beta_kernel<<<B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(T, Lmax, targets, ilen, tlen, lp, beta);
+  int rc = lasr_check_launch("ctc_beta");
+  if (rc) return rc;
+  const size_t shm = ((size_t)2 * (Lmax > 0 ? Lmax : 1) + (V + 31) / 32) * sizeof(float);
+  LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_ctc_bwd: vocab/labels too large for LDS");
+#define CTC_G(TT, TGG)                                                                      \
+  ctc_grad_kernel<TT, TGG><<<B * T, 256, shm, st>>>((const TT*)logits, B, T, V, targets, Lmax, \
+                                                    ilen, tlen, lse, lp, alpha, beta, nll,     \
+                                                    (TGG*)grad, gscale, gdev)
+  if (ldt == LASR_F32 && gdt == LASR_F32) CTC_G(float, float);
+  else if (ldt == LASR_F32) CTC_G(float, bf16_t);
+  else if (gdt == LASR_F32) CTC_G(bf16_t, float);
+  else CTC_G(bf16_t, bf16_t);
+#undef CTC_G
+  return lasr_check_launch("ctc_grad");
+}

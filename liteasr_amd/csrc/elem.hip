@@ -1,0 +1,151 @@
+// Elementwise kernels: casts, scaled adds, positional encodings, decoder embedding.
+// Reference: liteasr/nets/positional_encoding.py:49-56 (x*sqrt(d) + pe, dropout) and
+// :68-75 (relative: dropout(x*sqrt(d)), dropout(pe[:, :T])); decoder embedding
+// liteasr/nets/transformer_decoder.py:77-78.
+#include "common.h"
+
+static unsigned gridn(int64_t n) { return (unsigned)std::min<int64_t>(cdiv(n, 256), 16384); }
+
+template <typename TS, typename TD>
+__global__ void cast_kernel(const TS* s, TD* d, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = from_f<TD>(to_f(s[i]));
+}
+
+template <typename TA, typename TB, typename TO>
+__global__ void scale_add_kernel(const TA* a, const TB* b, float sa, float sb, TO* o, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = sa * to_f(a[i]);
+    if (b) v += sb * to_f(b[i]);
+    o[i] = from_f<TO>(v);
+  }
+}
+
+template <typename TX, typename TY>
+__global__ void pe_fwd_kernel(const TX* x, int64_t rows, int T, int D, const float* pe,
+                              float xscale, DropCfg d, TY* y) {
+  const int64_t n = rows * D;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / D;
+    const int c = (int)(e - r * D);
+    float v = x ? to_f(x[e]) * xscale : 0.f;
+    if (pe) v += pe[(r % T) * D + c];
+    y[e] = from_f<TY>(v * drop_mul(d, (uint64_t)e));
+  }
+}
+
+template <typename TY>
+__global__ void embed_pe_fwd_kernel(const int32_t* ids, int R, int L, int D, const float* E,
+                                    const float* pe, float xscale, DropCfg d, TY* y) {
+  const int64_t n = (int64_t)R * D;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / D), c = (int)(e - (int64_t)r * D);
+    const float v = E[(int64_t)ids[r] * D + c] * xscale + pe[(int64_t)(r % L) * D + c];
+    y[e] = from_f<TY>(v * drop_mul(d, (uint64_t)e));
+  }
+}
+
+// Deterministic embedding backward: the workgroup of the first row holding an id sums
+// every row with that id in row order and adds it to dE[id].
+template <typename TD>
+__global__ void embed_bwd_kernel(const int32_t* ids, int R, int D, const TD* dy, float xscale,
+                                 DropCfg d, float* dE) {
+  extern __shared__ int sid[];
+  for (int i = threadIdx.x; i < R; i += blockDim.x) sid[i] = ids[i];
+  __syncthreads();
+  const int r = blockIdx.x;
+  const int id = sid[r];
+  for (int k = 0; k < r; ++k)
+    if (sid[k] == id) return;  // not the first occurrence (uniform across the block)
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float acc = 0.f;
+    for (int k = r; k < R; ++k)
+      if (sid[k] == id) {
+        const int64_t e = (int64_t)k * D + c;
+        acc += to_f(dy[e]) * drop_mul(d, (uint64_t)e);
+      }
+    dE[(int64_t)id * D + c] += acc * xscale;
+  }
+}
+
+template <typename T>
+__global__ void fill_kernel(T* d, int64_t n, float v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = from_f<T>(v);
+}
+
+extern "C" int lasr_cast(const void* src, int sdt, void* dst, int ddt, int64_t n, void* stream) {
+  if (n <= 0) return LASR_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (sdt == LASR_F32 && ddt == LASR_F32) cast_kernel<float, float><<<gridn(n), 256, 0, st>>>((const float*)src, (float*)dst, n);
+  else if (sdt == LASR_F32) cast_kernel<float, bf16_t><<<gridn(n), 256, 0, st>>>((const float*)src, (bf16_t*)dst, n);
+  else if (ddt == LASR_F32) cast_kernel<bf16_t, float><<<gridn(n), 256, 0, st>>>((const bf16_t*)src, (float*)dst, n);
+  else cast_kernel<bf16_t, bf16_t><<<gridn(n), 256, 0, st>>>((const bf16_t*)src, (bf16_t*)dst, n);
+  return lasr_check_launch("cast");
+}
+
+extern "C" int lasr_scale_add(const void* a, int adt, const void* b, int bdt, float sa, float sb,
+                              void* out, int odt, int64_t n, void* stream) {
+  if (n <= 0) return LASR_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned g = gridn(n);
+#define SA(TA, TB, TO) scale_add_kernel<TA, TB, TO><<<g, 256, 0, st>>>((const TA*)a, (const TB*)b, sa, sb, (TO*)out, n)
+  const bool af = adt == LASR_F32, bf = bdt == LASR_F32, of = odt == LASR_F32;
+  if (af && bf && of) SA(float, float, float);
+  else if (af && bf) SA(float, float, bf16_t);
+  else if (af && of) SA(float, bf16_t, float);
+  else if (af) SA(float, bf16_t, bf16_t);
+  else if (bf && of) SA(bf16_t, float, float);
+  else if (bf) SA(bf16_t, float, bf16_t);
+  else if (of) SA(bf16_t, bf16_t, float);
+  else SA(bf16_t, bf16_t, bf16_t);
+#undef SA
+  return lasr_check_launch("scale_add");
+}
+
+extern "C" int lasr_pe_fwd(const void* x, int xdt, int64_t rows, int T, int D, const float* pe,
+                           float xscale, float p, uint64_t seed, void* y, int ydt, void* stream) {
+  const int64_t n = rows * D;
+  if (n <= 0) return LASR_OK;
+  DropCfg d{p, seed};
+  hipStream_t st = (hipStream_t)stream;
+#define PF(TX, TY) pe_fwd_kernel<TX, TY><<<gridn(n), 256, 0, st>>>((const TX*)x, rows, T, D, pe, xscale, d, (TY*)y)
+  if (xdt == LASR_F32 && ydt == LASR_F32) PF(float, float);
+  else if (xdt == LASR_F32) PF(float, bf16_t);
+  else if (ydt == LASR_F32) PF(bf16_t, float);
+  else PF(bf16_t, bf16_t);
+#undef PF
+  return lasr_check_launch("pe_fwd");
+}
+
+extern "C" int lasr_embed_pe_fwd(const int32_t* ids, int R, int L, int D, const float* E,
+                                 const float* pe, float xscale, float p, uint64_t seed, void* y,
+                                 int ydt, void* stream) {
+  const int64_t n = (int64_t)R * D;
+  if (n <= 0) return LASR_OK;
+  DropCfg d{p, seed};
+  hipStream_t st = (hipStream_t)stream;
+  if (ydt == LASR_F32) embed_pe_fwd_kernel<float><<<gridn(n), 256, 0, st>>>(ids, R, L, D, E, pe, xscale, d, (float*)y);
+  else embed_pe_fwd_kernel<bf16_t><<<gridn(n), 256, 0, st>>>(ids, R, L, D, E, pe, xscale, d, (bf16_t*)y);
+  return lasr_check_launch("embed_pe_fwd");
+}
+
+extern "C" int lasr_embed_bwd(const int32_t* ids, int R, int D, const void* dy, int dydt,
+                              float xscale, float p, uint64_t seed, float* dE, void* stream) {
+  if (R <= 0) return LASR_OK;
+  LASR_CHECK_ARG(R <= 16384, "lasr_embed_bwd: R=%d > 16384", R);
+  DropCfg d{p, seed};
+  hipStream_t st = (hipStream_t)stream;
+  const size_t shm = (size_t)R * sizeof(int);
+  if (dydt == LASR_F32) embed_bwd_kernel<float><<<R, 256, shm, st>>>(ids, R, D, (const float*)dy, xscale, d, dE);
+  else embed_bwd_kernel<bf16_t><<<R, 256, shm, st>>>(ids, R, D, (const bf16_t*)dy, xscale, d, dE);
+  return lasr_check_launch("embed_bwd");
+}
+
+extern "C" int lasr_fill(void* dst, int dt, int64_t n, float value, void* stream) {
+  if (n <= 0) return LASR_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (dt == LASR_F32) fill_kernel<float><<<gridn(n), 256, 0, st>>>((float*)dst, n, value);
+  else fill_kernel<bf16_t><<<gridn(n), 256, 0, st>>>((bf16_t*)dst, n, value);
+  return lasr_check_launch("fill");
+}

@@ -1,0 +1,449 @@
+// Batched GEMM with fused epilogues (lasr_gemm, include/liteasr_hip.h).
+//
+// bf16 path: 256-thread workgroups (4 waves, 2x2), BMxBNx32 tiles, register-staged
+// double-buffered LDS, v_mfma_f32_16x16x32_bf16, fp32 accumulation.  LDS tiles are
+// stored K-contiguous ([rows][32] bf16, 64-B rows) with a 16-B-chunk XOR swizzle
+// chunk' = chunk ^ H[(row>>2)&3], H = {0,2,3,1}: for the ds_read_b128 lane groups of
+// gfx950 every 16-lane group then covers all 16 slots of a 256-B bank row (no
+// conflicts).  Operands that are not K-contiguous in HBM (the dW "TN" GEMMs, the
+// attention dS^T products) are loaded 8-wide along M/N and transposed on the LDS
+// write (pairs of k -> one ds_write_b32).
+// fp32 path (parity build): 64x64x16 tiles on v_mfma_f32_16x16x4f32 (exact fp32 FMA
+// chain), element-wise staging; correctness first.
+//
+// Replaces aten addmm/mm/bmm at liteasr/nets/feed_forward.py:18-19,
+// attention.py:35-37,58,69,145,149, subsampling.py:34,47, conformer_convolution.py:48,55,
+// ctc.py:29, transformer_decoder.py:91 (and their autograd backward GEMMs).
+#include "common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct GemmP {
+  int M, N, K, batch, batch_div;
+  const void* A;
+  int64_t lda_m, lda_k, sa1, sa2;
+  const void* B;
+  int64_t ldb_n, ldb_k, sb1, sb2;
+  void* C;
+  int64_t ldc, sc1, sc2;
+  float alpha;
+  const float* alpha_dev;
+  float beta;
+  const float* bias;
+  int act;
+  void* zout;
+  const void* aux;
+  int aux_dtype;
+  int64_t ldaux;
+  int aux_act;
+  DropCfg drop;
+  const void* res;
+  int res_dtype;
+  int64_t ldres;
+  float res_scale;
+  int split_k;
+  int kchunk;
+  float* ws;
+  int a_vec, b_vec;
+};
+
+LASR_DEV float load_any(const void* p, int dt, int64_t i) {
+  return dt == LASR_F32 ? ((const float*)p)[i] : bf2f(((const bf16_t*)p)[i]);
+}
+
+// Full epilogue for one output element.
+template <typename TC>
+LASR_DEV void epi_store(const GemmP& p, int z1, int z2, int z, int m, int n, float acc,
+                        float alpha_eff) {
+  if (m >= p.M || n >= p.N) return;
+  float v = acc * alpha_eff;
+  if (p.bias) v += p.bias[n];
+  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
+  if (p.zout) ((TC*)p.zout)[cidx] = from_f<TC>(v);
+  if (p.act == LASR_ACT_RELU) v = fmaxf(v, 0.f);
+  else if (p.act == LASR_ACT_SWISH) v = swishf(v);
+  if (p.aux) {
+    const float a = load_any(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n);
+    v *= (p.aux_act == LASR_ACT_RELU) ? (a > 0.f ? 1.f : 0.f) : swish_grad(a);
+  }
+  if (p.drop.p > 0.f) v *= drop_mul(p.drop, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n);
+  if (p.res) v = load_any(p.res, p.res_dtype, (int64_t)m * p.ldres + n) + p.res_scale * v;
+  TC* C = (TC*)p.C;
+  if (p.beta != 0.f) v += p.beta * to_f(C[cidx]);
+  C[cidx] = from_f<TC>(v);
+}
+
+LASR_DEV float alpha_of(const GemmP& p) {
+  return p.alpha_dev ? p.alpha * p.alpha_dev[0] : p.alpha;
+}
+
+// ============================ bf16 MFMA kernel ===================================
+LASR_DEV int swz(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
+LASR_DEV int lds_off(int row, int chunk) { return row * 32 + ((chunk ^ swz(row)) << 3); }
+
+LASR_DEV uint32_t u4_get16(const uint4& v, int i) {
+  const uint32_t w = (i < 2) ? v.x : (i < 4) ? v.y : (i < 6) ? v.z : v.w;
+  return (i & 1) ? (w >> 16) : (w & 0xFFFFu);
+}
+
+// 8 consecutive elements along the contiguous axis; zero outside [0,lim).
+LASR_DEV uint4 load8(const bf16_t* src, int start, int lim, bool vec) {
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (vec && start + 8 <= lim) {
+    v = *(const uint4*)src;
+  } else {
+    uint32_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = (start + j < lim) ? (uint32_t)src[j] : 0u;
+    v.x = e[0] | (e[1] << 16);
+    v.y = e[2] | (e[3] << 16);
+    v.z = e[4] | (e[5] << 16);
+    v.w = e[6] | (e[7] << 16);
+  }
+  return v;
+}
+
+// Tile loader for one operand: R_TILE rows (M or N) x 32 k.
+template <int R_TILE, bool KC>
+struct TileLoader {
+  static constexpr int UNITS = KC ? R_TILE * 4 : R_TILE * 2;  // KC: (row,chunk); else (8 rows, 2 k)
+  static constexpr int PER = (UNITS + 255) / 256;
+  uint4 r0[PER], r1[PER];
+
+  LASR_DEV void load(const bf16_t* base, int64_t ld_r, int64_t ld_k, int row0, int R, int k0,
+                     int kend, bool vec, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int u = tid + i * 256;
+      if (u < UNITS) {
+        if (KC) {
+          const int r = u >> 2, c = u & 3;
+          const int gr = row0 + r, gk = k0 + c * 8;
+          if (gr < R) r0[i] = load8(base + (int64_t)gr * ld_r + gk, gk, kend, vec);
+          else r0[i] = make_uint4(0, 0, 0, 0);
+        } else {
+          const int rb = u % (R_TILE / 8), kp = u / (R_TILE / 8);
+          const int gr = row0 + rb * 8, gk = k0 + kp * 2;
+          if (gk < kend) r0[i] = load8(base + (int64_t)gk * ld_k + gr, gr, R, vec);
+          else r0[i] = make_uint4(0, 0, 0, 0);
+          if (gk + 1 < kend) r1[i] = load8(base + (int64_t)(gk + 1) * ld_k + gr, gr, R, vec);
+          else r1[i] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
+  }
+  LASR_DEV void store(bf16_t* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int u = tid + i * 256;
+      if (u < UNITS) {
+        if (KC) {
+          const int r = u >> 2, c = u & 3;
+          *(uint4*)(lds + lds_off(r, c)) = r0[i];
+        } else {
+          const int rb = u % (R_TILE / 8), kp = u / (R_TILE / 8);
+          const int k = kp * 2;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int r = rb * 8 + j;
+            const uint32_t w = u4_get16(r0[i], j) | (u4_get16(r1[i], j) << 16);
+            *(uint32_t*)(lds + lds_off(r, k >> 3) + (k & 7)) = w;
+          }
+        }
+      }
+    }
+  }
+};
+
+template <int BM, int BN, bool AKC, bool BKC, typename TC>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
+  constexpr int BK = 32;
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * BK];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const int zz = blockIdx.z;
+  const int s = zz % p.split_k, z = zz / p.split_k;
+  const int z1 = z / p.batch_div, z2 = z % p.batch_div;
+  const bf16_t* A = (const bf16_t*)p.A + z1 * p.sa1 + z2 * p.sa2;
+  const bf16_t* B = (const bf16_t*)p.B + z1 * p.sb1 + z2 * p.sb2;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = s * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  TileLoader<BM, AKC> la;
+  TileLoader<BN, BKC> lb;
+  const int64_t a_ldr = AKC ? p.lda_m : 0, a_ldk = AKC ? 0 : p.lda_k;
+  const int64_t b_ldr = BKC ? p.ldb_n : 0, b_ldk = BKC ? 0 : p.ldb_k;
+
+  if (nk > 0) {
+    la.load(A, a_ldr, a_ldk, m0, p.M, kbeg, kend, p.a_vec, tid);
+    lb.load(B, b_ldr, b_ldk, n0, p.N, kbeg, kend, p.b_vec, tid);
+    la.store(smem, tid);
+    lb.store(smem + BM * BK, tid);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    bf16_t* cur = smem + (kt & 1) * (BM + BN) * BK;
+    bf16_t* nxt = smem + ((kt + 1) & 1) * (BM + BN) * BK;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * BK;
+      la.load(A, a_ldr, a_ldk, m0, p.M, k0, kend, p.a_vec, tid);
+      lb.load(B, b_ldr, b_ldk, n0, p.N, k0, kend, p.b_vec, tid);
+    }
+    bf16x8 af[FM], bfr[FN];
+    const int ch = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wr * WM + i * 16 + (lane & 15);
+      af[i] = *(const bf16x8*)(cur + lds_off(row, ch));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wc * WN + j * 16 + (lane & 15);
+      bfr[j] = *(const bf16x8*)(cur + BM * BK + lds_off(row, ch));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (more) {
+      la.store(nxt, tid);
+      lb.store(nxt + BM * BK, tid);
+    }
+    __syncthreads();
+  }
+
+  const int rq = (lane >> 4) * 4, cl = lane & 15;
+  if (p.split_k > 1) {
+    float* ws = p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wr * WM + i * 16 + rq + e, n = n0 + wc * WN + j * 16 + cl;
+          if (m < p.M && n < p.N) ws[(int64_t)m * p.N + n] = acc[i][j][e];
+        }
+    return;
+  }
+  const float al = alpha_of(p);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wr * WM + i * 16 + rq + e, n = n0 + wc * WN + j * 16 + cl;
+        epi_store<TC>(p, z1, z2, z, m, n, acc[i][j][e], al);
+      }
+}
+
+// ============================ fp32 MFMA kernel ===================================
+template <bool AKC, bool BKC, typename TC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
+  constexpr int BM = 64, BN = 64, BK = 16, LD = BK + 1;
+  __shared__ float As[BM * LD], Bs[BN * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int zz = blockIdx.z;
+  const int s = zz % p.split_k, z = zz / p.split_k;
+  const int z1 = z / p.batch_div, z2 = z % p.batch_div;
+  const float* A = (const float*)p.A + z1 * p.sa1 + z2 * p.sa2;
+  const float* B = (const float*)p.B + z1 * p.sb1 + z2 * p.sb2;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = s * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + q * 256;
+      int r, k;
+      if (AKC) { r = e >> 4; k = e & 15; } else { r = e & 63; k = e >> 6; }
+      const int gm = m0 + r, gk = k0 + k;
+      As[r * LD + k] = (gm < p.M && gk < kend) ? A[(int64_t)gm * p.lda_m + (int64_t)gk * p.lda_k] : 0.f;
+      if (BKC) { r = e >> 4; k = e & 15; } else { r = e & 63; k = e >> 6; }
+      const int gn = n0 + r, gk2 = k0 + k;
+      Bs[r * LD + k] = (gn < p.N && gk2 < kend) ? B[(int64_t)gn * p.ldb_n + (int64_t)gk2 * p.ldb_k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      float af[2], bfv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = As[(wr * 32 + i * 16 + (lane & 15)) * LD + kk + (lane >> 4)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfv[j] = Bs[(wc * 32 + j * 16 + (lane & 15)) * LD + kk + (lane >> 4)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int rq = (lane >> 4) * 4, cl = lane & 15;
+  if (p.split_k > 1) {
+    float* ws = p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wr * 32 + i * 16 + rq + e, n = n0 + wc * 32 + j * 16 + cl;
+          if (m < p.M && n < p.N) ws[(int64_t)m * p.N + n] = acc[i][j][e];
+        }
+    return;
+  }
+  const float al = alpha_of(p);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wr * 32 + i * 16 + rq + e, n = n0 + wc * 32 + j * 16 + cl;
+        epi_store<TC>(p, z1, z2, z, m, n, acc[i][j][e], al);
+      }
+}
+
+// Split-K reduction: sums the split partials in fixed order, then the epilogue.
+template <typename TC>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
+  const int64_t MN = (int64_t)p.M * p.N;
+  const int64_t total = MN * p.batch;
+  const float al = alpha_of(p);
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int z = (int)(i / MN);
+    const int64_t r = i - (int64_t)z * MN;
+    float acc = 0.f;
+    for (int s = 0; s < p.split_k; ++s) acc += p.ws[((int64_t)s * p.batch + z) * MN + r];
+    const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
+    epi_store<TC>(p, z / p.batch_div, z % p.batch_div, z, m, n, acc, al);
+  }
+}
+
+// ================================ host launcher ==================================
+template <bool AKC, bool BKC, typename TC>
+static void launch_bf16(const GemmP& p, int BM, int BN, dim3 grid, hipStream_t st) {
+  if (BM == 128 && BN == 128) gemm_bf16_kernel<128, 128, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
+  else if (BM == 128) gemm_bf16_kernel<128, 64, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
+  else if (BN == 128) gemm_bf16_kernel<64, 128, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
+  else gemm_bf16_kernel<64, 64, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
+}
+
+template <typename TC>
+static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int BN, dim3 grid,
+                     hipStream_t st) {
+  if (bf16in) {
+    if (akc && bkc) launch_bf16<true, true, TC>(p, BM, BN, grid, st);
+    else if (akc) launch_bf16<true, false, TC>(p, BM, BN, grid, st);
+    else if (bkc) launch_bf16<false, true, TC>(p, BM, BN, grid, st);
+    else launch_bf16<false, false, TC>(p, BM, BN, grid, st);
+  } else {
+    if (akc && bkc) gemm_f32_kernel<true, true, TC><<<grid, 256, 0, st>>>(p);
+    else if (akc) gemm_f32_kernel<true, false, TC><<<grid, 256, 0, st>>>(p);
+    else if (bkc) gemm_f32_kernel<false, true, TC><<<grid, 256, 0, st>>>(p);
+    else gemm_f32_kernel<false, false, TC><<<grid, 256, 0, st>>>(p);
+  }
+}
+
+static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+
+extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
+  LASR_CHECK_ARG(a != nullptr, "lasr_gemm: null args");
+  LASR_CHECK_ARG(a->M >= 0 && a->N >= 0 && a->K >= 0, "lasr_gemm: negative size");
+  LASR_CHECK_ARG(a->in_dtype == LASR_F32 || a->in_dtype == LASR_BF16, "lasr_gemm: bad in_dtype");
+  LASR_CHECK_ARG(a->c_dtype == LASR_F32 || a->c_dtype == LASR_BF16, "lasr_gemm: bad c_dtype");
+  LASR_CHECK_ARG(a->lda_m == 1 || a->lda_k == 1, "lasr_gemm: A needs a unit stride");
+  LASR_CHECK_ARG(a->ldb_n == 1 || a->ldb_k == 1, "lasr_gemm: B needs a unit stride");
+  LASR_CHECK_ARG(a->A && a->B && a->C, "lasr_gemm: null operand");
+  if (a->M == 0 || a->N == 0 || a->batch == 0) return LASR_OK;
+  const int batch = a->batch > 0 ? a->batch : 1;
+  const int bdiv = a->batch_div > 0 ? a->batch_div : 1;
+  LASR_CHECK_ARG(batch == 1 || (!a->aux && !a->res && !a->zout),
+                 "lasr_gemm: aux/res/zout only supported for batch == 1");
+
+  GemmP p;
+  p.M = a->M; p.N = a->N; p.K = a->K; p.batch = batch; p.batch_div = bdiv;
+  p.A = a->A; p.lda_m = a->lda_m; p.lda_k = a->lda_k; p.sa1 = a->sa1; p.sa2 = a->sa2;
+  p.B = a->B; p.ldb_n = a->ldb_n; p.ldb_k = a->ldb_k; p.sb1 = a->sb1; p.sb2 = a->sb2;
+  p.C = a->C; p.ldc = a->ldc; p.sc1 = a->sc1; p.sc2 = a->sc2;
+  p.alpha = a->alpha; p.alpha_dev = a->alpha_dev; p.beta = a->beta;
+  p.bias = a->bias; p.act = a->act; p.zout = a->zout;
+  p.aux = a->aux; p.aux_dtype = a->aux_dtype; p.ldaux = a->ldaux; p.aux_act = a->aux_act;
+  p.drop.p = a->drop_p; p.drop.seed = a->drop_seed;
+  p.res = a->res; p.res_dtype = a->res_dtype; p.ldres = a->ldres; p.res_scale = a->res_scale;
+
+  const bool akc = (a->lda_k == 1);
+  const bool bkc = (a->ldb_k == 1);
+  const bool bf = a->in_dtype == LASR_BF16;
+  {
+    const int64_t s_a = akc ? a->lda_m : a->lda_k;
+    const int64_t s_b = bkc ? a->ldb_n : a->ldb_k;
+    p.a_vec = bf && aligned16(a->A) && s_a % 8 == 0 && a->sa1 % 8 == 0 && a->sa2 % 8 == 0;
+    p.b_vec = bf && aligned16(a->B) && s_b % 8 == 0 && a->sb1 % 8 == 0 && a->sb2 % 8 == 0;
+  }
+
+  int BM = 64, BN = 64;
+  if (bf) {
+    const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    for (int c = 0; c < 4; ++c) {
+      const int64_t nb = cdiv(a->M, cfg[c][0]) * cdiv(a->N, cfg[c][1]) * (int64_t)batch;
+      BM = cfg[c][0]; BN = cfg[c][1];
+      if (nb >= 512) break;
+    }
+  }
+
+  // split-K: explicit (split_k > 1) or automatic (split_k == 0) when the epilogue is plain.
+  int split = a->split_k > 0 ? a->split_k : 1;
+  const bool plain = !a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f;
+  if (a->split_k == 0 && plain && a->workspace) {
+    const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
+    const int kt = (int)cdiv(a->K, 32);
+    while (nb * split < 512 && split * 2 <= 32 && kt / (split * 2) >= 4) split *= 2;
+  }
+  if (split > 1) {
+    LASR_CHECK_ARG(plain, "lasr_gemm: split_k needs a plain epilogue");
+    const int64_t need = (int64_t)split * batch * a->M * a->N * 4;
+    if (!a->workspace || a->workspace_bytes < need) split = 1;
+  }
+  p.split_k = split;
+  const int kstep = bf ? 32 : 16;
+  p.kchunk = split > 1 ? (int)(cdiv(cdiv(a->K, split), kstep) * kstep) : a->K;
+  p.ws = (float*)a->workspace;
+
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM), (unsigned)(batch * split));
+  LASR_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lasr_gemm: grid too large");
+  if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, grid, st);
+  else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, grid, st);
+  int rc = lasr_check_launch("lasr_gemm");
+  if (rc || split == 1) return rc;
+  const int64_t total = (int64_t)a->M * a->N * batch;
+  const int nblk = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+  if (a->c_dtype == LASR_F32) splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);
+  else splitk_reduce_kernel<bf16_t><<<nblk, 256, 0, st>>>(p);
+  return lasr_check_launch("lasr_gemm/splitk_reduce");
+}

@@ -1,0 +1,261 @@
+// LayerNorm (eps 1e-12 in LiteASR: liteasr/nets/layer_norm.py:8-21) forward/backward,
+// residual-branch gradient fusion, and deterministic column sums (bias grads).
+// One wave per row, D/64 elements per lane held in registers (D % 64 == 0, D <= 1024).
+#include "common.h"
+
+constexpr int LN_ROWS_PER_WAVE = 8;
+constexpr int LN_WAVES = 4;
+constexpr int LN_ROWS_PER_BLOCK = LN_ROWS_PER_WAVE * LN_WAVES;
+
+template <int NPL, typename TX, typename TY, typename TY2>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, int64_t rows,
+                                                     const float* gamma, const float* beta,
+                                                     float eps, TY* y, float* mean, float* rstd,
+                                                     TY2* y2, DropCfg d2) {
+  constexpr int D = NPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TX* xr = x + row * D;
+  float v[NPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { v[i] = to_f(xr[lane + 64 * i]); s += v[i]; }
+  const float mu = wave_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { const float dv = v[i] - mu; q += dv * dv; }
+  const float var = wave_sum(q) * (1.f / D);
+  const float rs = rsqrtf(var + eps);
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + 64 * i;
+    const float o = (v[i] - mu) * rs * gamma[c] + beta[c];
+    y[row * D + c] = from_f<TY>(o);
+    if (y2) y2[row * D + c] = from_f<TY2>(o * drop_mul(d2, (uint64_t)row * D + c));
+  }
+}
+
+template <int NPL, typename TX, typename TD, typename TR, typename TDX, typename TGB>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TX* __restrict__ x,
+                                                     const TD* __restrict__ dy, int64_t rows,
+                                                     const float* gamma, const float* mean,
+                                                     const float* rstd, const TR* dres, TDX* dx,
+                                                     float* part, TGB* gb, float bscale,
+                                                     DropCfg bd) {
+  constexpr int D = NPL * 64;
+  __shared__ float sg[LN_WAVES][D], sb[LN_WAVES][D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float pg[NPL], pb[NPL], gm[NPL];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; gm[i] = gamma[lane + 64 * i]; }
+  for (int rr = 0; rr < LN_ROWS_PER_WAVE; ++rr) {
+    const int64_t row = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK + w * LN_ROWS_PER_WAVE + rr;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NPL], g[NPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int64_t idx = row * D + lane + 64 * i;
+      xh[i] = (to_f(x[idx]) - mu) * rs;
+      const float d = to_f(dy[idx]);
+      pg[i] += d * xh[i];
+      pb[i] += d;
+      g[i] = d * gm[i];
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+    }
+    s1 = wave_sum(s1) * (1.f / D);
+    s2 = wave_sum(s2) * (1.f / D);
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int64_t idx = row * D + lane + 64 * i;
+      float o = rs * (g[i] - s1 - xh[i] * s2);
+      if (dres) o += to_f(dres[idx]);
+      dx[idx] = from_f<TDX>(o);
+      if (gb) gb[idx] = from_f<TGB>(bscale * drop_mul(bd, (uint64_t)idx) * o);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { sg[w][lane + 64 * i] = pg[i]; sb[w][lane + 64 * i] = pb[i]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < LN_WAVES; ++k) { a += sg[k][c]; b += sb[k][c]; }
+    part[(int64_t)blockIdx.x * 2 * D + c] = a;
+    part[(int64_t)blockIdx.x * 2 * D + D + c] = b;
+  }
+}
+
+__global__ void ln_param_reduce_kernel(const float* part, int nblk, int D, float* dgamma,
+                                       float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nblk; ++k) {
+    a += part[(int64_t)k * 2 * D + c];
+    b += part[(int64_t)k * 2 * D + D + c];
+  }
+  if (dgamma) dgamma[c] += a;
+  if (dbeta) dbeta[c] += b;
+}
+
+// --------------------------- dispatch helpers ------------------------------------
+template <int NPL, typename TX, typename TY>
+static void ln_fwd_y2(const void* x, int64_t rows, const float* g, const float* b, float eps,
+                      void* y, float* mean, float* rstd, void* y2, int y2dt, DropCfg d2,
+                      hipStream_t st) {
+  const unsigned nb = (unsigned)cdiv(rows, LN_WAVES);
+  if (y2 && y2dt == LASR_F32)
+    ln_fwd_kernel<NPL, TX, TY, float><<<nb, 256, 0, st>>>((const TX*)x, rows, g, b, eps, (TY*)y, mean, rstd, (float*)y2, d2);
+  else
+    ln_fwd_kernel<NPL, TX, TY, bf16_t><<<nb, 256, 0, st>>>((const TX*)x, rows, g, b, eps, (TY*)y, mean, rstd, (bf16_t*)y2, d2);
+}
+template <int NPL>
+static void ln_fwd_npl(const void* x, int xdt, int64_t rows, const float* g, const float* b,
+                       float eps, void* y, int ydt, float* mean, float* rstd, void* y2, int y2dt,
+                       DropCfg d2, hipStream_t st) {
+  if (xdt == LASR_F32 && ydt == LASR_F32) ln_fwd_y2<NPL, float, float>(x, rows, g, b, eps, y, mean, rstd, y2, y2dt, d2, st);
+  else if (xdt == LASR_F32) ln_fwd_y2<NPL, float, bf16_t>(x, rows, g, b, eps, y, mean, rstd, y2, y2dt, d2, st);
+  else if (ydt == LASR_F32) ln_fwd_y2<NPL, bf16_t, float>(x, rows, g, b, eps, y, mean, rstd, y2, y2dt, d2, st);
+  else ln_fwd_y2<NPL, bf16_t, bf16_t>(x, rows, g, b, eps, y, mean, rstd, y2, y2dt, d2, st);
+}
+
+extern "C" int lasr_layernorm_fwd(const void* x, int x_dtype, int64_t rows, int D,
+                                  const float* gamma, const float* beta, float eps, void* y,
+                                  int y_dtype, float* mean, float* rstd, void* y2, int y2_dtype,
+                                  float p2, uint64_t seed2, void* stream) {
+  LASR_CHECK_ARG(D % 64 == 0 && D >= 64 && D <= 1024, "lasr_layernorm_fwd: D=%d unsupported", D);
+  if (rows <= 0) return LASR_OK;
+  DropCfg d2{p2, seed2};
+  hipStream_t st = (hipStream_t)stream;
+  switch (D / 64) {
+    case 1: ln_fwd_npl<1>(x, x_dtype, rows, gamma, beta, eps, y, y_dtype, mean, rstd, y2, y2_dtype, d2, st); break;
+    case 2: ln_fwd_npl<2>(x, x_dtype, rows, gamma, beta, eps, y, y_dtype, mean, rstd, y2, y2_dtype, d2, st); break;
+    case 4: ln_fwd_npl<4>(x, x_dtype, rows, gamma, beta, eps, y, y_dtype, mean, rstd, y2, y2_dtype, d2, st); break;
+    case 8: ln_fwd_npl<8>(x, x_dtype, rows, gamma, beta, eps, y, y_dtype, mean, rstd, y2, y2_dtype, d2, st); break;
+    case 16: ln_fwd_npl<16>(x, x_dtype, rows, gamma, beta, eps, y, y_dtype, mean, rstd, y2, y2_dtype, d2, st); break;
+    default: lasr_set_error("lasr_layernorm_fwd: D=%d unsupported", D); return LASR_ERR_INVALID;
+  }
+  return lasr_check_launch("layernorm_fwd");
+}
+
+// Backward dispatch: x/dy dtypes in {f32,bf16}; dres (f32/bf16/none), dx f32/bf16, gb bf16/f32.
+template <int NPL, typename TX, typename TD>
+static void ln_bwd_3(const void* x, const void* dy, int64_t rows, const float* gamma,
+                     const float* mean, const float* rstd, const void* dres, int dresdt, void* dx,
+                     int dxdt, float* part, void* gb, int gbdt, float bscale, DropCfg bd,
+                     hipStream_t st) {
+  const unsigned nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
+#define LNB(TR, TDX, TGB)                                                                     \
+  ln_bwd_kernel<NPL, TX, TD, TR, TDX, TGB><<<nb, 256, 0, st>>>(                               \
+      (const TX*)x, (const TD*)dy, rows, gamma, mean, rstd, (const TR*)dres, (TDX*)dx, part, \
+      (TGB*)gb, bscale, bd)
+  const bool rf = dresdt == LASR_F32, xf = dxdt == LASR_F32, gf = gbdt == LASR_F32;
+  if (rf && xf && gf) LNB(float, float, float);
+  else if (rf && xf) LNB(float, float, bf16_t);
+  else if (rf && gf) LNB(float, bf16_t, float);
+  else if (rf) LNB(float, bf16_t, bf16_t);
+  else if (xf && gf) LNB(bf16_t, float, float);
+  else if (xf) LNB(bf16_t, float, bf16_t);
+  else if (gf) LNB(bf16_t, bf16_t, float);
+  else LNB(bf16_t, bf16_t, bf16_t);
+#undef LNB
+}
+template <int NPL>
+static void ln_bwd_npl(const void* x, int xdt, const void* dy, int dydt, int64_t rows,
+                       const float* gamma, const float* mean, const float* rstd, const void* dres,
+                       int dresdt, void* dx, int dxdt, float* part, void* gb, int gbdt,
+                       float bscale, DropCfg bd, hipStream_t st) {
+  if (xdt == LASR_F32 && dydt == LASR_F32) ln_bwd_3<NPL, float, float>(x, dy, rows, gamma, mean, rstd, dres, dresdt, dx, dxdt, part, gb, gbdt, bscale, bd, st);
+  else if (xdt == LASR_F32) ln_bwd_3<NPL, float, bf16_t>(x, dy, rows, gamma, mean, rstd, dres, dresdt, dx, dxdt, part, gb, gbdt, bscale, bd, st);
+  else if (dydt == LASR_F32) ln_bwd_3<NPL, bf16_t, float>(x, dy, rows, gamma, mean, rstd, dres, dresdt, dx, dxdt, part, gb, gbdt, bscale, bd, st);
+  else ln_bwd_3<NPL, bf16_t, bf16_t>(x, dy, rows, gamma, mean, rstd, dres, dresdt, dx, dxdt, part, gb, gbdt, bscale, bd, st);
+}
+
+extern "C" int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype,
+                                  int64_t rows, int D, const float* gamma, const float* mean,
+                                  const float* rstd, const void* dres, int dres_dtype, void* dx,
+                                  int dx_dtype, float* dgamma, float* dbeta, float* workspace,
+                                  int64_t ws_floats, void* gb, int gb_dtype, float bscale,
+                                  float bp, uint64_t bseed, void* stream) {
+  LASR_CHECK_ARG(D % 64 == 0 && D >= 64 && D <= 1024, "lasr_layernorm_bwd: D=%d unsupported", D);
+  if (rows <= 0) return LASR_OK;
+  const int64_t nblk = cdiv(rows, LN_ROWS_PER_BLOCK);
+  LASR_CHECK_ARG(ws_floats >= nblk * 2 * D, "lasr_layernorm_bwd: workspace too small (%lld < %lld)",
+                 (long long)ws_floats, (long long)(nblk * 2 * D));
+  DropCfg bd{bp, bseed};
+  hipStream_t st = (hipStream_t)stream;
+  switch (D / 64) {
+#define CASE(n) case n: ln_bwd_npl<n>(x, x_dtype, dy, dy_dtype, rows, gamma, mean, rstd, dres, dres_dtype, dx, dx_dtype, workspace, gb, gb_dtype, bscale, bd, st); break;
+    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+    default: lasr_set_error("lasr_layernorm_bwd: D=%d unsupported", D); return LASR_ERR_INVALID;
+  }
+  int rc = lasr_check_launch("layernorm_bwd");
+  if (rc) return rc;
+  if (dgamma || dbeta) {
+    ln_param_reduce_kernel<<<(unsigned)cdiv(D, 256), 256, 0, st>>>(workspace, (int)nblk, D, dgamma, dbeta);
+    rc = lasr_check_launch("layernorm_bwd/reduce");
+  }
+  return rc;
+}
+
+// ----------------------------- branch grad ----------------------------------------
+template <typename TI, typename TO>
+__global__ void branch_grad_kernel(const TI* dx, int64_t n, TO* gb, float scale, DropCfg d) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    gb[i] = from_f<TO>(scale * drop_mul(d, (uint64_t)i) * to_f(dx[i]));
+}
+
+extern "C" int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_dtype,
+                                float scale, float p, uint64_t seed, void* stream) {
+  if (n <= 0) return LASR_OK;
+  DropCfg d{p, seed};
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned nb = (unsigned)std::min<int64_t>(cdiv(n, 256), 8192);
+  if (dx_dtype == LASR_F32 && gb_dtype == LASR_F32) branch_grad_kernel<float, float><<<nb, 256, 0, st>>>((const float*)dx, n, (float*)gb, scale, d);
+  else if (dx_dtype == LASR_F32) branch_grad_kernel<float, bf16_t><<<nb, 256, 0, st>>>((const float*)dx, n, (bf16_t*)gb, scale, d);
+  else if (gb_dtype == LASR_F32) branch_grad_kernel<bf16_t, float><<<nb, 256, 0, st>>>((const bf16_t*)dx, n, (float*)gb, scale, d);
+  else branch_grad_kernel<bf16_t, bf16_t><<<nb, 256, 0, st>>>((const bf16_t*)dx, n, (bf16_t*)gb, scale, d);
+  return lasr_check_launch("branch_grad");
+}
+
+// ----------------------------- column sums ----------------------------------------
+constexpr int CS_ROWS = 64;
+template <typename T>
+__global__ void colsum_partial_kernel(const T* X, int64_t M, int64_t N, int64_t ldx, float* part) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS;
+  const int64_t r1 = r0 + CS_ROWS < M ? r0 + CS_ROWS : M;
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += to_f(X[r * ldx + n]);
+  part[(int64_t)blockIdx.y * N + n] = s;
+}
+__global__ void colsum_final_kernel(const float* part, int nchunk, int64_t N, float* out, int acc) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int k = 0; k < nchunk; ++k) s += part[(int64_t)k * N + n];
+  out[n] = acc ? out[n] + s : s;
+}
+
+extern "C" int lasr_colsum(const void* X, int dtype, int64_t M, int64_t N, int64_t ldx, float* out,
+                           int accumulate, float* workspace, int64_t ws_floats, void* stream) {
+  if (N <= 0) return LASR_OK;
+  const int64_t nchunk = cdiv(M, CS_ROWS);
+  LASR_CHECK_ARG(nchunk <= 65535, "lasr_colsum: M too large");
+  LASR_CHECK_ARG(ws_floats >= nchunk * N, "lasr_colsum: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g1((unsigned)cdiv(N, 256), (unsigned)(nchunk > 0 ? nchunk : 1));
+  if (M > 0) {
+    if (dtype == LASR_F32) colsum_partial_kernel<float><<<g1, 256, 0, st>>>((const float*)X, M, N, ldx, workspace);
+    else colsum_partial_kernel<bf16_t><<<g1, 256, 0, st>>>((const bf16_t*)X, M, N, ldx, workspace);
+  }
+  colsum_final_kernel<<<(unsigned)cdiv(N, 256), 256, 0, st>>>(workspace, (int)nchunk, N, out, accumulate);
+  return lasr_check_launch("colsum");
+}

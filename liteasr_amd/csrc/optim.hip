@@ -1,0 +1,101 @@
+// Gradient clipping + NaN-skip + Noam/Adam over flat fp32 buffers, all on the device.
+// Reference: liteasr/trainer.py:152-171 (clip_grad_norm_(params, clip); skip the step
+// when the norm is NaN), liteasr/optims/noam.py:33-46 (lr = factor * d^-0.5 *
+// min(s^-0.5, s * warmup^-1.5), s counts *taken* steps), liteasr/optims/adam.py:24-34
+// (torch.optim.Adam: bias-corrected moments, eps outside the sqrt).
+// The host never reads the norm: step count, lr, norm and the skip flag live in a
+// small device `state` vector, so the whole step can be captured in a hipGraph.
+#include "common.h"
+
+constexpr int SQ_CHUNK = 16384;  // elements per partial
+
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* g, int64_t n, float* ws) {
+  __shared__ float red[32];
+  const int64_t base = (int64_t)blockIdx.x * SQ_CHUNK;
+  float s = 0.f;
+  for (int64_t i = base + threadIdx.x; i < base + SQ_CHUNK && i < n; i += 256) {
+    const float v = g[i];
+    s += v * v;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
+// state: [0] taken steps, [1] lr, [2] grad norm, [3] skipped flag, [4] clip coefficient
+__global__ __launch_bounds__(256) void opt_finalize_kernel(const float* ws, int nparts,
+                                                           float* state, float max_norm,
+                                                           int lr_mode, float lr, float factor,
+                                                           float model_dim, float warmup) {
+  __shared__ float red[32];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += ws[i];
+  s = block_sum(s, red);
+  if (threadIdx.x != 0) return;
+  const float norm = sqrtf(s);
+  float coef = 1.f;
+  if (max_norm > 0.f) coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+  const bool skip = isnan(norm);
+  state[2] = norm;
+  state[3] = skip ? 1.f : 0.f;
+  state[4] = coef;
+  if (!skip) {
+    const float step = state[0] + 1.f;
+    state[0] = step;
+    float r = lr;
+    if (lr_mode == 1) r = factor * powf(model_dim, -0.5f) * fminf(powf(step, -0.5f), step * powf(warmup, -1.5f));
+    state[1] = r;
+  }
+}
+
+template <typename TL>
+__global__ __launch_bounds__(256) void adam_kernel(float* p, TL* plp, const float* g, float* m,
+                                                   float* v, int64_t n, const float* state,
+                                                   float beta1, float beta2, float eps, float wd) {
+  if (state[3] != 0.f) return;  // NaN norm: step skipped (reference trainer.py:157)
+  const float step = state[0], lr = state[1], coef = state[4];
+  const float bc1 = 1.f - powf(beta1, step);
+  const float bc2 = 1.f - powf(beta2, step);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float gi = g[i] * coef;
+    float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    const float mi = m[i] + (1.f - beta1) * (gi - m[i]);  // lerp, as torch.optim.Adam
+    const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+    p[i] = pi;
+    if (plp) plp[i] = from_f<TL>(pi);
+  }
+}
+
+extern "C" int lasr_sumsq_nparts(int64_t n) { return (int)cdiv(n, SQ_CHUNK); }
+
+extern "C" int lasr_sumsq_partial(const float* g, int64_t n, float* ws, int64_t ws_floats,
+                                  void* stream) {
+  const int64_t np = cdiv(n, SQ_CHUNK);
+  LASR_CHECK_ARG(ws_floats >= np, "lasr_sumsq_partial: workspace too small");
+  if (np == 0) return LASR_OK;
+  sumsq_partial_kernel<<<(unsigned)np, 256, 0, (hipStream_t)stream>>>(g, n, ws);
+  return lasr_check_launch("sumsq_partial");
+}
+
+extern "C" int lasr_adam_step(float* param, void* param_lp, int lp_dtype, const float* grad,
+                              float* m, float* v, int64_t n, const float* ws, int nparts,
+                              float* state, float max_norm, int lr_mode, float lr, float factor,
+                              float model_dim, float warmup, float beta1, float beta2, float eps,
+                              float weight_decay, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  opt_finalize_kernel<<<1, 256, 0, st>>>(ws, nparts, state, max_norm, lr_mode, lr, factor,
+                                         model_dim, warmup);
+  int rc = lasr_check_launch("adam/finalize");
+  if (rc || n <= 0) return rc;
+  const unsigned g = (unsigned)std::min<int64_t>(cdiv(n, 256), 8192);
+  if (param_lp && lp_dtype == LASR_BF16)
+    adam_kernel<bf16_t><<<g, 256, 0, st>>>(param, (bf16_t*)param_lp, grad, m, v, n, state, beta1, beta2, eps, weight_decay);
+  else
+    adam_kernel<float><<<g, 256, 0, st>>>(param, (float*)param_lp, grad, m, v, n, state, beta1, beta2, eps, weight_decay);
+  return lasr_check_launch("adam");
+}

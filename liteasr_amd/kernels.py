@@ -1,0 +1,366 @@
+"""Torch-tensor front end of the HIP kernels (thin: strides/pointers/stream only).
+
+Every function here launches kernels from libliteasr_hip.so on the current HIP stream
+(``torch.cuda.current_stream()``) and never synchronises, so a training step built
+from them can be captured into a hipGraph.  Tensors must live on the GPU; there is
+no CPU path (the CPU restatement lives in ``oracle/`` and is test-only).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _native as N
+
+_DT = {torch.float32: N.F32, torch.bfloat16: N.BF16}
+
+
+def dt(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ------------------------------------------------------------------ workspace ---
+class _Workspace:
+    """One growing fp32 scratch buffer per device (stream-ordered reuse)."""
+
+    def __init__(self):
+        self.buf = {}
+        self.frozen = False
+
+    def get(self, nfloats: int, device) -> torch.Tensor:
+        nfloats = max(int(nfloats), 1)
+        key = torch.device(device).index
+        b = self.buf.get(key)
+        if b is None or b.numel() < nfloats:
+            if self.frozen or torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(
+                    "workspace growth during graph capture; run a warm-up step first"
+                )
+            b = torch.empty(int(nfloats * 1.25) + 1024, dtype=torch.float32, device=device)
+            self.buf[key] = b
+        return b
+
+
+WS = _Workspace()
+
+
+# ----------------------------------------------------------------------- GEMM ---
+def _split(t: torch.Tensor):
+    """(batch strides (s1, s2), batch shape (z1, z2), row stride, col stride)."""
+    nb = t.dim() - 2
+    assert 0 <= nb <= 2, "gemm operands take at most 2 batch dims"
+    st = t.stride()
+    sh = t.shape
+    if nb == 0:
+        return (0, 0), (1, 1), st[0], st[1]
+    if nb == 1:
+        return (st[0], 0), (sh[0], 1), st[1], st[2]
+    return (st[0], st[1]), (sh[0], sh[1]), st[2], st[3]
+
+
+def gemm(
+    a: torch.Tensor,
+    b: torch.Tensor,
+    c: torch.Tensor,
+    *,
+    alpha: float = 1.0,
+    alpha_dev: Optional[torch.Tensor] = None,
+    beta: float = 0.0,
+    bias: Optional[torch.Tensor] = None,
+    act: int = N.ACT_NONE,
+    zout: Optional[torch.Tensor] = None,
+    aux: Optional[torch.Tensor] = None,
+    aux_act: int = N.ACT_NONE,
+    drop_p: float = 0.0,
+    drop_seed: int = 0,
+    res: Optional[torch.Tensor] = None,
+    res_scale: float = 1.0,
+    split_k: int = 1,
+):
+    """c = epilogue(alpha * a @ b) for logical views a (..,M,K), b (..,K,N), c (..,M,N).
+
+    Views may be arbitrarily strided as long as each operand has one unit stride
+    (the kernel handles K-contiguous and M/N-contiguous operands)."""
+    M, K = a.shape[-2], a.shape[-1]
+    K2, Nn = b.shape[-2], b.shape[-1]
+    assert K == K2 and c.shape[-2] == M and c.shape[-1] == Nn, (a.shape, b.shape, c.shape)
+    assert a.dtype == b.dtype
+    (sa1, sa2), (za1, za2), a_m, a_k = _split(a)
+    (sb1, sb2), (zb1, zb2), b_k, b_n = _split(b)
+    (sc1, sc2), (zc1, zc2), c_m, c_n = _split(c)
+    assert c_n == 1, "C must be row-contiguous"
+    z1, z2 = zc1, zc2
+    assert (za1, za2) == (z1, z2) and (zb1, zb2) == (z1, z2), "batch shapes differ"
+    if a_k != 1 and a_m != 1:
+        raise ValueError("A needs a unit stride")
+    if b_k != 1 and b_n != 1:
+        raise ValueError("B needs a unit stride")
+    args = N.GemmArgs()
+    args.M, args.N, args.K = M, Nn, K
+    args.batch, args.batch_div = z1 * z2, z2
+    args.A, args.lda_m, args.lda_k, args.sa1, args.sa2 = ptr(a), a_m, a_k, sa1, sa2
+    # B logical [K,N]: kernel wants ldb_n (stride along n) and ldb_k (stride along k)
+    args.B, args.ldb_n, args.ldb_k, args.sb1, args.sb2 = ptr(b), b_n, b_k, sb1, sb2
+    args.C, args.ldc, args.sc1, args.sc2 = ptr(c), c_m, sc1, sc2
+    if a_k == 1 and a_m == 1:
+        args.lda_k = 1
+    if b_k == 1 and b_n == 1:
+        args.ldb_k = 1
+    args.in_dtype, args.c_dtype = dt(a), dt(c)
+    args.alpha, args.alpha_dev, args.beta = alpha, ptr(alpha_dev), beta
+    args.bias = ptr(bias)
+    args.act = act
+    args.zout = ptr(zout)
+    if aux is not None:
+        args.aux, args.aux_dtype, args.ldaux, args.aux_act = ptr(aux), dt(aux), aux.stride(0), aux_act
+    args.drop_p, args.drop_seed = drop_p, drop_seed
+    if res is not None:
+        args.res, args.res_dtype, args.ldres, args.res_scale = ptr(res), dt(res), res.stride(0), res_scale
+    args.split_k = split_k
+    if split_k != 1:
+        need = 32 * z1 * z2 * M * Nn if split_k == 0 else split_k * z1 * z2 * M * Nn
+        ws = WS.get(need, c.device)
+        args.workspace, args.workspace_bytes = ptr(ws), ws.numel() * 4
+    N.call("lasr_gemm", C.byref(args), stream())
+    return c
+
+
+def linear(x, w, out, bias=None, **kw):
+    """out[M,N] = x[M,K] @ w[N,K]^T (+bias, epilogue kw)."""
+    return gemm(x, w.t(), out, bias=bias, **kw)
+
+
+def colsum(x2d: torch.Tensor, out: torch.Tensor, accumulate=True):
+    M, Nn = x2d.shape
+    nchunk = (M + 63) // 64
+    ws = WS.get(nchunk * Nn, x2d.device)
+    N.call("lasr_colsum", ptr(x2d), dt(x2d), M, Nn, x2d.stride(0), ptr(out), int(accumulate),
+           ptr(ws), ws.numel(), stream())
+
+
+# ------------------------------------------------------------------ LayerNorm ---
+def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd, y2=None, p2=0.0, seed2=0):
+    rows, D = x.shape
+    N.call("lasr_layernorm_fwd", ptr(x), dt(x), rows, D, ptr(gamma), ptr(beta), eps, ptr(y),
+           dt(y), ptr(mean), ptr(rstd), ptr(y2), dt(y2) if y2 is not None else 0, p2, seed2,
+           stream())
+
+
+def layernorm_bwd(x, dy, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, gb=None,
+                  bscale=1.0, bp=0.0, bseed=0):
+    rows, D = x.shape
+    nblk = (rows + 31) // 32
+    ws = WS.get(nblk * 2 * D, x.device)
+    N.call("lasr_layernorm_bwd", ptr(x), dt(x), ptr(dy), dt(dy), rows, D, ptr(gamma), ptr(mean),
+           ptr(rstd), ptr(dres), dt(dres) if dres is not None else 0, ptr(dx), dt(dx),
+           ptr(dgamma), ptr(dbeta), ptr(ws), ws.numel(), ptr(gb),
+           dt(gb) if gb is not None else 0, bscale, bp, bseed, stream())
+
+
+def branch_grad(dx, gb, scale, p=0.0, seed=0):
+    N.call("lasr_branch_grad", ptr(dx), dt(dx), dx.numel(), ptr(gb), dt(gb), scale, p, seed,
+           stream())
+
+
+# ------------------------------------------------------------------------ CTC ---
+def ctc_fwd(logits, targets, ilen, tlen, lse, lp, alpha, nll):
+    B, T, V = logits.shape
+    Lmax = targets.shape[1]
+    N.call("lasr_ctc_fwd", ptr(logits), dt(logits), B, T, V, ptr(targets), Lmax, ptr(ilen),
+           ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), stream())
+
+
+def ctc_bwd(logits, targets, ilen, tlen, lse, lp, alpha, nll, beta, grad, gscale, gdev=None):
+    B, T, V = logits.shape
+    Lmax = targets.shape[1]
+    N.call("lasr_ctc_bwd", ptr(logits), dt(logits), B, T, V, ptr(targets), Lmax, ptr(ilen),
+           ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), ptr(beta), ptr(grad), dt(grad),
+           gscale, ptr(gdev), stream())
+
+
+def lsm_kl_fwd(logits, target, ignore, smoothing, lse, loss_rows):
+    R, V = logits.shape
+    N.call("lasr_lsm_kl_fwd", ptr(logits), dt(logits), R, V, ptr(target), ignore, smoothing,
+           ptr(lse), ptr(loss_rows), stream())
+
+
+def lsm_kl_bwd(logits, target, ignore, smoothing, lse, grad, gscale, gdev=None):
+    R, V = logits.shape
+    N.call("lasr_lsm_kl_bwd", ptr(logits), dt(logits), R, V, ptr(target), ignore, smoothing,
+           ptr(lse), ptr(grad), dt(grad), gscale, ptr(gdev), stream())
+
+
+def loss_combine(a, wa, b, wb, out):
+    N.call("lasr_loss_combine", ptr(a), a.numel(), wa, ptr(b), b.numel() if b is not None else 0,
+           wb, ptr(out), stream())
+
+
+# ------------------------------------------------------------------ attention ---
+def qbias_fwd(qkv, B, T, H, dk, bu, bv, qu, qv):
+    N.call("lasr_qbias_fwd", ptr(qkv), dt(qkv), B, T, H, dk, qkv.stride(0), ptr(bu), ptr(bv),
+           ptr(qu), ptr(qv), stream())
+
+
+def qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, du, dv):
+    rows = B * T
+    D = H * dk
+    ws = WS.get(((rows + 63) // 64) * 2 * D, dqu.device)
+    N.call("lasr_qbias_bwd", ptr(dqu), ptr(dqv), dt(dqu), B, T, H, dk, ptr(dqkv), dqkv.stride(0),
+           ptr(du), ptr(dv), ptr(ws), ws.numel(), stream())
+
+
+def attn_softmax_fwd(s_ac, s_bd, B, H, Tq, Tk, ldS, mask, msb, msq, P, drop_p=0.0, seed=0,
+                     Praw=None):
+    N.call("lasr_attn_softmax_fwd", ptr(s_ac), ptr(s_bd), int(s_bd is not None), B, H, Tq, Tk,
+           ldS, ptr(mask), msb, msq, ptr(P), dt(P), drop_p, seed, ptr(Praw), stream())
+
+
+def attn_softmax_bwd(P, dPd, B, H, Tq, Tk, ldS, mask, msb, msq, dS, drop_p=0.0, seed=0):
+    N.call("lasr_attn_softmax_bwd", ptr(P), dt(P), ptr(dPd), B, H, Tq, Tk, ldS, ptr(mask), msb,
+           msq, drop_p, seed, ptr(dS), dt(dS), stream())
+
+
+def relshift_bwd(dS, Z, T, ldS, dBD):
+    N.call("lasr_relshift_bwd", ptr(dS), dt(dS), Z, T, ldS, ptr(dBD), stream())
+
+
+def reduce_batch(src, B, H, T, dk, dst):
+    N.call("lasr_reduce_batch", ptr(src), B, H, T, dk, ptr(dst), dt(dst), stream())
+
+
+# ----------------------------------------------------------------------- conv ---
+def conv1_fwd(x, w, bias, y1):
+    B, T, F = x.shape
+    Cc = w.shape[0]
+    N.call("lasr_conv1_fwd", ptr(x), B, T, F, Cc, ptr(w), ptr(bias), ptr(y1), dt(y1), stream())
+
+
+def conv1_bwd(x, dy1, dw, db):
+    B, T, F = x.shape
+    Cc = dw.shape[0]
+    T1 = (T - 3) // 2 + 1
+    nparts = (B * T1 + 15) // 16
+    ws = WS.get(nparts * 10 * Cc, x.device)
+    N.call("lasr_conv1_bwd", ptr(x), B, T, F, Cc, ptr(dy1), dt(dy1), ptr(dw), ptr(db), ptr(ws),
+           ws.numel(), stream())
+
+
+def im2col(y1, col):
+    B, T1, F1, Cc = y1.shape
+    N.call("lasr_im2col3x3s2", ptr(y1), dt(y1), B, T1, F1, Cc, ptr(col), stream())
+
+
+def col2im(dcol, y1, dy1):
+    B, T1, F1, Cc = y1.shape
+    N.call("lasr_col2im3x3s2", ptr(dcol), dt(dcol), B, T1, F1, Cc, ptr(y1), ptr(dy1), stream())
+
+
+def permute_last2(src, Nn, A, Bd, dst, reverse=False, accumulate=False):
+    N.call("lasr_permute_last2", ptr(src), dt(src), Nn, A, Bd, ptr(dst), dt(dst), int(reverse),
+           int(accumulate), stream())
+
+
+def dwconv_nparts(B, T):
+    return N.load().lasr_dwconv_nparts(B, T)
+
+
+def glu_dwconv_fwd(z1, B, T, Cc, K, w, bias, y, stats):
+    N.call("lasr_glu_dwconv_fwd", ptr(z1), dt(z1), B, T, Cc, K, ptr(w), ptr(bias), ptr(y), dt(y),
+           ptr(stats), stream())
+
+
+def bn_finalize(stats, nparts, Cc, eps, momentum, gamma, beta, rmean, rvar, nbt, mean, rstd,
+                scale, shift, update):
+    N.call("lasr_bn_finalize", ptr(stats), nparts, Cc, eps, momentum, ptr(gamma), ptr(beta),
+           ptr(rmean), ptr(rvar), ptr(nbt), ptr(mean), ptr(rstd), ptr(scale), ptr(shift),
+           int(update), stream())
+
+
+def bn_swish_fwd(y, scale, shift, h):
+    rows, Cc = y.shape
+    N.call("lasr_bn_swish_fwd", ptr(y), dt(y), rows, Cc, ptr(scale), ptr(shift), ptr(h), dt(h),
+           stream())
+
+
+def bn_swish_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy):
+    rows, Cc = y.shape
+    ws = WS.get(((rows + 63) // 64 + 1) * 2 * Cc, y.device)
+    N.call("lasr_bn_swish_bwd", ptr(y), dt(y), ptr(dh), dt(dh), rows, Cc, ptr(scale), ptr(shift),
+           ptr(mean), ptr(rstd), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dy), dt(dy), ptr(ws),
+           ws.numel(), stream())
+
+
+def glu_dwconv_bwd(z1, dy, B, T, Cc, K, w, dz1, dw, db):
+    nparts = dwconv_nparts(B, T)
+    ws = WS.get(nparts * (K + 1) * Cc, z1.device)
+    N.call("lasr_glu_dwconv_bwd", ptr(z1), dt(z1), ptr(dy), dt(dy), B, T, Cc, K, ptr(w), ptr(dz1),
+           ptr(dw), ptr(db), ptr(ws), ws.numel(), stream())
+
+
+# ---------------------------------------------------------------- elementwise ---
+def cast(src, dst):
+    N.call("lasr_cast", ptr(src), dt(src), ptr(dst), dt(dst), src.numel(), stream())
+
+
+def scale_add(a, b, sa, sb, out):
+    N.call("lasr_scale_add", ptr(a), dt(a), ptr(b), dt(b) if b is not None else 0, sa, sb,
+           ptr(out), dt(out), out.numel(), stream())
+
+
+def pe_fwd(x, rows, T, D, pe, xscale, y, p=0.0, seed=0):
+    N.call("lasr_pe_fwd", ptr(x), dt(x) if x is not None else 0, rows, T, D, ptr(pe), xscale, p,
+           seed, ptr(y), dt(y), stream())
+
+
+def embed_pe_fwd(ids, L, E, pe, xscale, y, p=0.0, seed=0):
+    R = ids.numel()
+    D = E.shape[1]
+    N.call("lasr_embed_pe_fwd", ptr(ids), R, L, D, ptr(E), ptr(pe), xscale, p, seed, ptr(y),
+           dt(y), stream())
+
+
+def embed_bwd(ids, dy, xscale, dE, p=0.0, seed=0):
+    R = ids.numel()
+    D = dE.shape[1]
+    N.call("lasr_embed_bwd", ptr(ids), R, D, ptr(dy), dt(dy), xscale, p, seed, ptr(dE), stream())
+
+
+def fill(t, value):
+    N.call("lasr_fill", ptr(t), dt(t), t.numel(), float(value), stream())
+
+
+def u2_prep(xlens, ys, ylens, Tx, Tsub, sos, eos, chunk, out):
+    B, L = ys.shape
+    N.call("lasr_u2_prep", ptr(xlens), ptr(ys), ptr(ylens), B, Tx, L, Tsub, sos, eos, chunk,
+           ptr(out["ys_in"]), ptr(out["tgt"]), ptr(out["tgt_ctc"]), ptr(out["dec_mask"]),
+           ptr(out["enc_mask"]), ptr(out["pred_len"]), ptr(out["ylen"]), stream())
+
+
+def sumsq_nparts(n):
+    return N.load().lasr_sumsq_nparts(n)
+
+
+def sumsq_partial(g, ws):
+    N.call("lasr_sumsq_partial", ptr(g), g.numel(), ptr(ws), ws.numel(), stream())
+
+
+def adam_step(param, param_lp, grad, m, v, ws, nparts, state, max_norm, lr_mode, lr, factor,
+              model_dim, warmup, beta1, beta2, eps, weight_decay):
+    N.call("lasr_adam_step", ptr(param), ptr(param_lp),
+           dt(param_lp) if param_lp is not None else 0, ptr(grad), ptr(m), ptr(v), param.numel(),
+           ptr(ws), nparts, ptr(state), max_norm, lr_mode, lr, factor, model_dim, warmup, beta1,
+           beta2, eps, weight_decay, stream())

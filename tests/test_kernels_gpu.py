@@ -1,0 +1,511 @@
+"""Op-level parity of every HIP kernel against a plain PyTorch fp32/fp64 reference of
+the same op (run on the GPU box).  Tolerances: fp32 storage 1e-4 relative to the
+tensor's max-abs; bf16 storage 2e-2 (bf16 has an 8-bit mantissa)."""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def K():
+    from liteasr_amd import kernels
+
+    return kernels
+
+
+def close(got, ref, tol, what=""):
+    got = got.float().cpu()
+    ref = ref.float().cpu()
+    scale = ref.abs().max().item() + 1e-12
+    err = (got - ref).abs().max().item() / scale
+    assert err <= tol, f"{what}: max err {err:.3e} > {tol:.1e} (scale {scale:.3e})"
+
+
+# ------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("M,N,Kd", [(1, 1, 1), (37, 53, 29), (130, 70, 257), (300, 260, 96), (64, 128, 2304)])
+def test_gemm_layouts(dtype, ta, tb, M, N, Kd):
+    g = torch.Generator(device="cpu").manual_seed(M * 1000 + N + Kd)
+    A = torch.randn(M, Kd, generator=g)
+    B = torch.randn(Kd, N, generator=g)
+    a = (A.t().contiguous().t() if ta else A).to(DEV, dtype)
+    b = (B.t().contiguous().t() if tb else B).to(DEV, dtype)
+    c = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    K().gemm(a, b, c)
+    ref = a.double() @ b.double()
+    close(c, ref, 1e-5 if dtype == torch.float32 else 1e-2, "gemm")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dtype):
+    kn = K()
+    from liteasr_amd import _native as Nn
+
+    M, N, Kd = 200, 96, 64
+    x = torch.randn(M, Kd, device=DEV).to(dtype)
+    w = torch.randn(N, Kd, device=DEV).to(dtype)
+    bias = torch.randn(N, device=DEV)
+    base = x.double() @ w.double().t()
+    # bias + swish with pre-activation out
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    z = torch.empty(M, N, device=DEV, dtype=dtype)
+    kn.linear(x, w, out, bias=bias, act=Nn.ACT_SWISH, zout=z)
+    zr = base + bias.double()
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    close(z, zr, tol, "zout")
+    close(out, zr * torch.sigmoid(zr), tol, "swish")
+    # relu
+    kn.linear(x, w, out, bias=bias, act=Nn.ACT_RELU)
+    close(out, torch.relu(zr), tol, "relu")
+    # residual add with scale (fp32 residual), alpha
+    res = torch.randn(M, N, device=DEV)
+    o32 = torch.empty(M, N, device=DEV)
+    kn.linear(x, w, o32, bias=bias, res=res, res_scale=0.5, alpha=2.0)
+    close(o32, res.double() + 0.5 * (2 * base + bias.double()), tol, "residual")
+    # aux swish-grad multiply
+    aux = torch.randn(M, N, device=DEV).to(dtype)
+    kn.linear(x, w, o32, aux=aux, aux_act=Nn.ACT_SWISH)
+    s = torch.sigmoid(aux.double())
+    close(o32, base * s * (1 + aux.double() * (1 - s)), tol, "aux swish")
+    kn.linear(x, w, o32, aux=aux, aux_act=Nn.ACT_RELU)
+    close(o32, base * (aux.double() > 0), tol, "aux relu")
+    # beta accumulate + alpha_dev
+    acc = torch.randn(M, N, device=DEV)
+    acc0 = acc.clone()
+    ad = torch.tensor([3.0], device=DEV)
+    kn.linear(x, w, acc, beta=1.0, alpha_dev=ad)
+    close(acc, acc0.double() + 3 * base, tol, "beta/alpha_dev")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_and_batched(dtype):
+    kn = K()
+    # dW-style TN gemm with split-K accumulate
+    R, N1, K1 = 3001, 96, 160
+    dy = torch.randn(R, N1, device=DEV).to(dtype)
+    x = torch.randn(R, K1, device=DEV).to(dtype)
+    dw = torch.randn(N1, K1, device=DEV)
+    dw0 = dw.clone()
+    kn.gemm(dy.t(), x, dw, beta=1.0, split_k=0)
+    ref = dw0.double() + dy.double().t() @ x.double()
+    close(dw, ref, 1e-5 if dtype == torch.float32 else 1e-2, "splitk")
+    # 2-level batched with head-strided views (attention layout)
+    B, T, H, dk = 3, 41, 4, 16
+    qkv = torch.randn(B, T, 3, H, dk, device=DEV).to(dtype)
+    q = qkv[:, :, 0].permute(0, 2, 1, 3)  # (B,H,T,dk) strided
+    k = qkv[:, :, 1].permute(0, 2, 1, 3)
+    S = torch.empty(B, H, T, 48, device=DEV)
+    kn.gemm(q, k.transpose(-1, -2), S[..., :T], alpha=0.25)
+    ref = 0.25 * (q.double() @ k.double().transpose(-1, -2))
+    close(S[..., :T], ref, 1e-5 if dtype == torch.float32 else 1e-2, "batched")
+    # broadcast operand (stride-0 batch) like the shared positional projection
+    p = torch.randn(T, H, dk, device=DEV).to(dtype).permute(1, 0, 2).unsqueeze(0).expand(B, H, T, dk)
+    kn.gemm(q, p.transpose(-1, -2), S[..., :T])
+    close(S[..., :T], q.double() @ p.double().transpose(-1, -2), 1e-5 if dtype == torch.float32 else 1e-2, "bcast")
+
+
+def test_gemm_dropout_matches_branch_grad():
+    kn = K()
+    M, N, Kd = 128, 256, 64
+    x = torch.randn(M, Kd, device=DEV)
+    w = torch.randn(N, Kd, device=DEV)
+    out = torch.empty(M, N, device=DEV)
+    kn.linear(x, w, out, drop_p=0.1, drop_seed=1234)
+    ref = x @ w.t()
+    mask = torch.empty(M, N, device=DEV)
+    kn.branch_grad(torch.ones(M, N, device=DEV), mask, 1.0, 0.1, 1234)
+    close(out, ref * mask, 1e-5, "dropout consistency")
+    keep = (mask > 0).float().mean().item()
+    assert abs(keep - 0.9) < 0.01, keep
+    assert torch.allclose(mask[mask > 0], torch.full_like(mask[mask > 0], 1 / 0.9))
+
+
+# ------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("D", [64, 256, 512])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm(D, dtype):
+    kn = K()
+    rows = 333
+    x = (torch.randn(rows, D, device=DEV) * 3 + 1)
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    y = torch.empty(rows, D, device=DEV, dtype=dtype)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    kn.layernorm_fwd(x, g, b, 1e-12, y, mean, rstd)
+    xr = x.double().requires_grad_()
+    yr = F.layer_norm(xr, (D,), g.double(), b.double(), 1e-12)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    close(y, yr, tol, "ln fwd")
+    dy = torch.randn(rows, D, device=DEV)
+    dres = torch.randn(rows, D, device=DEV)
+    dx = torch.empty(rows, D, device=DEV)
+    dg = torch.zeros(D, device=DEV)
+    db = torch.zeros(D, device=DEV)
+    gb = torch.empty(rows, D, device=DEV, dtype=dtype)
+    kn.layernorm_bwd(x, dy, g, mean, rstd, dx, dg, db, dres=dres, gb=gb, bscale=0.5)
+    gr = torch.autograd.grad(yr, xr, dy.double())[0]
+    close(dx, gr + dres.double(), 1e-5, "ln dx")
+    close(gb, 0.5 * (gr + dres.double()), tol, "ln gb")
+    xh = (x.double() - x.double().mean(-1, keepdim=True)) / x.double().var(-1, unbiased=False, keepdim=True).add(1e-12).sqrt()
+    close(dg, (dy.double() * xh).sum(0), 1e-5, "ln dgamma")
+    close(db, dy.double().sum(0), 1e-5, "ln dbeta")
+
+
+def test_colsum():
+    kn = K()
+    x = torch.randn(1000, 300, device=DEV).bfloat16()
+    out = torch.ones(300, device=DEV)
+    kn.colsum(x, out, accumulate=True)
+    close(out, 1 + x.double().sum(0), 1e-5, "colsum")
+
+
+# ------------------------------------------------------------------------- CTC
+def _ctc_case(B, T, V, L, seed, dtype):
+    g = torch.Generator().manual_seed(seed)
+    logits = torch.randn(B, T, V, generator=g) * 2
+    ilen = torch.randint(max(1, T // 2), T + 1, (B,), generator=g)
+    ilen[0] = T
+    tlen = torch.randint(0, L + 1, (B,), generator=g)
+    tlen[0] = L
+    tg = torch.randint(1, V, (B, L), generator=g)
+    if L >= 3:
+        tg[0, 1] = tg[0, 0]  # repeated label
+    for b in range(B):
+        tg[b, tlen[b]:] = -1
+    return logits.to(dtype), tg, ilen, tlen
+
+
+@pytest.mark.parametrize("B,T,V,L", [(4, 50, 30, 12), (3, 249, 4233, 40), (2, 120, 200, 70)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ctc(B, T, V, L, dtype):
+    kn = K()
+    logits, tg, ilen, tlen = _ctc_case(B, T, V, L, B * T + L, dtype)
+    if L == 70:
+        ilen[1] = 30  # infeasible: 2*L_b+... > T_b when tlen[1] large
+        tlen[1] = 60
+        tg[1, :60] = torch.randint(1, V, (60,))
+        tg[1, 60:] = -1
+    # reference: fp64 CPU log_softmax -> ctc_loss(sum) and autograd
+    lr = logits.double().requires_grad_()
+    lp = lr.log_softmax(-1).transpose(0, 1)
+    nll_ref = F.ctc_loss(lp, tg.clamp(min=0), ilen, tlen, blank=0, reduction="none", zero_infinity=False)
+    gref = torch.autograd.grad(nll_ref[torch.isfinite(nll_ref)].sum(), lr)[0]
+    d_log = logits.to(DEV)
+    tg32 = tg.to(DEV, torch.int32)
+    il = ilen.to(DEV, torch.int32)
+    tl = tlen.to(DEV, torch.int32)
+    S = 2 * L + 1
+    lse = torch.empty(B * T, device=DEV)
+    lpb = torch.empty(B * T * (L + 1), device=DEV)
+    alpha = torch.empty(B * T * S, device=DEV)
+    beta = torch.empty(B * T * S, device=DEV)
+    nll = torch.empty(B, device=DEV)
+    kn.ctc_fwd(d_log, tg32, il, tl, lse, lpb, alpha, nll)
+    fin = torch.isfinite(nll_ref)
+    tol = 1e-5 if dtype == torch.float32 else 1e-5
+    got = nll.cpu().double()
+    assert torch.equal(torch.isfinite(got), fin), (got, nll_ref)
+    assert ((got[fin] - nll_ref[fin].detach()).abs() <= tol * nll_ref[fin].detach().abs().clamp(min=1)).all(), (got, nll_ref)
+    grad = torch.empty(B, T, V, device=DEV, dtype=torch.float32)
+    kn.ctc_bwd(d_log, tg32, il, tl, lse, lpb, alpha, nll, beta, grad, 1.0)
+    gg = grad.cpu().double()
+    # torch's own fp32 ctc_loss is 5.8e-4 (max-abs) off its fp64 result on the 249x4233
+    # case (the lattice sums ~600-nat log terms in fp32); allow 2e-3.
+    close(gg[fin], gref[fin], 2e-3, "ctc grad")
+
+
+# ----------------------------------------------------------- label-smoothed KL
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_lsm_kl(dtype):
+    kn = K()
+    R, V, s = 77, 4233, 0.1
+    logits = (torch.randn(R, V) * 3).to(dtype)
+    tg = torch.randint(0, V, (R,))
+    tg[::5] = -1
+    x = logits.double().requires_grad_()
+    td = torch.full((R, V), s / (V - 1), dtype=torch.float64)
+    td.scatter_(1, tg.clamp(min=0).unsqueeze(1), 1 - s)
+    kl = F.kl_div(x.log_softmax(1), td, reduction="none").masked_fill((tg == -1).unsqueeze(1), 0)
+    ref_rows = kl.sum(1)
+    gref = torch.autograd.grad(kl.sum() * 0.5, x)[0]
+    lse = torch.empty(R, device=DEV)
+    rows = torch.empty(R, device=DEV)
+    dl = logits.to(DEV)
+    t32 = tg.to(DEV, torch.int32)
+    kn.lsm_kl_fwd(dl, t32, -1, s, lse, rows)
+    close(rows, ref_rows.detach(), 1e-5, "kl rows")
+    grad = torch.empty(R, V, device=DEV)
+    kn.lsm_kl_bwd(dl, t32, -1, s, lse, grad, 0.5)
+    close(grad, gref, 1e-5, "kl grad")
+    out = torch.empty(1, device=DEV)
+    kn.loss_combine(rows, 0.7, rows[:5].contiguous(), 0.3, out)
+    close(out, 0.7 * ref_rows.sum() + 0.3 * ref_rows[:5].sum(), 1e-5, "combine")
+
+
+# ------------------------------------------------------------------ attention
+def _rel_shift_ref(x):
+    # literal restatement of liteasr/nets/attention.py:99-118 (zero_triu=False)
+    zero_pad = torch.zeros((x.size()[:3] + (1,)), dtype=x.dtype)
+    xp = torch.cat([zero_pad, x], dim=-1).view(x.size()[:2] + (x.size(3) + 1, x.size(2)))
+    return xp[:, :, 1:].view_as(x)
+
+
+@pytest.mark.parametrize("relpos", [True, False])
+def test_attn_softmax(relpos):
+    kn = K()
+    B, H, T, ldS = 3, 2, 37, 40
+    ac = torch.randn(B, H, T, ldS)
+    bd = torch.randn(B, H, T, ldS)
+    xl = torch.tensor([37, 20, 5])
+    mask = (torch.arange(T)[None, :] >= xl[:, None]).to(torch.uint8)  # (B, T) key padding
+    s = ac[..., :T].double() + (_rel_shift_ref(bd[..., :T].double()) if relpos else 0)
+    s = s.masked_fill(mask.bool()[:, None, None, :], -1e38)
+    sr = s.clone().requires_grad_()
+    P_ref = torch.softmax(sr, -1)
+    P = torch.empty(B, H, T, ldS, device=DEV)
+    kn.attn_softmax_fwd(ac.to(DEV), bd.to(DEV) if relpos else None, B, H, T, T, ldS,
+                        mask.to(DEV), T, 0, P)
+    close(P[..., :T], P_ref.detach(), 1e-5, "softmax fwd")
+    assert (P[..., T:] == 0).all()
+    dP = torch.randn(B, H, T, ldS)
+    dS_ref = torch.autograd.grad(P_ref, sr, dP[..., :T].double())[0]
+    dS_ref = dS_ref.masked_fill(mask.bool()[:, None, None, :], 0)
+    dS = torch.empty(B, H, T, ldS, device=DEV)
+    kn.attn_softmax_bwd(P, dP.to(DEV), B, H, T, T, ldS, mask.to(DEV), T, 0, dS)
+    close(dS[..., :T], dS_ref, 1e-5, "softmax bwd")
+    if relpos:
+        # rel_shift backward == autograd of the literal rel_shift
+        bdr = bd[..., :T].double().requires_grad_()
+        y = _rel_shift_ref(bdr)
+        gref = torch.autograd.grad(y, bdr, dS_ref)[0]
+        dBD = torch.empty(B * H, T, ldS, device=DEV)
+        kn.relshift_bwd(dS.view(B * H, T, ldS), B * H, T, ldS, dBD)
+        close(dBD.view(B, H, T, ldS)[..., :T], gref, 1e-6, "relshift bwd")
+
+
+def test_qbias_and_reduce():
+    kn = K()
+    B, T, H, dk = 2, 9, 4, 8
+    D = H * dk
+    qkv = torch.randn(B * T, 3 * D, device=DEV)
+    bu = torch.randn(D, device=DEV)
+    bv = torch.randn(D, device=DEV)
+    qu = torch.empty(B * T, D, device=DEV)
+    qv = torch.empty(B * T, D, device=DEV)
+    kn.qbias_fwd(qkv, B, T, H, dk, bu, bv, qu, qv)
+    close(qu, qkv[:, :D] + bu, 1e-6)
+    close(qv, qkv[:, :D] + bv, 1e-6)
+    dqkv = torch.zeros(B * T, 3 * D, device=DEV)
+    du = torch.zeros(D, device=DEV)
+    dv = torch.zeros(D, device=DEV)
+    kn.qbias_bwd(qu, qv, B, T, H, dk, dqkv, du, dv)
+    close(dqkv[:, :D], qu + qv, 1e-6)
+    close(du, qu.sum(0), 1e-5)
+    close(dv, qv.sum(0), 1e-5)
+    src = torch.randn(B, H, T, dk, device=DEV)
+    dst = torch.empty(T, D, device=DEV)
+    kn.reduce_batch(src, B, H, T, dk, dst)
+    close(dst, src.sum(0).permute(1, 0, 2).reshape(T, D), 1e-6)
+
+
+# ----------------------------------------------------------------------- conv
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_subsampling_convs(dtype):
+    kn = K()
+    B, T, Fd, Cc = 2, 41, 80, 32
+    x = torch.randn(B, T, Fd, device=DEV)
+    w1 = torch.randn(Cc, 1, 3, 3, device=DEV) * 0.3
+    b1 = torch.randn(Cc, device=DEV) * 0.1
+    T1, F1 = (T - 3) // 2 + 1, (Fd - 3) // 2 + 1
+    y1 = torch.empty(B, T1, F1, Cc, device=DEV, dtype=dtype)
+    kn.conv1_fwd(x, w1.view(Cc, 9), b1, y1)
+    xr = x.double().requires_grad_()
+    w1r = w1.double().requires_grad_()
+    b1r = b1.double().requires_grad_()
+    y1r = F.relu(F.conv2d(xr.unsqueeze(1), w1r, b1r, stride=2))  # (B,C,T1,F1)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    close(y1, y1r.permute(0, 2, 3, 1), tol, "conv1")
+    # conv2 via im2col + gemm
+    w2 = torch.randn(Cc, Cc, 3, 3, device=DEV) * 0.1
+    b2 = torch.randn(Cc, device=DEV) * 0.1
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    col = torch.empty(B * T2 * F2, 9 * Cc, device=DEV, dtype=dtype)
+    kn.im2col(y1, col)
+    w2p = torch.empty(Cc, 9 * Cc, device=DEV, dtype=dtype)
+    kn.permute_last2(w2.reshape(Cc, Cc, 9), Cc, Cc, 9, w2p)  # [Cout][Cin][9] -> [Cout][9][Cin]
+    y2 = torch.empty(B * T2 * F2, Cc, device=DEV, dtype=dtype)
+    from liteasr_amd import _native as Nn
+    kn.linear(col, w2p, y2, bias=b2, act=Nn.ACT_RELU)
+    y2r = F.relu(F.conv2d(y1r, w2.double(), b2.double(), stride=2))
+    close(y2.view(B, T2, F2, Cc), y2r.permute(0, 2, 3, 1), 5e-5 if dtype == torch.float32 else 3e-2, "conv2")
+    # backward: dcol = dy2 @ w2p ; col2im with relu mask ; conv1 weight grad
+    dy2 = torch.randn(B * T2 * F2, Cc, device=DEV).to(dtype)
+    dcol = torch.empty(B * T2 * F2, 9 * Cc, device=DEV, dtype=dtype)
+    kn.gemm(dy2, w2p, dcol)
+    dy1 = torch.empty_like(y1)
+    kn.col2im(dcol, y1, dy1)
+    y2pre = F.conv2d(y1r, w2.double(), b2.double(), stride=2)
+    gy1 = torch.autograd.grad(y2pre, y1r, dy2.double().view(B, T2, F2, Cc).permute(0, 3, 1, 2), retain_graph=True)[0]
+    close(dy1, (gy1 * (y1r > 0)).permute(0, 2, 3, 1), 5e-5 if dtype == torch.float32 else 3e-2, "col2im")
+    dw1 = torch.zeros(Cc, 9, device=DEV)
+    db1 = torch.zeros(Cc, device=DEV)
+    kn.conv1_bwd(x, dy1, dw1, db1)
+    y1pre = F.conv2d(xr.unsqueeze(1), w1r, b1r, stride=2)
+    gw, gb = torch.autograd.grad(y1pre, (w1r, b1r), dy1.double().permute(0, 3, 1, 2))
+    close(dw1, gw.view(Cc, 9), 1e-5, "conv1 dw")
+    close(db1, gb, 1e-5, "conv1 db")
+    # reverse permute with accumulate
+    acc = torch.ones(Cc, Cc, 9, device=DEV)
+    kn.permute_last2(w2p.float(), Cc, Cc, 9, acc, reverse=True, accumulate=True)
+    close(acc, 1 + w2p.float().view(Cc, 9, Cc).permute(0, 2, 1), 1e-6, "permute rev")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conformer_conv_module_pieces(dtype):
+    kn = K()
+    B, T, Cc, Kk = 3, 70, 64, 15
+    z1 = torch.randn(B, T, 2 * Cc, device=DEV).to(dtype)
+    w = torch.randn(Cc, Kk, device=DEV) * 0.2
+    bias = torch.randn(Cc, device=DEV) * 0.1
+    y = torch.empty(B, T, Cc, device=DEV, dtype=dtype)
+    nparts = kn.dwconv_nparts(B, T)
+    stats = torch.empty(nparts * 3 * Cc, device=DEV)
+    kn.glu_dwconv_fwd(z1, B, T, Cc, Kk, w, bias, y, stats)
+    zr = z1.double().requires_grad_()
+    g = F.glu(zr.transpose(1, 2), dim=1)
+    wr = w.double().requires_grad_()
+    br = bias.double().requires_grad_()
+    yr = F.conv1d(g, wr.unsqueeze(1), br, padding=(Kk - 1) // 2, groups=Cc)  # (B,C,T)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    close(y, yr.transpose(1, 2), tol, "dwconv fwd")
+    gamma = torch.randn(Cc, device=DEV)
+    beta_ = torch.randn(Cc, device=DEV)
+    rm = torch.zeros(Cc, device=DEV)
+    rv = torch.ones(Cc, device=DEV)
+    nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    mean, rstd, scale, shift = [torch.empty(Cc, device=DEV) for _ in range(4)]
+    kn.bn_finalize(stats, nparts, Cc, 1e-5, 0.1, gamma, beta_, rm, rv, nbt, mean, rstd, scale, shift, True)
+    bn = torch.nn.BatchNorm1d(Cc).double()
+    with torch.no_grad():
+        bn.weight.copy_(gamma.double())
+        bn.bias.copy_(beta_.double())
+    yq = y.double().cpu().transpose(1, 2).requires_grad_()  # BN on the stored y
+    u = bn(yq)
+    close(rm, bn.running_mean, 1e-5, "running_mean")
+    close(rv, bn.running_var, 1e-5, "running_var")
+    assert int(nbt.item()) == 1
+    h = torch.empty(B * T, Cc, device=DEV, dtype=dtype)
+    kn.bn_swish_fwd(y.view(B * T, Cc), scale, shift, h)
+    hr = u * torch.sigmoid(u)
+    close(h, hr.transpose(1, 2).reshape(B * T, Cc), tol, "bn swish fwd")
+    dh = torch.randn(B * T, Cc, device=DEV).to(dtype)
+    dgm = torch.zeros(Cc, device=DEV)
+    dbt = torch.zeros(Cc, device=DEV)
+    dyb = torch.empty(B * T, Cc, device=DEV, dtype=torch.float32)
+    kn.bn_swish_bwd(y.view(B * T, Cc), dh, scale, shift, mean, rstd, gamma, dgm, dbt, dyb)
+    gy, gw_, gb_ = torch.autograd.grad(hr, (yq, bn.weight, bn.bias), dh.double().cpu().view(B, T, Cc).transpose(1, 2))
+    close(dyb, gy.transpose(1, 2).reshape(B * T, Cc), 1e-4, "bn dy")
+    close(dgm, gw_, 1e-4, "bn dgamma")
+    close(dbt, gb_, 1e-4, "bn dbeta")
+    # dwconv backward from an arbitrary dy
+    dy = torch.randn(B, T, Cc, device=DEV)
+    dz1 = torch.empty_like(z1)
+    dw = torch.zeros(Cc, Kk, device=DEV)
+    db = torch.zeros(Cc, device=DEV)
+    kn.glu_dwconv_bwd(z1, dy, B, T, Cc, Kk, w, dz1, dw, db)
+    gz, gw2, gb2 = torch.autograd.grad(yr, (zr, wr, br), dy.double().transpose(1, 2))
+    close(dz1, gz, tol, "dwconv dz1")
+    close(dw, gw2, 1e-5 if dtype == torch.float32 else 1e-2, "dwconv dw")
+    close(db, gb2, 1e-5, "dwconv db")
+
+
+# ------------------------------------------------------------------ elementwise
+def test_embed_pe_and_prep():
+    kn = K()
+    B, L, D, V = 3, 5, 16, 11
+    ids = torch.randint(0, V, (B, L + 1), device=DEV, dtype=torch.int32)
+    ids[0, 0] = ids[1, 2] = ids[2, 4] = 3
+    E = torch.randn(V, D, device=DEV)
+    pe = torch.randn(50, D, device=DEV)
+    y = torch.empty(B * (L + 1), D, device=DEV)
+    kn.embed_pe_fwd(ids, L + 1, E, pe, 4.0, y)
+    ref = E[ids.long()] * 4.0 + pe[: L + 1].unsqueeze(0)
+    close(y, ref.view(-1, D), 1e-6, "embed fwd")
+    dy = torch.randn(B * (L + 1), D, device=DEV)
+    dE = torch.zeros(V, D, device=DEV)
+    kn.embed_bwd(ids, dy, 4.0, dE)
+    ref = torch.zeros(V, D, device=DEV, dtype=torch.float64).index_add_(0, ids.view(-1).long(), dy.double() * 4)
+    close(dE, ref, 1e-6, "embed bwd")
+    # u2 bookkeeping vs literal python restatement
+    xlens = torch.tensor([100, 97, 3], device=DEV)
+    ys = torch.tensor([[5, 6, 7, 8], [2, 2, -1, -1], [-1, -1, -1, -1]], device=DEV)
+    ylens = torch.tensor([4, 2, 0], device=DEV)
+    Tx, Tsub = 100, ((100 - 1) // 2 - 1) // 2
+    out = {
+        "ys_in": torch.empty(3, 5, dtype=torch.int32, device=DEV),
+        "tgt": torch.empty(3, 5, dtype=torch.int32, device=DEV),
+        "tgt_ctc": torch.empty(3, 4, dtype=torch.int32, device=DEV),
+        "dec_mask": torch.empty(3, 5, 5, dtype=torch.uint8, device=DEV),
+        "enc_mask": torch.empty(3, Tsub, dtype=torch.uint8, device=DEV),
+        "pred_len": torch.empty(3, dtype=torch.int32, device=DEV),
+        "ylen": torch.empty(3, dtype=torch.int32, device=DEV),
+    }
+    kn.u2_prep(xlens, ys, ylens, Tx, Tsub, 9, 9, 0, out)
+    assert out["ys_in"].tolist() == [[9, 5, 6, 7, 8], [9, 2, 2, 9, 9], [9, 9, 9, 9, 9]]
+    assert out["tgt"].tolist() == [[5, 6, 7, 8, 9], [2, 2, 9, -1, -1], [9, -1, -1, -1, -1]]
+    assert out["pred_len"].tolist() == [((x - 1) // 2 - 1) // 2 for x in [100, 97, 3]]
+    pm = torch.arange(Tx)[None, :] >= xlens.cpu()[:, None]
+    assert torch.equal(out["enc_mask"].cpu().bool(), pm[:, :-2:2][:, :-2:2])
+    tri = torch.arange(5)[None, :] > torch.arange(5)[:, None]
+    ysm = torch.arange(5)[None, :] >= (ylens.cpu() + 1)[:, None]
+    assert torch.equal(out["dec_mask"].cpu().bool(), ysm[:, None, :] | tri[None])
+
+
+def test_adam_noam_clip():
+    kn = K()
+    n = 50000
+    torch.manual_seed(0)
+    p0 = torch.randn(n)
+    g = torch.randn(n) * 3
+    ref_p = p0.clone().requires_grad_()
+    opt = torch.optim.Adam([ref_p], lr=1.0, betas=(0.9, 0.98), eps=1e-9)
+    p = p0.to(DEV)
+    plp = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    state = torch.zeros(5, device=DEV)
+    nparts = kn.sumsq_nparts(n)
+    ws = torch.empty(nparts, device=DEV)
+    for step in range(1, 4):
+        gs = g * step
+        ref_p.grad = gs.clone()
+        norm = torch.nn.utils.clip_grad_norm_([ref_p], 5.0)
+        lr = 1.0 * 256 ** -0.5 * min(step ** -0.5, step * 25000 ** -1.5)
+        for grp in opt.param_groups:
+            grp["lr"] = lr
+        opt.step()
+        gd = gs.to(DEV)
+        kn.sumsq_partial(gd, ws)
+        kn.adam_step(p, plp, gd, m, v, ws, nparts, state, 5.0, 1, 0.0, 1.0, 256.0, 25000.0, 0.9, 0.98, 1e-9, 0.0)
+        st = state.cpu()
+        assert st[0].item() == step
+        assert abs(st[2].item() - norm.item()) <= 1e-4 * norm.item()
+        assert abs(st[1].item() - lr) <= 1e-6 * lr
+    close(p, ref_p.detach(), 1e-5, "adam params")
+    close(plp, ref_p.detach(), 1e-2, "adam bf16 copy")
+    # NaN norm skips the step and leaves everything untouched
+    p_before = p.clone()
+    gnan = g.clone()
+    gnan[7] = float("nan")
+    kn.sumsq_partial(gnan.to(DEV), ws)
+    kn.adam_step(p, None, gnan.to(DEV), m, v, ws, nparts, state, 5.0, 1, 0.0, 1.0, 256.0, 25000.0, 0.9, 0.98, 1e-9, 0.0)
+    assert state[3].item() == 1.0 and state[0].item() == 3
+    assert torch.equal(p, p_before)
