@@ -1,0 +1,238 @@
+#!/usr/bin/env python
+"""Throughput of the U2-Conformer + hybrid CTC-attention training step on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W] [--config small|large|long|tiny]
+
+A step = one full training iteration on one synthetic batch per rank: forward, hybrid
+loss, backward, gradient all-reduce (N > 1), clip_grad_norm(5) + NaN-skip + Noam/Adam,
+zero_grad -- the reference's Trainer.run body (liteasr/trainer.py:140-171) with
+accum_grad = 1.  Inputs are resident on the GPU before timing starts.
+
+Prints ONE JSON line (rank 0).  value = utterances/s over all ranks (weak scaling:
+B utterances per rank per step).  Also reports, for the dominant kernel, an achieved
+vs peak roofline measured live with HIP events, and the CPU baseline (the oracle
+restatement, pinned to the reference by tests/test_oracle_golden.py) on a bounded
+sample timed on this host.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: model widths, batch shape, hybrid weight; GFLOP/utt fwd+bwd from SURVEY §6
+    "small": dict(d=256, H=4, ff=2048, enc=12, dec=6, B=32, T=1000, L=40, w=0.3, gflop=80.14, chunk=0),
+    "large": dict(d=512, H=16, ff=2048, enc=12, dec=6, B=32, T=1000, L=40, w=0.3, gflop=230.77, chunk=16),
+    "long": dict(d=256, H=4, ff=2048, enc=12, dec=6, B=8, T=4000, L=150, w=1.0, gflop=364.51, chunk=0),
+    "tiny": dict(d=64, H=4, ff=256, enc=2, dec=1, B=16, T=1000, L=20, w=0.3, gflop=1.74, chunk=0),
+}
+V = 4233
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build(cfgd, dtype, dropout, dev):
+    from liteasr_amd.models.u2 import U2, U2Config
+    from liteasr_amd.utils.cfg import resolve_self
+
+    c = U2Config(input_dim=80, vocab_size=V, enc_dim=cfgd["d"], enc_ff_dim=cfgd["ff"], enc_attn_heads=cfgd["H"],
+                 enc_layers=cfgd["enc"], dec_dim=cfgd["d"], dec_ff_dim=cfgd["ff"], dec_attn_heads=cfgd["H"],
+                 dec_layers=cfgd["dec"], dropout_rate=dropout, compute_dtype=dtype, chunk_size=cfgd["chunk"])
+    resolve_self(c)
+    # my_U2.yaml: attention dropout 0, everything else model.dropout_rate
+    c.enc_attn_dropout_rate = 0.0
+    c.dec_self_attn_dropout_rate = 0.0
+    c.dec_src_attn_dropout_rate = 0.0
+    return U2(c).to(dev).train()
+
+
+def synthetic(cfgd, rank, dev):
+    from oracle.u2_oracle import synthetic_batch  # input generator only (SURVEY §8d recipe)
+
+    xs, xlens, ys, ylens = synthetic_batch(cfgd["B"], cfgd["T"], cfgd["L"], V, seed=1234 + rank)
+    return [t.to(dev) for t in (xs, xlens, ys, ylens)]
+
+
+def dominant_kernel_roofline(cfgd, dev, iters=50):
+    """FFN fc1 GEMM of one Conformer layer at the step's shape (M = B*T', N = ff, K = d,
+    bf16 in, fused bias + Swish + pre-activation store): the largest GEMM family of the step
+    (4 launches per layer fwd+bwd of this size).  Timed live with HIP events on the stream it
+    is launched on."""
+    import torch
+
+    from liteasr_amd import kernels as K
+    from liteasr_amd._native import ACT_SWISH
+
+    T1 = (cfgd["T"] - 3) // 2 + 1
+    Tp = (T1 - 3) // 2 + 1
+    M, N, Kd = cfgd["B"] * Tp, cfgd["ff"], cfgd["d"]
+    x = torch.randn(M, Kd, device=dev).bfloat16()
+    w = (torch.randn(N, Kd, device=dev) / math.sqrt(Kd)).bfloat16()
+    b = torch.randn(N, device=dev)
+    h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    z = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    for _ in range(5):
+        K.linear(x, w, h, bias=b, act=ACT_SWISH, zout=z)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        K.linear(x, w, h, bias=b, act=ACT_SWISH, zout=z)
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2.0 * M * N * Kd
+    bytes_ = 2.0 * (M * Kd + N * Kd + 2 * M * N) + 4 * N
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"kernel": f"gemm_bf16 fc1+bias+swish M={M} N={N} K={Kd}", "bound": "mfma",
+            "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
+            "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_,
+            "avg_launch_us": round(ms * 1e3, 2),
+            "achieved_hbm_GBs": round(bytes_ / (ms * 1e-3) / 1e9, 1)}
+
+
+def cpu_baseline(cfgd_name, budget_s=25.0):
+    """The oracle restatement (pinned to the reference) on this host's CPU cores: U2 of the
+    same config, a bounded batch, 1 warm-up + timed steps until ~budget_s."""
+    import torch
+
+    from oracle import u2_oracle as O
+
+    cfgd = CONFIGS[cfgd_name]
+    n = len(os.sched_getaffinity(0))
+    n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    torch.set_num_threads(n)
+    cfg = O.default_cfg(enc_dim=cfgd["d"], enc_heads=cfgd["H"], enc_ff=cfgd["ff"], enc_layers=cfgd["enc"],
+                        dec_dim=cfgd["d"], dec_heads=cfgd["H"], dec_ff=cfgd["ff"], dec_layers=cfgd["dec"],
+                        vocab_size=V, dropout=0.1, ff_dropout=0.1, pos_dropout=0.1, dec_dropout=0.1,
+                        dec_pos_dropout=0.1, dec_ff_dropout=0.1)
+    params = O.init_params(cfg, seed=1)
+    bufs = O.init_buffers(cfg)
+    Bs = 2 if cfgd["T"] > 2000 else 4
+    batch = O.synthetic_batch(Bs, cfgd["T"], cfgd["L"], V, seed=5)
+    st = None
+    t0 = time.perf_counter()
+    _, _, params, st, _ = O.train_step(params, bufs, batch, cfg, ctc_weight=cfgd["w"], opt_state=st,
+                                       model_dim=cfgd["d"])
+    warm = time.perf_counter() - t0
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        _, _, params, st, _ = O.train_step(params, bufs, batch, cfg, ctc_weight=cfgd["w"], opt_state=st,
+                                           model_dim=cfgd["d"])
+        steps += 1
+        el = time.perf_counter() - t0
+        if el + el / steps > budget_s or steps >= 3:
+            break
+    return {"value": round(Bs * steps / el, 3), "unit": "utterances/sec", "cores": n, "kind": "port",
+            "sample": f"oracle (torch CPU fp32) {cfgd_name} U2, B={Bs} T={cfgd['T']} L={cfgd['L']}, dropout 0.1, "
+                      f"{steps} timed step(s) after 1 warm-up ({warm:.1f}s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="small", choices=sorted(CONFIGS))
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfgd = CONFIGS[args.config]
+
+    from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+    from liteasr_amd.optims.noam import Noam, NoamConfig
+
+    torch.manual_seed(42)
+    model = build(cfgd, args.dtype, args.dropout, dev)
+    net = model
+    if world > 1:
+        from liteasr_amd.distributed.ddp import DistributedDataParallel
+
+        net = DistributedDataParallel(model)
+    crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=V, smoothing=0.1, ctc_weight=cfgd["w"]))
+    opt = Noam(model.parameters(), NoamConfig(model_dim=cfgd["d"]))
+    batch = synthetic(cfgd, rank, dev)
+
+    def step():
+        loss = crit(net, *batch)
+        loss.backward()
+        opt.clip_and_step(5.0)
+        opt.zero_grad()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    final_loss = loss.item()
+    st = opt.device_state()
+    utt = world * cfgd["B"] * args.steps / el
+    if rank == 0:
+        out = {
+            "metric": "utterances/sec (U2-Conformer+CTC, 80-d fbank T≈1000) at 1/2/4/8 MI355X",
+            "value": round(utt, 2), "unit": "utterances/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (SURVEY §8d: N(0,1) 80-d fbank, xlens~U[0.95T,T], random token ids), random-init weights",
+            "config": {"workload": f"U2-Conformer-{args.config} hybrid CTC-attention training step "
+                                    f"(fwd+loss+bwd+allreduce+clip+Noam/Adam)",
+                       "model": f"U2 enc {cfgd['enc']}x conformer d{cfgd['d']} H{cfgd['H']} ff{cfgd['ff']}, "
+                                f"dec {cfgd['dec']}x, V {V}", "global_batch": world * cfgd["B"],
+                       "per_gpu_batch": cfgd["B"], "seq_len": cfgd["T"], "label_len": cfgd["L"],
+                       "ctc_weight": cfgd["w"], "dropout": args.dropout, "chunk_size": cfgd["chunk"],
+                       "parallelism": f"dp{world}"},
+            "step_tflops_per_gpu": round(cfgd["gflop"] * utt / world / 1e3, 2),
+            "step_mfma_frac": round(cfgd["gflop"] * utt / world / 1e3 / PEAK_BF16_TFLOPS, 4),
+            "final_loss": round(final_loss, 4), "optimizer_state": st,
+        }
+        if not args.no_roofline:
+            out["roofline"] = dominant_kernel_roofline(cfgd, dev)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.config)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

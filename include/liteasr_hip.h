@@ -34,6 +34,11 @@ enum { LASR_ACT_NONE = 0, LASR_ACT_RELU = 1, LASR_ACT_SWISH = 2 };
 
 const char* lasr_last_error(void);
 int lasr_version(void);
+/* Register a device uint64 step counter mixed into every dropout seed at kernel run
+ * time (so graph replays draw fresh masks); NULL disables.  lasr_counter_add bumps it
+ * on the stream (called once per training forward). */
+int lasr_set_dropout_counter(const uint64_t* dev_counter);
+int lasr_counter_add(uint64_t* dev_counter, uint64_t v, void* stream);
 
 /* ------------------------------------------------------------------------
  * Batched GEMM with fused epilogue.
@@ -200,7 +205,8 @@ int lasr_dwconv_nparts(int B, int T);
 int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float eps, float momentum,
                      const float* gamma, const float* beta, float* running_mean,
                      float* running_var, int64_t* num_batches, float* mean, float* rstd,
-                     float* scale, float* shift, int update_running, void* stream);
+                     float* scale, float* shift, int mode, void* stream);
+/* mode: 0 batch stats, 1 batch stats + running-stat update (train), 2 running stats (eval) */
 int lasr_bn_swish_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
                       const float* shift, void* h, int hdt, void* stream);
 /* BN(train)+Swish backward: dgamma/dbeta accumulated, dy = BN'(dh * swish'(u)).

@@ -221,8 +221,7 @@ extern "C" int lasr_qbias_bwd(const void* dqu, const void* dqv, int dt, int B, i
   else qbias_bwd_kernel<bf16_t><<<g, 256, 0, st>>>((const bf16_t*)dqu, (const bf16_t*)dqv, rows, D, (bf16_t*)dqkv, ld, ws);
   int rc = lasr_check_launch("qbias_bwd");
   if (rc) return rc;
-  qbias_reduce_kernel<<<(unsigned)cdiv(D, 256), 256, 0, st>>>(ws, (int)nchunk, D, du, dv);
-  return lasr_check_launch("qbias_bwd/reduce");
+  return lasr_reduce_cols(ws, (int)nchunk, 2 * D, du, dv, D, 1, st);
 }
 
 extern "C" int lasr_attn_softmax_fwd(const float* s_ac, const float* s_bd, int relpos, int B,
@@ -234,7 +233,7 @@ extern "C" int lasr_attn_softmax_fwd(const float* s_ac, const float* s_bd, int r
   LASR_CHECK_ARG(!relpos || Tq == Tk, "lasr_attn_softmax_fwd: relpos needs Tq == Tk");
   const int64_t rows = (int64_t)B * H * Tq;
   if (rows == 0) return LASR_OK;
-  DropCfg d{drop_p, seed};
+  DropCfg d = mkdrop(drop_p, seed);
   hipStream_t st = (hipStream_t)stream;
   const unsigned g = (unsigned)cdiv(rows, 4);
   if (pdt == LASR_F32)
@@ -251,7 +250,7 @@ extern "C" int lasr_attn_softmax_bwd(const void* P, int pdt, const float* dPd, i
   LASR_CHECK_ARG(Tk <= 64 * SM_MAXC, "lasr_attn_softmax_bwd: Tk too large");
   const int64_t rows = (int64_t)B * H * Tq;
   if (rows == 0) return LASR_OK;
-  DropCfg d{drop_p, seed};
+  DropCfg d = mkdrop(drop_p, seed);
   hipStream_t st = (hipStream_t)stream;
   const unsigned g = (unsigned)cdiv(rows, 4);
 #define SMB(TP, TS)                                                                            \

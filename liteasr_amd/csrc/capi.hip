@@ -24,3 +24,16 @@ int lasr_check_launch(const char* what) {
 
 extern "C" const char* lasr_last_error(void) { return g_err; }
 extern "C" int lasr_version(void) { return 1; }
+
+static const uint64_t* g_drop_ctr = nullptr;
+const uint64_t* lasr_dropout_counter() { return g_drop_ctr; }
+extern "C" int lasr_set_dropout_counter(const uint64_t* dev_counter) {
+  g_drop_ctr = dev_counter;
+  return LASR_OK;
+}
+
+__global__ void counter_add_kernel(uint64_t* c, uint64_t v) { c[0] += v; }
+extern "C" int lasr_counter_add(uint64_t* dev_counter, uint64_t v, void* stream) {
+  counter_add_kernel<<<1, 1, 0, (hipStream_t)stream>>>(dev_counter, v);
+  return lasr_check_launch("counter_add");
+}

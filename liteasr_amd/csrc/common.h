@@ -26,6 +26,31 @@ template <> LASR_DEV bf16_t from_f<bf16_t>(float x) { return f2bf(x); }
 template <typename T> LASR_DEV float ldf(const T* p, int64_t i) { return to_f(p[i]); }
 template <typename T> LASR_DEV void stf(T* p, int64_t i, float v) { p[i] = from_f<T>(v); }
 
+// ---- 8-wide vector load/store (16-B aligned for bf16, 32-B for fp32) ----------
+LASR_DEV void ld8(const float* p, float v[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+LASR_DEV void ld8(const bf16_t* p, float v[8]) {
+  const uint4 u = *(const uint4*)p;
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+LASR_DEV void st8(float* p, const float v[8]) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+LASR_DEV void st8(bf16_t* p, const float v[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // ---- wave (64-lane) reductions ------------------------------------------------
 LASR_DEV float wave_sum(float v) {
 #pragma unroll
@@ -76,14 +101,25 @@ LASR_DEV uint32_t lasr_hash(uint64_t seed, uint64_t idx) {
   return (uint32_t)(z >> 32);
 }
 struct DropCfg {
-  float p;        // drop probability (0 = off)
-  uint64_t seed;  // per-site, per-step seed
+  float p;              // drop probability (0 = off)
+  uint64_t seed;        // per-site seed (host)
+  const uint64_t* ctr;  // optional device step counter (read at run time, graph-safe)
 };
+// Host: the process-wide device counter registered by lasr_set_dropout_counter().
+const uint64_t* lasr_dropout_counter();
+static inline DropCfg mkdrop(float p, uint64_t seed) {
+  DropCfg d;
+  d.p = p;
+  d.seed = seed;
+  d.ctr = p > 0.f ? lasr_dropout_counter() : nullptr;
+  return d;
+}
 // Returns the multiplier for element idx: 0 or 1/(1-p); 1 when dropout is off.
 LASR_DEV float drop_mul(const DropCfg& d, uint64_t idx) {
   if (d.p <= 0.f) return 1.f;
+  const uint64_t seed = d.seed + (d.ctr ? d.ctr[0] * 0xD1B54A32D192ED03ull : 0ull);
   const uint32_t thr = (uint32_t)fminf(d.p * 4294967296.0f, 4294967295.0f);
-  return lasr_hash(d.seed, idx) >= thr ? 1.f / (1.f - d.p) : 0.f;
+  return lasr_hash(seed, idx) >= thr ? 1.f / (1.f - d.p) : 0.f;
 }
 
 LASR_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
@@ -106,3 +142,10 @@ int lasr_check_launch(const char* what);
   } while (0)
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// reduce.hip: out[n] (+)= sum_p part[p*N+n]; columns >= split go to out1[n-split].
+int lasr_reduce_cols(const float* part, int P, int64_t N, float* out0, float* out1, int64_t split,
+                     int accumulate, hipStream_t st);
+// dst[c*ld+k] += src[k*C+c] (k<K); bias[c] += src[K*C+c] when bias != nullptr.
+int lasr_scatter_kc(const float* src, int K, int C, int ld, float* dst, float* bias,
+                    hipStream_t st);

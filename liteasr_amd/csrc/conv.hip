@@ -111,34 +111,39 @@ __global__ void im2col_kernel(const T* __restrict__ y1, int B, int T1, int F1, i
 template <typename T>
 __global__ void col2im_kernel(const T* __restrict__ dcol, int B, int T1, int F1, int C, int T2,
                               int F2, const T* __restrict__ y1, T* dy1) {
-  const int64_t n = (int64_t)B * T1 * F1 * C;
+  // 8 channels per thread (C % 8 == 0): 16-B loads/stores along cin
+  const int C8 = C / 8;
+  const int64_t n = (int64_t)B * T1 * F1 * C8;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int cin = (int)(e % C);
-    const int64_t pix = e / C;
+    const int cin = (int)(e % C8) * 8;
+    const int64_t pix = e / C8;
     const int fi = (int)(pix % F1);
     const int64_t bt = pix / F1;
     const int ti = (int)(bt % T1);
     const int64_t b = bt / T1;
-    float s = 0.f;
-    if (to_f(y1[e]) > 0.f) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t[8], yv[8];
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int tt = ti - kh;
-        if (tt < 0 || (tt & 1)) continue;
-        const int t2 = tt >> 1;
-        if (t2 >= T2) continue;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int tt = ti - kh;
+      if (tt < 0 || (tt & 1)) continue;
+      const int t2 = tt >> 1;
+      if (t2 >= T2) continue;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int ff = fi - kw;
-          if (ff < 0 || (ff & 1)) continue;
-          const int f2 = ff >> 1;
-          if (f2 >= F2) continue;
-          const int64_t m = (b * T2 + t2) * F2 + f2;
-          s += to_f(dcol[m * 9 * C + (kh * 3 + kw) * C + cin]);
-        }
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ff = fi - kw;
+        if (ff < 0 || (ff & 1)) continue;
+        const int f2 = ff >> 1;
+        if (f2 >= F2) continue;
+        const int64_t m = (b * T2 + t2) * F2 + f2;
+        ld8(dcol + m * 9 * C + (kh * 3 + kw) * C + cin, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += t[j];
       }
     }
-    dy1[e] = from_f<T>(s);
+    ld8(y1 + pix * C + cin, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = yv[j] > 0.f ? s[j] : 0.f;
+    st8(dy1 + pix * C + cin, s);
   }
 }
 
@@ -282,8 +287,17 @@ __global__ void bn_finalize_kernel(const float* stats, int nparts, int C, float 
                                    float* rmean, float* rvar, int64_t* nbt, float* mean,
                                    float* rstd, float* scale, float* shift, int update) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && update && nbt) nbt[0] += 1;
+  if (c == 0 && update == 1 && nbt) nbt[0] += 1;
   if (c >= C) return;
+  if (update == 2) {  // eval mode: normalise with the running statistics
+    const float rs = rsqrtf(rvar[c] + eps);
+    mean[c] = rmean[c];
+    rstd[c] = rs;
+    const float sc = gamma[c] * rs;
+    scale[c] = sc;
+    shift[c] = beta[c] - rmean[c] * sc;
+    return;
+  }
   // Chan's parallel combination, fixed order
   double n = 0.0, mu = 0.0, m2 = 0.0;
   for (int p = 0; p < nparts; ++p) {
@@ -304,7 +318,71 @@ __global__ void bn_finalize_kernel(const float* stats, int nparts, int C, float 
   const float sc = gamma[c] * rs;
   scale[c] = sc;
   shift[c] = beta[c] - (float)mu * sc;
-  if (update) {
+  if (update == 1) {
+    const float uvar = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * uvar;
+  }
+}
+
+// Parallel form: 256 threads = 32 channels x 8 partial-groups, Chan-combined in double
+// (fixed order), then one thread per channel finalises.
+__global__ __launch_bounds__(256) void bn_finalize_par_kernel(
+    const float* stats, int nparts, int C, float eps, float momentum, const float* gamma,
+    const float* beta, float* rmean, float* rvar, int64_t* nbt, float* mean, float* rstd,
+    float* scale, float* shift, int update) {
+  __shared__ double sn[8][33], smu[8][33], sm2[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + tx;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && update == 1 && nbt) nbt[0] += 1;
+  if (update == 2) {  // eval mode: normalise with the running statistics
+    if (ty == 0 && c < C) {
+      const float rs = rsqrtf(rvar[c] + eps);
+      mean[c] = rmean[c];
+      rstd[c] = rs;
+      const float sc = gamma[c] * rs;
+      scale[c] = sc;
+      shift[c] = beta[c] - rmean[c] * sc;
+    }
+    return;
+  }
+  double n = 0.0, mu = 0.0, m2 = 0.0;
+  if (c < C) {
+    for (int p = ty; p < nparts; p += 8) {
+      const float* st = stats + (int64_t)p * 3 * C;
+      const double nb = st[c];
+      if (nb <= 0.0) continue;
+      const double mb = st[C + c], m2b = st[2 * C + c];
+      const double nt = n + nb;
+      const double dl = mb - mu;
+      mu += dl * nb / nt;
+      m2 += m2b + dl * dl * n * nb / nt;
+      n = nt;
+    }
+  }
+  sn[ty][tx] = n;
+  smu[ty][tx] = mu;
+  sm2[ty][tx] = m2;
+  __syncthreads();
+  if (ty != 0 || c >= C) return;
+  n = 0.0; mu = 0.0; m2 = 0.0;
+  for (int g = 0; g < 8; ++g) {
+    const double nb = sn[g][tx];
+    if (nb <= 0.0) continue;
+    const double nt = n + nb;
+    const double dl = smu[g][tx] - mu;
+    mu += dl * nb / nt;
+    m2 += sm2[g][tx] + dl * dl * n * nb / nt;
+    n = nt;
+  }
+  const float var = (float)(m2 / n);
+  const float rs = rsqrtf(var + eps);
+  mean[c] = (float)mu;
+  rstd[c] = rs;
+  const float sc = gamma[c] * rs;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mu * sc;
+  if (update == 1) {
     const float uvar = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
     rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
     rvar[c] = (1.f - momentum) * rvar[c] + momentum * uvar;
@@ -355,6 +433,13 @@ __global__ void bn_bwd_total_kernel(const float* part, int nparts, int C, float*
   dbeta[c] += s1;
   dgamma[c] += s2;
 }
+__global__ void bn_bwd_accum_kernel(const float* tot, int C, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  dbeta[c] += tot[c];
+  dgamma[c] += tot[C + c];
+}
+
 template <typename TY, typename TH, typename TD>
 __global__ void bn_swish_bwd_apply_kernel(const TY* y, const TH* dh, int64_t rows, int C,
                                           const float* scale, const float* shift,
@@ -391,15 +476,18 @@ extern "C" int lasr_conv1_bwd(const float* x, int B, int T, int F, int C, const 
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const int nrows = B * T1;
   const int nparts = (int)cdiv(nrows, C1B_ROWS);
-  LASR_CHECK_ARG(ws_floats >= (int64_t)nparts * 10 * C, "lasr_conv1_bwd: workspace too small");
+  LASR_CHECK_ARG(ws_floats >= (int64_t)(nparts + 1) * 10 * C, "lasr_conv1_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const size_t shm = (size_t)C1B_ROWS * 3 * F * sizeof(float);
   if (dt == LASR_F32) conv1_bwd_kernel<float><<<nparts, 256, shm, st>>>(x, T, F, C, T1, F1, nrows, (const float*)dy1, ws);
   else conv1_bwd_kernel<bf16_t><<<nparts, 256, shm, st>>>(x, T, F, C, T1, F1, nrows, (const bf16_t*)dy1, ws);
   int rc = lasr_check_launch("conv1_bwd");
   if (rc) return rc;
-  conv1_bwd_reduce_kernel<<<(unsigned)cdiv(C * 10, 256), 256, 0, st>>>(ws, nparts, C, dw, db);
-  return lasr_check_launch("conv1_bwd/reduce");
+  // partials [nparts][10][C] -> tot[10*C] (after the partials) -> dw[c*9+k], db[c]
+  float* tot = ws + (int64_t)nparts * 10 * C;
+  rc = lasr_reduce_cols(ws, nparts, (int64_t)10 * C, tot, nullptr, 10 * C, 0, st);
+  if (rc) return rc;
+  return lasr_scatter_kc(tot, 9, C, 9, dw, db, st);
 }
 
 extern "C" int lasr_im2col3x3s2(const void* y1, int dt, int B, int T1, int F1, int C, void* col,
@@ -415,8 +503,9 @@ extern "C" int lasr_im2col3x3s2(const void* y1, int dt, int B, int T1, int F1, i
 
 extern "C" int lasr_col2im3x3s2(const void* dcol, int dt, int B, int T1, int F1, int C,
                                 const void* y1, void* dy1, void* stream) {
+  LASR_CHECK_ARG(C % 8 == 0, "lasr_col2im3x3s2: C %% 8 != 0");
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
-  const int64_t n = (int64_t)B * T1 * F1 * C;
+  const int64_t n = (int64_t)B * T1 * F1 * (C / 8);
   hipStream_t st = (hipStream_t)stream;
   if (dt == LASR_F32) col2im_kernel<float><<<gridn(n), 256, 0, st>>>((const float*)dcol, B, T1, F1, C, T2, F2, (const float*)y1, (float*)dy1);
   else col2im_kernel<bf16_t><<<gridn(n), 256, 0, st>>>((const bf16_t*)dcol, B, T1, F1, C, T2, F2, (const bf16_t*)y1, (bf16_t*)dy1);
@@ -460,7 +549,7 @@ extern "C" int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float 
                                 float* running_mean, float* running_var, int64_t* num_batches,
                                 float* mean, float* rstd, float* scale, float* shift,
                                 int update_running, void* stream) {
-  bn_finalize_kernel<<<(unsigned)cdiv(C, 256), 256, 0, (hipStream_t)stream>>>(
+  bn_finalize_par_kernel<<<(unsigned)cdiv(C, 32), 256, 0, (hipStream_t)stream>>>(
       stats_ws, nparts, C, eps, momentum, gamma, beta, running_mean, running_var, num_batches,
       mean, rstd, scale, shift, update_running);
   return lasr_check_launch("bn_finalize");
@@ -500,8 +589,10 @@ extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt
 #undef BR
   int rc = lasr_check_launch("bn_swish_bwd/reduce");
   if (rc) return rc;
-  bn_bwd_total_kernel<<<(unsigned)cdiv(C, 256), 256, 0, st>>>(ws, (int)nparts, C, tot, dgamma, dbeta);
-  rc = lasr_check_launch("bn_swish_bwd/total");
+  rc = lasr_reduce_cols(ws, (int)nparts, 2 * C, tot, nullptr, 2 * C, 0, st);
+  if (rc) return rc;
+  bn_bwd_accum_kernel<<<(unsigned)cdiv(C, 256), 256, 0, st>>>(tot, C, dgamma, dbeta);
+  rc = lasr_check_launch("bn_swish_bwd/accum");
   if (rc) return rc;
   const int64_t n = rows * C;
 #define BA(TY, TH, TD) bn_swish_bwd_apply_kernel<TY, TH, TD><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy)
@@ -524,7 +615,7 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
   LASR_CHECK_ARG(K == DW_K, "lasr_glu_dwconv_bwd: only kernel size %d is built", DW_K);
   const int nchunk = (int)cdiv(T, DW_TT);
   const int nparts = B * nchunk;
-  LASR_CHECK_ARG(ws_floats >= (int64_t)nparts * (DW_K + 1) * C, "lasr_glu_dwconv_bwd: workspace too small");
+  LASR_CHECK_ARG(ws_floats >= (int64_t)(nparts + 1) * (DW_K + 1) * C, "lasr_glu_dwconv_bwd: workspace too small");
   dim3 g((unsigned)nparts, (unsigned)cdiv(C, 256));
   hipStream_t st = (hipStream_t)stream;
 #define GB(TT, TD) glu_dwconv_bwd_kernel<TT, TD><<<g, 256, 0, st>>>((const TT*)z1, (const TD*)dy, T, C, w, (TT*)dz1, ws)
@@ -535,6 +626,8 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
 #undef GB
   int rc = lasr_check_launch("glu_dwconv_bwd");
   if (rc) return rc;
-  dw_reduce_kernel<<<(unsigned)cdiv(C * (DW_K + 1), 256), 256, 0, st>>>(ws, nparts, C, dw, db);
-  return lasr_check_launch("glu_dwconv_bwd/reduce");
+  float* tot = ws + (int64_t)nparts * (DW_K + 1) * C;
+  rc = lasr_reduce_cols(ws, nparts, (int64_t)(DW_K + 1) * C, tot, nullptr, (DW_K + 1) * C, 0, st);
+  if (rc) return rc;
+  return lasr_scatter_kc(tot, DW_K, C, DW_K, dw, db, st);
 }

@@ -107,7 +107,7 @@ extern "C" int lasr_pe_fwd(const void* x, int xdt, int64_t rows, int T, int D, c
                            float xscale, float p, uint64_t seed, void* y, int ydt, void* stream) {
   const int64_t n = rows * D;
   if (n <= 0) return LASR_OK;
-  DropCfg d{p, seed};
+  DropCfg d = mkdrop(p, seed);
   hipStream_t st = (hipStream_t)stream;
 #define PF(TX, TY) pe_fwd_kernel<TX, TY><<<gridn(n), 256, 0, st>>>((const TX*)x, rows, T, D, pe, xscale, d, (TY*)y)
   if (xdt == LASR_F32 && ydt == LASR_F32) PF(float, float);
@@ -123,7 +123,7 @@ extern "C" int lasr_embed_pe_fwd(const int32_t* ids, int R, int L, int D, const 
                                  int ydt, void* stream) {
   const int64_t n = (int64_t)R * D;
   if (n <= 0) return LASR_OK;
-  DropCfg d{p, seed};
+  DropCfg d = mkdrop(p, seed);
   hipStream_t st = (hipStream_t)stream;
   if (ydt == LASR_F32) embed_pe_fwd_kernel<float><<<gridn(n), 256, 0, st>>>(ids, R, L, D, E, pe, xscale, d, (float*)y);
   else embed_pe_fwd_kernel<bf16_t><<<gridn(n), 256, 0, st>>>(ids, R, L, D, E, pe, xscale, d, (bf16_t*)y);
@@ -134,7 +134,7 @@ extern "C" int lasr_embed_bwd(const int32_t* ids, int R, int D, const void* dy, 
                               float xscale, float p, uint64_t seed, float* dE, void* stream) {
   if (R <= 0) return LASR_OK;
   LASR_CHECK_ARG(R <= 16384, "lasr_embed_bwd: R=%d > 16384", R);
-  DropCfg d{p, seed};
+  DropCfg d = mkdrop(p, seed);
   hipStream_t st = (hipStream_t)stream;
   const size_t shm = (size_t)R * sizeof(int);
   if (dydt == LASR_F32) embed_bwd_kernel<float><<<R, 256, shm, st>>>(ids, R, D, (const float*)dy, xscale, d, dE);

@@ -46,6 +46,7 @@ struct GemmP {
   int kchunk;
   float* ws;
   int a_vec, b_vec;
+  int c_vec, aux_vec, res_vec, ws_vec;  // 8-wide epilogue access allowed
 };
 
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
@@ -72,6 +73,72 @@ LASR_DEV void epi_store(const GemmP& p, int z1, int z2, int z, int m, int n, flo
   TC* C = (TC*)p.C;
   if (p.beta != 0.f) v += p.beta * to_f(C[cidx]);
   C[cidx] = from_f<TC>(v);
+}
+
+// 8 values of a (f32|bf16) matrix row starting at element idx; cnt < 8 -> tail.
+LASR_DEV void ld_any8(const void* base, int dt, int64_t idx, bool vec, int cnt, float* o) {
+  if (vec && cnt == 8) {
+    if (dt == LASR_F32) ld8((const float*)base + idx, o);
+    else ld8((const bf16_t*)base + idx, o);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = q < cnt ? load_any(base, dt, idx + q) : 0.f;
+  }
+}
+template <typename T>
+LASR_DEV void st_8(T* dst, const float* v, bool vec, int cnt) {
+  if (vec && cnt == 8) st8(dst, v);
+  else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < cnt) dst[q] = from_f<T>(v[q]);
+  }
+}
+
+// Epilogue for 8 consecutive columns n..n+7 of row m (same order as epi_store).
+template <typename TC>
+LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, const float* acc,
+                         float alpha_eff) {
+  const int cnt = min(8, p.N - n);
+  float v[8], t[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff;
+  if (p.bias) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += q < cnt ? p.bias[n + q] : 0.f;
+  }
+  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
+  if (p.zout) st_8((TC*)p.zout + cidx, v, p.c_vec, cnt);
+  if (p.act == LASR_ACT_RELU) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+  } else if (p.act == LASR_ACT_SWISH) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = swishf(v[q]);
+  }
+  if (p.aux) {
+    ld_any8(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, p.aux_vec, cnt, t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      v[q] *= (p.aux_act == LASR_ACT_RELU) ? (t[q] > 0.f ? 1.f : 0.f) : swish_grad(t[q]);
+  }
+  if (p.drop.p > 0.f) {
+    const uint64_t base = ((uint64_t)z * p.M + m) * (uint64_t)p.N + n;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] *= drop_mul(p.drop, base + q);
+  }
+  if (p.res) {
+    ld_any8(p.res, p.res_dtype, (int64_t)m * p.ldres + n, p.res_vec, cnt, t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = t[q] + p.res_scale * v[q];
+  }
+  TC* C = (TC*)p.C + cidx;
+  if (p.beta != 0.f) {
+    ld_any8(C, sizeof(TC) == 4 ? LASR_F32 : LASR_BF16, 0, p.c_vec, cnt, t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += p.beta * t[q];
+  }
+  st_8(C, v, p.c_vec, cnt);
 }
 
 LASR_DEV float alpha_of(const GemmP& p) {
@@ -160,7 +227,10 @@ template <int BM, int BN, bool AKC, bool BKC, typename TC>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
   constexpr int BK = 32;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * BK];
+  constexpr int MAIN_BYTES = 2 * (BM + BN) * BK * 2;
+  constexpr int EPI_BYTES = WM * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(16))) char smem_epi[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
+  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_epi);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
 
@@ -226,30 +296,45 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
     __syncthreads();
   }
 
+  // ---- epilogue: stage each half of the C tile (WM rows x BN cols, fp32) through LDS,
+  // then every thread finishes 8 contiguous columns of a row with 16-B loads/stores.
+  constexpr int LDC = BN + 4;  // +4 floats: the 4 row-groups of a write land on distinct banks
+  float* cs = reinterpret_cast<float*>(smem_epi);
   const int rq = (lane >> 4) * 4, cl = lane & 15;
-  if (p.split_k > 1) {
-    float* ws = p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + wr * WM + i * 16 + rq + e, n = n0 + wc * WN + j * 16 + cl;
-          if (m < p.M && n < p.N) ws[(int64_t)m * p.N + n] = acc[i][j][e];
-        }
-    return;
-  }
   const float al = alpha_of(p);
+  const bool split = p.split_k > 1;
+  float* wsp = split ? p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N : nullptr;
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int h = 0; h < 2; ++h) {
+    if (wr == h) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wr * WM + i * 16 + rq + e, n = n0 + wc * WN + j * 16 + cl;
-        epi_store<TC>(p, z1, z2, z, m, n, acc[i][j][e], al);
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cs[(i * 16 + rq + e) * LDC + wc * WN + j * 16 + cl] = acc[i][j][e];
+    }
+    __syncthreads();
+    constexpr int NV = WM * BN / 8;
+    for (int v = tid; v < NV; v += 256) {
+      const int r = v / (BN / 8), c8 = (v % (BN / 8)) * 8;
+      const int m = m0 + h * WM + r, n = n0 + c8;
+      if (m < p.M && n < p.N) {
+        float a8[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + c8 + q];
+        if (split) {
+          float* dst = wsp + (int64_t)m * p.N + n;
+          if (p.ws_vec && n + 8 <= p.N) st8(dst, a8);
+          else
+            for (int q = 0; q < 8 && n + q < p.N; ++q) dst[q] = a8[q];
+        } else {
+          epi_store8<TC>(p, z1, z2, z, m, n, a8, al);
+        }
       }
+    }
+    __syncthreads();
+  }
 }
 
 // ============================ fp32 MFMA kernel ===================================
@@ -393,7 +478,7 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   p.alpha = a->alpha; p.alpha_dev = a->alpha_dev; p.beta = a->beta;
   p.bias = a->bias; p.act = a->act; p.zout = a->zout;
   p.aux = a->aux; p.aux_dtype = a->aux_dtype; p.ldaux = a->ldaux; p.aux_act = a->aux_act;
-  p.drop.p = a->drop_p; p.drop.seed = a->drop_seed;
+  p.drop = mkdrop(a->drop_p, a->drop_seed);
   p.res = a->res; p.res_dtype = a->res_dtype; p.ldres = a->ldres; p.res_scale = a->res_scale;
 
   const bool akc = (a->lda_k == 1);
@@ -405,9 +490,24 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
     p.a_vec = bf && aligned16(a->A) && s_a % 8 == 0 && a->sa1 % 8 == 0 && a->sa2 % 8 == 0;
     p.b_vec = bf && aligned16(a->B) && s_b % 8 == 0 && a->sb1 % 8 == 0 && a->sb2 % 8 == 0;
   }
+  p.c_vec = aligned16(a->C) && a->ldc % 8 == 0 && a->sc1 % 8 == 0 && a->sc2 % 8 == 0 &&
+            (!a->zout || aligned16(a->zout));
+  p.aux_vec = a->aux && aligned16(a->aux) && a->ldaux % 8 == 0;
+  p.res_vec = a->res && aligned16(a->res) && a->ldres % 8 == 0;
+  p.ws_vec = a->N % 8 == 0;
 
   int BM = 64, BN = 64;
-  if (bf) {
+  int split = a->split_k > 0 ? a->split_k : 1;
+  const bool plain = !a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f;
+  const bool autosplit = a->split_k == 0 && plain && a->workspace;
+  const int kt = (int)cdiv(a->K, 32);
+  if (bf && autosplit && kt >= 16) {
+    // long-K (weight-gradient) GEMMs: big tiles, fill the chip with K slices instead
+    BM = a->M >= 96 ? 128 : 64;
+    BN = a->N >= 96 ? 128 : 64;
+    const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
+    while (nb * split < 512 && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
+  } else if (bf) {
     const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
     for (int c = 0; c < 4; ++c) {
       const int64_t nb = cdiv(a->M, cfg[c][0]) * cdiv(a->N, cfg[c][1]) * (int64_t)batch;
@@ -415,13 +515,8 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
       if (nb >= 512) break;
     }
   }
-
-  // split-K: explicit (split_k > 1) or automatic (split_k == 0) when the epilogue is plain.
-  int split = a->split_k > 0 ? a->split_k : 1;
-  const bool plain = !a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f;
-  if (a->split_k == 0 && plain && a->workspace) {
+  if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
-    const int kt = (int)cdiv(a->K, 32);
     while (nb * split < 512 && split * 2 <= 32 && kt / (split * 2) >= 4) split *= 2;
   }
   if (split > 1) {

@@ -130,7 +130,7 @@ extern "C" int lasr_layernorm_fwd(const void* x, int x_dtype, int64_t rows, int 
                                   float p2, uint64_t seed2, void* stream) {
   LASR_CHECK_ARG(D % 64 == 0 && D >= 64 && D <= 1024, "lasr_layernorm_fwd: D=%d unsupported", D);
   if (rows <= 0) return LASR_OK;
-  DropCfg d2{p2, seed2};
+  DropCfg d2 = mkdrop(p2, seed2);
   hipStream_t st = (hipStream_t)stream;
   switch (D / 64) {
     case 1: ln_fwd_npl<1>(x, x_dtype, rows, gamma, beta, eps, y, y_dtype, mean, rstd, y2, y2_dtype, d2, st); break;
@@ -187,7 +187,7 @@ extern "C" int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, in
   const int64_t nblk = cdiv(rows, LN_ROWS_PER_BLOCK);
   LASR_CHECK_ARG(ws_floats >= nblk * 2 * D, "lasr_layernorm_bwd: workspace too small (%lld < %lld)",
                  (long long)ws_floats, (long long)(nblk * 2 * D));
-  DropCfg bd{bp, bseed};
+  DropCfg bd = mkdrop(bp, bseed);
   hipStream_t st = (hipStream_t)stream;
   switch (D / 64) {
 #define CASE(n) case n: ln_bwd_npl<n>(x, x_dtype, dy, dy_dtype, rows, gamma, mean, rstd, dres, dres_dtype, dx, dx_dtype, workspace, gb, gb_dtype, bscale, bd, st); break;
@@ -197,7 +197,9 @@ extern "C" int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, in
   }
   int rc = lasr_check_launch("layernorm_bwd");
   if (rc) return rc;
-  if (dgamma || dbeta) {
+  if (dgamma && dbeta) {
+    rc = lasr_reduce_cols(workspace, (int)nblk, 2 * D, dgamma, dbeta, D, 1, st);
+  } else if (dgamma || dbeta) {
     ln_param_reduce_kernel<<<(unsigned)cdiv(D, 256), 256, 0, st>>>(workspace, (int)nblk, D, dgamma, dbeta);
     rc = lasr_check_launch("layernorm_bwd/reduce");
   }
@@ -214,7 +216,7 @@ __global__ void branch_grad_kernel(const TI* dx, int64_t n, TO* gb, float scale,
 extern "C" int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_dtype,
                                 float scale, float p, uint64_t seed, void* stream) {
   if (n <= 0) return LASR_OK;
-  DropCfg d{p, seed};
+  DropCfg d = mkdrop(p, seed);
   hipStream_t st = (hipStream_t)stream;
   const unsigned nb = (unsigned)std::min<int64_t>(cdiv(n, 256), 8192);
   if (dx_dtype == LASR_F32 && gb_dtype == LASR_F32) branch_grad_kernel<float, float><<<nb, 256, 0, st>>>((const float*)dx, n, (float*)gb, scale, d);
@@ -225,7 +227,7 @@ extern "C" int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* g
 }
 
 // ----------------------------- column sums ----------------------------------------
-constexpr int CS_ROWS = 64;
+constexpr int CS_ROWS = 16;
 template <typename T>
 __global__ void colsum_partial_kernel(const T* X, int64_t M, int64_t N, int64_t ldx, float* part) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -256,6 +258,7 @@ extern "C" int lasr_colsum(const void* X, int dtype, int64_t M, int64_t N, int64
     if (dtype == LASR_F32) colsum_partial_kernel<float><<<g1, 256, 0, st>>>((const float*)X, M, N, ldx, workspace);
     else colsum_partial_kernel<bf16_t><<<g1, 256, 0, st>>>((const bf16_t*)X, M, N, ldx, workspace);
   }
-  colsum_final_kernel<<<(unsigned)cdiv(N, 256), 256, 0, st>>>(workspace, (int)nchunk, N, out, accumulate);
-  return lasr_check_launch("colsum");
+  int rc = lasr_check_launch("colsum");
+  if (rc) return rc;
+  return lasr_reduce_cols(workspace, (int)nchunk, N, out, nullptr, N, accumulate, st);
 }

@@ -1,0 +1,183 @@
+"""Data parallelism for FlatParams models: bucketed gradient all-reduce over RCCL,
+overlapped with the backward pass.
+
+Replaces torch DistributedDataParallel as used by the reference (liteasr/trainer.py:76-88,
+DDP defaults: 25 MiB buckets, broadcast_buffers=True).  Because every parameter lives
+in one flat fp32 buffer laid out module by module, a bucket is simply a contiguous slice
+of the flat grad buffer: no bucket copies, no per-parameter hooks.  The fused backward
+nodes call ``module.on_grads_ready()`` after writing a module's weight gradients; the
+reducer launches ``all_reduce`` (RCCL, async, its own stream) on a bucket as soon as all
+modules inside it are done, in backward order (ctc/decoder -> encoder layers 11..0 ->
+subsampling), so communication overlaps the remaining backward compute.
+
+Semantics kept from torch DDP: initial parameter + buffer broadcast from rank 0;
+gradient *average*; BatchNorm running stats re-broadcast from rank 0 at every forward
+(the constant positional-encoding tables are skipped -- identical on every rank);
+``no_sync()`` skips the all-reduce for gradient accumulation (trainer.py:142-147).
+"""
+
+from __future__ import annotations
+
+from contextlib import contextmanager
+from typing import List
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..nets.modules import _Bound
+
+BUCKET_BYTES = 25 * 1024 * 1024
+
+
+class _Unit:
+    def __init__(self, name, lo, hi):
+        self.name, self.lo, self.hi = name, lo, hi
+
+
+class FlatReducer:
+    def __init__(self, model, process_group=None, bucket_bytes=BUCKET_BYTES):
+        self.model = model
+        self.store = model.store
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group)
+        self.enabled = True
+        units = self._units()
+        # buckets in backward order: group consecutive units until >= bucket_bytes
+        self.buckets: List[List[_Unit]] = []
+        cur, size = [], 0
+        for u in units:
+            cur.append(u)
+            size += (u.hi - u.lo) * 4
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.unit_bucket = {}
+        for bi, b in enumerate(self.buckets):
+            for u in b:
+                self.unit_bucket[u.name] = bi
+        self._reset()
+        for mod in model.modules():
+            if isinstance(mod, _Bound):
+                mod._ready_hook = self._on_ready
+        model.encoder._after_norm_hook = self._on_ready
+
+    def _units(self):
+        """Hook units (module prefix -> flat range) in the order backward completes them."""
+        st, m = self.store, self.model
+        enc, dec = m.encoder, m.decoder
+        order = [("ctc", m.ctc), ("decoder", dec), ("encoder.after_norm", None)]
+        order += [(l._pfx, l) for l in reversed(list(enc.enc_layers))]
+        order += [("encoder.embed", enc.embed)]
+        units, covered = [], set()
+        for name, _ in order:
+            names = [n for n in st.names if n == name or n.startswith(name + ".")]
+            assert names, name
+            lo = min(st.offsets[n] for n in names)
+            hi = max(st.offsets[n] + st.shapes[n].numel() for n in names)
+            units.append(_Unit(name, lo, hi))
+            covered.update(names)
+        missing = [n for n in st.names if n not in covered]
+        assert not missing, f"parameters outside any reducer unit: {missing[:5]}"
+        # extend ranges so buckets tile the buffer contiguously (alignment gaps included)
+        units_sorted = sorted(units, key=lambda u: u.lo)
+        for a, b in zip(units_sorted, units_sorted[1:]):
+            assert a.hi <= b.lo, "units overlap"
+            a.hi = b.lo
+        units_sorted[0].lo = 0
+        units_sorted[-1].hi = st.numel
+        return units
+
+    def _reset(self):
+        self.ready = [0] * len(self.buckets)
+        self.works = []
+        self.next_bucket = 0
+        self.active = False
+
+    def _on_ready(self, mod):
+        if not self.enabled:
+            return
+        name = mod if isinstance(mod, str) else mod._pfx
+        if name not in self.unit_bucket:
+            return
+        if not self.active:
+            self.active = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        bi = self.unit_bucket[name]
+        self.ready[bi] += 1
+        # launch buckets strictly in order (every rank issues the same collective sequence)
+        while self.next_bucket < len(self.buckets) and self.ready[self.next_bucket] == len(self.buckets[self.next_bucket]):
+            self._launch(self.next_bucket)
+            self.next_bucket += 1
+
+    def _slice(self, b):
+        lo = min(u.lo for u in b)
+        hi = max(u.hi for u in b)
+        return self.store.grad[lo:hi]
+
+    def _launch(self, bi):
+        g = self._slice(self.buckets[bi])
+        if g.is_cuda:
+            w = dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
+        else:  # gloo (CPU plumbing tests): SUM then scale
+            w = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        self.works.append((w, g))
+
+    def _finalize(self):
+        for bi in range(self.next_bucket, len(self.buckets)):  # units that never fired
+            self._launch(bi)
+        for w, g in self.works:
+            w.wait()
+            if not g.is_cuda:
+                g.div_(self.world)
+        self._reset()
+
+
+class DistributedDataParallel(nn.Module):
+    """torch-DDP-shaped wrapper (``.module``, ``no_sync()``) around a FlatParams model."""
+
+    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_cap_mb=25, **_):
+        super().__init__()
+        self.module = module
+        self.process_group = process_group
+        self.broadcast_buffers = broadcast_buffers
+        st = module.store
+        st.ensure_grad()
+        dist.broadcast(st.flat, 0, group=process_group)
+        self._bn_buffers = [b for n, b in module.named_buffers() if not n.endswith(".pe") and not n.startswith("_")]
+        self._sync_buffers()
+        st._work_version = -1  # weights changed under the working copy
+        self.reducer = FlatReducer(module, process_group, int(bucket_cap_mb * 1024 * 1024))
+
+    def _sync_buffers(self):
+        if not self._bn_buffers:
+            return
+        coalesced = getattr(dist, "_broadcast_coalesced", None)
+        if coalesced is not None and self._bn_buffers[0].is_cuda:
+            pg = self.process_group if self.process_group is not None else dist.group.WORLD
+            coalesced(pg, self._bn_buffers, 1 << 20, 0)
+        else:
+            for b in self._bn_buffers:
+                dist.broadcast(b, 0, group=self.process_group)
+
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(self.module, name)
+
+    def forward(self, *args, **kwargs):
+        if self.broadcast_buffers and self.module.training:
+            self._sync_buffers()
+        return self.module(*args, **kwargs)
+
+    @contextmanager
+    def no_sync(self):
+        old = self.reducer.enabled
+        self.reducer.enabled = False
+        try:
+            yield
+        finally:
+            self.reducer.enabled = old

@@ -132,7 +132,7 @@ def gemm(
         args.res, args.res_dtype, args.ldres, args.res_scale = ptr(res), dt(res), res.stride(0), res_scale
     args.split_k = split_k
     if split_k != 1:
-        need = 32 * z1 * z2 * M * Nn if split_k == 0 else split_k * z1 * z2 * M * Nn
+        need = 64 * z1 * z2 * M * Nn if split_k == 0 else split_k * z1 * z2 * M * Nn
         ws = WS.get(need, c.device)
         args.workspace, args.workspace_bytes = ptr(ws), ws.numel() * 4
     N.call("lasr_gemm", C.byref(args), stream())
@@ -146,7 +146,7 @@ def linear(x, w, out, bias=None, **kw):
 
 def colsum(x2d: torch.Tensor, out: torch.Tensor, accumulate=True):
     M, Nn = x2d.shape
-    nchunk = (M + 63) // 64
+    nchunk = (M + 15) // 16  # CS_ROWS in norm.hip
     ws = WS.get(nchunk * Nn, x2d.device)
     N.call("lasr_colsum", ptr(x2d), dt(x2d), M, Nn, x2d.stride(0), ptr(out), int(accumulate),
            ptr(ws), ws.numel(), stream())
@@ -254,7 +254,7 @@ def conv1_bwd(x, dy1, dw, db):
     Cc = dw.shape[0]
     T1 = (T - 3) // 2 + 1
     nparts = (B * T1 + 15) // 16
-    ws = WS.get(nparts * 10 * Cc, x.device)
+    ws = WS.get((nparts + 1) * 10 * Cc, x.device)
     N.call("lasr_conv1_bwd", ptr(x), B, T, F, Cc, ptr(dy1), dt(dy1), ptr(dw), ptr(db), ptr(ws),
            ws.numel(), stream())
 
@@ -285,6 +285,7 @@ def glu_dwconv_fwd(z1, B, T, Cc, K, w, bias, y, stats):
 
 def bn_finalize(stats, nparts, Cc, eps, momentum, gamma, beta, rmean, rvar, nbt, mean, rstd,
                 scale, shift, update):
+    """update: 0 batch stats, 1 batch stats + running update (train), 2 eval (running stats)."""
     N.call("lasr_bn_finalize", ptr(stats), nparts, Cc, eps, momentum, ptr(gamma), ptr(beta),
            ptr(rmean), ptr(rvar), ptr(nbt), ptr(mean), ptr(rstd), ptr(scale), ptr(shift),
            int(update), stream())
@@ -306,7 +307,7 @@ def bn_swish_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy):
 
 def glu_dwconv_bwd(z1, dy, B, T, Cc, K, w, dz1, dw, db):
     nparts = dwconv_nparts(B, T)
-    ws = WS.get(nparts * (K + 1) * Cc, z1.device)
+    ws = WS.get((nparts + 1) * (K + 1) * Cc, z1.device)
     N.call("lasr_glu_dwconv_bwd", ptr(z1), dt(z1), ptr(dy), dt(dy), B, T, Cc, K, ptr(w), ptr(dz1),
            ptr(dw), ptr(db), ptr(ws), ws.numel(), stream())
 
@@ -364,3 +365,11 @@ def adam_step(param, param_lp, grad, m, v, ws, nparts, state, max_norm, lr_mode,
            dt(param_lp) if param_lp is not None else 0, ptr(grad), ptr(m), ptr(v), param.numel(),
            ptr(ws), nparts, ptr(state), max_norm, lr_mode, lr, factor, model_dim, warmup, beta1,
            beta2, eps, weight_decay, stream())
+
+
+def set_dropout_counter(ctr):
+    N.call("lasr_set_dropout_counter", ptr(ctr))
+
+
+def counter_add(ctr, v=1):
+    N.call("lasr_counter_add", ptr(ctr), int(v), stream())

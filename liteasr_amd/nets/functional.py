@@ -1,0 +1,609 @@
+"""Fused forward/backward of the U2 hot path on the HIP kernels.
+
+Granularity (one autograd node each, so torch's engine only chains a handful of
+nodes and never casts/sums tensors itself):
+  EmbedFn          Conv2d subsampling + x*sqrt(d) (+dropout)           subsampling.py, positional_encoding.py:68-75
+  ConformerLayerFn one RelativeEncoderLayer (macaron FFN, rel-pos MHSA,  conformer_layer.py:130-147
+                   conv module, FFN, final LN)
+  HeadsFn          encoder after_norm + CTC head (input dropout always   transformer_encoder.py:126, ctc.py:28-30,
+                   on) + the whole Transformer decoder                  transformer_decoder.py:70-93
+  HybridLossFn     label-smoothed KL + CTC, combined                    criterions/hybrid_ctc_attn.py:39-79
+
+Weight gradients never travel through autograd: the backward kernels accumulate them
+(beta = 1) straight into the flat fp32 grad buffer of FlatParams; autograd only
+carries the residual-stream gradient between nodes.  Each node takes one "anchor"
+parameter as an input so that its output requires grad whenever the model does.
+
+Storage: residual streams fp32; GEMM operands / activations in the model's compute
+dtype ``adt`` (bf16, or fp32 for the parity build); attention scores fp32.
+"""
+
+from __future__ import annotations
+
+import math
+from types import SimpleNamespace
+
+import torch
+
+from .. import kernels as K
+from .._native import ACT_NONE, ACT_RELU, ACT_SWISH
+
+F32 = torch.float32
+LN_EPS = 1e-12
+
+
+def _e(shape, dtype, dev):
+    return torch.empty(shape, dtype=dtype, device=dev)
+
+
+def ld_scores(T):
+    return (T + 7) // 8 * 8
+
+
+def _seed(base, k):
+    return (base * 0x100000001B3 + k * 0x9E3779B1 + 1) & 0xFFFFFFFFFFFFFFFF
+
+
+# ===================================================================== helpers ===
+def ln_forward(x, g, b, adt, y2=False, p2=0.0, seed2=0):
+    rows, D = x.shape
+    dev = x.device
+    y = _e((rows, D), adt, dev)
+    mean = _e(rows, F32, dev)
+    rstd = _e(rows, F32, dev)
+    yd = _e((rows, D), adt, dev) if y2 else None
+    K.layernorm_fwd(x, g, b, LN_EPS, y, mean, rstd, yd, p2, seed2)
+    return y, yd, mean, rstd
+
+
+def ffn_forward(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res):
+    M = ln.shape[0]
+    dev, adt = ln.device, ln.dtype
+    z = _e((M, W1.shape[0]), adt, dev)
+    h = _e((M, W1.shape[0]), adt, dev)
+    K.linear(ln, W1, h, bias=b1, act=act, zout=z, drop_p=p_ff, drop_seed=s_ff)
+    out = _e((M, W2.shape[0]), F32, dev)
+    K.linear(h, W2, out, bias=b2, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res)
+    return out, z, h
+
+
+def ffn_backward(gb, ln, z, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
+    """gb: gradient of the FFN output (after the residual-branch dropout/scale)."""
+    M = gb.shape[0]
+    dev, adt = gb.device, gb.dtype
+    K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0)
+    K.colsum(gb, gb2)
+    dz = _e((M, W1.shape[0]), adt, dev)
+    K.gemm(gb, W2, dz, aux=z, aux_act=act, drop_p=p_ff, drop_seed=s_ff)
+    K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0)
+    K.colsum(dz, gb1)
+    dln = _e((M, W1.shape[1]), adt, dev)
+    K.gemm(dz, W1, dln)
+    return dln
+
+
+def _heads(t, B, T, H, dk):
+    """[B*T, H*dk] (row stride arbitrary) -> (B, H, T, dk) view."""
+    return t.view(B, T, H, dk).permute(0, 2, 1, 3) if t.is_contiguous() else \
+        t.unflatten(0, (B, T)).unflatten(2, (H, dk)).permute(0, 2, 1, 3)
+
+
+def _slot(t, B, T, nslot, k, H, dk):
+    """Slot k of a fused [B*T, nslot*H*dk] projection as (B, H, T, dk)."""
+    return t.view(B, T, nslot, H, dk)[:, :, k].permute(0, 2, 1, 3)
+
+
+# ============================================================ rel-pos MHSA ======
+def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res):
+    B, T, H = env.B, env.T, env.H
+    d = ln.shape[1]
+    dk = d // H
+    dev, adt = ln.device, ln.dtype
+    M = B * T
+    scale = dk ** -0.5
+    qkv = _e((M, 3 * d), adt, dev)
+    K.linear(ln, w.Wqkv, qkv, bias=w.bqkv)
+    p = _e((T, d), adt, dev)
+    K.linear(pos, w.Wpos, p)
+    qu = _e((M, d), adt, dev)
+    qv = _e((M, d), adt, dev)
+    K.qbias_fwd(qkv, B, T, H, dk, w.u, w.v, qu, qv)
+    ldS = ld_scores(T)
+    Sac = _e((B, H, T, ldS), F32, dev)
+    Sbd = _e((B, H, T, ldS), F32, dev)
+    k4 = _slot(qkv, B, T, 3, 1, H, dk)
+    v4 = _slot(qkv, B, T, 3, 2, H, dk)
+    p4 = p.view(T, H, dk).permute(1, 0, 2).unsqueeze(0).expand(B, H, T, dk)
+    K.gemm(_heads(qu, B, T, H, dk), k4.transpose(-1, -2), Sac[..., :T], alpha=scale)
+    K.gemm(_heads(qv, B, T, H, dk), p4.transpose(-1, -2), Sbd[..., :T], alpha=scale)
+    P = _e((B, H, T, ldS), adt, dev)
+    Praw = _e((B, H, T, ldS), adt, dev) if p_att > 0 else None
+    K.attn_softmax_fwd(Sac, Sbd, B, H, T, T, ldS, env.mask, env.msb, env.msq, P, p_att, s_att, Praw)
+    ctx = _e((M, d), adt, dev)
+    K.gemm(P[..., :T], v4, _heads(ctx, B, T, H, dk))
+    out = _e((M, d), F32, dev)
+    K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+    saved = SimpleNamespace(qkv=qkv, p=p, qu=qu, qv=qv, P=P, Praw=Praw, ctx=ctx)
+    return out, saved
+
+
+def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
+    B, T, H = env.B, env.T, env.H
+    d = ln.shape[1]
+    dk = d // H
+    dev, adt = ln.device, ln.dtype
+    M = B * T
+    scale = dk ** -0.5
+    ldS = ld_scores(T)
+    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0)
+    K.colsum(gb, g.bo)
+    dctx = _e((M, d), adt, dev)
+    K.gemm(gb, w.Wo, dctx)
+    dctx4 = _heads(dctx, B, T, H, dk)
+    v4 = _slot(sv.qkv, B, T, 3, 2, H, dk)
+    k4 = _slot(sv.qkv, B, T, 3, 1, H, dk)
+    dPd = _e((B, H, T, ldS), F32, dev)
+    K.gemm(dctx4, v4.transpose(-1, -2), dPd[..., :T])
+    dqkv = _e((M, 3 * d), adt, dev)
+    K.gemm(sv.P[..., :T].transpose(-1, -2), dctx4, _slot(dqkv, B, T, 3, 2, H, dk))
+    dS = _e((B, H, T, ldS), adt, dev)
+    K.attn_softmax_bwd(sv.Praw if sv.Praw is not None else sv.P, dPd, B, H, T, T, ldS, env.mask,
+                       env.msb, env.msq, dS, p_att, s_att)
+    dBD = _e((B, H, T, ldS), adt, dev)
+    K.relshift_bwd(dS.view(B * H, T, ldS), B * H, T, ldS, dBD)
+    dqu = _e((M, d), adt, dev)
+    K.gemm(dS[..., :T], k4, _heads(dqu, B, T, H, dk), alpha=scale)
+    K.gemm(dS[..., :T].transpose(-1, -2), _heads(sv.qu, B, T, H, dk), _slot(dqkv, B, T, 3, 1, H, dk),
+           alpha=scale)
+    p4 = sv.p.view(T, H, dk).permute(1, 0, 2).unsqueeze(0).expand(B, H, T, dk)
+    dqv = _e((M, d), adt, dev)
+    K.gemm(dBD[..., :T], p4, _heads(dqv, B, T, H, dk), alpha=scale)
+    dpb = _e((B, H, T, dk), F32, dev)
+    K.gemm(dBD[..., :T].transpose(-1, -2), _heads(sv.qv, B, T, H, dk), dpb, alpha=scale)
+    dp = _e((T, d), adt, dev)
+    K.reduce_batch(dpb, B, H, T, dk, dp)
+    K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
+    K.gemm(dp.t(), pos, g.Wpos, beta=1.0)
+    K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0)
+    K.colsum(dqkv, g.bqkv)
+    dln = _e((M, d), adt, dev)
+    K.gemm(dqkv, w.Wqkv, dln)
+    return dln
+
+
+# ============================================================ plain MHA =========
+def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_res, s_res):
+    """Decoder self (mem None) / source attention (liteasr/nets/attention.py:61-71)."""
+    d = ln.shape[1]
+    dk = d // H
+    dev, adt = ln.device, ln.dtype
+    R = B * Tq
+    scale = dk ** -0.5
+    if mem is None:
+        qkv = _e((R, 3 * d), adt, dev)
+        K.linear(ln, w.Wqkv, qkv, bias=w.bqkv)
+        q4 = _slot(qkv, B, Tq, 3, 0, H, dk)
+        k4 = _slot(qkv, B, Tk, 3, 1, H, dk)
+        v4 = _slot(qkv, B, Tk, 3, 2, H, dk)
+        q = kv = None
+    else:
+        q = _e((R, d), adt, dev)
+        K.linear(ln, w.Wq, q, bias=w.bq)
+        kv = _e((B * Tk, 2 * d), adt, dev)
+        K.linear(mem, w.Wkv, kv, bias=w.bkv)
+        q4 = _heads(q, B, Tq, H, dk)
+        k4 = _slot(kv, B, Tk, 2, 0, H, dk)
+        v4 = _slot(kv, B, Tk, 2, 1, H, dk)
+        qkv = None
+    ldS = ld_scores(Tk)
+    S = _e((B, H, Tq, ldS), F32, dev)
+    K.gemm(q4, k4.transpose(-1, -2), S[..., :Tk], alpha=scale)
+    P = _e((B, H, Tq, ldS), adt, dev)
+    Praw = _e((B, H, Tq, ldS), adt, dev) if p_att > 0 else None
+    K.attn_softmax_fwd(S, None, B, H, Tq, Tk, ldS, mask, msb, msq, P, p_att, s_att, Praw)
+    ctx = _e((R, d), adt, dev)
+    K.gemm(P[..., :Tk], v4, _heads(ctx, B, Tq, H, dk))
+    out = _e((R, d), F32, dev)
+    K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+    return out, SimpleNamespace(qkv=qkv, q=q, kv=kv, P=P, Praw=Praw, ctx=ctx)
+
+
+def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_att, dmem):
+    d = ln.shape[1]
+    dk = d // H
+    dev, adt = ln.device, ln.dtype
+    R = B * Tq
+    scale = dk ** -0.5
+    ldS = ld_scores(Tk)
+    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0)
+    K.colsum(gb, g.bo)
+    dctx = _e((R, d), adt, dev)
+    K.gemm(gb, w.Wo, dctx)
+    dctx4 = _heads(dctx, B, Tq, H, dk)
+    if mem is None:
+        q4 = _slot(sv.qkv, B, Tq, 3, 0, H, dk)
+        k4 = _slot(sv.qkv, B, Tk, 3, 1, H, dk)
+        v4 = _slot(sv.qkv, B, Tk, 3, 2, H, dk)
+        dqkv = _e((R, 3 * d), adt, dev)
+        dq4, dk4, dv4 = (_slot(dqkv, B, Tq, 3, i, H, dk) for i in range(3))
+    else:
+        q4 = _heads(sv.q, B, Tq, H, dk)
+        k4 = _slot(sv.kv, B, Tk, 2, 0, H, dk)
+        v4 = _slot(sv.kv, B, Tk, 2, 1, H, dk)
+        dq = _e((R, d), adt, dev)
+        dkv = _e((B * Tk, 2 * d), adt, dev)
+        dq4 = _heads(dq, B, Tq, H, dk)
+        dk4 = _slot(dkv, B, Tk, 2, 0, H, dk)
+        dv4 = _slot(dkv, B, Tk, 2, 1, H, dk)
+    dPd = _e((B, H, Tq, ldS), F32, dev)
+    K.gemm(dctx4, v4.transpose(-1, -2), dPd[..., :Tk])
+    K.gemm(sv.P[..., :Tk].transpose(-1, -2), dctx4, dv4)
+    dS = _e((B, H, Tq, ldS), adt, dev)
+    K.attn_softmax_bwd(sv.Praw if sv.Praw is not None else sv.P, dPd, B, H, Tq, Tk, ldS, mask, msb,
+                       msq, dS, p_att, s_att)
+    K.gemm(dS[..., :Tk], k4, dq4, alpha=scale)
+    K.gemm(dS[..., :Tk].transpose(-1, -2), q4, dk4, alpha=scale)
+    dln = _e((R, d), adt, dev)
+    if mem is None:
+        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0)
+        K.colsum(dqkv, g.bqkv)
+        K.gemm(dqkv, w.Wqkv, dln)
+    else:
+        K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0)
+        K.colsum(dq, g.bq)
+        K.gemm(dq, w.Wq, dln)
+        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0)
+        K.colsum(dkv, g.bkv)
+        K.gemm(dkv, w.Wkv, dmem, beta=1.0)
+    return dln
+
+
+# ========================================================= conformer conv =======
+def conv_forward(ln, w, env, x_in, p_res, s_res, training):
+    B, T = env.B, env.T
+    M, d = ln.shape
+    dev, adt = ln.device, ln.dtype
+    z1 = _e((M, 2 * d), adt, dev)
+    K.linear(ln, w.Wpw1, z1, bias=w.bpw1)
+    y = _e((M, d), adt, dev)
+    nparts = K.dwconv_nparts(B, T)
+    stats = _e(nparts * 3 * d, F32, dev)
+    K.glu_dwconv_fwd(z1, B, T, d, w.kernel, w.wdw, w.bdw, y, stats)
+    mean, rstd, scale, shift = (_e(d, F32, dev) for _ in range(4))
+    K.bn_finalize(stats, nparts, d, 1e-5, 0.1, w.gamma, w.beta, w.rmean, w.rvar, w.nbt, mean, rstd,
+                  scale, shift, 1 if training else 2)
+    h3 = _e((M, d), adt, dev)
+    K.bn_swish_fwd(y, scale, shift, h3)
+    out = _e((M, d), F32, dev)
+    K.linear(h3, w.Wpw2, out, bias=w.bpw2, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+    return out, SimpleNamespace(z1=z1, y=y, mean=mean, rstd=rstd, scale=scale, shift=shift, h3=h3)
+
+
+def conv_backward(gb, ln, sv, w, g, env):
+    B, T = env.B, env.T
+    M, d = ln.shape
+    dev, adt = ln.device, ln.dtype
+    K.gemm(gb.t(), sv.h3, g.Wpw2, beta=1.0, split_k=0)
+    K.colsum(gb, g.bpw2)
+    dh3 = _e((M, d), adt, dev)
+    K.gemm(gb, w.Wpw2, dh3)
+    dy = _e((M, d), F32, dev)
+    K.bn_swish_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy)
+    dz1 = _e((M, 2 * d), adt, dev)
+    K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
+    K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0)
+    K.colsum(dz1, g.bpw1)
+    dln = _e((M, d), adt, dev)
+    K.gemm(dz1, w.Wpw1, dln)
+    return dln
+
+
+# ============================================================ autograd nodes ====
+class EmbedFn(torch.autograd.Function):
+    """Conv2DLayer (liteasr/nets/subsampling.py:42-48) + RelativePositionalEncoding's
+    x*sqrt(d) and dropout (positional_encoding.py:68-75).  Channels-last throughout;
+    the c-major flatten of the reference is folded into a column permutation of
+    embed.out.weight (repacked working copy)."""
+
+    @staticmethod
+    def forward(ctx, xs, anchor, mod, env):
+        B, Tx, Fd = xs.shape
+        w = mod.weights()
+        C = w.C
+        adt, dev = env.adt, xs.device
+        T1, F1 = (Tx - 3) // 2 + 1, (Fd - 3) // 2 + 1
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        xs = xs.contiguous()
+        y1 = _e((B, T1, F1, C), adt, dev)
+        K.conv1_fwd(xs, w.W1, w.b1, y1)
+        col = _e((B * T2 * F2, 9 * C), adt, dev)
+        K.im2col(y1, col)
+        y2 = _e((B * T2 * F2, C), adt, dev)
+        K.linear(col, w.W2p, y2, bias=w.b2, act=ACT_RELU)
+        xl = _e((B * T2, w.d), F32, dev)
+        y2f = y2.view(B * T2, F2 * C)
+        K.linear(y2f, w.Woutp, xl, bias=w.bout)
+        x0 = _e((B * T2, w.d), F32, dev)
+        K.pe_fwd(xl, B * T2, T2, w.d, None, math.sqrt(w.d), x0, env.p_pos, env.seed + 1)
+        ctx.sv = SimpleNamespace(xs=xs, y1=y1, col=col, y2=y2, dims=(B, T1, F1, T2, F2, C))
+        ctx.mod, ctx.env = mod, env
+        return x0
+
+    @staticmethod
+    def backward(ctx, dx0):
+        sv, mod, env = ctx.sv, ctx.mod, ctx.env
+        B, T1, F1, T2, F2, C = sv.dims
+        w, g = mod.weights(), mod.grads()
+        adt, dev = env.adt, dx0.device
+        d = w.d
+        M = B * T2
+        gb = _e((M, d), adt, dev)
+        K.branch_grad(dx0.contiguous(), gb, math.sqrt(d), env.p_pos, env.seed + 1)
+        y2f = sv.y2.view(M, F2 * C)
+        dWo = _e((d, F2 * C), F32, dev)
+        K.gemm(gb.t(), y2f, dWo, split_k=0)
+        K.permute_last2(dWo, d, C, F2, g.out_w, reverse=True, accumulate=True)
+        K.colsum(gb, g.bout)
+        dy2 = _e((M, F2 * C), adt, dev)
+        K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
+        dy2 = dy2.view(M * F2, C)
+        dW2 = _e((C, 9 * C), F32, dev)
+        K.gemm(dy2.t(), sv.col, dW2, split_k=0)
+        K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
+        K.colsum(dy2, g.b2)
+        dcol = _e((M * F2, 9 * C), adt, dev)
+        K.gemm(dy2, w.W2p, dcol)
+        dy1 = torch.empty_like(sv.y1)
+        K.col2im(dcol, sv.y1, dy1)
+        K.conv1_bwd(sv.xs, dy1, g.W1, g.b1)
+        mod.on_grads_ready()
+        return None, None, None, None
+
+
+class ConformerLayerFn(torch.autograd.Function):
+    """RelativeEncoderLayer.forward (liteasr/nets/conformer_layer.py:130-147), pre-norm."""
+
+    @staticmethod
+    def forward(ctx, x0, pos, anchor, layer, env):
+        w = layer.weights()
+        s = layer.seed
+        tr = env.training
+        pd = env.p_drop if tr else 0.0
+        pff = env.p_ff if tr else 0.0
+        pat = env.p_att if tr else 0.0
+        adt = env.adt
+        x0 = x0.contiguous()
+        # (a) macaron FFN, scale 0.5
+        ln_a, _, ma, ra = ln_forward(x0, w.ln_a.g, w.ln_a.b, adt)
+        x1, za, ha = ffn_forward(ln_a, w.ffm.W1, w.ffm.b1, w.ffm.W2, w.ffm.b2, ACT_SWISH, pff,
+                                 _seed(s, 1), x0, 0.5, pd, _seed(s, 2))
+        # (b) relative-position MHSA
+        ln_b, _, mb, rb = ln_forward(x1, w.ln_b.g, w.ln_b.b, adt)
+        x2, svb = relmha_forward(ln_b, pos, w.att, env, x1, pat, _seed(s, 3), pd, _seed(s, 4))
+        # (c) convolution module
+        ln_c, _, mc, rc = ln_forward(x2, w.ln_c.g, w.ln_c.b, adt)
+        x3, svc = conv_forward(ln_c, w.conv, env, x2, pd, _seed(s, 5), tr)
+        # (d) FFN, scale 0.5
+        ln_d, _, md, rd = ln_forward(x3, w.ln_d.g, w.ln_d.b, adt)
+        x4, zd, hd = ffn_forward(ln_d, w.ff.W1, w.ff.b1, w.ff.W2, w.ff.b2, ACT_SWISH, pff,
+                                 _seed(s, 6), x3, 0.5, pd, _seed(s, 7))
+        # final LN -> next layer's residual stream (fp32)
+        x5 = _e(x4.shape, F32, x4.device)
+        mf = _e(x4.shape[0], F32, x4.device)
+        rf = _e(x4.shape[0], F32, x4.device)
+        K.layernorm_fwd(x4, w.ln_f.g, w.ln_f.b, LN_EPS, x5, mf, rf)
+        if torch.is_grad_enabled() or anchor.requires_grad:
+            ctx.sv = SimpleNamespace(x=(x0, x1, x2, x3, x4), ln=(ln_a, ln_b, ln_c, ln_d),
+                                     st=((ma, ra), (mb, rb), (mc, rc), (md, rd), (mf, rf)),
+                                     za=za, ha=ha, zd=zd, hd=hd, svb=svb, svc=svc, pos=pos,
+                                     p=(pd, pff, pat))
+        ctx.layer, ctx.env = layer, env
+        return x5
+
+    @staticmethod
+    def backward(ctx, dx5):
+        sv, layer, env = ctx.sv, ctx.layer, ctx.env
+        w, g = layer.weights(), layer.grads()
+        s = layer.seed
+        pd, pff, pat = sv.p
+        x0, x1, x2, x3, x4 = sv.x
+        ln_a, ln_b, ln_c, ln_d = sv.ln
+        (ma, ra), (mb, rb), (mc, rc), (md, rd), (mf, rf) = sv.st
+        dev, adt = dx5.device, env.adt
+        M, d = x4.shape
+        dx5 = dx5.contiguous()
+        # final LN; emits the (d)-branch gradient 0.5*drop(dx4)
+        dx4 = _e((M, d), F32, dev)
+        gb = _e((M, d), adt, dev)
+        K.layernorm_bwd(x4, dx5, w.ln_f.g, mf, rf, dx4, g.ln_f.g, g.ln_f.b, gb=gb, bscale=0.5,
+                        bp=pd, bseed=_seed(s, 7))
+        dln = ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2,
+                           g.ff.b2, ACT_SWISH, pff, _seed(s, 6))
+        dx3 = _e((M, d), F32, dev)
+        K.layernorm_bwd(x3, dln, w.ln_d.g, md, rd, dx3, g.ln_d.g, g.ln_d.b, dres=dx4, gb=gb,
+                        bscale=1.0, bp=pd, bseed=_seed(s, 5))
+        dln = conv_backward(gb, ln_c, sv.svc, w.conv, g.conv, env)
+        dx2 = _e((M, d), F32, dev)
+        K.layernorm_bwd(x2, dln, w.ln_c.g, mc, rc, dx2, g.ln_c.g, g.ln_c.b, dres=dx3, gb=gb,
+                        bscale=1.0, bp=pd, bseed=_seed(s, 4))
+        dln = relmha_backward(gb, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3))
+        dx1 = _e((M, d), F32, dev)
+        K.layernorm_bwd(x1, dln, w.ln_b.g, mb, rb, dx1, g.ln_b.g, g.ln_b.b, dres=dx2, gb=gb,
+                        bscale=0.5, bp=pd, bseed=_seed(s, 2))
+        dln = ffn_backward(gb, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1,
+                           g.ffm.W2, g.ffm.b2, ACT_SWISH, pff, _seed(s, 1))
+        dx0 = _e((M, d), F32, dev)
+        K.layernorm_bwd(x0, dln, w.ln_a.g, ma, ra, dx0, g.ln_a.g, g.ln_a.b, dres=dx1)
+        ctx.sv = None
+        layer.on_grads_ready()
+        return dx0, None, None, None, None
+
+
+class HeadsFn(torch.autograd.Function):
+    """Encoder after_norm (transformer_encoder.py:126), CTC head with its always-on
+    input dropout (ctc.py:28-30) and the full Transformer decoder
+    (transformer_decoder.py:70-93, transformer_layer.py:179-221)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, model, env):
+        dev, adt = x.device, env.adt
+        enc, dec = model.encoder, model.decoder
+        B, T, L1 = env.B, env.T, env.L1
+        M, R = B * T, B * L1
+        tr = env.training
+        x = x.contiguous()
+        we = enc.after_norm_weights()
+        h, hd, me, re = ln_forward(x, we.g, we.b, adt, y2=True, p2=env.p_ctc, seed2=env.seed + 2)
+        wc = model.ctc.weights()
+        V = wc.W.shape[0]
+        h_ctc = _e((M, V), adt, dev)
+        K.linear(hd, wc.W, h_ctc, bias=wc.b)
+        # ---- decoder
+        wd = dec.weights()
+        d = wd.d
+        pd = env.p_dec if tr else 0.0
+        pff = env.p_dec_ff if tr else 0.0
+        pat = env.p_dec_att if tr else 0.0
+        pca = env.p_dec_src_att if tr else 0.0
+        y = _e((R, d), F32, dev)
+        K.embed_pe_fwd(env.ys_in, L1, wd.E, wd.pe, math.sqrt(d), y, env.p_dec_pos if tr else 0.0,
+                       env.seed + 3)
+        layers_sv = []
+        for i, lw in enumerate(wd.layers):
+            s = dec.dec_layers[i].seed
+            l1, _, m1, r1 = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
+            y1, sa = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, env.dec_mask, L1 * L1, L1, y,
+                                 pat, _seed(s, 1), pd, _seed(s, 2))
+            l2, _, m2, r2 = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
+            y2, ca = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, env.mask_k, T, 0, y1, pca,
+                                 _seed(s, 3), pd, _seed(s, 4))
+            l3, _, m3, r3 = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)
+            y3, z, hh = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, pff,
+                                    _seed(s, 5), y2, 1.0, pd, _seed(s, 6))
+            layers_sv.append(SimpleNamespace(y=(y, y1, y2), ln=(l1, l2, l3),
+                                             st=((m1, r1), (m2, r2), (m3, r3)), sa=sa, ca=ca, z=z,
+                                             hh=hh))
+            y = y3
+        yf, _, mf, rf = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
+        h_attn = _e((R, V), adt, dev)
+        K.linear(yf, wd.Wout, h_attn, bias=wd.bout)
+        ctx.sv = SimpleNamespace(x=x, h=h, hd=hd, me=me, re=re, layers=layers_sv, yL=y, yf=yf,
+                                 mf=mf, rf=rf, p=(pd, pff, pat, pca))
+        ctx.model, ctx.env = model, env
+        return h_attn, h_ctc
+
+    @staticmethod
+    def backward(ctx, g_attn, g_ctc):
+        sv, model, env = ctx.sv, ctx.model, ctx.env
+        enc, dec = model.encoder, model.decoder
+        dev, adt = sv.x.device, env.adt
+        B, T, L1 = env.B, env.T, env.L1
+        M, R = B * T, B * L1
+        pd, pff, pat, pca = sv.p
+        d_enc = sv.x.shape[1]
+        dh = _e((M, d_enc), F32, dev)  # accumulated gradient of h_enc
+        # ---- CTC head
+        wc, gc = model.ctc.weights(), model.ctc.grads()
+        if g_ctc is not None:
+            g_ctc = g_ctc.contiguous().view(M, -1)
+            K.gemm(g_ctc.t(), sv.hd, gc.W, beta=1.0, split_k=0)
+            K.colsum(g_ctc, gc.b)
+            dhd = _e((M, d_enc), F32, dev)
+            K.gemm(g_ctc, wc.W, dhd)
+            K.branch_grad(dhd, dh, 1.0, env.p_ctc, env.seed + 2)
+        else:
+            K.fill(dh, 0.0)
+        model.ctc.on_grads_ready()
+        # ---- decoder
+        wd, gd = dec.weights(), dec.grads()
+        d = wd.d
+        if g_attn is not None:
+            g_attn = g_attn.contiguous().view(R, -1)
+            K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0)
+            K.colsum(g_attn, gd.bout)
+            dyf = _e((R, d), adt, dev)
+            K.gemm(g_attn, wd.Wout, dyf)
+            dy = _e((R, d), F32, dev)
+            K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
+            gb = _e((R, d), adt, dev)
+            for i in range(len(wd.layers) - 1, -1, -1):
+                lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
+                s = dec.dec_layers[i].seed
+                y0, y1, y2 = ls.y
+                l1, l2, l3 = ls.ln
+                (m1, r1), (m2, r2), (m3, r3) = ls.st
+                K.branch_grad(dy, gb, 1.0, pd, _seed(s, 6))
+                dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1,
+                                   lg.ff.W2, lg.ff.b2, ACT_RELU, pff, _seed(s, 5))
+                dy2 = _e((R, d), F32, dev)
+                K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb,
+                                bscale=1.0, bp=pd, bseed=_seed(s, 4))
+                dln = mha_backward(gb, l2, sv.h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, env.mask_k, T,
+                                   0, pca, _seed(s, 3), dh)
+                dy1 = _e((R, d), F32, dev)
+                K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb,
+                                bscale=1.0, bp=pd, bseed=_seed(s, 2))
+                dln = mha_backward(gb, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, env.dec_mask,
+                                   L1 * L1, L1, pat, _seed(s, 1), None)
+                dy0 = _e((R, d), F32, dev)
+                K.layernorm_bwd(y0, dln, lw.ln1.g, m1, r1, dy0, lg.ln1.g, lg.ln1.b, dres=dy1)
+                dy = dy0
+            K.embed_bwd(env.ys_in, dy, math.sqrt(d), gd.E, env.p_dec_pos if env.training else 0.0,
+                        env.seed + 3)
+        dec.on_grads_ready()
+        # ---- encoder after_norm
+        we, ge = enc.after_norm_weights(), enc.after_norm_grads()
+        dx = _e((M, d_enc), F32, dev)
+        K.layernorm_bwd(sv.x, dh, we.g, sv.me, sv.re, dx, ge.g, ge.b)
+        enc.after_norm_ready()
+        ctx.sv = None
+        return dx, None, None, None
+
+
+class HybridLossFn(torch.autograd.Function):
+    """HybridCTCLoss.__call__ (liteasr/criterions/hybrid_ctc_attn.py:39-79):
+    ctc_weight * CTC(sum)/B + (1 - ctc_weight) * smoothed-KL(sum)/B.
+    Forward computes losses only; backward computes both logits gradients scaled by the
+    incoming (device) gradient without a host round trip."""
+
+    @staticmethod
+    def forward(ctx, h_attn, h_ctc, prep, ctc_weight, smoothing, ignore):
+        dev = h_attn.device
+        B, L1 = prep.ys_in.shape
+        V = h_attn.shape[-1]
+        Tp = h_ctc.shape[1]
+        ha = h_attn.reshape(B * L1, V)
+        hc = h_ctc.reshape(B, Tp, V)
+        L = prep.tgt_ctc.shape[1]
+        lse_a = _e(B * L1, F32, dev)
+        rows = _e(B * L1, F32, dev)
+        K.lsm_kl_fwd(ha, prep.tgt, ignore, smoothing, lse_a, rows)
+        S = 2 * L + 1
+        lse = _e(B * Tp, F32, dev)
+        lp = _e(B * Tp * (L + 1), F32, dev)
+        alpha = _e(B * Tp * S, F32, dev)
+        nll = _e(B, F32, dev)
+        K.ctc_fwd(hc, prep.tgt_ctc, prep.pred_len, prep.ylen, lse, lp, alpha, nll)
+        loss = _e(1, F32, dev)
+        K.loss_combine(nll, ctc_weight / B, rows, (1.0 - ctc_weight) / B, loss)
+        ctx.sv = SimpleNamespace(ha=ha, hc=hc, prep=prep, lse_a=lse_a, lse=lse, lp=lp, alpha=alpha,
+                                 nll=nll, w=ctc_weight, s=smoothing, ign=ignore, B=B,
+                                 shapes=(h_attn.shape, h_ctc.shape))
+        ctx.parts = (nll, rows)
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        sv = ctx.sv
+        g = g.contiguous().float()
+        dev = g.device
+        B = sv.B
+        ga = torch.empty_like(sv.ha)
+        K.lsm_kl_bwd(sv.ha, sv.prep.tgt, sv.ign, sv.s, sv.lse_a, ga, (1.0 - sv.w) / B, gdev=g)
+        gc = torch.empty_like(sv.hc)
+        L = sv.prep.tgt_ctc.shape[1]
+        beta = _e(sv.alpha.numel(), F32, dev)
+        K.ctc_bwd(sv.hc, sv.prep.tgt_ctc, sv.prep.pred_len, sv.prep.ylen, sv.lse, sv.lp, sv.alpha,
+                  sv.nll, beta, gc, sv.w / B, gdev=g)
+        ctx.sv = None
+        return ga.view(sv.shapes[0]), gc.view(sv.shapes[1]), None, None, None, None

@@ -1,0 +1,196 @@
+"""Generate golden vectors by running the *reference* (/root/reference, imported through
+refshim) in the build container.  Outputs small .npz fixtures next to this script;
+those fixtures (data only) are what the tests and the GPU box use.
+
+    python tests/golden/make_golden.py
+
+Fixtures
+  relshift.npz    rel_shift (attention.py:99-118) on random score matrices, T = 1..9
+  lengths.npz     get_pred_len (u2.py:319-321) and the subsampled-mask length
+                  (transformer_encoder.py:117-120) for xlen = 1..1100
+  ctc.npz         HybridCTCLoss with ctc_weight=1 (pure CTC, reduction sum / B) on fixed
+                  logits: loss + d loss / d logits; repeated labels, L_b = 0, infeasible
+  kl.npz          HybridCTCLoss with ctc_weight=0 (label-smoothed KL), loss + grad
+  u2_step.npz     tiny U2 (d 32, 2 enc / 1 dec, V 20, F 40): seed-42 init state_dict, a
+                  batch, h_attn / h_ctc / loss / grads, params after clip(5) + Noam step,
+                  BN running stats; plus a chunk-mask (stage 4) forward for config 4
+"""
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import refshim  # noqa: E402
+
+refshim.install()
+
+from liteasr.criterions.hybrid_ctc_attn import HybridCTCLoss  # noqa: E402
+from liteasr.models.u2 import U2, DecoderArch, EncoderArch  # noqa: E402
+from liteasr.nets.attention import RelativeMultiHeadAttention  # noqa: E402
+from liteasr.utils.mask import padding_mask, triangle_mask  # noqa: E402
+
+
+def save(name, **arrs):
+    out = {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in arrs.items()}
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print("wrote", name, sum(a.nbytes for a in out.values()), "bytes")
+
+
+def gen_relshift():
+    g = torch.Generator().manual_seed(0)
+    mha = RelativeMultiHeadAttention(1, 4, 0.0)
+    arrs = {}
+    for T in range(1, 10):
+        x = torch.randn(2, 3, T, T, generator=g)
+        arrs[f"in_{T}"] = x
+        arrs[f"out_{T}"] = mha.rel_shift(x)
+    save("relshift.npz", **arrs)
+
+
+def gen_lengths():
+    xl = torch.arange(1, 1101)
+    m = U2.__new__(U2)
+    pl = U2.get_pred_len(m, xl)
+    sub = []
+    for x in xl.tolist():
+        T = max(x, 3)
+        mask = padding_mask(torch.tensor([x, T]))[:1]  # width max(x, T)
+        mm = mask[:, :-2:2][:, :-2:2]
+        sub.append(int((~mm).sum()))
+    tri = triangle_mask(8, stage=2).to(torch.uint8)
+    tri2 = triangle_mask(3, 5, diagonal=2).to(torch.uint8)
+    save("lengths.npz", xlen=xl, pred_len=pl, sub_valid=np.array(sub), tri_8_s2=tri, tri_3_5_d2=tri2)
+
+
+class _FakeModel:
+    """Feeds fixed logits into the reference criterion (it only calls these)."""
+
+    def __init__(self, h_attn, h_ctc, V):
+        self.h_attn, self.h_ctc = h_attn, h_ctc
+        self.ignore, self.eos = -1, V - 1
+
+    def __call__(self, xs, xlens, ys, ylens):
+        return self.h_attn, self.h_ctc
+
+    def get_pred_len(self, xlens):
+        return U2.get_pred_len(self, xlens)
+
+    def get_target(self, ys, ylens):
+        return U2.get_target(self, ys, ylens)
+
+
+def _crit(V, w, s=0.1):
+    return HybridCTCLoss(types.SimpleNamespace(vocab_size=V, padding_idx=-1, smoothing=s,
+                                               normalize_length=False, ctc_weight=w))
+
+
+def gen_ctc_kl():
+    g = torch.Generator().manual_seed(1)
+    B, Tx, V, L = 4, 210, 30, 12
+    T = ((Tx - 1) // 2 - 1) // 2  # 51
+    xlens = torch.tensor([210, 190, 150, 40])
+    ylens = torch.tensor([12, 7, 0, 11])  # utt 3: 40 frames -> 8 CTC frames < needed: infeasible
+    ys = torch.randint(1, V - 1, (B, L), generator=g)
+    ys[0, 3] = ys[0, 2]  # repeated label
+    ys[0, 4] = ys[0, 2]
+    ys = ys.masked_fill(padding_mask(ylens) if ylens.max() == L else torch.zeros(B, L, dtype=torch.bool), -1)
+    for b in range(B):
+        ys[b, ylens[b]:] = -1
+    h_ctc = (torch.randn(B, T, V, generator=g) * 2).requires_grad_()
+    h_attn = torch.zeros(B, L + 1, V)
+    loss = _crit(V, 1.0)(_FakeModel(h_attn, h_ctc, V), None, xlens, ys, ylens)
+    fin = torch.isfinite(loss)
+    save("ctc.npz", xlens=xlens, ys=ys, ylens=ylens, h_ctc=h_ctc.detach(), loss=loss.detach(),
+         finite=fin)
+    # finite subset for gradients
+    keep = torch.tensor([0, 1, 2])
+    h2 = h_ctc.detach()[keep].clone().requires_grad_()
+    l2 = _crit(V, 1.0)(_FakeModel(h_attn[keep], h2, V), None, xlens[keep], ys[keep], ylens[keep])
+    l2.backward()
+    save("ctc_grad.npz", xlens=xlens[keep], ys=ys[keep], ylens=ylens[keep], h_ctc=h2.detach(),
+         loss=l2.detach(), grad=h2.grad)
+    # label-smoothed KL (ctc_weight = 0)
+    h_attn = (torch.randn(B, L + 1, V, generator=g) * 3).requires_grad_()
+    h_ctc0 = torch.zeros(B, T, V)
+    l3 = _crit(V, 0.0)(_FakeModel(h_attn, h_ctc0, V), None, xlens.clone().fill_(210), ys, ylens)
+    l3.backward()
+    save("kl.npz", ys=ys, ylens=ylens, h_attn=h_attn.detach(), loss=l3.detach(), grad=h_attn.grad)
+
+
+def tiny_cfg(**kw):
+    c = dict(enc_arch=EncoderArch.Conformer, use_rel=True, input_dim=40, enc_dim=32, enc_ff_dim=64,
+             enc_attn_heads=4, enc_layers=2, activation="swish", dec_arch=DecoderArch.Transformer,
+             vocab_size=20, dec_dim=32, dec_ff_dim=64, dec_attn_heads=4, dec_layers=1, dropout_rate=0.0,
+             enc_dropout_rate=0.0, enc_pos_dropout_rate=0.0, enc_attn_dropout_rate=0.0,
+             enc_ff_dropout_rate=0.0, dec_dropout_rate=0.0, dec_pos_dropout_rate=0.0,
+             dec_self_attn_dropout_rate=0.0, dec_src_attn_dropout_rate=0.0, dec_ff_dropout_rate=0.0)
+    c.update(kw)
+    return types.SimpleNamespace(**c)
+
+
+def gen_u2_step():
+    torch.manual_seed(42)
+    model = U2(tiny_cfg())
+    model.train()
+    init = {k: v.clone() for k, v in model.state_dict().items() if not k.endswith(".pe.pe")}
+    g = torch.Generator().manual_seed(3)
+    B, Tx, L, V = 3, 120, 6, 20
+    xlens = torch.tensor([120, 113, 97])
+    xs = torch.randn(B, Tx, 40, generator=g).masked_fill(padding_mask(xlens).unsqueeze(-1), 0.0)
+    ylens = torch.tensor([6, 4, 2])
+    ys = torch.randint(1, V - 1, (B, L), generator=g).masked_fill(padding_mask(ylens), -1)
+    crit = _crit(V, 0.3)
+    rec = {}
+
+    class _Rec:  # one forward only (BN running stats must be updated exactly once)
+        def __call__(self, *a):
+            rec["out"] = model(*a)
+            return rec["out"]
+
+        def get_pred_len(self, xl):
+            return model.get_pred_len(xl)
+
+        def get_target(self, y, yl):
+            return model.get_target(y, yl)
+
+    loss = crit(_Rec(), xs, xlens, ys, ylens)
+    h_attn, h_ctc = rec["out"]
+    loss.backward()
+    grads = {"grad." + n: p.grad.clone() for n, p in model.named_parameters()}
+    norm = torch.nn.utils.clip_grad_norm_(model.parameters(), 5.0)
+    opt = torch.optim.Adam(model.parameters(), lr=1.0, betas=(0.9, 0.98), eps=1e-9)
+    step, dim, warm = 1, 32, 25000
+    lr = 1.0 * dim ** -0.5 * min(step ** -0.5, step * warm ** -1.5)  # liteasr/optims/noam.py:41-46
+    for grp in opt.param_groups:
+        grp["lr"] = lr
+    opt.step()
+    after = {"new." + k: v.clone() for k, v in model.state_dict().items() if not k.endswith(".pe.pe")}
+    # config-4 composition: chunk mask (stage 4) passed straight to the layers
+    torch.manual_seed(42)
+    m2 = U2(tiny_cfg())
+    m2.train()
+    enc = m2.encoder
+    xmask = padding_mask(xlens)
+    x = enc.pe(enc.embed(xs))
+    km = xmask[:, :-2:2][:, :-2:2]
+    Tp = km.shape[1]
+    cm = km[:, None, None, :] | triangle_mask(Tp, stage=4)[None, None]
+    for layer in enc.enc_layers:
+        x = layer(x, mask=cm)
+    h_chunk = enc.after_norm(x[0])
+    save("u2_step.npz", xs=xs, xlens=xlens, ys=ys, ylens=ylens, h_attn=h_attn.detach(),
+         h_ctc=h_ctc.detach(), loss=loss.detach(), grad_norm=norm, lr=np.array(lr), h_enc_chunk4=h_chunk.detach(),
+         **{"init." + k: v for k, v in init.items()}, **grads, **after)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(4)
+    gen_relshift()
+    gen_lengths()
+    gen_ctc_kl()
+    gen_u2_step()

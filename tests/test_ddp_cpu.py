@@ -1,0 +1,123 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the FlatParams DDP reducer: initial
+broadcast, bucket launch order driven by the backward-node hooks, gradient averaging,
+no_sync(), and BN-buffer re-broadcast.  The HIP kernels are not involved: a stand-in
+autograd node writes rank-dependent gradients into the flat grad buffer and fires the
+same ``on_grads_ready`` hooks, in the same order, as the fused backward nodes."""
+
+import os
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _tiny():
+    from liteasr_amd.models.u2 import U2, U2Config
+    from liteasr_amd.utils.cfg import resolve_self
+
+    c = U2Config(input_dim=40, vocab_size=20, enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_layers=3,
+                 dec_dim=32, dec_ff_dim=64, dec_attn_heads=4, dec_layers=2)
+    resolve_self(c)
+    return U2(c)
+
+
+class _FakeBackward(torch.autograd.Function):
+    """Writes grad = (rank+1) * unit_index into each unit's flat range, firing hooks in
+    the fused backward's order (ctc, decoder, encoder.after_norm, layers N-1..0, embed)."""
+
+    @staticmethod
+    def forward(ctx, x, model, rank):
+        ctx.model, ctx.rank = model, rank
+        return x * 1.0
+
+    @staticmethod
+    def backward(ctx, g):
+        m, r = ctx.model, ctx.rank
+        st = m.store
+        grad = st.ensure_grad()
+        order = [m.ctc, m.decoder, "encoder.after_norm"] + list(reversed(list(m.encoder.enc_layers))) + [m.encoder.embed]
+        for i, mod in enumerate(order):
+            pfx = mod if isinstance(mod, str) else mod._pfx
+            for n in st.names:
+                if n == pfx or n.startswith(pfx + "."):
+                    o, k = st.offsets[n], st.shapes[n].numel()
+                    grad[o:o + k] += (r + 1) * (i + 1)
+            if isinstance(mod, str):
+                m.encoder.after_norm_ready()
+            else:
+                mod.on_grads_ready()
+        return g, None, None
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from liteasr_amd.distributed.ddp import DistributedDataParallel
+
+        torch.manual_seed(100 + rank)  # different init per rank -> broadcast must fix it
+        model = _tiny()
+        bn = model.encoder.enc_layers[0].conv.norm.running_mean
+        bn.fill_(float(rank + 7))
+        ddp = DistributedDataParallel(model, bucket_cap_mb=0.05)
+        res = {"nbuckets": len(ddp.reducer.buckets)}
+        flat0 = model.store.flat.clone()
+        res["bn_after_init"] = float(bn[0])
+        x = torch.ones(3, requires_grad=True)
+        # step 1: synced
+        model.store.ensure_grad().zero_()
+        _FakeBackward.apply(x, model, rank).sum().backward()
+        res["grad_sync"] = model.store.grad.clone()
+        # step 2: no_sync accumulates locally
+        model.store.grad.zero_()
+        with ddp.no_sync():
+            _FakeBackward.apply(x, model, rank).sum().backward()
+        res["grad_nosync"] = model.store.grad.clone()
+        res["flat"] = flat0
+        # forward-time buffer broadcast (BN running stats from rank 0)
+        bn.fill_(float(rank + 20))
+        ddp._sync_buffers()
+        res["bn_after_sync"] = float(bn[0])
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flat_ddp_gloo_world2():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a, b = out[0], out[1]
+    assert a["nbuckets"] > 2  # several buckets -> ordered launches were exercised
+    assert torch.equal(a["flat"], b["flat"])  # rank-0 parameters broadcast
+    assert a["bn_after_init"] == b["bn_after_init"] == 7.0
+    # averaged: ((0+1)*i + (1+1)*i) / 2 = 1.5 * i on every rank
+    assert torch.equal(a["grad_sync"], b["grad_sync"])
+    st = _tiny().store  # same layout on every rank
+    g = a["grad_sync"]
+    nz = g[g != 0]
+    assert len(nz) > 0
+    vals = torch.unique(nz)
+    assert torch.allclose(vals / 1.5, torch.round(vals / 1.5)), vals
+    # no_sync: rank-local values ((r+1) * i)
+    assert torch.equal(b["grad_nosync"], 2 * a["grad_nosync"])
+    assert a["bn_after_sync"] == b["bn_after_sync"] == 20.0
+    del st

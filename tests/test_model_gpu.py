@@ -1,0 +1,225 @@
+"""End-to-end parity: liteasr_amd U2 + HybridCTCLoss (+ fused Noam/Adam) on the GPU vs the
+CPU oracle (oracle/u2_oracle.py, pinned to the reference by test_oracle_golden.py).
+
+Tolerances (stated):
+  fp32 build  loss rel 1e-5; logits / grads / updated params 2e-4 of each tensor's max-abs
+  bf16 build  loss rel 5e-3; logits 5e-2; grads cosine >= 0.995 and 2.5e-1 of max-abs
+              (a few-row dW such as the decoder FFN's sums ~27 bf16 products)
+Bookkeeping (targets, lengths, masks) is bit-exact (checked in test_kernels_gpu.py)."""
+
+import math
+import sys
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import u2_oracle as O  # noqa: E402
+
+
+def build(cfg_o, dtype, chunk=0, dropout=0.0):
+    from liteasr_amd.models.u2 import U2, U2Config
+    from liteasr_amd.utils.cfg import resolve_self
+
+    c = U2Config(input_dim=cfg_o["input_dim"], vocab_size=cfg_o["vocab_size"], enc_dim=cfg_o["enc_dim"],
+                 enc_ff_dim=cfg_o["enc_ff"], enc_attn_heads=cfg_o["enc_heads"], enc_layers=cfg_o["enc_layers"],
+                 dec_dim=cfg_o["dec_dim"], dec_ff_dim=cfg_o["dec_ff"], dec_attn_heads=cfg_o["dec_heads"],
+                 dec_layers=cfg_o["dec_layers"], dropout_rate=dropout, compute_dtype=dtype, chunk_size=chunk)
+    resolve_self(c)
+    return U2(c)
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return (a - b).abs().max().item() / (b.abs().max().item() + 1e-30)
+
+
+def grad_errs(g, go):
+    """Per-tensor error relative to max(|ref|max, 1e-3 * largest grad of the model):
+    some gradients are analytically zero (e.g. linear_k.bias: softmax is invariant to a
+    per-row constant), so their reference is ~1e-18 and a pure relative error is noise."""
+    floor = 1e-3 * max(v.abs().max().item() for v in go.values())
+    out = {}
+    for k in go:
+        a, b = g[k].double().cpu(), go[k].double().cpu()
+        out[k] = (a - b).abs().max().item() / max(b.abs().max().item(), floor)
+    return out, floor
+
+
+def cos(a, b):
+    a, b = a.double().cpu().flatten(), b.double().cpu().flatten()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+def run_case(cfg_o, B, T, L, dtype, chunk=0, ctc_weight=0.3, seed=0):
+    from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+    from liteasr_amd.optims.noam import Noam, NoamConfig
+
+    params = O.init_params(cfg_o, seed=seed + 11)
+    buffers = O.init_buffers(cfg_o)
+    batch = O.synthetic_batch(B, T, L, cfg_o["vocab_size"], seed=seed)
+    # oracle in fp64
+    p64 = {k: v.double() for k, v in params.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in buffers.items()}
+    xs, xlens, ys, ylens = batch
+    with torch.no_grad():
+        ha_o, hc_o, _, _ = O.u2_forward(xs.double(), xlens, ys, ylens, p64, cfg_o, {k: v.clone() for k, v in b64.items()}, True, chunk)
+    loss_o, grads_o, new_o, _, norm_o = O.train_step(p64, b64, (xs.double(), xlens, ys, ylens), cfg_o,
+                                                       ctc_weight=ctc_weight, smoothing=0.1, clip=5.0,
+                                                       model_dim=cfg_o["enc_dim"], chunk=chunk)
+    # liteasr_amd on the GPU
+    model = build(cfg_o, dtype, chunk)
+    missing, unexpected = model.load_state_dict({**params, **buffers}, strict=False)
+    assert not unexpected and all(k.endswith(".pe.pe") for k in missing), (missing, unexpected)
+    model = model.cuda().train()
+    crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=cfg_o["vocab_size"], smoothing=0.1, ctc_weight=ctc_weight))
+    opt = Noam(model.parameters(), NoamConfig(model_dim=cfg_o["enc_dim"]))
+    opt.zero_grad()
+    dev = "cuda"
+    xs_d, xl_d, ys_d, yl_d = xs.to(dev), xlens.to(dev), ys.to(dev), ylens.to(dev)
+    rec = {}
+
+    class _Once(torch.nn.Module):  # one forward: BN running stats update exactly once
+        def forward(self, *a):
+            rec["out"] = model(*a)
+            return rec["out"]
+
+        @property
+        def last_prep(self):
+            return model.last_prep
+
+    loss = crit(_Once(), xs_d, xl_d, ys_d, yl_d)
+    h_attn, h_ctc = rec["out"]
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    opt.clip_and_step(5.0)
+    st = opt.device_state()
+    torch.cuda.synchronize()
+    return dict(loss=(loss.item(), loss_o.item()), h_attn=(h_attn, ha_o), h_ctc=(h_ctc, hc_o),
+                grads=(grads, grads_o), params=(dict(model.named_parameters()), new_o),
+                bn=(dict(model.named_buffers()), b64), norm=(st["grad_norm"], norm_o), st=st)
+
+
+TINY = O.default_cfg(enc_dim=64, enc_heads=4, enc_ff=256, enc_layers=2, dec_dim=64, dec_heads=4, dec_ff=256,
+                     dec_layers=1, vocab_size=30)
+SMALL = O.default_cfg(enc_layers=2, dec_layers=1)  # small-model widths (d 256, ff 2048, V 4233), 2+1 layers
+
+
+@pytest.mark.parametrize("cfg,B,T,L", [(TINY, 3, 130, 8), (SMALL, 2, 210, 12)])
+def test_parity_fp32(cfg, B, T, L):
+    r = run_case(cfg, B, T, L, "fp32")
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 1e-5 * abs(lo), r["loss"]
+    assert rel(*r["h_attn"]) < 2e-4
+    assert rel(*r["h_ctc"]) < 2e-4
+    g, go = r["grads"]
+    errs, _ = grad_errs(g, go)
+    # Subsampling conv grads sit behind two ReLUs over ~5e5 units: a pre-activation within
+    # fp32 rounding of 0 can take the other branch than in the fp64 oracle and moves one
+    # output channel's weight grad (observed: 1 channel of 256, 7.6e-3).  Allow 2e-2 there.
+    kink = {k for k in errs if k.startswith("encoder.embed.conv.")}
+    worst = max((v, k) for k, v in errs.items() if k not in kink)
+    assert worst[0] < 2e-4, worst
+    assert max(errs[k] for k in kink) < 2e-2, {k: errs[k] for k in kink}
+    assert abs(r["norm"][0] - r["norm"][1]) <= 1e-4 * r["norm"][1]
+    p, po = r["params"]
+    worst = max((rel(p[k].detach(), po[k]), k) for k in po)
+    assert worst[0] < 2e-4, worst
+    # Noam step 1: lr = d^-0.5 * warmup^-1.5 (the update itself is below fp32 resolution of
+    # the weights at step 1; the Adam arithmetic is pinned by test_kernels_gpu.py::test_adam_noam_clip)
+    assert abs(r["st"]["lr"] - O.noam_lr(1, cfg["enc_dim"])) <= 1e-6 * O.noam_lr(1, cfg["enc_dim"])
+    assert r["st"]["step"] == 1 and not r["st"]["skipped"]
+    bufs, bo = r["bn"]
+    for k, v in bo.items():
+        if v.is_floating_point():
+            assert rel(bufs[k], v) < 1e-4, k
+        else:
+            assert int(bufs[k]) == int(v), k
+
+
+@pytest.mark.parametrize("cfg,B,T,L", [(TINY, 3, 130, 8), (SMALL, 2, 210, 12)])
+def test_parity_bf16(cfg, B, T, L):
+    r = run_case(cfg, B, T, L, "bf16")
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 5e-3 * abs(lo), r["loss"]
+    assert rel(*r["h_attn"]) < 5e-2
+    assert rel(*r["h_ctc"]) < 5e-2
+    g, go = r["grads"]
+    errs, floor = grad_errs(g, go)
+    for k in go:
+        if go[k].abs().max().item() > floor:
+            assert cos(g[k], go[k]) > 0.995, (k, cos(g[k], go[k]))
+        assert errs[k] < 2.5e-1, (k, errs[k])
+
+
+def test_parity_chunk_mask_fp32():
+    r = run_case(TINY, 2, 150, 6, "fp32", chunk=8)
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 1e-5 * abs(lo)
+    g, go = r["grads"]
+    errs, _ = grad_errs(g, go)
+    assert max(errs.values()) < 2e-4, max((v, k) for k, v in errs.items())
+
+
+def test_parity_ctc_only_fp32():
+    r = run_case(TINY, 3, 120, 7, "fp32", ctc_weight=1.0)
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 1e-5 * abs(lo)
+    g, go = r["grads"]
+    errs, _ = grad_errs(g, go)
+    for k in go:
+        if k.startswith("decoder."):
+            assert g[k].abs().max().item() == 0.0, k  # decoder gets exactly zero gradient
+        else:
+            assert errs[k] < 2e-4, (k, errs[k])
+
+
+def test_eval_forward_uses_running_stats():
+    from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+
+    params = O.init_params(TINY, seed=3)
+    buffers = O.init_buffers(TINY)
+    for k in buffers:
+        if k.endswith("running_mean"):
+            buffers[k] = torch.randn(TINY["enc_dim"]) * 0.1
+        elif k.endswith("running_var"):
+            buffers[k] = torch.rand(TINY["enc_dim"]) + 0.5
+    xs, xlens, ys, ylens = O.synthetic_batch(2, 100, 5, TINY["vocab_size"], seed=5)
+    model = build(TINY, "fp32")
+    model.load_state_dict({**params, **buffers}, strict=False)
+    model = model.cuda().eval()
+    with torch.no_grad():
+        ha, hc = model(xs.cuda(), xlens.cuda(), ys.cuda(), ylens.cuda())
+        ha_o, hc_o, _, _ = O.u2_forward(xs.double(), xlens, ys, ylens, {k: v.double() for k, v in params.items()},
+                                        TINY, {k: (v.double() if v.is_floating_point() else v) for k, v in buffers.items()},
+                                        False)
+    assert rel(ha, ha_o) < 2e-4
+    assert rel(hc, hc_o) < 2e-4
+
+
+def test_dropout_train_step_runs_and_is_deterministic():
+    """Dropout cannot match torch's RNG bit-for-bit; check the step is finite, that the
+    same device counter reproduces the same loss, and that the keep rate is right
+    (kernel level: test_gemm_dropout_matches_branch_grad)."""
+    from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+
+    params = O.init_params(TINY, seed=1)
+    model = build(TINY, "bf16", dropout=0.1)
+    model.load_state_dict({**params, **O.init_buffers(TINY)}, strict=False)
+    model = model.cuda().train()
+    crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=30, smoothing=0.1, ctc_weight=0.3))
+    xs, xlens, ys, ylens = [t.cuda() for t in O.synthetic_batch(2, 100, 5, 30, seed=2)]
+    losses = []
+    for _ in range(2):
+        model._drop_ctr.zero_()
+        l = crit(model, xs, xlens, ys, ylens)
+        l.backward()
+        losses.append(l.item())
+    assert math.isfinite(losses[0]) and losses[0] == losses[1]
+    l3 = crit(model, xs, xlens, ys, ylens).item()  # counter advanced -> new masks
+    assert l3 != losses[0]

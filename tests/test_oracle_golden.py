@@ -1,0 +1,176 @@
+"""Pin the CPU oracle (oracle/u2_oracle.py) to golden vectors produced by running the
+reference itself (tests/golden/make_golden.py).  CPU only."""
+
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oracle import u2_oracle as O  # noqa: E402
+
+G = os.path.join(ROOT, "tests", "golden")
+
+
+def load(name):
+    return {k: torch.from_numpy(v) for k, v in np.load(os.path.join(G, name)).items()}
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+def test_rel_shift_closed_form():
+    d = load("relshift.npz")
+    for T in range(1, 10):
+        assert torch.equal(O.rel_shift(d[f"in_{T}"]), d[f"out_{T}"]), T
+
+
+def test_lengths_and_masks():
+    d = load("lengths.npz")
+    assert torch.equal(O.pred_len(d["xlen"]), d["pred_len"])
+    sub = []
+    for x in d["xlen"].tolist():
+        T = max(x, 3)
+        m = O.encoder_key_mask(torch.tensor([x]), T)
+        sub.append(int((~m).sum()))
+    assert sub == d["sub_valid"].tolist()
+    # frame t' valid iff 4 t' < xlen  (closed form used by the HIP prep kernel)
+    for x in d["xlen"].tolist():
+        T = max(x, 3)
+        Tp = O.subsampled_len(T)
+        assert sum(1 for t in range(Tp) if 4 * t < x) == sub[x - 1]
+    assert torch.equal(O.triangle_mask(8, stage=2).to(torch.uint8), d["tri_8_s2"])
+    assert torch.equal(O.triangle_mask(3, 5, diagonal=2).to(torch.uint8), d["tri_3_5_d2"])
+
+
+def _ctc_loss(h_ctc, xlens, ys, ylens, w):
+    V = h_ctc.shape[-1]
+    L = ys.shape[1]
+    h_attn = torch.zeros(h_ctc.shape[0], L + 1, V, dtype=h_ctc.dtype)
+    _, _, tgt = O.decoder_io(ys, ylens, V - 1, V - 1)
+    return O.hybrid_loss(h_attn, h_ctc, tgt, ys, xlens, ylens, w, 0.1)
+
+
+def test_ctc_loss_and_grad():
+    d = load("ctc.npz")
+    loss, lc, la = _ctc_loss(d["h_ctc"].double(), d["xlens"], d["ys"], d["ylens"], 1.0)
+    assert torch.isfinite(loss).item() == bool(d["finite"])
+    g = load("ctc_grad.npz")
+    h = g["h_ctc"].double().requires_grad_()
+    loss, _, _ = _ctc_loss(h, g["xlens"], g["ys"], g["ylens"], 1.0)
+    assert abs(loss.item() - g["loss"].item()) <= 1e-5 * abs(g["loss"].item())
+    loss.backward()
+    assert rel(h.grad, g["grad"]) < 1e-4
+
+
+def test_ctc_numpy_restatement_matches_reference():
+    """Independent float64 alpha/beta recursion (oracle/ctc_ref.py) vs the reference's
+    aten ctc_loss on the same logits."""
+    from oracle import ctc_ref
+
+    g = load("ctc_grad.npz")
+    B = g["h_ctc"].shape[0]
+    h = g["h_ctc"].double()
+    tot = 0.0
+    grad = np.zeros(h.shape)
+    ilen = O.pred_len(g["xlens"])
+    for b in range(B):
+        lp = torch.log_softmax(h[b, : ilen[b]], -1).numpy()
+        lab = g["ys"][b, : g["ylens"][b]].numpy()
+        nll, glog = ctc_ref.ctc_nll_and_grad(lp, lab)
+        tot += nll
+        grad[b, : ilen[b]] = glog
+    assert abs(tot / B - g["loss"].item()) <= 1e-6 * abs(g["loss"].item())
+    # the golden is the reference run in fp32 (aten fp32 CTC is ~1e-4 off fp64)
+    assert rel(torch.from_numpy(grad / B), g["grad"]) < 1e-4
+
+
+def test_label_smoothed_kl():
+    d = load("kl.npz")
+    h = d["h_attn"].double().requires_grad_()
+    ys, ylens = d["ys"], d["ylens"]
+    V = h.shape[-1]
+    _, _, tgt = O.decoder_io(ys, ylens, V - 1, V - 1)
+    T = 51
+    h_ctc = torch.zeros(ys.shape[0], T, V, dtype=torch.float64)
+    loss, _, _ = O.hybrid_loss(h, h_ctc, tgt, ys, torch.full((ys.shape[0],), 210), ylens, 0.0, 0.1)
+    assert abs(loss.item() - d["loss"].item()) <= 1e-5 * abs(d["loss"].item())
+    loss.backward()
+    assert rel(h.grad, d["grad"]) < 1e-5
+
+
+TINY_GOLDEN = O.default_cfg(enc_dim=32, enc_heads=4, enc_ff=64, enc_layers=2, dec_dim=32, dec_heads=4,
+                            dec_ff=64, dec_layers=1, vocab_size=20, input_dim=40)
+
+
+def _golden_params(d, prefix):
+    p, b = {}, {}
+    for k, v in d.items():
+        if k.startswith(prefix):
+            name = k[len(prefix):]
+            if "running_" in name or "num_batches" in name:
+                b[name] = v.clone()
+            else:
+                p[name] = v.clone()
+    return p, b
+
+
+def test_u2_step_against_reference():
+    d = load("u2_step.npz")
+    params, buffers = _golden_params(d, "init.")
+    p64 = {k: v.double() for k, v in params.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in buffers.items()}
+    batch = (d["xs"].double(), d["xlens"], d["ys"], d["ylens"])
+    with torch.no_grad():
+        ha, hc, _, _ = O.u2_forward(*batch, p64, TINY_GOLDEN, {k: v.clone() for k, v in b64.items()}, True)
+    assert rel(ha, d["h_attn"]) < 1e-5
+    assert rel(hc, d["h_ctc"]) < 1e-5
+    loss, grads, new, st, norm = O.train_step(p64, b64, batch, TINY_GOLDEN, model_dim=32)
+    assert abs(loss.item() - d["loss"].item()) <= 1e-5 * abs(d["loss"].item())
+    gmax = max(v.abs().max().item() for k, v in d.items() if k.startswith("grad."))
+    for k, g in grads.items():
+        ref = d["grad." + k].double()
+        err = (g - ref).abs().max().item() / max(ref.abs().max().item(), 1e-3 * gmax)
+        assert err < 1e-4, (k, err)
+    assert abs(norm - d["grad_norm"].item()) <= 1e-5 * d["grad_norm"].item()
+    for k, v in new.items():
+        assert rel(v, d["new." + k]) < 1e-5, k
+    for k, v in b64.items():
+        ref = d["new." + k]
+        if v.is_floating_point():
+            assert rel(v, ref) < 1e-5, k
+        else:
+            assert int(v) == int(ref), k
+
+
+def test_chunk_mask_composition_against_reference():
+    d = load("u2_step.npz")
+    params, buffers = _golden_params(d, "init.")
+    p64 = {k: v.double() for k, v in params.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in buffers.items()}
+    with torch.no_grad():
+        h, _ = O.encoder(d["xs"].double(), d["xlens"], p64, TINY_GOLDEN, b64, True, chunk=4)
+    assert rel(h, d["h_enc_chunk4"]) < 1e-5
+
+
+def test_liteasr_amd_init_matches_reference():
+    """torch.manual_seed(42); U2(cfg) builds bit-identical weights + identical keys."""
+    from liteasr_amd.models.u2 import U2, U2Config
+    from liteasr_amd.utils.cfg import resolve_self
+
+    d = load("u2_step.npz")
+    c = U2Config(input_dim=40, vocab_size=20, enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_layers=2,
+                 dec_dim=32, dec_ff_dim=64, dec_attn_heads=4, dec_layers=1)
+    resolve_self(c)
+    torch.manual_seed(42)
+    m = U2(c)
+    sd = {k: v for k, v in m.state_dict().items() if not k.endswith(".pe.pe")}
+    ref = {k[5:]: v for k, v in d.items() if k.startswith("init.")}
+    assert set(sd) == set(ref)
+    for k in ref:
+        assert torch.equal(sd[k].to(ref[k].dtype), ref[k]), k
