@@ -93,13 +93,6 @@ LASR_DEV float block_max(float v, float* red) {
 // ---- counter-based dropout RNG -----------------------------------------------
 // keep(seed, idx) is a pure function of (seed, logical element index), so the
 // backward pass regenerates the forward mask instead of storing it.
-LASR_DEV uint32_t lasr_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
-}
 struct DropCfg {
   float p;              // drop probability (0 = off)
   uint64_t seed;        // per-site seed (host)
@@ -114,15 +107,34 @@ static inline DropCfg mkdrop(float p, uint64_t seed) {
   d.ctr = p > 0.f ? lasr_dropout_counter() : nullptr;
   return d;
 }
-// Returns the multiplier for element idx: 0 or 1/(1-p); 1 when dropout is off.
+// 32-bit finaliser (lowbias32: 2 multiplies, 3 xor-shifts) for the per-element draws.
+LASR_DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// Per-site/step key (wave-uniform: derived from kernel args + the device counter).
+LASR_DEV uint32_t drop_key(const DropCfg& d) {
+  const uint64_t s = d.seed + (d.ctr ? d.ctr[0] * 0xD1B54A32D192ED03ull : 0ull);
+  return mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + 0x9E3779B9u));
+}
+// Multiplier of element idx (0 or 1/(1-p)): draw = mix32(idx * golden ^ key ^ hi-word
+// term); the site's mask is a pure function of (seed, step counter, idx).
+LASR_DEV float drop_mul_k(const DropCfg& d, uint32_t key, uint64_t idx) {
+  const uint32_t thr = (uint32_t)fminf(d.p * 4294967296.0f, 4294967295.0f);
+  const uint32_t x = ((uint32_t)idx * 0x9E3779B1u) ^ key ^ ((uint32_t)(idx >> 32) * 0x85EBCA77u);
+  return mix32(x) >= thr ? 1.f / (1.f - d.p) : 0.f;
+}
+// Multiplier for element idx; 1 when dropout is off.
 LASR_DEV float drop_mul(const DropCfg& d, uint64_t idx) {
   if (d.p <= 0.f) return 1.f;
-  const uint64_t seed = d.seed + (d.ctr ? d.ctr[0] * 0xD1B54A32D192ED03ull : 0ull);
-  const uint32_t thr = (uint32_t)fminf(d.p * 4294967296.0f, 4294967295.0f);
-  return lasr_hash(seed, idx) >= thr ? 1.f / (1.f - d.p) : 0.f;
+  return drop_mul_k(d, drop_key(d), idx);
 }
 
-LASR_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+LASR_DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }  // v_rcp_f32 (1 ulp)
 LASR_DEV float swishf(float x) { return x * sigmoidf_(x); }
 LASR_DEV float swish_grad(float z) {
   const float s = sigmoidf_(z);

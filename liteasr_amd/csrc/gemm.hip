@@ -5,9 +5,9 @@
 // stored K-contiguous ([rows][32] bf16, 64-B rows) with a 16-B-chunk XOR swizzle
 // chunk' = chunk ^ H[(row>>2)&3], H = {0,2,3,1}: for the ds_read_b128 lane groups of
 // gfx950 every 16-lane group then covers all 16 slots of a 256-B bank row (no
-// conflicts).  Operands that are not K-contiguous in HBM (the dW "TN" GEMMs, the
-// attention dS^T products) are loaded 8-wide along M/N and transposed on the LDS
-// write (pairs of k -> one ds_write_b32).
+// conflicts).  Operands that are not K-contiguous in HBM (the dW "TN" GEMMs, the dX "NN"
+// GEMMs, the attention P.V / dS^T products) keep their HBM orientation in LDS ([k][rows])
+// and are read with the gfx950 transposed read ds_read_b64_tr_b16 (TileLoader below).
 // fp32 path (parity build): 64x64x16 tiles on v_mfma_f32_16x16x4f32 (exact fp32 FMA
 // chain), element-wise staging; correctness first.
 //
@@ -47,6 +47,10 @@ struct GemmP {
   float* ws;
   int a_vec, b_vec;
   int c_vec, aux_vec, res_vec, ws_vec;  // 8-wide epilogue access allowed
+  // Epilogue mode of the bf16 kernel: 0 = no per-element loads, 1 = exactly one of
+  // aux/res, 16-B aligned and prefetched before the staging barrier, 2 = generic.
+  int epi_mode;
+  int bias_vec;
 };
 
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
@@ -124,8 +128,9 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
   }
   if (p.drop.p > 0.f) {
     const uint64_t base = ((uint64_t)z * p.M + m) * (uint64_t)p.N + n;
+    const uint32_t key = drop_key(p.drop);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] *= drop_mul(p.drop, base + q);
+    for (int q = 0; q < 8; ++q) v[q] *= drop_mul_k(p.drop, key, base + q);
   }
   if (p.res) {
     ld_any8(p.res, p.res_dtype, (int64_t)m * p.ldres + n, p.res_vec, cnt, t);
@@ -141,6 +146,41 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
   st_8(C, v, p.c_vec, cnt);
 }
 
+// Epilogue modes 0/1: bias already in registers (bv), the one aux/res source prefetched
+// (sv, mode 1 only), full 8-column vector (N % 8 == 0), beta == 0.
+template <typename TC>
+LASR_DEV void epi_fast8(const GemmP& p, int z1, int z2, int z, int m, int n, const float* acc,
+                        float alpha_eff, const float* bv, const float* sv) {
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff + bv[q];
+  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
+  if (p.zout) st8((TC*)p.zout + cidx, v);
+  if (p.act == LASR_ACT_RELU) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+  } else if (p.act == LASR_ACT_SWISH) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = swishf(v[q]);
+  }
+  if (p.aux) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      v[q] *= (p.aux_act == LASR_ACT_RELU) ? (sv[q] > 0.f ? 1.f : 0.f) : swish_grad(sv[q]);
+  }
+  if (p.drop.p > 0.f) {
+    const uint64_t base = ((uint64_t)z * p.M + m) * (uint64_t)p.N + n;
+    const uint32_t key = drop_key(p.drop);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] *= drop_mul_k(p.drop, key, base + q);
+  }
+  if (p.res) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = sv[q] + p.res_scale * v[q];
+  }
+  st8((TC*)p.C + cidx, v);
+}
+
 LASR_DEV float alpha_of(const GemmP& p) {
   return p.alpha_dev ? p.alpha * p.alpha_dev[0] : p.alpha;
 }
@@ -148,11 +188,6 @@ LASR_DEV float alpha_of(const GemmP& p) {
 // ============================ bf16 MFMA kernel ===================================
 LASR_DEV int swz(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
 LASR_DEV int lds_off(int row, int chunk) { return row * 32 + ((chunk ^ swz(row)) << 3); }
-
-LASR_DEV uint32_t u4_get16(const uint4& v, int i) {
-  const uint32_t w = (i < 2) ? v.x : (i < 4) ? v.y : (i < 6) ? v.z : v.w;
-  return (i & 1) ? (w >> 16) : (w & 0xFFFFu);
-}
 
 // 8 consecutive elements along the contiguous axis; zero outside [0,lim).
 LASR_DEV uint4 load8(const bf16_t* src, int start, int lim, bool vec) {
@@ -171,12 +206,27 @@ LASR_DEV uint4 load8(const bf16_t* src, int start, int lim, bool vec) {
   return v;
 }
 
-// Tile loader for one operand: R_TILE rows (M or N) x 32 k.
+// Tile loader for one operand: R_TILE rows (M or N) x 32 k, 16-B global loads.
+//  KC (operand K-contiguous in HBM): image [R_TILE][32 k], 64-B rows, chunk swizzle above;
+//     fragments read with ds_read_b128.
+//  !KC (operand M/N-contiguous, e.g. dW = dY^T X, dX = dY W): image [32 k][R_TILE] stored as
+//     it arrives (no transposing writes); 32-B column slots XOR-swizzled per k row by
+//     htr(k) so the 8 k-rows a 32-lane half touches in one ds_read_b64_tr_b16 land on 8
+//     distinct 32-B bank groups (conflict-free); fragments read with 2 transposed reads.
+template <int R_TILE>
+LASR_DEV int htr(int k) {
+  return R_TILE == 128 ? ((k & 3) | ((k >> 1) & 4)) : (((k >> 1) & 1) | ((k >> 2) & 2));
+}
+template <int R_TILE>
+LASR_DEV int tr_off(int k, int col) {  // element offset of (k, col), col % 4 == 0
+  return k * R_TILE + ((((col >> 4) ^ htr<R_TILE>(k))) << 4) + (col & 15);
+}
+
 template <int R_TILE, bool KC>
 struct TileLoader {
-  static constexpr int UNITS = KC ? R_TILE * 4 : R_TILE * 2;  // KC: (row,chunk); else (8 rows, 2 k)
+  static constexpr int UNITS = R_TILE * 4;  // 16-B units per 32-deep k tile
   static constexpr int PER = (UNITS + 255) / 256;
-  uint4 r0[PER], r1[PER];
+  uint4 r0[PER];
 
   LASR_DEV void load(const bf16_t* base, int64_t ld_r, int64_t ld_k, int row0, int R, int k0,
                      int kend, bool vec, int tid) {
@@ -190,12 +240,10 @@ struct TileLoader {
           if (gr < R) r0[i] = load8(base + (int64_t)gr * ld_r + gk, gk, kend, vec);
           else r0[i] = make_uint4(0, 0, 0, 0);
         } else {
-          const int rb = u % (R_TILE / 8), kp = u / (R_TILE / 8);
-          const int gr = row0 + rb * 8, gk = k0 + kp * 2;
+          const int c = u % (R_TILE / 8), k = u / (R_TILE / 8);
+          const int gr = row0 + c * 8, gk = k0 + k;
           if (gk < kend) r0[i] = load8(base + (int64_t)gk * ld_k + gr, gr, R, vec);
           else r0[i] = make_uint4(0, 0, 0, 0);
-          if (gk + 1 < kend) r1[i] = load8(base + (int64_t)(gk + 1) * ld_k + gr, gr, R, vec);
-          else r1[i] = make_uint4(0, 0, 0, 0);
         }
       }
     }
@@ -209,19 +257,138 @@ struct TileLoader {
           const int r = u >> 2, c = u & 3;
           *(uint4*)(lds + lds_off(r, c)) = r0[i];
         } else {
-          const int rb = u % (R_TILE / 8), kp = u / (R_TILE / 8);
-          const int k = kp * 2;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int r = rb * 8 + j;
-            const uint32_t w = u4_get16(r0[i], j) | (u4_get16(r1[i], j) << 16);
-            *(uint32_t*)(lds + lds_off(r, k >> 3) + (k & 7)) = w;
-          }
+          const int c = u % (R_TILE / 8), k = u / (R_TILE / 8);
+          *(uint4*)(lds + tr_off<R_TILE>(k, c * 8)) = r0[i];
         }
       }
     }
   }
 };
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// MFMA 16x16x32 operand fragment of rows rbase..rbase+15: lane l gets row rbase + (l&15),
+// k = 8(l>>4) .. 8(l>>4)+7.  EXEC must be full for the transposed reads (no divergence).
+template <int R_TILE, bool KC>
+LASR_DEV bf16x8 frag(const bf16_t* tile, int rbase, int lane) {
+  if (KC) return *(const bf16x8*)(tile + lds_off(rbase + (lane & 15), lane >> 4));
+  const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + tr_off<R_TILE>(8 * g + q, rbase + pc)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + tr_off<R_TILE>(8 * g + 4 + q, rbase + pc)));
+  const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Epilogue shared by the bf16 kernels: stage each half of the C tile (WM rows x BN cols,
+// fp32) through LDS, then every thread finishes 8 contiguous columns of a row with 16-B
+// loads/stores (or writes its split-K partial).  The caller has passed a barrier after its
+// last LDS read of the main loop.
+template <int BM, int BN, typename TC>
+LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem_epi, int m0,
+                            int n0, int s, int z, int z1, int z2) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  constexpr int LDC = BN + 4;  // +4 floats: the 4 row-groups of a write land on distinct banks
+  float* cs = reinterpret_cast<float*>(smem_epi);
+  const int rq = (lane >> 4) * 4, cl = lane & 15;
+  const float al = alpha_of(p);
+  const bool split = p.split_k > 1;
+  float* wsp = split ? p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N : nullptr;
+  // A thread's 8-column slot is the same in every epilogue iteration (256 % (BN/8) == 0):
+  // its bias is loaded once; the aux/res rows of a half are prefetched before the barrier.
+  constexpr int CPR = BN / 8, RPI = 256 / CPR, ITERS = WM / RPI;
+  static_assert(WM % RPI == 0, "epilogue tiling");
+  const int ec8 = (tid % CPR) * 8, er0 = tid / CPR;
+  const int en = n0 + ec8;
+  const bool fast = !split && p.epi_mode < 2;
+  float bv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bv[q] = 0.f;
+  if (fast && p.bias && en < p.N) {
+    if (p.bias_vec) ld8(p.bias + en, bv);
+    else
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bv[q] = p.bias[en + q];
+  }
+  const void* src = p.aux ? p.aux : p.res;
+  const int src_dt = p.aux ? p.aux_dtype : p.res_dtype;
+  const int64_t src_ld = p.aux ? p.ldaux : p.ldres;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // prefetch PF row-iterations of the aux/res source at a time (register budget)
+    constexpr int PF = ITERS < 2 ? ITERS : 2;
+    float sv[PF][8];
+    auto prefetch = [&](int b) {
+      if (!(fast && p.epi_mode == 1)) return;
+      const int mlast = p.M - 1, nc = min(en, p.N - 8);
+      if (src_dt == LASR_F32) {
+#pragma unroll
+        for (int it = 0; it < PF; ++it) {
+          const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
+          ld8((const float*)src + (int64_t)m * src_ld + nc, sv[it]);
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < PF; ++it) {
+          const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
+          ld8((const bf16_t*)src + (int64_t)m * src_ld + nc, sv[it]);
+        }
+      }
+    };
+    prefetch(0);
+    if (wr == h) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cs[(i * 16 + rq + e) * LDC + wc * WN + j * 16 + cl] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (fast) {
+#pragma unroll
+      for (int b = 0; b < ITERS; b += PF) {
+        if (b > 0) prefetch(b);
+#pragma unroll
+        for (int it = 0; it < PF; ++it) {
+          const int r = er0 + (b + it) * RPI;
+          const int m = m0 + h * WM + r;
+          if (m < p.M && en < p.N) {
+            float a8[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + ec8 + q];
+            epi_fast8<TC>(p, z1, z2, z, m, en, a8, al, bv, sv[it]);
+          }
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    constexpr int NV = WM * BN / 8;
+    for (int v = tid; v < NV; v += 256) {
+      const int r = v / (BN / 8), c8 = (v % (BN / 8)) * 8;
+      const int m = m0 + h * WM + r, n = n0 + c8;
+      if (m < p.M && n < p.N) {
+        float a8[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + c8 + q];
+        if (split) {
+          float* dst = wsp + (int64_t)m * p.N + n;
+          if (p.ws_vec && n + 8 <= p.N) st8(dst, a8);
+          else
+            for (int q = 0; q < 8 && n + q < p.N; ++q) dst[q] = a8[q];
+        } else {
+          epi_store8<TC>(p, z1, z2, z, m, n, a8, al);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
 
 template <int BM, int BN, bool AKC, bool BKC, typename TC>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
@@ -273,17 +440,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
       lb.load(B, b_ldr, b_ldk, n0, p.N, k0, kend, p.b_vec, tid);
     }
     bf16x8 af[FM], bfr[FN];
-    const int ch = lane >> 4;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int row = wr * WM + i * 16 + (lane & 15);
-      af[i] = *(const bf16x8*)(cur + lds_off(row, ch));
-    }
+    for (int i = 0; i < FM; ++i) af[i] = frag<BM, AKC>(cur, wr * WM + i * 16, lane);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int row = wc * WN + j * 16 + (lane & 15);
-      bfr[j] = *(const bf16x8*)(cur + BM * BK + lds_off(row, ch));
-    }
+    for (int j = 0; j < FN; ++j) bfr[j] = frag<BN, BKC>(cur + BM * BK, wc * WN + j * 16, lane);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -296,45 +456,202 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
     __syncthreads();
   }
 
-  // ---- epilogue: stage each half of the C tile (WM rows x BN cols, fp32) through LDS,
-  // then every thread finishes 8 contiguous columns of a row with 16-B loads/stores.
-  constexpr int LDC = BN + 4;  // +4 floats: the 4 row-groups of a write land on distinct banks
-  float* cs = reinterpret_cast<float*>(smem_epi);
-  const int rq = (lane >> 4) * 4, cl = lane & 15;
-  const float al = alpha_of(p);
-  const bool split = p.split_k > 1;
-  float* wsp = split ? p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N : nullptr;
+  gemm_epilogue<BM, BN, TC>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
+}
+
+// ---------------- bf16 kernel, LDS-DMA pipeline (16-B aligned operands) ----------------
+// Same tiles, LDS images, fragment reads and epilogue as gemm_bf16_kernel, but every full
+// 32-deep k tile is copied HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging) into an
+// S-stage ring, S-1 tiles in flight.  The image is lane-linear per wave instruction, so the
+// swizzles of lds_off / tr_off are applied to the SOURCE address (the XOR maps are
+// involutions).  One raw barrier per k tile, preceded by a counted vmcnt that retires only
+// the tile about to be read.  A ragged last k tile goes through the register loader
+// (zero fill).  Rows past M/N read clamped (valid) addresses; they only feed discarded
+// outputs.  Blocks are remapped so consecutive tiles share an XCD (and its L2).
+template <int N>
+LASR_DEV void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+LASR_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+// Transposed LDS read in inline asm: hipcc would otherwise treat the builtin as possibly
+// aliasing the in-flight LDS-DMA and drain the ring (vmcnt(0)) before every k step.  asm
+// loads are invisible to hipcc's waitcnt bookkeeping, so the caller waits explicitly
+// (tie_lgkm) before the results are used.
+LASR_DEV v2i ds_tr_asm(const bf16_t* p) {
+  v2i r;
+  const uint32_t a = (uint32_t)(uintptr_t)(lptr_t)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// s_waitcnt lgkmcnt(0) that the consumers of r[0..N) depend on (in/out operands).
+template <int N>
+LASR_DEV void tie_lgkm(v2i* r) {
+  if constexpr (N == 4)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]));
+  else if constexpr (N == 8)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]),
+                 "+v"(r[5]), "+v"(r[6]), "+v"(r[7]));
+  else
+    static_assert(N < 0, "tie_lgkm: unsupported count");
+}
+// Raw halves of a transposed fragment (see frag<>): k = 8g+q and 8g+4+q rows.
+template <int R_TILE>
+LASR_DEV void frag_tr_raw(const bf16_t* tile, int rbase, int lane, v2i* r) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
+  r[0] = ds_tr_asm(tile + tr_off<R_TILE>(8 * g + q, rbase + pc));
+  r[1] = ds_tr_asm(tile + tr_off<R_TILE>(8 * g + 4 + q, rbase + pc));
+}
+LASR_DEV bf16x8 frag_from_raw(const v2i* r) {
+  const int __attribute__((ext_vector_type(4))) v = {r[0][0], r[0][1], r[1][0], r[1][1]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Issue the glds of one operand tile (R_TILE rows x 32 k) into `dst`.
+template <int R_TILE, bool KC>
+LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0, bf16_t* dst,
+                        int tid) {
+  constexpr int PER = R_TILE * 4 / 256;  // 16-B positions per thread
+  const int wid = tid >> 6, lane = tid & 63;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (wr == h) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) cs[(i * 16 + rq + e) * LDC + wc * WN + j * 16 + cl] = acc[i][j][e];
+  for (int i = 0; i < PER; ++i) {
+    const int P = i * 256 + tid;  // linear 16-B position in the image
+    const bf16_t* src;
+    if (KC) {
+      const int r = P >> 2, c = (P & 3) ^ swz(r);
+      const int gr = min(row0 + r, R - 1);
+      src = base + (int64_t)gr * ld + k0 + c * 8;
+    } else {
+      constexpr int CPR = R_TILE / 8;
+      const int k = P / CPR, ps = P % CPR;
+      const int ls = ((((ps >> 1) ^ htr<R_TILE>(k))) << 1) | (ps & 1);
+      const int gc = min(row0 + ls * 8, R - 8);
+      src = base + (int64_t)(k0 + k) * ld + gc;
     }
-    __syncthreads();
-    constexpr int NV = WM * BN / 8;
-    for (int v = tid; v < NV; v += 256) {
-      const int r = v / (BN / 8), c8 = (v % (BN / 8)) * 8;
-      const int m = m0 + h * WM + r, n = n0 + c8;
-      if (m < p.M && n < p.N) {
-        float a8[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + c8 + q];
-        if (split) {
-          float* dst = wsp + (int64_t)m * p.N + n;
-          if (p.ws_vec && n + 8 <= p.N) st8(dst, a8);
-          else
-            for (int q = 0; q < 8 && n + q < p.N; ++q) dst[q] = a8[q];
-        } else {
-          epi_store8<TC>(p, z1, z2, z, m, n, a8, al);
-        }
-      }
-    }
-    __syncthreads();
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * 256 + wid * 64) * 8), 16, 0, 0);
+    (void)lane;
   }
+}
+
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S>
+__global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
+  constexpr int BK = 32;
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int TILE = (BM + BN) * BK;  // elements per ring stage
+  constexpr int MAIN_BYTES = S * TILE * 2;
+  constexpr int EPI_BYTES = WM * (BN + 4) * 4;
+  constexpr int GL = (BM + BN) * 4 / 256;  // glds per thread per k tile
+  __shared__ __attribute__((aligned(16))) char smem_epi[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
+  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_epi);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+
+  // XCD-aware (bijective) remap of the 2-D tile index
+  const int nx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int orig = blockIdx.y * nx + blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tx = wg % nx, ty = wg / nx;
+
+  const int zz = blockIdx.z;
+  const int s = zz % p.split_k, z = zz / p.split_k;
+  const int z1 = z / p.batch_div, z2 = z % p.batch_div;
+  const bf16_t* A = (const bf16_t*)p.A + z1 * p.sa1 + z2 * p.sa2;
+  const bf16_t* B = (const bf16_t*)p.B + z1 * p.sb1 + z2 * p.sb2;
+  const int m0 = ty * BM, n0 = tx * BN;
+  const int kbeg = s * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int64_t lda = AKC ? p.lda_m : p.lda_k, ldb = BKC ? p.ldb_n : p.ldb_k;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // full 32-deep tiles go through the glds ring; a ragged last tile is handled after the
+  // loop (ordinary loads inside the loop would make hipcc drain the ring with vmcnt(0))
+  const int nfull = (kend - kbeg) > 0 ? (kend - kbeg) / BK : 0;
+  auto issue = [&](int t) {
+    bf16_t* dst = smem + (t % S) * TILE;
+    const int k0 = kbeg + t * BK;
+    glds_tile<BM, AKC>(A, lda, m0, p.M, k0, dst, tid);
+    glds_tile<BN, BKC>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
+  };
+  auto compute = [&](const bf16_t* cur) {
+    bf16x8 af[FM], bfr[FN];
+    v2i ra[2 * FM], rb[2 * FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if constexpr (AKC) af[i] = frag<BM, true>(cur, wr * WM + i * 16, lane);
+      else frag_tr_raw<BM>(cur, wr * WM + i * 16, lane, ra + 2 * i);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (BKC) bfr[j] = frag<BN, true>(cur + BM * BK, wc * WN + j * 16, lane);
+      else frag_tr_raw<BN>(cur + BM * BK, wc * WN + j * 16, lane, rb + 2 * j);
+    }
+    if constexpr (!AKC) {
+      tie_lgkm<2 * FM>(ra);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = frag_from_raw(ra + 2 * i);
+    }
+    if constexpr (!BKC) {
+      tie_lgkm<2 * FN>(rb);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = frag_from_raw(rb + 2 * j);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  };
+
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t)
+    if (t < nfull) issue(t);
+
+  for (int kt = 0; kt < nfull; ++kt) {
+    const int after = min(S - 2, nfull - 1 - kt);  // tiles issued after kt (still in flight)
+    if (S >= 4 && after >= 2) wait_vmcnt<2 * GL>();
+    else if (after >= 1) wait_vmcnt<GL>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    if (kt + S - 1 < nfull) issue(kt + S - 1);
+    compute(smem + (kt % S) * TILE);
+  }
+  if (nfull < nk) {  // ragged tail: register loader with zero fill
+    __syncthreads();
+    TileLoader<BM, AKC> la;
+    TileLoader<BN, BKC> lb;
+    const int k0 = kbeg + nfull * BK;
+    la.load(A, AKC ? p.lda_m : 0, AKC ? 0 : p.lda_k, m0, p.M, k0, kend, true, tid);
+    lb.load(B, BKC ? p.ldb_n : 0, BKC ? 0 : p.ldb_k, n0, p.N, k0, kend, true, tid);
+    la.store(smem, tid);
+    lb.store(smem + BM * BK, tid);
+    __syncthreads();
+    compute(smem);
+  }
+  __syncthreads();
+  gemm_epilogue<BM, BN, TC>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
 }
 
 // ============================ fp32 MFMA kernel ===================================
@@ -431,7 +748,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
 
 // ================================ host launcher ==================================
 template <bool AKC, bool BKC, typename TC>
-static void launch_bf16(const GemmP& p, int BM, int BN, dim3 grid, hipStream_t st) {
+static void launch_bf16(const GemmP& p, int BM, int BN, bool glds, dim3 grid, hipStream_t st) {
+  if (glds) {
+    if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
+    else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
+    else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
+    else gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
+    return;
+  }
   if (BM == 128 && BN == 128) gemm_bf16_kernel<128, 128, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
   else if (BM == 128) gemm_bf16_kernel<128, 64, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
   else if (BN == 128) gemm_bf16_kernel<64, 128, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
@@ -439,13 +763,13 @@ static void launch_bf16(const GemmP& p, int BM, int BN, dim3 grid, hipStream_t s
 }
 
 template <typename TC>
-static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int BN, dim3 grid,
-                     hipStream_t st) {
+static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int BN, bool glds,
+                     dim3 grid, hipStream_t st) {
   if (bf16in) {
-    if (akc && bkc) launch_bf16<true, true, TC>(p, BM, BN, grid, st);
-    else if (akc) launch_bf16<true, false, TC>(p, BM, BN, grid, st);
-    else if (bkc) launch_bf16<false, true, TC>(p, BM, BN, grid, st);
-    else launch_bf16<false, false, TC>(p, BM, BN, grid, st);
+    if (akc && bkc) launch_bf16<true, true, TC>(p, BM, BN, glds, grid, st);
+    else if (akc) launch_bf16<true, false, TC>(p, BM, BN, glds, grid, st);
+    else if (bkc) launch_bf16<false, true, TC>(p, BM, BN, glds, grid, st);
+    else launch_bf16<false, false, TC>(p, BM, BN, glds, grid, st);
   } else {
     if (akc && bkc) gemm_f32_kernel<true, true, TC><<<grid, 256, 0, st>>>(p);
     else if (akc) gemm_f32_kernel<true, false, TC><<<grid, 256, 0, st>>>(p);
@@ -455,6 +779,14 @@ static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int
 }
 
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+static bool getenv_flag(const char* name) {
+  static int cached = -1;  // read once (A/B switch for benchmarking the register-staged path)
+  if (cached < 0) {
+    const char* v = getenv(name);
+    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
+  }
+  return cached == 1;
+}
 
 extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   LASR_CHECK_ARG(a != nullptr, "lasr_gemm: null args");
@@ -495,6 +827,13 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   p.aux_vec = a->aux && aligned16(a->aux) && a->ldaux % 8 == 0;
   p.res_vec = a->res && aligned16(a->res) && a->ldres % 8 == 0;
   p.ws_vec = a->N % 8 == 0;
+  p.bias_vec = a->bias && aligned16(a->bias);
+  {
+    const bool full8 = a->N % 8 == 0 && p.c_vec && a->beta == 0.f;
+    const int nsrc = (a->aux ? 1 : 0) + (a->res ? 1 : 0);
+    const bool src_ok = nsrc == 0 || (a->aux ? p.aux_vec : p.res_vec);
+    p.epi_mode = (full8 && nsrc <= 1 && src_ok) ? nsrc : 2;
+  }
 
   int BM = 64, BN = 64;
   int split = a->split_k > 0 ? a->split_k : 1;
@@ -532,8 +871,12 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM), (unsigned)(batch * split));
   LASR_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lasr_gemm: grid too large");
-  if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, grid, st);
-  else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, grid, st);
+  // LDS-DMA path: 16-B aligned rows/columns; non-K-contiguous extents a multiple of 8
+  // (a 16-B chunk never straddles the end of a row); the x/y grid fits the XCD remap.
+  const bool glds = bf && p.a_vec && p.b_vec && (akc || a->M % 8 == 0) && (bkc || a->N % 8 == 0) &&
+                    (int64_t)grid.x * grid.y < (1ll << 31) && !getenv_flag("LASR_GEMM_NO_GLDS");
+  if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, glds, grid, st);
+  else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, glds, grid, st);
   int rc = lasr_check_launch("lasr_gemm");
   if (rc || split == 1) return rc;
   const int64_t total = (int64_t)a->M * a->N * batch;

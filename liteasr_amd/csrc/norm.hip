@@ -227,36 +227,67 @@ extern "C" int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* g
 }
 
 // ----------------------------- column sums ----------------------------------------
-constexpr int CS_ROWS = 16;
-template <typename T>
-__global__ void colsum_partial_kernel(const T* X, int64_t M, int64_t N, int64_t ldx, float* part) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS;
-  const int64_t r1 = r0 + CS_ROWS < M ? r0 + CS_ROWS : M;
-  float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += to_f(X[r * ldx + n]);
-  part[(int64_t)blockIdx.y * N + n] = s;
+// Column sums (bias gradients): blocks of 32 column-octets x 8 row groups sum a chunk of
+// rows with 16-B loads, combine the 8 groups in LDS (fixed order) and emit one partial
+// row per chunk; at most CS_MAXCHUNK chunks, so the final reduce_cols stays short.
+constexpr int CS_MAXCHUNK = 128;
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* X, int64_t M, int64_t N,
+                                                             int64_t ldx, int64_t rpc, float* part) {
+  __shared__ float sh[8][256 + 4];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t n = ((int64_t)blockIdx.x * 32 + tx) * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rpc;
+  const int64_t r1 = r0 + rpc < M ? r0 + rpc : M;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    for (int64_t r = r0 + ty; r < r1; r += 8) {
+      float v[8];
+      if (VEC) {
+        ld8(X + r * ldx + n, v);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = n + q < N ? to_f(X[r * ldx + n + q]) : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += v[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) sh[ty][tx * 8 + q] = s[q];
+  __syncthreads();
+  // 256 columns of this block: thread t finishes column t
+  const int c = threadIdx.x;
+  const int64_t nc = (int64_t)blockIdx.x * 256 + c;
+  if (nc < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += sh[g][c];
+    part[(int64_t)blockIdx.y * N + nc] = t;
+  }
 }
-__global__ void colsum_final_kernel(const float* part, int nchunk, int64_t N, float* out, int acc) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int k = 0; k < nchunk; ++k) s += part[(int64_t)k * N + n];
-  out[n] = acc ? out[n] + s : s;
-}
+
+static int64_t colsum_chunks(int64_t M) { return std::min<int64_t>(cdiv(M, 64), CS_MAXCHUNK); }
 
 extern "C" int lasr_colsum(const void* X, int dtype, int64_t M, int64_t N, int64_t ldx, float* out,
                            int accumulate, float* workspace, int64_t ws_floats, void* stream) {
   if (N <= 0) return LASR_OK;
-  const int64_t nchunk = cdiv(M, CS_ROWS);
-  LASR_CHECK_ARG(nchunk <= 65535, "lasr_colsum: M too large");
+  const int64_t nchunk = M > 0 ? colsum_chunks(M) : 1;
+  const int64_t rpc = M > 0 ? cdiv(M, nchunk) : 0;
   LASR_CHECK_ARG(ws_floats >= nchunk * N, "lasr_colsum: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  dim3 g1((unsigned)cdiv(N, 256), (unsigned)(nchunk > 0 ? nchunk : 1));
+  dim3 g1((unsigned)cdiv(N, 256), (unsigned)nchunk);
+  const bool vec = N % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X & 15) == 0;
   if (M > 0) {
-    if (dtype == LASR_F32) colsum_partial_kernel<float><<<g1, 256, 0, st>>>((const float*)X, M, N, ldx, workspace);
-    else colsum_partial_kernel<bf16_t><<<g1, 256, 0, st>>>((const bf16_t*)X, M, N, ldx, workspace);
+    if (dtype == LASR_F32) {
+      if (vec) colsum_partial_kernel<float, true><<<g1, 256, 0, st>>>((const float*)X, M, N, ldx, rpc, workspace);
+      else colsum_partial_kernel<float, false><<<g1, 256, 0, st>>>((const float*)X, M, N, ldx, rpc, workspace);
+    } else {
+      if (vec) colsum_partial_kernel<bf16_t, true><<<g1, 256, 0, st>>>((const bf16_t*)X, M, N, ldx, rpc, workspace);
+      else colsum_partial_kernel<bf16_t, false><<<g1, 256, 0, st>>>((const bf16_t*)X, M, N, ldx, rpc, workspace);
+    }
+  } else {
+    hipMemsetAsync(workspace, 0, N * sizeof(float), st);
   }
   int rc = lasr_check_launch("colsum");
   if (rc) return rc;

@@ -14,10 +14,19 @@ __global__ __launch_bounds__(256) void reduce_cols_kernel(const float* __restric
   __shared__ float sh[RC_GROUPS][RC_COLS + 1];
   const int tx = threadIdx.x & (RC_COLS - 1), ty = threadIdx.x / RC_COLS;
   const int64_t n = (int64_t)blockIdx.x * RC_COLS + tx;
-  float s = 0.f;
-  if (n < N)
-    for (int p = ty; p < P; p += RC_GROUPS) s += part[(int64_t)p * N + n];
-  sh[ty][tx] = s;
+  // 4 independent accumulators (4 loads in flight per thread), combined in fixed order
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (n < N) {
+    int p = ty;
+    for (; p + 3 * RC_GROUPS < P; p += 4 * RC_GROUPS) {
+      s0 += part[(int64_t)p * N + n];
+      s1 += part[(int64_t)(p + RC_GROUPS) * N + n];
+      s2 += part[(int64_t)(p + 2 * RC_GROUPS) * N + n];
+      s3 += part[(int64_t)(p + 3 * RC_GROUPS) * N + n];
+    }
+    for (; p < P; p += RC_GROUPS) s0 += part[(int64_t)p * N + n];
+  }
+  sh[ty][tx] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (ty == 0 && n < N) {
     float t = 0.f;

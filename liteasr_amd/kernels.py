@@ -146,7 +146,7 @@ def linear(x, w, out, bias=None, **kw):
 
 def colsum(x2d: torch.Tensor, out: torch.Tensor, accumulate=True):
     M, Nn = x2d.shape
-    nchunk = (M + 15) // 16  # CS_ROWS in norm.hip
+    nchunk = max(1, min((M + 63) // 64, 128))  # colsum_chunks in norm.hip
     ws = WS.get(nchunk * Nn, x2d.device)
     N.call("lasr_colsum", ptr(x2d), dt(x2d), M, Nn, x2d.stride(0), ptr(out), int(accumulate),
            ptr(ws), ws.numel(), stream())

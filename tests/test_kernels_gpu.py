@@ -84,6 +84,48 @@ def test_gemm_epilogues(dtype):
     close(acc, acc0.double() + 3 * base, tol, "beta/alpha_dev")
 
 
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_large_tiles_bf16(ta, tb):
+    """Shapes that select the 128x128 tile (>= 512 workgroups): K-contiguous and
+    transposed-read (ds_read_b64_tr_b16) LDS images on both operands, ragged M."""
+    M, N, Kd = 4100, 2048, 96
+    g = torch.Generator(device="cpu").manual_seed(7)
+    A = torch.randn(M, Kd, generator=g)
+    B = torch.randn(Kd, N, generator=g)
+    a = (A.t().contiguous().t() if ta else A).to(DEV, torch.bfloat16)
+    b = (B.t().contiguous().t() if tb else B).to(DEV, torch.bfloat16)
+    c = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    K().gemm(a, b, c)
+    close(c, a.cpu().double() @ b.cpu().double(), 1e-2, "gemm128")
+
+
+def test_gemm_large_tile_epilogues_bf16():
+    """Register-prefetched epilogue (bias once per thread, one aux/res source prefetched)
+    on 128x128 tiles with a ragged last row tile."""
+    kn = K()
+    from liteasr_amd import _native as Nn
+
+    M, N, Kd = 4100, 2048, 64
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = torch.randn(N, Kd, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    base = (x.double() @ w.double().t()).cpu()
+    zr = base + bias.double().cpu()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    kn.linear(x, w, out, bias=bias, act=Nn.ACT_SWISH, zout=z)
+    close(z, zr, 2e-2, "zout128")
+    close(out, zr * torch.sigmoid(zr), 2e-2, "swish128")
+    res = torch.randn(M, N, device=DEV)
+    o32 = torch.empty(M, N, device=DEV)
+    kn.linear(x, w, o32, bias=bias, res=res, res_scale=0.5)
+    close(o32, res.double().cpu() + 0.5 * zr, 2e-2, "res128")
+    aux = torch.randn(M, N, device=DEV).bfloat16()
+    kn.linear(x, w, o32, aux=aux, aux_act=Nn.ACT_SWISH)
+    s = torch.sigmoid(aux.double().cpu())
+    close(o32, base * s * (1 + aux.double().cpu() * (1 - s)), 2e-2, "aux128")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_and_batched(dtype):
     kn = K()

@@ -163,7 +163,10 @@ def test_parity_chunk_mask_fp32():
     assert abs(lg - lo) <= 1e-5 * abs(lo)
     g, go = r["grads"]
     errs, _ = grad_errs(g, go)
-    assert max(errs.values()) < 2e-4, max((v, k) for k, v in errs.items())
+    # 5e-4: per-channel sums over B*T rows (conv/BN/bias grads) are associated differently
+    # from the CPU oracle's (fixed-order partials, deterministic); the chunk mask leaves
+    # few unmasked frames per row, so these sums carry more cancellation here.
+    assert max(errs.values()) < 5e-4, max((v, k) for k, v in errs.items())
 
 
 def test_parity_ctc_only_fp32():
