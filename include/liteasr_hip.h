@@ -110,17 +110,19 @@ int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_d
  * CTC (blank=0, reduction=sum) fused with log_softmax over the vocab.
  * Replaces liteasr/criterions/hybrid_ctc_attn.py:67-75 (h_ctc.transpose(0,1)
  * .log_softmax(-1) -> nn.CTCLoss) and aten's ctc_loss / _ctc_loss_backward.
- * logits: [B, T, V] (batch-major, ld = V), dtype `ldt`.
+ * logits: [B, T, V] (batch-major; row (b,t) starts at (b*T+t)*ld, ld >= V — a padded
+ *         leading dimension keeps the vocab GEMMs 16-B vectorised), dtype `ldt`;
+ *         grad uses the same row stride.
  * targets: [B, Lmax] int32, padded; tlen/ilen: [B] int32.
  * fwd: writes nll[B] (fp32; +inf when infeasible), and saves lse[B*T], lp[B*T*(Lmax+1)]
  *      (log-probs of blank and each target position) and alpha[B*T*(2*Lmax+1)].
  * bwd: grad[b,t,:] = g * (softmax - gamma_t) for t < ilen[b], 0 otherwise, where
  *      g = gscale * (*gdev if gdev).  Uses beta[B*T*(2*Lmax+1)] scratch.
  * ---------------------------------------------------------------------- */
-int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, const int32_t* targets,
+int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, int64_t ld, const int32_t* targets,
                  int Lmax, const int32_t* ilen, const int32_t* tlen, float* lse, float* lp,
                  float* alpha, float* nll, void* stream);
-int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, const int32_t* targets,
+int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, int64_t ld, const int32_t* targets,
                  int Lmax, const int32_t* ilen, const int32_t* tlen, const float* lse,
                  const float* lp, const float* alpha, const float* nll, float* beta,
                  void* grad, int gdt, float gscale, const float* gdev, void* stream);
@@ -130,10 +132,11 @@ int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, const int32_t
  *   row loss = sum_c td_c (log td_c - log_softmax(h)_c), td = s/(V-1), 1-s at target;
  *   rows with target == ignore contribute 0.
  * fwd: loss_rows[R] fp32, lse[R]. bwd: grad = g*(softmax - td) (0 on ignored rows).
+ * logits/grad rows are `ld` elements apart (ld >= V).
  * ---------------------------------------------------------------------- */
-int lasr_lsm_kl_fwd(const void* logits, int ldt, int R, int V, const int32_t* target,
+int lasr_lsm_kl_fwd(const void* logits, int ldt, int R, int V, int64_t ld, const int32_t* target,
                     int ignore, float smoothing, float* lse, float* loss_rows, void* stream);
-int lasr_lsm_kl_bwd(const void* logits, int ldt, int R, int V, const int32_t* target,
+int lasr_lsm_kl_bwd(const void* logits, int ldt, int R, int V, int64_t ld, const int32_t* target,
                     int ignore, float smoothing, const float* lse, void* grad, int gdt,
                     float gscale, const float* gdev, void* stream);
 /* out[0] = wa * sum(a[0:na]) + wb * sum(b[0:nb])   (hybrid loss combine,

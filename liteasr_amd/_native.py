@@ -58,10 +58,10 @@ SIGNATURES = {
     "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,
                            _p, _i, _f, _f, _u, _p],
     "lasr_branch_grad": [_p, _i, _l, _p, _i, _f, _f, _u, _p],
-    "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _p, _p],
-    "lasr_ctc_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p],
-    "lasr_lsm_kl_fwd": [_p, _i, _i, _i, _p, _i, _f, _p, _p, _p],
-    "lasr_lsm_kl_bwd": [_p, _i, _i, _i, _p, _i, _f, _p, _p, _i, _f, _p, _p],
+    "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p],
+    "lasr_ctc_bwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p],
+    "lasr_lsm_kl_fwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _p],
+    "lasr_lsm_kl_bwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _i, _f, _p, _p],
     "lasr_loss_combine": [_p, _i, _f, _p, _i, _f, _p, _p],
     "lasr_qbias_fwd": [_p, _i, _i, _i, _i, _i, _l, _p, _p, _p, _p, _p],
     "lasr_qbias_bwd": [_p, _p, _i, _i, _i, _i, _i, _p, _l, _p, _p, _p, _l, _p],

@@ -19,7 +19,7 @@
 
 template <typename T>
 __global__ __launch_bounds__(256) void ctc_lse_gather_kernel(const T* __restrict__ logits, int B,
-                                                             int T_, int V,
+                                                             int T_, int V, int64_t ld,
                                                              const int32_t* __restrict__ targets,
                                                              int Lmax, const int32_t* ilen,
                                                              const int32_t* tlen, float* lse,
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void ctc_lse_gather_kernel(const T* __restrict
     for (int j = threadIdx.x; j <= Lmax; j += blockDim.x) lprow[j] = 0.f;
     return;
   }
-  const T* x = logits + (int64_t)row * V;
+  const T* x = logits + (int64_t)row * ld;
   float m = -INFINITY, s = 0.f;
   for (int c = threadIdx.x; c < V; c += blockDim.x) {
     const float v = to_f(x[c]);
@@ -155,7 +155,8 @@ __global__ void ctc_beta_kernel(int T_, int Lmax, const int32_t* __restrict__ ta
 
 template <typename T, typename TG>
 __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ logits, int B, int T_,
-                                                       int V, const int32_t* __restrict__ targets,
+                                                       int V, int64_t ld,
+                                                       const int32_t* __restrict__ targets,
                                                        int Lmax, const int32_t* ilen,
                                                        const int32_t* tlen, const float* lse,
                                                        const float* lp, const float* alpha,
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
   uint32_t* bits = (uint32_t*)(sh + 2 * Lmax);
   const int row = blockIdx.x;
   const int b = row / T_, t = row - b * T_;
-  TG* g = grad + (int64_t)row * V;
+  TG* g = grad + (int64_t)row * ld;
   const int Tb = ilen[b];
   if (t >= Tb) {
     for (int c = threadIdx.x; c < V; c += blockDim.x) g[c] = from_f<TG>(0.f);
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
   }
   __syncthreads();
   const float gs = gscale * (gdev ? gdev[0] : 1.f);
-  const T* x = logits + (int64_t)row * V;
+  const T* x = logits + (int64_t)row * ld;
   const float l = lse[row];
   for (int c = threadIdx.x; c < V; c += blockDim.x) {
     float sub = (c == 0) ? gb : 0.f;
@@ -212,18 +213,18 @@ static int ctc_block(int S) {
   return nt < 64 ? 64 : (nt > 1024 ? 1024 : nt);
 }
 
-extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V,
+extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, int64_t ld,
                             const int32_t* targets, int Lmax, const int32_t* ilen,
                             const int32_t* tlen, float* lse, float* lp, float* alpha, float* nll,
                             void* stream) {
-  LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0, "lasr_ctc_fwd: bad sizes");
+  LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0 && ld >= V, "lasr_ctc_fwd: bad sizes");
   LASR_CHECK_ARG(ldt == LASR_F32 || ldt == LASR_BF16, "lasr_ctc_fwd: bad dtype");
   LASR_CHECK_ARG(2 * (2 * Lmax + 1) * 4 <= 160 * 1024, "lasr_ctc_fwd: Lmax too large");
   hipStream_t st = (hipStream_t)stream;
   if (ldt == LASR_F32)
-    ctc_lse_gather_kernel<float><<<B * T, 256, 0, st>>>((const float*)logits, B, T, V, targets, Lmax, ilen, tlen, lse, lp);
+    ctc_lse_gather_kernel<float><<<B * T, 256, 0, st>>>((const float*)logits, B, T, V, ld, targets, Lmax, ilen, tlen, lse, lp);
   else
-    ctc_lse_gather_kernel<bf16_t><<<B * T, 256, 0, st>>>((const bf16_t*)logits, B, T, V, targets, Lmax, ilen, tlen, lse, lp);
+    ctc_lse_gather_kernel<bf16_t><<<B * T, 256, 0, st>>>((const bf16_t*)logits, B, T, V, ld, targets, Lmax, ilen, tlen, lse, lp);
   int rc = lasr_check_launch("ctc_lse_gather");
   if (rc) return rc;
   const int Smax = 2 * Lmax + 1;
@@ -231,12 +232,12 @@ extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V,
   return lasr_check_launch("ctc_alpha");
 }
 
-extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V,
+extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, int64_t ld,
                             const int32_t* targets, int Lmax, const int32_t* ilen,
                             const int32_t* tlen, const float* lse, const float* lp,
                             const float* alpha, const float* nll, float* beta, void* grad, int gdt,
                             float gscale, const float* gdev, void* stream) {
-  LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0, "lasr_ctc_bwd: bad sizes");
+  LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0 && ld >= V, "lasr_ctc_bwd: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   const int Smax = 2 * Lmax + 1;
   ctc_beta_kernel<<<B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(T, Lmax, targets, ilen, tlen, lp, beta);
@@ -245,7 +246,7 @@ extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V,
   const size_t shm = ((size_t)2 * (Lmax > 0 ? Lmax : 1) + (V + 31) / 32) * sizeof(float);
   LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_ctc_bwd: vocab/labels too large for LDS");
 #define CTC_G(TT, TGG)                                                                      \
-  ctc_grad_kernel<TT, TGG><<<B * T, 256, shm, st>>>((const TT*)logits, B, T, V, targets, Lmax, \
+  ctc_grad_kernel<TT, TGG><<<B * T, 256, shm, st>>>((const TT*)logits, B, T, V, ld, targets, Lmax,\
                                                     ilen, tlen, lse, lp, alpha, beta, nll,     \
                                                     (TGG*)grad, gscale, gdev)
   if (ldt == LASR_F32 && gdt == LASR_F32) CTC_G(float, float);

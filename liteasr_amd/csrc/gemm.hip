@@ -147,15 +147,15 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
 }
 
 // Epilogue modes 0/1: bias already in registers (bv), the one aux/res source prefetched
-// (sv, mode 1 only), full 8-column vector (N % 8 == 0), beta == 0.
+// (sv, mode 1 only; N % 8 == 0 there), beta == 0; cnt < 8 only on a ragged last vector.
 template <typename TC>
-LASR_DEV void epi_fast8(const GemmP& p, int z1, int z2, int z, int m, int n, const float* acc,
-                        float alpha_eff, const float* bv, const float* sv) {
+LASR_DEV void epi_fast8(const GemmP& p, int z1, int z2, int z, int m, int n, int cnt,
+                        const float* acc, float alpha_eff, const float* bv, const float* sv) {
   float v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff + bv[q];
   const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
-  if (p.zout) st8((TC*)p.zout + cidx, v);
+  if (p.zout) st_8((TC*)p.zout + cidx, v, true, cnt);
   if (p.act == LASR_ACT_RELU) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
@@ -178,7 +178,7 @@ LASR_DEV void epi_fast8(const GemmP& p, int z1, int z2, int z, int m, int n, con
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = sv[q] + p.res_scale * v[q];
   }
-  st8((TC*)p.C + cidx, v);
+  st_8((TC*)p.C + cidx, v, true, cnt);
 }
 
 LASR_DEV float alpha_of(const GemmP& p) {
@@ -309,10 +309,10 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
 #pragma unroll
   for (int q = 0; q < 8; ++q) bv[q] = 0.f;
   if (fast && p.bias && en < p.N) {
-    if (p.bias_vec) ld8(p.bias + en, bv);
+    if (p.bias_vec && en + 8 <= p.N) ld8(p.bias + en, bv);
     else
 #pragma unroll
-      for (int q = 0; q < 8; ++q) bv[q] = p.bias[en + q];
+      for (int q = 0; q < 8; ++q) bv[q] = en + q < p.N ? p.bias[en + q] : 0.f;
   }
   const void* src = p.aux ? p.aux : p.res;
   const int src_dt = p.aux ? p.aux_dtype : p.res_dtype;
@@ -361,7 +361,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
             float a8[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + ec8 + q];
-            epi_fast8<TC>(p, z1, z2, z, m, en, a8, al, bv, sv[it]);
+            epi_fast8<TC>(p, z1, z2, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
           }
         }
       }
@@ -541,7 +541,7 @@ LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0,
       constexpr int CPR = R_TILE / 8;
       const int k = P / CPR, ps = P % CPR;
       const int ls = ((((ps >> 1) ^ htr<R_TILE>(k))) << 1) | (ps & 1);
-      const int gc = min(row0 + ls * 8, R - 8);
+      const int gc = min(row0 + ls * 8, ((R + 7) & ~7) - 8);  // host: row stride >= roundup8(R)
       src = base + (int64_t)(k0 + k) * ld + gc;
     }
     __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * 256 + wid * 64) * 8), 16, 0, 0);
@@ -829,10 +829,10 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   p.ws_vec = a->N % 8 == 0;
   p.bias_vec = a->bias && aligned16(a->bias);
   {
-    const bool full8 = a->N % 8 == 0 && p.c_vec && a->beta == 0.f;
     const int nsrc = (a->aux ? 1 : 0) + (a->res ? 1 : 0);
-    const bool src_ok = nsrc == 0 || (a->aux ? p.aux_vec : p.res_vec);
-    p.epi_mode = (full8 && nsrc <= 1 && src_ok) ? nsrc : 2;
+    const bool base_ok = p.c_vec && a->beta == 0.f;
+    const bool src_ok = nsrc == 1 && a->N % 8 == 0 && (a->aux ? p.aux_vec : p.res_vec);
+    p.epi_mode = !base_ok ? 2 : nsrc == 0 ? 0 : src_ok ? 1 : 2;
   }
 
   int BM = 64, BN = 64;
@@ -871,9 +871,11 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM), (unsigned)(batch * split));
   LASR_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lasr_gemm: grid too large");
-  // LDS-DMA path: 16-B aligned rows/columns; non-K-contiguous extents a multiple of 8
-  // (a 16-B chunk never straddles the end of a row); the x/y grid fits the XCD remap.
-  const bool glds = bf && p.a_vec && p.b_vec && (akc || a->M % 8 == 0) && (bkc || a->N % 8 == 0) &&
+  // LDS-DMA path: 16-B aligned rows/columns; for a non-K-contiguous operand the row stride
+  // covers the extent rounded up to 8 (a 16-B chunk never leaves its row; the padding
+  // columns only feed discarded outputs).
+  const int64_t M8 = cdiv(a->M, 8) * 8, N8 = cdiv(a->N, 8) * 8;
+  const bool glds = bf && p.a_vec && p.b_vec && (akc || a->lda_k >= M8) && (bkc || a->ldb_k >= N8) &&
                     (int64_t)grid.x * grid.y < (1ll << 31) && !getenv_flag("LASR_GEMM_NO_GLDS");
   if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, glds, grid, st);
   else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, glds, grid, st);

@@ -9,7 +9,7 @@
 LASR_DEV float xlogx(float x) { return x > 0.f ? x * __logf(x) : 0.f; }
 
 template <typename T>
-__global__ __launch_bounds__(256) void lsm_kl_fwd_kernel(const T* __restrict__ logits, int V,
+__global__ __launch_bounds__(256) void lsm_kl_fwd_kernel(const T* __restrict__ logits, int V, int64_t ld,
                                                          const int32_t* target, int ignore,
                                                          float smoothing, float* lse, float* loss) {
   __shared__ float red[32];
@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void lsm_kl_fwd_kernel(const T* __restrict__ l
     if (threadIdx.x == 0) { loss[r] = 0.f; lse[r] = 0.f; }
     return;
   }
-  const T* x = logits + (int64_t)r * V;
+  const T* x = logits + (int64_t)r * ld;
   float m = -INFINITY, s = 0.f, sx = 0.f;
   for (int c = threadIdx.x; c < V; c += blockDim.x) {
     const float v = to_f(x[c]);
@@ -44,14 +44,14 @@ __global__ __launch_bounds__(256) void lsm_kl_fwd_kernel(const T* __restrict__ l
 }
 
 template <typename T, typename TG>
-__global__ __launch_bounds__(256) void lsm_kl_bwd_kernel(const T* __restrict__ logits, int V,
+__global__ __launch_bounds__(256) void lsm_kl_bwd_kernel(const T* __restrict__ logits, int V, int64_t ld,
                                                          const int32_t* target, int ignore,
                                                          float smoothing, const float* lse,
                                                          TG* grad, float gscale,
                                                          const float* gdev) {
   const int r = blockIdx.x;
   const int tg = target[r];
-  TG* g = grad + (int64_t)r * V;
+  TG* g = grad + (int64_t)r * ld;
   if (tg == ignore) {
     for (int c = threadIdx.x; c < V; c += blockDim.x) g[c] = from_f<TG>(0.f);
     return;
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void lsm_kl_bwd_kernel(const T* __restrict__ l
   const float gs = gscale * (gdev ? gdev[0] : 1.f);
   const float eps = smoothing / (float)(V - 1), conf = 1.f - smoothing;
   const float l = lse[r];
-  const T* x = logits + (int64_t)r * V;
+  const T* x = logits + (int64_t)r * ld;
   for (int c = threadIdx.x; c < V; c += blockDim.x) {
     const float td = (c == tg) ? conf : eps;
     g[c] = from_f<TG>(gs * (__expf(to_f(x[c]) - l) - td));
@@ -77,27 +77,29 @@ __global__ void loss_combine_kernel(const float* a, int na, float wa, const floa
   if (threadIdx.x == 0) out[0] = wa * sa + wb * sb;
 }
 
-extern "C" int lasr_lsm_kl_fwd(const void* logits, int ldt, int R, int V, const int32_t* target,
+extern "C" int lasr_lsm_kl_fwd(const void* logits, int ldt, int R, int V, int64_t ld,
+                               const int32_t* target,
                                int ignore, float smoothing, float* lse, float* loss_rows,
                                void* stream) {
-  LASR_CHECK_ARG(R >= 0 && V > 1, "lasr_lsm_kl_fwd: bad sizes");
+  LASR_CHECK_ARG(R >= 0 && V > 1 && ld >= V, "lasr_lsm_kl_fwd: bad sizes");
   if (R == 0) return LASR_OK;
   hipStream_t st = (hipStream_t)stream;
   if (ldt == LASR_F32)
-    lsm_kl_fwd_kernel<float><<<R, 256, 0, st>>>((const float*)logits, V, target, ignore, smoothing, lse, loss_rows);
+    lsm_kl_fwd_kernel<float><<<R, 256, 0, st>>>((const float*)logits, V, ld, target, ignore, smoothing, lse, loss_rows);
   else
-    lsm_kl_fwd_kernel<bf16_t><<<R, 256, 0, st>>>((const bf16_t*)logits, V, target, ignore, smoothing, lse, loss_rows);
+    lsm_kl_fwd_kernel<bf16_t><<<R, 256, 0, st>>>((const bf16_t*)logits, V, ld, target, ignore, smoothing, lse, loss_rows);
   return lasr_check_launch("lsm_kl_fwd");
 }
 
-extern "C" int lasr_lsm_kl_bwd(const void* logits, int ldt, int R, int V, const int32_t* target,
+extern "C" int lasr_lsm_kl_bwd(const void* logits, int ldt, int R, int V, int64_t ld,
+                               const int32_t* target,
                                int ignore, float smoothing, const float* lse, void* grad, int gdt,
                                float gscale, const float* gdev, void* stream) {
-  LASR_CHECK_ARG(R >= 0 && V > 1, "lasr_lsm_kl_bwd: bad sizes");
+  LASR_CHECK_ARG(R >= 0 && V > 1 && ld >= V, "lasr_lsm_kl_bwd: bad sizes");
   if (R == 0) return LASR_OK;
   hipStream_t st = (hipStream_t)stream;
 #define KLB(TT, TGG)                                                                      \
-  lsm_kl_bwd_kernel<TT, TGG><<<R, 256, 0, st>>>((const TT*)logits, V, target, ignore, smoothing, \
+  lsm_kl_bwd_kernel<TT, TGG><<<R, 256, 0, st>>>((const TT*)logits, V, ld, target, ignore, smoothing, \
                                                 lse, (TGG*)grad, gscale, gdev)
   if (ldt == LASR_F32 && gdt == LASR_F32) KLB(float, float);
   else if (ldt == LASR_F32) KLB(float, bf16_t);

@@ -9,6 +9,7 @@ no CPU path (the CPU restatement lives in ``oracle/`` and is test-only).
 from __future__ import annotations
 
 import ctypes as C
+import math
 from typing import Optional
 
 import torch
@@ -177,31 +178,50 @@ def branch_grad(dx, gb, scale, p=0.0, seed=0):
 
 
 # ------------------------------------------------------------------------ CTC ---
+def _rows_ld(x, lead):
+    """Row stride of a logits view whose rows are (possibly padded) vocab vectors."""
+    ld = x.stride(-2)
+    assert x.stride(-1) == 1 and ld >= x.shape[-1], "logits rows must be unit-stride"
+    for d in range(lead):
+        assert x.stride(d) == ld * math.prod(x.shape[d + 1:-1]), "logits rows must be evenly spaced"
+    return ld
+
+
 def ctc_fwd(logits, targets, ilen, tlen, lse, lp, alpha, nll):
     B, T, V = logits.shape
     Lmax = targets.shape[1]
-    N.call("lasr_ctc_fwd", ptr(logits), dt(logits), B, T, V, ptr(targets), Lmax, ptr(ilen),
-           ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), stream())
+    N.call("lasr_ctc_fwd", ptr(logits), dt(logits), B, T, V, _rows_ld(logits, 1), ptr(targets), Lmax,
+           ptr(ilen), ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), stream())
 
 
 def ctc_bwd(logits, targets, ilen, tlen, lse, lp, alpha, nll, beta, grad, gscale, gdev=None):
     B, T, V = logits.shape
     Lmax = targets.shape[1]
-    N.call("lasr_ctc_bwd", ptr(logits), dt(logits), B, T, V, ptr(targets), Lmax, ptr(ilen),
+    ld = _rows_ld(logits, 1)
+    assert grad.shape == logits.shape and _rows_ld(grad, 1) == ld
+    N.call("lasr_ctc_bwd", ptr(logits), dt(logits), B, T, V, ld, ptr(targets), Lmax, ptr(ilen),
            ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), ptr(beta), ptr(grad), dt(grad),
            gscale, ptr(gdev), stream())
 
 
 def lsm_kl_fwd(logits, target, ignore, smoothing, lse, loss_rows):
     R, V = logits.shape
-    N.call("lasr_lsm_kl_fwd", ptr(logits), dt(logits), R, V, ptr(target), ignore, smoothing,
-           ptr(lse), ptr(loss_rows), stream())
+    N.call("lasr_lsm_kl_fwd", ptr(logits), dt(logits), R, V, _rows_ld(logits, 0), ptr(target), ignore,
+           smoothing, ptr(lse), ptr(loss_rows), stream())
 
 
 def lsm_kl_bwd(logits, target, ignore, smoothing, lse, grad, gscale, gdev=None):
     R, V = logits.shape
-    N.call("lasr_lsm_kl_bwd", ptr(logits), dt(logits), R, V, ptr(target), ignore, smoothing,
+    ld = _rows_ld(logits, 0)
+    assert grad.shape == logits.shape and _rows_ld(grad, 0) == ld
+    N.call("lasr_lsm_kl_bwd", ptr(logits), dt(logits), R, V, ld, ptr(target), ignore, smoothing,
            ptr(lse), ptr(grad), dt(grad), gscale, ptr(gdev), stream())
+
+
+def padded_rows(rows, V, dtype, device, align=8):
+    """[rows, V] view of a [rows, roundup(V, align)] buffer (16-B aligned vocab rows)."""
+    Vp = (V + align - 1) // align * align
+    return torch.empty(rows, Vp, dtype=dtype, device=device)[:, :V]
 
 
 def loss_combine(a, wa, b, wb, out):

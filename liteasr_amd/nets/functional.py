@@ -439,6 +439,13 @@ class ConformerLayerFn(torch.autograd.Function):
         return dx0, None, None, None, None
 
 
+def _rows2d(g, rows):
+    """(…, V) logits gradient -> [rows, V] view with unit column stride (padded row stride
+    kept); anything else is made contiguous."""
+    g2 = g.reshape(rows, g.shape[-1])
+    return g2 if g2.stride(1) == 1 else g2.contiguous()
+
+
 class HeadsFn(torch.autograd.Function):
     """Encoder after_norm (transformer_encoder.py:126), CTC head with its always-on
     input dropout (ctc.py:28-30) and the full Transformer decoder
@@ -456,7 +463,7 @@ class HeadsFn(torch.autograd.Function):
         h, hd, me, re = ln_forward(x, we.g, we.b, adt, y2=True, p2=env.p_ctc, seed2=env.seed + 2)
         wc = model.ctc.weights()
         V = wc.W.shape[0]
-        h_ctc = _e((M, V), adt, dev)
+        h_ctc = K.padded_rows(M, V, adt, dev)  # [M, V] view of [M, roundup8(V)]
         K.linear(hd, wc.W, h_ctc, bias=wc.b)
         # ---- decoder
         wd = dec.weights()
@@ -485,7 +492,7 @@ class HeadsFn(torch.autograd.Function):
                                              hh=hh))
             y = y3
         yf, _, mf, rf = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
-        h_attn = _e((R, V), adt, dev)
+        h_attn = K.padded_rows(R, V, adt, dev)
         K.linear(yf, wd.Wout, h_attn, bias=wd.bout)
         ctx.sv = SimpleNamespace(x=x, h=h, hd=hd, me=me, re=re, layers=layers_sv, yL=y, yf=yf,
                                  mf=mf, rf=rf, p=(pd, pff, pat, pca))
@@ -505,7 +512,7 @@ class HeadsFn(torch.autograd.Function):
         # ---- CTC head
         wc, gc = model.ctc.weights(), model.ctc.grads()
         if g_ctc is not None:
-            g_ctc = g_ctc.contiguous().view(M, -1)
+            g_ctc = _rows2d(g_ctc, M)
             K.gemm(g_ctc.t(), sv.hd, gc.W, beta=1.0, split_k=0)
             K.colsum(g_ctc, gc.b)
             dhd = _e((M, d_enc), F32, dev)
@@ -518,7 +525,7 @@ class HeadsFn(torch.autograd.Function):
         wd, gd = dec.weights(), dec.grads()
         d = wd.d
         if g_attn is not None:
-            g_attn = g_attn.contiguous().view(R, -1)
+            g_attn = _rows2d(g_attn, R)
             K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0)
             K.colsum(g_attn, gd.bout)
             dyf = _e((R, d), adt, dev)
@@ -598,9 +605,9 @@ class HybridLossFn(torch.autograd.Function):
         g = g.contiguous().float()
         dev = g.device
         B = sv.B
-        ga = torch.empty_like(sv.ha)
+        ga = K.padded_rows(sv.ha.shape[0], sv.ha.shape[1], sv.ha.dtype, dev)
         K.lsm_kl_bwd(sv.ha, sv.prep.tgt, sv.ign, sv.s, sv.lse_a, ga, (1.0 - sv.w) / B, gdev=g)
-        gc = torch.empty_like(sv.hc)
+        gc = K.padded_rows(sv.hc.shape[0] * sv.hc.shape[1], sv.hc.shape[2], sv.hc.dtype, dev).view(sv.hc.shape)
         L = sv.prep.tgt_ctc.shape[1]
         beta = _e(sv.alpha.numel(), F32, dev)
         K.ctc_bwd(sv.hc, sv.prep.tgt_ctc, sv.prep.pred_len, sv.prep.ylen, sv.lse, sv.lp, sv.alpha,

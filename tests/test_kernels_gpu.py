@@ -126,6 +126,30 @@ def test_gemm_large_tile_epilogues_bf16():
     close(o32, base * s * (1 + aux.double().cpu() * (1 - s)), 2e-2, "aux128")
 
 
+def test_gemm_padded_vocab_bf16():
+    """Vocab GEMMs on [rows, V] views of [rows, roundup8(V)] buffers: ragged-N fast epilogue
+    (bias), dX with a padded K-contiguous A, and the dW product whose M-contiguous A
+    (g^T) is LDS-DMA loaded through the padding columns."""
+    kn = K()
+    rows, V, d = 3000, 4233, 256
+    g = torch.Generator().manual_seed(5)
+    hd = torch.randn(rows, d, generator=g).to(DEV, torch.bfloat16)
+    W = torch.randn(V, d, generator=g).to(DEV, torch.bfloat16)
+    b = torch.randn(V, generator=g).to(DEV)
+    logits = kn.padded_rows(rows, V, torch.bfloat16, DEV)
+    kn.linear(hd, W, logits, bias=b)
+    ref = hd.cpu().double() @ W.cpu().double().t() + b.cpu().double()
+    close(logits, ref, 2e-2, "padded logits")
+    gl = torch.full((rows, 4240), float("nan"), dtype=torch.bfloat16, device=DEV)[:, :V]
+    gl.copy_(torch.randn(rows, V, generator=g))  # padding columns stay NaN: must not leak
+    dx = torch.empty(rows, d, device=DEV)
+    kn.gemm(gl, W, dx)
+    close(dx, gl.cpu().double() @ W.cpu().double(), 1e-2, "padded dX")
+    dW = torch.zeros(V, d, device=DEV)
+    kn.gemm(gl.t(), hd, dW, beta=1.0, split_k=0)
+    close(dW, gl.cpu().double().t() @ hd.cpu().double(), 1e-2, "padded dW")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_and_batched(dtype):
     kn = K()
@@ -290,6 +314,36 @@ def test_lsm_kl(dtype):
     out = torch.empty(1, device=DEV)
     kn.loss_combine(rows, 0.7, rows[:5].contiguous(), 0.3, out)
     close(out, 0.7 * ref_rows.sum() + 0.3 * ref_rows[:5].sum(), 1e-5, "combine")
+
+
+def test_losses_padded_rows():
+    """CTC / smoothed-KL on [.., V] views of [.., roundup8(V)] buffers (the model's logits
+    layout) give bit-identical results to the contiguous layout."""
+    kn = K()
+    B, T, V, L = 3, 40, 4233, 6
+    logits, tg, ilen, tlen = _ctc_case(B, T, V, L, 11, torch.bfloat16)
+    d_log = logits.to(DEV)
+    pad = kn.padded_rows(B * T, V, torch.bfloat16, DEV).view(B, T, V)
+    pad.copy_(d_log)
+    tg32, il, tl = tg.to(DEV, torch.int32), ilen.to(DEV, torch.int32), tlen.to(DEV, torch.int32)
+    S = 2 * L + 1
+    outs = []
+    for x in (d_log, pad):
+        lse, lpb = torch.empty(B * T, device=DEV), torch.empty(B * T * (L + 1), device=DEV)
+        alpha, beta = torch.empty(B * T * S, device=DEV), torch.empty(B * T * S, device=DEV)
+        nll = torch.empty(B, device=DEV)
+        kn.ctc_fwd(x, tg32, il, tl, lse, lpb, alpha, nll)
+        g = kn.padded_rows(B * T, V, torch.bfloat16, DEV).view(B, T, V) if x is pad else torch.empty_like(x)
+        kn.ctc_bwd(x, tg32, il, tl, lse, lpb, alpha, nll, beta, g, 1.0)
+        rows, lse2 = torch.empty(B * T, device=DEV), torch.empty(B * T, device=DEV)
+        t2 = torch.randint(0, V, (B * T,), generator=torch.Generator().manual_seed(3)).to(DEV, torch.int32)
+        x2 = x.reshape(B * T, V)
+        kn.lsm_kl_fwd(x2, t2, -1, 0.1, lse2, rows)
+        g2 = kn.padded_rows(B * T, V, torch.bfloat16, DEV) if x is pad else torch.empty_like(x2)
+        kn.lsm_kl_bwd(x2, t2, -1, 0.1, lse2, g2, 0.5)
+        outs.append((nll.cpu(), g.float().cpu(), rows.cpu(), g2.float().cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 # ------------------------------------------------------------------ attention
