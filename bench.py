@@ -65,43 +65,95 @@ def synthetic(cfgd, rank, dev):
     return [t.to(dev) for t in (xs, xlens, ys, ylens)]
 
 
-def dominant_kernel_roofline(cfgd, dev, iters=50):
-    """FFN fc1 GEMM of one Conformer layer at the step's shape (M = B*T', N = ff, K = d,
-    bf16 in, fused bias + Swish + pre-activation store): the largest GEMM family of the step
-    (4 launches per layer fwd+bwd of this size).  Timed live with HIP events on the stream it
-    is launched on."""
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
+ROOFLINE_KERNEL = "gemm_bf16_glds_kernel<128, 128, false, false, float, 3>"
+
+
+def roofline_case(cfgd, dev):
+    """The dominant kernel of the step (rocprof, profiles/r01): the weight-gradient GEMM
+    gemm_bf16_glds_kernel<128,128,false,false,float,3> (both operands M/N-contiguous, LDS
+    transposed reads, split-K fp32 partials).  Representative launch: the FFN fc1 dW,
+    dW1[ff, d] = dZ^T[ff, rows] @ LN[rows, d] with rows = B*T' — the largest and most frequent
+    shape of the family (4 of its 11 launches per Conformer layer).  Run in the library's
+    partials-only mode (split_k=-1) so the timed launches are that kernel alone; the
+    fixed-order split-K reduction is a separate kernel (splitk_reduce_kernel)."""
     import torch
 
     from liteasr_amd import kernels as K
-    from liteasr_amd._native import ACT_SWISH
 
     T1 = (cfgd["T"] - 3) // 2 + 1
-    Tp = (T1 - 3) // 2 + 1
-    M, N, Kd = cfgd["B"] * Tp, cfgd["ff"], cfgd["d"]
-    x = torch.randn(M, Kd, device=dev).bfloat16()
-    w = (torch.randn(N, Kd, device=dev) / math.sqrt(Kd)).bfloat16()
-    b = torch.randn(N, device=dev)
-    h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    z = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    rows = cfgd["B"] * ((T1 - 3) // 2 + 1)
+    M, N, Kd = cfgd["ff"], cfgd["d"], rows
+    dz = torch.randn(rows, M, device=dev).bfloat16()
+    ln = torch.randn(rows, N, device=dev).bfloat16()
+    dw = torch.zeros(M, N, device=dev)
+    _, _, split = K.gemm_plan(dz.t(), ln, dw, beta=1.0, split_k=-1)
+
+    def launch():
+        K.gemm(dz.t(), ln, dw, beta=1.0, split_k=-1)
+
+    flops = 2.0 * M * N * Kd
+    # algorithmic bytes of one launch: each bf16 operand read once + the fp32 partial slabs
+    bytes_ = 2.0 * (Kd * M + Kd * N) + 4.0 * split * M * N
+    meta = {"kernel": ROOFLINE_KERNEL, "shape": f"M={M} N={N} K={Kd} split_k={split}",
+            "grid": [-(-N // 128), -(-M // 128), split]}
+    return launch, flops, bytes_, meta
+
+
+def dominant_kernel_roofline(cfgd, dev, iters=50):
+    """Average launch duration of the dominant kernel measured live with HIP events on the
+    stream it is launched on; bound = whichever of FLOP time (dense bf16 MFMA peak) and
+    byte time (HBM peak) is larger for its algorithmic work."""
+    import torch
+
+    from liteasr_amd import kernels as K
+
+    launch, flops, bytes_, meta = roofline_case(cfgd, dev)
     for _ in range(5):
-        K.linear(x, w, h, bias=b, act=ACT_SWISH, zout=z)
-    st = torch.cuda.current_stream()
+        launch()
+    st = torch.cuda.current_stream()  # lasr_* launches go to kernels.stream() == this stream
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(iters):
-        K.linear(x, w, h, bias=b, act=ACT_SWISH, zout=z)
+        launch()
     e1.record(st)
     e1.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    flops = 2.0 * M * N * Kd
-    bytes_ = 2.0 * (M * Kd + N * Kd + 2 * M * N) + 4 * N
-    tf = flops / (ms * 1e-3) / 1e12
-    return {"kernel": f"gemm_bf16 fc1+bias+swish M={M} N={N} K={Kd}", "bound": "mfma",
-            "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
-            "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_,
-            "avg_launch_us": round(ms * 1e3, 2),
-            "achieved_hbm_GBs": round(bytes_ / (ms * 1e-3) / 1e9, 1)}
+    sec = e0.elapsed_time(e1) / iters * 1e-3
+    t_flop = flops / (PEAK_BF16_TFLOPS * 1e12)
+    t_byte = bytes_ / (PEAK_HBM_GBS * 1e9)
+    if t_byte >= t_flop:
+        bound, ach, peak, unit = "hbm", bytes_ / sec / 1e9, PEAK_HBM_GBS, "GB/s"
+    else:
+        bound, ach, peak, unit = "mfma", flops / sec / 1e12, PEAK_BF16_TFLOPS, "TFLOP/s"
+    traffic = pmc_traffic(meta)
+    out = {"kernel": meta["kernel"], "shape": meta["shape"], "bound": bound, "achieved": round(ach, 2),
+           "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+           "traffic": traffic["bytes_per_launch"] if traffic else None,
+           "algorithmic_bytes_per_launch": bytes_, "algorithmic_flops_per_launch": flops,
+           "avg_launch_us": round(sec * 1e6, 2),
+           "achieved_tflops": round(flops / sec / 1e12, 2)}
+    if traffic:
+        out["traffic_source"] = traffic["source"]
+    return out
+
+
+def pmc_traffic(meta):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
+    (profiles/*/roofline_pmc.json, written by tools/pmc_traffic.py: separate FETCH_SIZE and
+    WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), matched on kernel
+    and shape; None when absent."""
+    import glob
+    import json
+
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*",
+                                              "roofline_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == meta["kernel"] and d.get("shape") == meta["shape"]:
+            return {"bytes_per_launch": d["hbm_bytes_per_launch"], "source": os.path.relpath(path)}
+    return None
 
 
 def cpu_baseline(cfgd_name, budget_s=25.0):
@@ -151,10 +203,22 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-only", type=int, default=0, metavar="N",
+                    help="only launch the roofline kernel N times (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
+
+    if args.roofline_only:
+        torch.cuda.set_device(0)
+        launch, flops, bytes_, meta = roofline_case(CONFIGS[args.config], torch.device("cuda", 0))
+        for _ in range(args.roofline_only):
+            launch()
+        torch.cuda.synchronize()
+        print(json.dumps({**meta, "launches": args.roofline_only, "algorithmic_bytes_per_launch": bytes_,
+                          "algorithmic_flops_per_launch": flops}), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -53,8 +53,12 @@ int lasr_counter_add(uint64_t* dev_counter, uint64_t v, void* stream);
  * Epilogue order: v = alpha*acc (* *alpha_dev); v += bias[n]; zout = v; v = act(v);
  *   v *= act'(aux[m,n]); v *= dropmask(z*M*N + m*N + n); v = res[m,n] + res_scale*v;
  *   C = beta*C + v.
- * split_k > 1 (dW GEMMs): partial sums go to `workspace` (split_k*batch*M*N fp32),
- *   then are reduced; only alpha/alpha_dev/beta/bias are honoured in that mode.
+ * split_k (plain epilogues only: alpha/alpha_dev/beta/bias; otherwise 1 is used):
+ *   1 = no split; > 1 = that many K slices; 0 = automatic (long-K dW GEMMs).  Slice
+ *   partial sums go to `workspace` ([split][batch][M][N] fp32) and a second kernel reduces
+ *   them in fixed order (deterministic).  -1 = automatic, partials only: the reduction
+ *   is skipped (callers that fuse it elsewhere; profiling the GEMM kernel alone).
+ *   The split (and tile) lasr_gemm would use is reported by lasr_gemm_plan.
  * ---------------------------------------------------------------------- */
 typedef struct lasr_gemm_args {
   int M, N, K;
@@ -75,6 +79,7 @@ typedef struct lasr_gemm_args {
   int split_k; void* workspace; int64_t workspace_bytes;
 } lasr_gemm_args;
 int lasr_gemm(const lasr_gemm_args* args, void* stream);
+int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k);
 
 /* Column sums: out[n] (+)= sum_m X[m,n]  (bias gradients; fp32 out).
  * Two-pass deterministic; workspace >= ceil(M/rows_per_block)*N floats (see impl). */

@@ -51,6 +51,56 @@ LASR_DEV void st8(bf16_t* p, const float v[8]) {
   *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// N consecutive elements (N in 1,2,4,8,16; pointer aligned to N elements) <-> fp32.
+template <int N>
+LASR_DEV void ldv(const float* p, float* v) {
+  if constexpr (N == 1) v[0] = p[0];
+  else if constexpr (N == 2) { const float2 a = *(const float2*)p; v[0] = a.x; v[1] = a.y; }
+  else {
+#pragma unroll
+    for (int j = 0; j < N; j += 4) {
+      const float4 a = *(const float4*)(p + j);
+      v[j] = a.x; v[j + 1] = a.y; v[j + 2] = a.z; v[j + 3] = a.w;
+    }
+  }
+}
+template <int N>
+LASR_DEV void ldv(const bf16_t* p, float* v) {
+  if constexpr (N == 1) v[0] = bf2f(p[0]);
+  else if constexpr (N == 2) {
+    const uint32_t w = *(const uint32_t*)p;
+    v[0] = __uint_as_float(w << 16); v[1] = __uint_as_float(w & 0xFFFF0000u);
+  } else if constexpr (N == 4) {
+    const uint2 w = *(const uint2*)p;
+    v[0] = __uint_as_float(w.x << 16); v[1] = __uint_as_float(w.x & 0xFFFF0000u);
+    v[2] = __uint_as_float(w.y << 16); v[3] = __uint_as_float(w.y & 0xFFFF0000u);
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; j += 8) ld8(p + j, v + j);
+  }
+}
+template <int N>
+LASR_DEV void stv(float* p, const float* v) {
+  if constexpr (N == 1) p[0] = v[0];
+  else if constexpr (N == 2) *(float2*)p = make_float2(v[0], v[1]);
+  else {
+#pragma unroll
+    for (int j = 0; j < N; j += 4) *(float4*)(p + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+  }
+}
+template <int N>
+LASR_DEV void stv(bf16_t* p, const float* v) {
+  if constexpr (N == 1) p[0] = f2bf(v[0]);
+  else if constexpr (N == 2) *(uint32_t*)p = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  else if constexpr (N == 4)
+    *(uint2*)p = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                            (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  else {
+#pragma unroll
+    for (int j = 0; j < N; j += 8) st8(p + j, v + j);
+  }
+}
+
 // ---- wave (64-lane) reductions ------------------------------------------------
 LASR_DEV float wave_sum(float v) {
 #pragma unroll

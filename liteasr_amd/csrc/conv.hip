@@ -282,56 +282,14 @@ __global__ void dw_reduce_kernel(const float* part, int nparts, int C, float* dw
 }
 
 // ------------------------------- BatchNorm ---------------------------------------
-__global__ void bn_finalize_kernel(const float* stats, int nparts, int C, float eps,
-                                   float momentum, const float* gamma, const float* beta,
-                                   float* rmean, float* rvar, int64_t* nbt, float* mean,
-                                   float* rstd, float* scale, float* shift, int update) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && update == 1 && nbt) nbt[0] += 1;
-  if (c >= C) return;
-  if (update == 2) {  // eval mode: normalise with the running statistics
-    const float rs = rsqrtf(rvar[c] + eps);
-    mean[c] = rmean[c];
-    rstd[c] = rs;
-    const float sc = gamma[c] * rs;
-    scale[c] = sc;
-    shift[c] = beta[c] - rmean[c] * sc;
-    return;
-  }
-  // Chan's parallel combination, fixed order
-  double n = 0.0, mu = 0.0, m2 = 0.0;
-  for (int p = 0; p < nparts; ++p) {
-    const float* st = stats + (int64_t)p * 3 * C;
-    const double nb = st[c];
-    if (nb <= 0.0) continue;
-    const double mb = st[C + c], m2b = st[2 * C + c];
-    const double nt = n + nb;
-    const double dl = mb - mu;
-    mu += dl * nb / nt;
-    m2 += m2b + dl * dl * n * nb / nt;
-    n = nt;
-  }
-  const float var = (float)(m2 / n);
-  const float rs = rsqrtf(var + eps);
-  mean[c] = (float)mu;
-  rstd[c] = rs;
-  const float sc = gamma[c] * rs;
-  scale[c] = sc;
-  shift[c] = beta[c] - (float)mu * sc;
-  if (update == 1) {
-    const float uvar = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * uvar;
-  }
-}
-
-// Parallel form: 256 threads = 32 channels x 8 partial-groups, Chan-combined in double
-// (fixed order), then one thread per channel finalises.
-__global__ __launch_bounds__(256) void bn_finalize_par_kernel(
+// 1024 threads = 32 channels x BNF_G partial-groups, combined exactly in double (fixed
+// order), then one thread per channel finalises.
+constexpr int BNF_G = 32;
+__global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
     const float* stats, int nparts, int C, float eps, float momentum, const float* gamma,
     const float* beta, float* rmean, float* rvar, int64_t* nbt, float* mean, float* rstd,
     float* scale, float* shift, int update) {
-  __shared__ double sn[8][33], smu[8][33], sm2[8][33];
+  __shared__ double sn[BNF_G][33], smu[BNF_G][33], sm2[BNF_G][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + tx;
   if (blockIdx.x == 0 && threadIdx.x == 0 && update == 1 && nbt) nbt[0] += 1;
@@ -346,35 +304,37 @@ __global__ __launch_bounds__(256) void bn_finalize_par_kernel(
     }
     return;
   }
-  double n = 0.0, mu = 0.0, m2 = 0.0;
-  if (c < C) {
-    for (int p = ty; p < nparts; p += 8) {
+  // two-pass exact combine in double: (N, sum n_b mu_b) -> mu; then
+  // M2 = sum_b [m2_b + n_b (mu_b - mu)^2]; fixed partial order, no per-partial division.
+  double n = 0.0, s = 0.0;
+  if (c < C)
+    for (int p = ty; p < nparts; p += BNF_G) {
       const float* st = stats + (int64_t)p * 3 * C;
       const double nb = st[c];
-      if (nb <= 0.0) continue;
-      const double mb = st[C + c], m2b = st[2 * C + c];
-      const double nt = n + nb;
-      const double dl = mb - mu;
-      mu += dl * nb / nt;
-      m2 += m2b + dl * dl * n * nb / nt;
-      n = nt;
+      n += nb;
+      s += nb * (double)st[C + c];
     }
-  }
   sn[ty][tx] = n;
-  smu[ty][tx] = mu;
+  smu[ty][tx] = s;
+  __syncthreads();
+  n = 0.0;
+  s = 0.0;
+#pragma unroll
+  for (int g = 0; g < BNF_G; ++g) { n += sn[g][tx]; s += smu[g][tx]; }
+  const double mu = n > 0.0 ? s / n : 0.0;
+  double m2 = 0.0;
+  if (c < C)
+    for (int p = ty; p < nparts; p += BNF_G) {
+      const float* st = stats + (int64_t)p * 3 * C;
+      const double nb = st[c], dl = (double)st[C + c] - mu;
+      m2 += (double)st[2 * C + c] + nb * dl * dl;
+    }
   sm2[ty][tx] = m2;
   __syncthreads();
   if (ty != 0 || c >= C) return;
-  n = 0.0; mu = 0.0; m2 = 0.0;
-  for (int g = 0; g < 8; ++g) {
-    const double nb = sn[g][tx];
-    if (nb <= 0.0) continue;
-    const double nt = n + nb;
-    const double dl = smu[g][tx] - mu;
-    mu += dl * nb / nt;
-    m2 += sm2[g][tx] + dl * dl * n * nb / nt;
-    n = nt;
-  }
+  m2 = 0.0;
+#pragma unroll
+  for (int g = 0; g < BNF_G; ++g) m2 += sm2[g][tx];
   const float var = (float)(m2 / n);
   const float rs = rsqrtf(var + eps);
   mean[c] = (float)mu;
@@ -549,7 +509,7 @@ extern "C" int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float 
                                 float* running_mean, float* running_var, int64_t* num_batches,
                                 float* mean, float* rstd, float* scale, float* shift,
                                 int update_running, void* stream) {
-  bn_finalize_par_kernel<<<(unsigned)cdiv(C, 32), 256, 0, (hipStream_t)stream>>>(
+  bn_finalize_par_kernel<<<(unsigned)cdiv(C, 32), 32 * BNF_G, 0, (hipStream_t)stream>>>(
       stats_ws, nparts, C, eps, momentum, gamma, beta, running_mean, running_var, num_batches,
       mean, rstd, scale, shift, update_running);
   return lasr_check_launch("bn_finalize");

@@ -788,6 +788,49 @@ static bool getenv_flag(const char* name) {
   return cached == 1;
 }
 
+// Tile and split-K choice for one call (shared by lasr_gemm and lasr_gemm_plan).
+static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) {
+  const int batch = a->batch > 0 ? a->batch : 1;
+  const bool bf = a->in_dtype == LASR_BF16;
+  int BM = 64, BN = 64;
+  int split = a->split_k > 0 ? a->split_k : 1;
+  const bool plain = !a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f;
+  const bool autosplit = a->split_k <= 0 && plain && a->workspace;
+  const int kt = (int)cdiv(a->K, 32);
+  if (bf && autosplit && kt >= 16) {
+    // long-K (weight-gradient) GEMMs: big tiles, fill the chip with K slices instead
+    BM = a->M >= 96 ? 128 : 64;
+    BN = a->N >= 96 ? 128 : 64;
+    const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
+    // >= 512 workgroups (2 per CU) with >= 8 k tiles per slice (in-model best: fewer
+    // slices starve the 4- and 12-tile dW GEMMs of the attention/conv projections)
+    while (nb * split < 512 && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
+  } else if (bf) {
+    const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    for (int c = 0; c < 4; ++c) {
+      const int64_t nb = cdiv(a->M, cfg[c][0]) * cdiv(a->N, cfg[c][1]) * (int64_t)batch;
+      BM = cfg[c][0]; BN = cfg[c][1];
+      if (nb >= 512) break;
+    }
+  }
+  if (!bf && autosplit) {
+    const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
+    while (nb * split < 512 && split * 2 <= 32 && kt / (split * 2) >= 4) split *= 2;
+  }
+  if (split > 1 && (!plain || !a->workspace ||
+                    a->workspace_bytes < (int64_t)split * batch * a->M * a->N * 4))
+    split = 1;
+  *BMo = BM;
+  *BNo = BN;
+  *splito = split;
+}
+
+extern "C" int lasr_gemm_plan(const lasr_gemm_args* a, int* tile_m, int* tile_n, int* split_k) {
+  LASR_CHECK_ARG(a && tile_m && tile_n && split_k, "lasr_gemm_plan: null argument");
+  gemm_plan(a, tile_m, tile_n, split_k);
+  return LASR_OK;
+}
+
 extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   LASR_CHECK_ARG(a != nullptr, "lasr_gemm: null args");
   LASR_CHECK_ARG(a->M >= 0 && a->N >= 0 && a->K >= 0, "lasr_gemm: negative size");
@@ -835,34 +878,8 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
     p.epi_mode = !base_ok ? 2 : nsrc == 0 ? 0 : src_ok ? 1 : 2;
   }
 
-  int BM = 64, BN = 64;
-  int split = a->split_k > 0 ? a->split_k : 1;
-  const bool plain = !a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f;
-  const bool autosplit = a->split_k == 0 && plain && a->workspace;
-  const int kt = (int)cdiv(a->K, 32);
-  if (bf && autosplit && kt >= 16) {
-    // long-K (weight-gradient) GEMMs: big tiles, fill the chip with K slices instead
-    BM = a->M >= 96 ? 128 : 64;
-    BN = a->N >= 96 ? 128 : 64;
-    const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
-    while (nb * split < 512 && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
-  } else if (bf) {
-    const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
-    for (int c = 0; c < 4; ++c) {
-      const int64_t nb = cdiv(a->M, cfg[c][0]) * cdiv(a->N, cfg[c][1]) * (int64_t)batch;
-      BM = cfg[c][0]; BN = cfg[c][1];
-      if (nb >= 512) break;
-    }
-  }
-  if (!bf && autosplit) {
-    const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
-    while (nb * split < 512 && split * 2 <= 32 && kt / (split * 2) >= 4) split *= 2;
-  }
-  if (split > 1) {
-    LASR_CHECK_ARG(plain, "lasr_gemm: split_k needs a plain epilogue");
-    const int64_t need = (int64_t)split * batch * a->M * a->N * 4;
-    if (!a->workspace || a->workspace_bytes < need) split = 1;
-  }
+  int BM, BN, split;
+  gemm_plan(a, &BM, &BN, &split);
   p.split_k = split;
   const int kstep = bf ? 32 : 16;
   p.kchunk = split > 1 ? (int)(cdiv(cdiv(a->K, split), kstep) * kstep) : a->K;
@@ -880,7 +897,7 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, glds, grid, st);
   else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, glds, grid, st);
   int rc = lasr_check_launch("lasr_gemm");
-  if (rc || split == 1) return rc;
+  if (rc || split == 1 || a->split_k < 0) return rc;  // split_k < 0: leave the partials
   const int64_t total = (int64_t)a->M * a->N * batch;
   const int nblk = (int)std::min<int64_t>(cdiv(total, 256), 4096);
   if (a->c_dtype == LASR_F32) splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);

@@ -1,12 +1,14 @@
 // LayerNorm (eps 1e-12 in LiteASR: liteasr/nets/layer_norm.py:8-21) forward/backward,
 // residual-branch gradient fusion, and deterministic column sums (bias grads).
-// One wave per row, D/64 elements per lane held in registers (D % 64 == 0, D <= 1024).
+// One wave per row, D/64 contiguous elements per lane in registers (D % 64 == 0, D <= 1024).
+#include <algorithm>
+
 #include "common.h"
 
-constexpr int LN_ROWS_PER_WAVE = 8;
-constexpr int LN_WAVES = 4;
-constexpr int LN_ROWS_PER_BLOCK = LN_ROWS_PER_WAVE * LN_WAVES;
+constexpr int LN_WAVES = 4;           // forward: one row per wave
+constexpr int LN_ROWS_PER_BLOCK = 32;  // backward: rows per block (one partial row each)
 
+// Lane l owns the NPL contiguous columns [l*NPL, (l+1)*NPL) of a row (vector loads).
 template <int NPL, typename TX, typename TY, typename TY2>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, int64_t rows,
                                                      const float* gamma, const float* beta,
@@ -16,11 +18,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, i
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const TX* xr = x + row * D;
-  float v[NPL];
+  const int c0 = lane * NPL;
+  float v[NPL], g[NPL], b[NPL];
+  ldv<NPL>(x + row * D + c0, v);
+  ldv<NPL>(gamma + c0, g);
+  ldv<NPL>(beta + c0, b);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) { v[i] = to_f(xr[lane + 64 * i]); s += v[i]; }
+  for (int i = 0; i < NPL; ++i) s += v[i];
   const float mu = wave_sum(s) * (1.f / D);
   float q = 0.f;
 #pragma unroll
@@ -28,65 +33,89 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, i
   const float var = wave_sum(q) * (1.f / D);
   const float rs = rsqrtf(var + eps);
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+  float o[NPL];
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    const int c = lane + 64 * i;
-    const float o = (v[i] - mu) * rs * gamma[c] + beta[c];
-    y[row * D + c] = from_f<TY>(o);
-    if (y2) y2[row * D + c] = from_f<TY2>(o * drop_mul(d2, (uint64_t)row * D + c));
+  for (int i = 0; i < NPL; ++i) o[i] = (v[i] - mu) * rs * g[i] + b[i];
+  stv<NPL>(y + row * D + c0, o);
+  if (y2) {
+    const uint32_t key = d2.p > 0.f ? drop_key(d2) : 0u;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i)
+      o[i] *= d2.p > 0.f ? drop_mul_k(d2, key, (uint64_t)row * D + c0 + i) : 1.f;
+    stv<NPL>(y2 + row * D + c0, o);
   }
 }
 
+// Backward: LnbCfg::WAVES waves per block, each LN_ROWS_PER_BLOCK / WAVES rows; the
+// block's dgamma/dbeta partials are combined in fixed order through LDS (deterministic).
+template <int NPL>
+struct LnbCfg {
+  static constexpr int WAVES = NPL <= 8 ? 16 : 8;
+  static constexpr int RPW = LN_ROWS_PER_BLOCK / WAVES;
+};
+
 template <int NPL, typename TX, typename TD, typename TR, typename TDX, typename TGB>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const TX* __restrict__ x,
-                                                     const TD* __restrict__ dy, int64_t rows,
-                                                     const float* gamma, const float* mean,
-                                                     const float* rstd, const TR* dres, TDX* dx,
-                                                     float* part, TGB* gb, float bscale,
-                                                     DropCfg bd) {
-  constexpr int D = NPL * 64;
-  __shared__ float sg[LN_WAVES][D], sb[LN_WAVES][D];
+__global__ __launch_bounds__(1024) void ln_bwd_kernel(const TX* __restrict__ x,
+                                                      const TD* __restrict__ dy, int64_t rows,
+                                                      const float* gamma, const float* mean,
+                                                      const float* rstd, const TR* dres, TDX* dx,
+                                                      float* part, TGB* gb, float bscale,
+                                                      DropCfg bd) {
+  constexpr int D = NPL * 64, WAVES = LnbCfg<NPL>::WAVES, RPW = LnbCfg<NPL>::RPW;
+  __shared__ float sp[WAVES][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = lane * NPL;
   float pg[NPL], pb[NPL], gm[NPL];
+  ldv<NPL>(gamma + c0, gm);
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; gm[i] = gamma[lane + 64 * i]; }
-  for (int rr = 0; rr < LN_ROWS_PER_WAVE; ++rr) {
-    const int64_t row = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK + w * LN_ROWS_PER_WAVE + rr;
-    if (row >= rows) break;
-    const float mu = mean[row], rs = rstd[row];
-    float xh[NPL], g[NPL];
-    float s1 = 0.f, s2 = 0.f;
+  for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  const uint32_t key = (gb && bd.p > 0.f) ? drop_key(bd) : 0u;
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-      const int64_t idx = row * D + lane + 64 * i;
-      xh[i] = (to_f(x[idx]) - mu) * rs;
-      const float d = to_f(dy[idx]);
-      pg[i] += d * xh[i];
-      pb[i] += d;
-      g[i] = d * gm[i];
-      s1 += g[i];
-      s2 += g[i] * xh[i];
-    }
-    s1 = wave_sum(s1) * (1.f / D);
-    s2 = wave_sum(s2) * (1.f / D);
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int64_t row = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK + w * RPW + rr;
+    if (row < rows) {
+      const float mu = mean[row], rs = rstd[row];
+      float xv[NPL], d[NPL], g[NPL];
+      ldv<NPL>(x + row * D + c0, xv);
+      ldv<NPL>(dy + row * D + c0, d);
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-      const int64_t idx = row * D + lane + 64 * i;
-      float o = rs * (g[i] - s1 - xh[i] * s2);
-      if (dres) o += to_f(dres[idx]);
-      dx[idx] = from_f<TDX>(o);
-      if (gb) gb[idx] = from_f<TGB>(bscale * drop_mul(bd, (uint64_t)idx) * o);
+      for (int i = 0; i < NPL; ++i) {
+        xv[i] = (xv[i] - mu) * rs;  // x-hat
+        pg[i] += d[i] * xv[i];
+        pb[i] += d[i];
+        g[i] = d[i] * gm[i];
+        s1 += g[i];
+        s2 += g[i] * xv[i];
+      }
+      s1 = wave_sum(s1) * (1.f / D);
+      s2 = wave_sum(s2) * (1.f / D);
+      float o[NPL], r[NPL];
+      if (dres) ldv<NPL>(dres + row * D + c0, r);
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) o[i] = rs * (g[i] - s1 - xv[i] * s2) + (dres ? r[i] : 0.f);
+      stv<NPL>(dx + row * D + c0, o);
+      if (gb) {
+#pragma unroll
+        for (int i = 0; i < NPL; ++i)
+          o[i] *= bscale * (bd.p > 0.f ? drop_mul_k(bd, key, (uint64_t)(row * D + c0 + i)) : 1.f);
+        stv<NPL>(gb + row * D + c0, o);
+      }
     }
   }
+  // fixed-order combine of the WAVES partials: dgamma then dbeta through one LDS array
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) { sg[w][lane + 64 * i] = pg[i]; sb[w][lane + 64 * i] = pb[i]; }
-  __syncthreads();
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float a = 0.f, b = 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-    for (int k = 0; k < LN_WAVES; ++k) { a += sg[k][c]; b += sb[k][c]; }
-    part[(int64_t)blockIdx.x * 2 * D + c] = a;
-    part[(int64_t)blockIdx.x * 2 * D + D + c] = b;
+    for (int i = 0; i < NPL; ++i) sp[w][c0 + i] = pass == 0 ? pg[i] : pb[i];
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < WAVES; ++k) a += sp[k][c];
+      part[(int64_t)blockIdx.x * 2 * D + pass * D + c] = a;
+    }
+    __syncthreads();
   }
 }
 
@@ -124,11 +153,22 @@ static void ln_fwd_npl(const void* x, int xdt, int64_t rows, const float* g, con
   else ln_fwd_y2<NPL, bf16_t, bf16_t>(x, rows, g, b, eps, y, mean, rstd, y2, y2dt, d2, st);
 }
 
+// Rows are read/written D/64 contiguous elements per lane: pointers must be aligned to that
+// (capped at 16 B).
+static bool ln_aligned(const void* p, int D, int dt) {
+  const int esz = dt == LASR_F32 ? 4 : 2;
+  const int a = std::min(16, (D / 64) * esz);
+  return p == nullptr || ((uintptr_t)p % a) == 0;
+}
+
 extern "C" int lasr_layernorm_fwd(const void* x, int x_dtype, int64_t rows, int D,
                                   const float* gamma, const float* beta, float eps, void* y,
                                   int y_dtype, float* mean, float* rstd, void* y2, int y2_dtype,
                                   float p2, uint64_t seed2, void* stream) {
   LASR_CHECK_ARG(D % 64 == 0 && D >= 64 && D <= 1024, "lasr_layernorm_fwd: D=%d unsupported", D);
+  LASR_CHECK_ARG(ln_aligned(x, D, x_dtype) && ln_aligned(y, D, y_dtype) && ln_aligned(y2, D, y2_dtype) &&
+                     ln_aligned(gamma, D, LASR_F32) && ln_aligned(beta, D, LASR_F32),
+                 "lasr_layernorm_fwd: misaligned row pointer");
   if (rows <= 0) return LASR_OK;
   DropCfg d2 = mkdrop(p2, seed2);
   hipStream_t st = (hipStream_t)stream;
@@ -151,7 +191,7 @@ static void ln_bwd_3(const void* x, const void* dy, int64_t rows, const float* g
                      hipStream_t st) {
   const unsigned nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
 #define LNB(TR, TDX, TGB)                                                                     \
-  ln_bwd_kernel<NPL, TX, TD, TR, TDX, TGB><<<nb, 256, 0, st>>>(                               \
+  ln_bwd_kernel<NPL, TX, TD, TR, TDX, TGB><<<nb, LnbCfg<NPL>::WAVES * 64, 0, st>>>(          \
       (const TX*)x, (const TD*)dy, rows, gamma, mean, rstd, (const TR*)dres, (TDX*)dx, part, \
       (TGB*)gb, bscale, bd)
   const bool rf = dresdt == LASR_F32, xf = dxdt == LASR_F32, gf = gbdt == LASR_F32;
@@ -183,6 +223,10 @@ extern "C" int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, in
                                   int64_t ws_floats, void* gb, int gb_dtype, float bscale,
                                   float bp, uint64_t bseed, void* stream) {
   LASR_CHECK_ARG(D % 64 == 0 && D >= 64 && D <= 1024, "lasr_layernorm_bwd: D=%d unsupported", D);
+  LASR_CHECK_ARG(ln_aligned(x, D, x_dtype) && ln_aligned(dy, D, dy_dtype) &&
+                     ln_aligned(dres, D, dres_dtype) && ln_aligned(dx, D, dx_dtype) &&
+                     ln_aligned(gb, D, gb_dtype) && ln_aligned(gamma, D, LASR_F32),
+                 "lasr_layernorm_bwd: misaligned row pointer");
   if (rows <= 0) return LASR_OK;
   const int64_t nblk = cdiv(rows, LN_ROWS_PER_BLOCK);
   LASR_CHECK_ARG(ws_floats >= nblk * 2 * D, "lasr_layernorm_bwd: workspace too small (%lld < %lld)",

@@ -91,6 +91,7 @@ def gemm(
     res: Optional[torch.Tensor] = None,
     res_scale: float = 1.0,
     split_k: int = 1,
+    plan_only: bool = False,
 ):
     """c = epilogue(alpha * a @ b) for logical views a (..,M,K), b (..,K,N), c (..,M,N).
 
@@ -133,11 +134,20 @@ def gemm(
         args.res, args.res_dtype, args.ldres, args.res_scale = ptr(res), dt(res), res.stride(0), res_scale
     args.split_k = split_k
     if split_k != 1:
-        need = 64 * z1 * z2 * M * Nn if split_k == 0 else split_k * z1 * z2 * M * Nn
+        need = 64 * z1 * z2 * M * Nn if split_k <= 0 else split_k * z1 * z2 * M * Nn
         ws = WS.get(need, c.device)
         args.workspace, args.workspace_bytes = ptr(ws), ws.numel() * 4
+    if plan_only:
+        tm, tn, sp = C.c_int(), C.c_int(), C.c_int()
+        N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp))
+        return tm.value, tn.value, sp.value
     N.call("lasr_gemm", C.byref(args), stream())
     return c
+
+
+def gemm_plan(a, b, c, **kw):
+    """(tile_m, tile_n, split_k) lasr_gemm would use for this call (nothing is launched)."""
+    return gemm(a, b, c, plan_only=True, **kw)
 
 
 def linear(x, w, out, bias=None, **kw):
