@@ -4,10 +4,18 @@ ARCH  ?= gfx950
 SRC   := $(wildcard liteasr_amd/csrc/*.hip)
 OBJ   := $(patsubst liteasr_amd/csrc/%.hip,build/obj/%.o,$(SRC))
 LIB   := liteasr_amd/lib/libliteasr_hip.so
+IOLIB := liteasr_amd/lib/libliteasr_io.so
+CXX   ?= g++
 HDRS  := liteasr_amd/csrc/common.h include/liteasr_hip.h
 FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC
 
-all: $(LIB)
+all: $(LIB) $(IOLIB)
+
+# host-only native feature reader (no device code); -ffp-contract=off keeps the decode
+# arithmetic bit-identical to the reference's numpy float32 expressions
+$(IOLIB): liteasr_amd/csrc/io/ark_io.cpp include/liteasr_io.h
+	@mkdir -p liteasr_amd/lib
+	$(CXX) -O2 -std=c++17 -fPIC -shared -ffp-contract=off -pthread -o $@ $<
 
 build/obj/%.o: liteasr_amd/csrc/%.hip $(HDRS)
 	@mkdir -p build/obj
@@ -18,6 +26,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(IOLIB)
 
 .PHONY: all clean

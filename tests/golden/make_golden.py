@@ -11,6 +11,11 @@ Fixtures
   ctc.npz         HybridCTCLoss with ctc_weight=1 (pure CTC, reduction sum / B) on fixed
                   logits: loss + d loss / d logits; repeated labels, L_b = 0, infeasible
   kl.npz          HybridCTCLoss with ctc_weight=0 (label-smoothed KL), loss + grad
+  loader/         16-utt synthetic Kaldi data dir (FM ark + CM ark, feats.scp with the
+                  placeholder @DIR@, utt2num_frames, text, vocab.txt) written by the
+                  reference's kaldiio.save_ark; loader.npz = the reference AudioFileDataset's
+                  batch composition and collated (xs, xlens, ys, ylens) for SeqBatch/FrameBatch
+                  configs, plus load_mat of every entry (FM and CM)
   u2_step.npz     tiny U2 (d 32, 2 enc / 1 dec, V 20, F 40): seed-42 init state_dict, a
                   batch, h_attn / h_ctc / loss / grads, params after clip(5) + Noam step,
                   BN running stats; plus a chunk-mask (stage 4) forward for config 4
@@ -188,9 +193,93 @@ def gen_u2_step():
          **{"init." + k: v for k, v in init.items()}, **grads, **after)
 
 
+def gen_loader():
+    import shutil
+    import tempfile
+
+    from liteasr.dataclass.vocab import Vocab
+    from liteasr.dataset.asr_dataset import AudioFileDataset
+    from liteasr.utils.kaldiio import load_mat, save_ark
+
+    rng = np.random.default_rng(11)
+    out_dir = os.path.join(HERE, "loader")
+    shutil.rmtree(out_dir, ignore_errors=True)
+    os.makedirs(out_dir)
+    chars = [chr(ord("a") + i) for i in range(20)]
+    with open(os.path.join(out_dir, "vocab.txt"), "w") as f:
+        f.write("<unk> 1\n")
+        for i, ch in enumerate(chars):
+            f.write(f"{ch} {i + 2}\n")
+    F = 20
+    utts = {}
+    lens = rng.integers(30, 121, size=16)
+    lens[5] = lens[9]  # a tie: the length sort must be stable
+    for i, T in enumerate(lens):
+        utts[f"utt{i:02d}"] = (rng.standard_normal((int(T), F)) * 2 + 0.5).astype(np.float32)
+    texts = {}
+    for i, k in enumerate(utts):
+        L = int(rng.integers(1, 16))
+        t = "".join(rng.choice(chars + ["z"], size=L))  # 'z' is out of vocab -> <unk>
+        texts[k] = t
+    tmp = tempfile.mkdtemp()
+    arrs = {}
+    for tag, cm in (("fm", None), ("cm", 2)):
+        ark = os.path.join(out_dir, f"feats_{tag}.ark")
+        scp = os.path.join(tmp, f"{tag}.scp")
+        save_ark(ark, utts, scp=scp, compression_method=cm)
+        lines = open(scp).read().replace(out_dir, "@DIR@")
+        open(os.path.join(out_dir, f"feats_{tag}.scp"), "w").write(lines)
+        for line in open(scp):
+            k, p = line.split()
+            arrs[f"mat_{tag}_{k}"] = load_mat(p)
+    with open(os.path.join(out_dir, "utt2num_frames"), "w") as f:
+        for k, v in utts.items():
+            f.write(f"{k} {v.shape[0]}\n")
+    with open(os.path.join(out_dir, "text"), "w") as f:
+        for k, t in texts.items():
+            f.write(f"{k} {t}\n")
+    # run the reference dataset on a resolved copy
+    data = os.path.join(tmp, "data")
+    os.makedirs(data)
+    for fn in ("utt2num_frames", "text"):
+        shutil.copy(os.path.join(out_dir, fn), data)
+    vocab = Vocab(os.path.join(out_dir, "vocab.txt"))
+    cfgs = [dict(batch_count="seq", batch_size=4, min_batch_size=1, max_len_in=60, max_len_out=10),
+            dict(batch_count="seq", batch_size=6, min_batch_size=2, max_len_in=100, max_len_out=8),
+            dict(batch_count="frame", max_frame_in=300, max_frame_out=None, max_frame_inout=None),
+            dict(batch_count="frame", max_frame_in=None, max_frame_out=30, max_frame_inout=350)]
+    pp = types.SimpleNamespace(workflow=[], spec_aug=None)
+    for tag in ("fm", "cm"):
+        lines = open(os.path.join(out_dir, f"feats_{tag}.scp")).read().replace("@DIR@", out_dir)
+        open(os.path.join(data, "feats.scp"), "w").write(lines)
+        for ci, c in enumerate(cfgs):
+            full = dict(batch_count="seq", batch_size=None, min_batch_size=None, max_len_in=None, max_len_out=None,
+                        max_frame_in=None, max_frame_out=None, max_frame_inout=None)
+            full.update(c)
+            ds = AudioFileDataset("train", data, None, types.SimpleNamespace(**full), pp, vocab)
+            comp = [list(ds.batchify_policy[b]) for b in range(len(ds))]
+            arrs[f"{tag}_c{ci}_batch_sizes"] = np.array([len(b) for b in comp])
+            arrs[f"{tag}_c{ci}_batch_idx"] = np.array(sum(comp, []))
+            for b in range(len(ds)):
+                xs, xl, ys, yl = ds.collator([ds[b]])
+                if ci == 0:
+                    arrs[f"{tag}_c{ci}_b{b}_xs"] = xs
+                else:  # same matrices, other grouping: shape + exact float64 sum suffice
+                    arrs[f"{tag}_c{ci}_b{b}_xs_shape"] = np.array(xs.shape)
+                    arrs[f"{tag}_c{ci}_b{b}_xs_sum"] = xs.double().sum()
+                arrs[f"{tag}_c{ci}_b{b}_xlens"] = xl
+                arrs[f"{tag}_c{ci}_b{b}_ys"] = ys
+                arrs[f"{tag}_c{ci}_b{b}_ylens"] = yl
+    arrs["vocab_len"] = np.array(len(vocab))
+    arrs["lookup_all"] = np.array(vocab.lookup("".join(chars) + "z?"))
+    shutil.rmtree(tmp)
+    save("loader.npz", **arrs)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(4)
     gen_relshift()
     gen_lengths()
     gen_ctc_kl()
     gen_u2_step()
+    gen_loader()

@@ -10,6 +10,9 @@ from liteasr_amd import kernels as K
 from liteasr_amd._native import ACT_SWISH
 
 
+TORCH_REF = os.environ.get("GEMM_TORCH_REF", "1") == "1"
+
+
 def timeit(fn, iters=30):
     for _ in range(3):
         fn()
@@ -51,10 +54,20 @@ def case(name, M, N, Kd, layout="nt", out=torch.bfloat16, **kw):
         extra["beta"] = 1.0
     us = timeit(lambda: K.gemm(a, b, c, **extra))
     tf = 2 * M * N * Kd / us / 1e6
-    print(f"{name:38s} M={M:6d} N={N:5d} K={Kd:5d} {layout}  {us:8.1f} us  {tf:7.1f} TF/s", flush=True)
+    ref = ""
+    if TORCH_REF and not kw.get("split"):
+        # hipBLASLt (torch.matmul) on the same operands, plain product, same output dtype
+        cc = torch.empty(M, N, device=dev, dtype=out)
+        ut = timeit(lambda: torch.matmul(a, b, out=cc) if out == torch.bfloat16 else cc.copy_(a @ b))
+        ref = f"   torch {ut:8.1f} us"
+    print(f"{name:38s} M={M:6d} N={N:5d} K={Kd:5d} {layout}  {us:8.1f} us  {tf:7.1f} TF/s{ref}", flush=True)
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "fc1":
+        for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 1):
+            case("fc1 plain", 7968, 2048, 256, "nt")
+        sys.exit(0)
     case("square 4096 nt f32out", 4096, 4096, 4096, "nt", torch.float32)
     case("square 4096 nt bf16out", 4096, 4096, 4096, "nt")
     case("fc1 plain", 7968, 2048, 256, "nt")
