@@ -201,6 +201,8 @@ def main():
     ap.add_argument("--config", default="small", choices=sorted(CONFIGS))
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--graph", default="on", choices=["on", "off"],
+                    help="replay the step from hipGraphs (liteasr_amd/graph_step.py) or launch eagerly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", type=int, default=0, metavar="N",
@@ -243,12 +245,17 @@ def main():
     opt = Noam(model.parameters(), NoamConfig(model_dim=cfgd["d"]))
     batch = synthetic(cfgd, rank, dev)
 
-    def step():
-        loss = crit(net, *batch)
-        loss.backward()
-        opt.clip_and_step(5.0)
-        opt.zero_grad()
-        return loss
+    if args.graph == "on":
+        from liteasr_amd.graph_step import GraphedTrainStep
+
+        step = GraphedTrainStep(net, crit, opt, batch, clip=5.0, warmup=2)
+    else:
+        def step():
+            loss = crit(net, *batch)
+            loss.backward()
+            opt.clip_and_step(5.0)
+            opt.zero_grad()
+            return loss
 
     for _ in range(args.warmup):
         step()
@@ -284,7 +291,7 @@ def main():
                                 f"dec {cfgd['dec']}x, V {V}", "global_batch": world * cfgd["B"],
                        "per_gpu_batch": cfgd["B"], "seq_len": cfgd["T"], "label_len": cfgd["L"],
                        "ctc_weight": cfgd["w"], "dropout": args.dropout, "chunk_size": cfgd["chunk"],
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "launch": "hipgraph" if args.graph == "on" else "eager"},
             "step_tflops_per_gpu": round(cfgd["gflop"] * utt / world / 1e3, 2),
             "step_mfma_frac": round(cfgd["gflop"] * utt / world / 1e3 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(final_loss, 4), "optimizer_state": st,

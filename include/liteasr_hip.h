@@ -77,6 +77,10 @@ typedef struct lasr_gemm_args {
   float drop_p; uint64_t drop_seed;
   const void* res; int res_dtype; int64_t ldres; float res_scale;
   int split_k; void* workspace; int64_t workspace_bytes;
+  /* optional fused bias gradient: rowsum[m] += sum_k A[m,k] (fp32, batch == 1, A
+   * M-contiguous i.e. lda_m == 1: the dW = dY^T X GEMMs, rowsum = dbias).  Replaces the
+   * separate column sum of dY (aten sum over rows in Linear's backward). */
+  float* rowsum;
 } lasr_gemm_args;
 int lasr_gemm(const lasr_gemm_args* args, void* stream);
 int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k);

@@ -43,6 +43,7 @@ class GemmArgs(C.Structure):
         ("drop_p", _f), ("drop_seed", _u),
         ("res", _p), ("res_dtype", _i), ("ldres", _l), ("res_scale", _f),
         ("split_k", _i), ("workspace", _p), ("workspace_bytes", _l),
+        ("rowsum", _p),
     ]
 
 

@@ -85,6 +85,105 @@ __global__ void conv1_bwd_reduce_kernel(const float* part, int nparts, int C, fl
   else db[c] += s;
 }
 
+// Vectorised conv1 (C % 8 == 0, 256 % (C/8) == 0): a thread owns 8 consecutive channels
+// (their 8x10 weights in registers) and a strided set of output columns f1, so every
+// y1 / dy1 access is one 16-B (bf16) vector and a wave covers whole 512-B channel rows.
+// Same per-output arithmetic order as the scalar kernels above.
+template <typename T>
+__global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restrict__ x, int T_, int F,
+                                                           int C, int T1, int F1, const float* w,
+                                                           const float* bias, T* y1) {
+  extern __shared__ float xs[];  // the 3 contiguous input rows 2*t1 .. 2*t1+2
+  const int bt = blockIdx.x;
+  const int b = bt / T1, t1 = bt - b * T1;
+  const float* src = x + ((int64_t)b * T_ + 2 * t1) * F;
+  for (int i = threadIdx.x; i < 3 * F; i += 256) xs[i] = src[i];
+  const int CG = C >> 3, cg = threadIdx.x % CG, fg = threadIdx.x / CG, NFG = 256 / CG;
+  const int c0 = cg * 8;
+  float wr[8][9], bv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bv[q] = bias[c0 + q];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wr[q][k] = w[(c0 + q) * 9 + k];
+  }
+  __syncthreads();
+  T* out = y1 + (int64_t)bt * F1 * C + c0;
+  for (int f1 = fg; f1 < F1; f1 += NFG) {
+    float xv[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xs[kh * F + 2 * f1 + kw];
+    float o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float acc = bv[q];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc += wr[q][k] * xv[k];
+      o[q] = fmaxf(acc, 0.f);
+    }
+    st8(out + (int64_t)f1 * C, o);
+  }
+}
+
+constexpr int C1V_ROWS = 32;  // (b,t1) rows per vectorised conv1-bwd block
+template <typename T>
+__global__ __launch_bounds__(256) void conv1_bwd_v8_kernel(const float* __restrict__ x, int T_, int F,
+                                                           int C, int T1, int F1, int nrows,
+                                                           const T* __restrict__ dy1, float* part) {
+  extern __shared__ float sh[];  // C1V_ROWS x 3F input rows, then the 8*256 reduce slab
+  float* xs = sh;
+  float* red = sh + C1V_ROWS * 3 * F;
+  const int r0 = blockIdx.x * C1V_ROWS;
+  const int nr = min(C1V_ROWS, nrows - r0);
+  for (int i = threadIdx.x; i < nr * 3 * F; i += 256) {
+    const int rr = i / (3 * F), q = i - rr * 3 * F;
+    const int r = r0 + rr;
+    const int b = r / T1, t1 = r - b * T1;
+    xs[i] = x[((int64_t)b * T_ + 2 * t1) * F + q];
+  }
+  __syncthreads();
+  const int CG = C >> 3, cg = threadIdx.x % CG, fg = threadIdx.x / CG, NFG = 256 / CG;
+  const int c0 = cg * 8;
+  float acc[8][10];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[q][k] = 0.f;
+  for (int rr = 0; rr < nr; ++rr) {
+    const float* xr = xs + rr * 3 * F;
+    const T* d = dy1 + (int64_t)(r0 + rr) * F1 * C + c0;
+    for (int f1 = fg; f1 < F1; f1 += NFG) {
+      float g[8], xv[9];
+      ld8(d + (int64_t)f1 * C, g);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xr[kh * F + 2 * f1 + kw];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        acc[q][9] += g[q];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[q][k] += g[q] * xv[k];
+      }
+    }
+  }
+  // combine the NFG column groups in fixed order, one tap at a time (8 KB slab)
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[fg * C + c0 + q] = acc[q][k];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float t = 0.f;
+      for (int g2 = 0; g2 < NFG; ++g2) t += red[g2 * C + c];
+      part[((int64_t)blockIdx.x * 10 + k) * C + c] = t;
+    }
+    __syncthreads();
+  }
+}
+
 // ----------------------------- im2col / col2im ----------------------------------------
 template <typename T>
 __global__ void im2col_kernel(const T* __restrict__ y1, int B, int T1, int F1, int C, int T2,
@@ -426,6 +525,12 @@ extern "C" int lasr_conv1_fwd(const float* x, int B, int T, int F, int C, const 
   const size_t shm = (size_t)(3 * F + 10 * C) * sizeof(float);
   LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_conv1_fwd: too much LDS");
   hipStream_t st = (hipStream_t)stream;
+  if (C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)y1 & 15) == 0) {
+    const size_t shv = (size_t)3 * F * sizeof(float);
+    if (dt == LASR_F32) conv1_fwd_v8_kernel<float><<<B * T1, 256, shv, st>>>(x, T, F, C, T1, F1, w, bias, (float*)y1);
+    else conv1_fwd_v8_kernel<bf16_t><<<B * T1, 256, shv, st>>>(x, T, F, C, T1, F1, w, bias, (bf16_t*)y1);
+    return lasr_check_launch("conv1_fwd");
+  }
   if (dt == LASR_F32) conv1_fwd_kernel<float><<<B * T1, 256, shm, st>>>(x, T, F, C, T1, F1, w, bias, (float*)y1);
   else conv1_fwd_kernel<bf16_t><<<B * T1, 256, shm, st>>>(x, T, F, C, T1, F1, w, bias, (bf16_t*)y1);
   return lasr_check_launch("conv1_fwd");
@@ -435,12 +540,20 @@ extern "C" int lasr_conv1_bwd(const float* x, int B, int T, int F, int C, const 
                               float* dw, float* db, float* ws, int64_t ws_floats, void* stream) {
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const int nrows = B * T1;
-  const int nparts = (int)cdiv(nrows, C1B_ROWS);
+  const bool vec = C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)dy1 & 15) == 0 &&
+                   (size_t)(C1V_ROWS * 3 * F + 8 * 256) * sizeof(float) <= 64 * 1024;
+  const int nparts = (int)cdiv(nrows, vec ? C1V_ROWS : C1B_ROWS);
   LASR_CHECK_ARG(ws_floats >= (int64_t)(nparts + 1) * 10 * C, "lasr_conv1_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  const size_t shm = (size_t)C1B_ROWS * 3 * F * sizeof(float);
-  if (dt == LASR_F32) conv1_bwd_kernel<float><<<nparts, 256, shm, st>>>(x, T, F, C, T1, F1, nrows, (const float*)dy1, ws);
-  else conv1_bwd_kernel<bf16_t><<<nparts, 256, shm, st>>>(x, T, F, C, T1, F1, nrows, (const bf16_t*)dy1, ws);
+  if (vec) {
+    const size_t shv = (size_t)(C1V_ROWS * 3 * F + 8 * 256) * sizeof(float);
+    if (dt == LASR_F32) conv1_bwd_v8_kernel<float><<<nparts, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, (const float*)dy1, ws);
+    else conv1_bwd_v8_kernel<bf16_t><<<nparts, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, (const bf16_t*)dy1, ws);
+  } else {
+    const size_t shm = (size_t)C1B_ROWS * 3 * F * sizeof(float);
+    if (dt == LASR_F32) conv1_bwd_kernel<float><<<nparts, 256, shm, st>>>(x, T, F, C, T1, F1, nrows, (const float*)dy1, ws);
+    else conv1_bwd_kernel<bf16_t><<<nparts, 256, shm, st>>>(x, T, F, C, T1, F1, nrows, (const bf16_t*)dy1, ws);
+  }
   int rc = lasr_check_launch("conv1_bwd");
   if (rc) return rc;
   // partials [nparts][10][C] -> tot[10*C] (after the partials) -> dw[c*9+k], db[c]

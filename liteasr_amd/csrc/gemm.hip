@@ -51,6 +51,11 @@ struct GemmP {
   // aux/res, 16-B aligned and prefetched before the staging barrier, 2 = generic.
   int epi_mode;
   int bias_vec;
+  // rowsum[m] += sum_k A[m,k] (bias gradient of a dW = dY^T X GEMM): computed by the
+  // n-tile-0 blocks of the LDS-DMA kernel (A M-contiguous); split-K slices write
+  // partials to rs_ws[s*M + m], summed in fixed order by splitk_reduce_kernel.
+  float* rowsum;
+  float* rs_ws;
 };
 
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
@@ -518,6 +523,34 @@ LASR_DEV void frag_tr_raw(const bf16_t* tile, int rbase, int lane, v2i* r) {
   r[0] = ds_tr_asm(tile + tr_off<R_TILE>(8 * g + q, rbase + pc));
   r[1] = ds_tr_asm(tile + tr_off<R_TILE>(8 * g + 4 + q, rbase + pc));
 }
+typedef int v4i __attribute__((ext_vector_type(4)));
+LASR_DEV v4i ds_b128_asm(const bf16_t* p) {
+  v4i r;
+  const uint32_t a = (uint32_t)(uintptr_t)(lptr_t)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// Row sums of an M-contiguous A tile image ([32 k][BM], tr_off layout): thread owns the 8
+// rows 8*(tid % (BM/8)).. and k rows tid / (BM/8) + j * (256 / (BM/8)).
+template <int BM>
+LASR_DEV void rowsum_tile(const bf16_t* tile, int tid, float* rs) {
+  constexpr int CH = BM / 8, KG = 256 / CH, KR = 32 / KG;
+  const int c = tid % CH, k0 = tid / CH;
+  v4i r[KR];
+#pragma unroll
+  for (int j = 0; j < KR; ++j) r[j] = ds_b128_asm(tile + tr_off<BM>(k0 + j * KG, 8 * c));
+  if constexpr (KR == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]));
+  else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]));
+#pragma unroll
+  for (int j = 0; j < KR; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t u = (uint32_t)r[j][q];
+      rs[2 * q] += __uint_as_float(u << 16);
+      rs[2 * q + 1] += __uint_as_float(u & 0xffff0000u);
+    }
+}
+
 LASR_DEV bf16x8 frag_from_raw(const v2i* r) {
   const int __attribute__((ext_vector_type(4))) v = {r[0][0], r[0][1], r[1][0], r[1][1]};
   return __builtin_bit_cast(bf16x8, v);
@@ -625,6 +658,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   };
 
+  // fused bias gradient (rowsum of A) on the n-tile-0 blocks; uniform per block
+  const bool do_rs = !AKC && p.rowsum != nullptr && tx == 0;
+  float rs[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) rs[q] = 0.f;
+
 #pragma unroll
   for (int t = 0; t < S - 1; ++t)
     if (t < nfull) issue(t);
@@ -637,6 +676,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
     lds_barrier();
     if (kt + S - 1 < nfull) issue(kt + S - 1);
     compute(smem + (kt % S) * TILE);
+    if constexpr (!AKC)
+      if (do_rs) rowsum_tile<BM>(smem + (kt % S) * TILE, tid, rs);
   }
   if (nfull < nk) {  // ragged tail: register loader with zero fill
     __syncthreads();
@@ -649,8 +690,30 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
     lb.store(smem + BM * BK, tid);
     __syncthreads();
     compute(smem);
+    if constexpr (!AKC)
+      if (do_rs) rowsum_tile<BM>(smem, tid, rs);
   }
   __syncthreads();
+  if constexpr (!AKC) {
+    if (do_rs) {  // combine the k groups in fixed order, then one slot per row
+      constexpr int CH = BM / 8, KG = 256 / CH;
+      float* red = reinterpret_cast<float*>(smem_epi);
+      const int c = tid % CH, kg = tid / CH;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) red[kg * BM + 8 * c + q] = rs[q];
+      __syncthreads();
+      if (tid < BM) {
+        float t = 0.f;
+        for (int g = 0; g < KG; ++g) t += red[g * BM + tid];
+        const int m = m0 + tid;
+        if (m < p.M) {
+          if (p.split_k > 1) p.rs_ws[(int64_t)s * p.M + m] = t;
+          else p.rowsum[m] += t;
+        }
+      }
+      __syncthreads();
+    }
+  }
   gemm_epilogue<BM, BN, TC>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
 }
 
@@ -744,6 +807,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
     const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
     epi_store<TC>(p, z / p.batch_div, z % p.batch_div, z, m, n, acc, al);
   }
+  if (p.rs_ws) {  // bias-gradient partials (batch == 1)
+    for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < p.M; m += (int64_t)gridDim.x * 256) {
+      float acc = 0.f;
+      for (int s = 0; s < p.split_k; ++s) acc += p.rs_ws[(int64_t)s * p.M + m];
+      p.rowsum[m] += acc;
+    }
+  }
 }
 
 // ================================ host launcher ==================================
@@ -817,8 +887,9 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
     while (nb * split < 512 && split * 2 <= 32 && kt / (split * 2) >= 4) split *= 2;
   }
+  const int64_t rs_floats = a->rowsum ? (int64_t)split * a->M : 0;
   if (split > 1 && (!plain || !a->workspace ||
-                    a->workspace_bytes < (int64_t)split * batch * a->M * a->N * 4))
+                    a->workspace_bytes < ((int64_t)split * batch * a->M * a->N + rs_floats) * 4))
     split = 1;
   *BMo = BM;
   *BNo = BN;
@@ -842,8 +913,9 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   if (a->M == 0 || a->N == 0 || a->batch == 0) return LASR_OK;
   const int batch = a->batch > 0 ? a->batch : 1;
   const int bdiv = a->batch_div > 0 ? a->batch_div : 1;
-  LASR_CHECK_ARG(batch == 1 || (!a->aux && !a->res && !a->zout),
-                 "lasr_gemm: aux/res/zout only supported for batch == 1");
+  LASR_CHECK_ARG(batch == 1 || (!a->aux && !a->res && !a->zout && !a->rowsum),
+                 "lasr_gemm: aux/res/zout/rowsum only supported for batch == 1");
+  LASR_CHECK_ARG(!a->rowsum || a->lda_m == 1, "lasr_gemm: rowsum needs an M-contiguous A");
 
   GemmP p;
   p.M = a->M; p.N = a->N; p.K = a->K; p.batch = batch; p.batch_div = bdiv;
@@ -884,6 +956,8 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   const int kstep = bf ? 32 : 16;
   p.kchunk = split > 1 ? (int)(cdiv(cdiv(a->K, split), kstep) * kstep) : a->K;
   p.ws = (float*)a->workspace;
+  p.rowsum = nullptr;
+  p.rs_ws = nullptr;
 
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM), (unsigned)(batch * split));
@@ -894,13 +968,24 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   const int64_t M8 = cdiv(a->M, 8) * 8, N8 = cdiv(a->N, 8) * 8;
   const bool glds = bf && p.a_vec && p.b_vec && (akc || a->lda_k >= M8) && (bkc || a->ldb_k >= N8) &&
                     (int64_t)grid.x * grid.y < (1ll << 31) && !getenv_flag("LASR_GEMM_NO_GLDS");
+  // fused bias gradient: in the LDS-DMA kernel when A is M-contiguous, else a column sum
+  const bool rs_fused = a->rowsum && glds && !akc && a->split_k >= 0;
+  if (rs_fused) {
+    p.rowsum = a->rowsum;
+    if (split > 1) p.rs_ws = p.ws + (int64_t)split * batch * a->M * a->N;
+  }
   if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, glds, grid, st);
   else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, glds, grid, st);
   int rc = lasr_check_launch("lasr_gemm");
-  if (rc || split == 1 || a->split_k < 0) return rc;  // split_k < 0: leave the partials
-  const int64_t total = (int64_t)a->M * a->N * batch;
-  const int nblk = (int)std::min<int64_t>(cdiv(total, 256), 4096);
-  if (a->c_dtype == LASR_F32) splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);
-  else splitk_reduce_kernel<bf16_t><<<nblk, 256, 0, st>>>(p);
-  return lasr_check_launch("lasr_gemm/splitk_reduce");
+  if (!rc && split > 1 && a->split_k >= 0) {
+    const int64_t total = (int64_t)a->M * a->N * batch;
+    const int nblk = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+    if (a->c_dtype == LASR_F32) splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);
+    else splitk_reduce_kernel<bf16_t><<<nblk, 256, 0, st>>>(p);
+    rc = lasr_check_launch("lasr_gemm/splitk_reduce");
+  }
+  if (rc || !a->rowsum || rs_fused) return rc;
+  // unfused: rowsum of A[M, K] (lda_m == 1) = column sums of the [K, M] matrix, ld lda_k
+  return lasr_colsum(a->A, a->in_dtype, a->K, a->M, a->lda_k, a->rowsum, 1, (float*)a->workspace,
+                     a->workspace_bytes / 4, stream);
 }

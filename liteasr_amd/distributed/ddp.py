@@ -119,18 +119,27 @@ class FlatReducer:
 
     def _launch(self, bi):
         g = self._slice(self.buckets[bi])
-        if g.is_cuda:
+        if g.is_cuda and dist.get_backend(self.pg) == "nccl":
             w = dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
         else:  # gloo (CPU plumbing tests): SUM then scale
             w = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         self.works.append((w, g))
+
+    def allreduce_all(self):
+        """Average the whole flat grad buffer now, bucket by bucket (used between the two
+        graphs of liteasr_amd.graph_step: the exchange is never captured)."""
+        self._reset()
+        for bi in range(len(self.buckets)):
+            self._launch(bi)
+        self.next_bucket = len(self.buckets)
+        self._finalize()
 
     def _finalize(self):
         for bi in range(self.next_bucket, len(self.buckets)):  # units that never fired
             self._launch(bi)
         for w, g in self.works:
             w.wait()
-            if not g.is_cuda:
+            if not (g.is_cuda and dist.get_backend(self.pg) == "nccl"):
                 g.div_(self.world)
         self._reset()
 

@@ -91,6 +91,7 @@ def gemm(
     res: Optional[torch.Tensor] = None,
     res_scale: float = 1.0,
     split_k: int = 1,
+    rowsum: Optional[torch.Tensor] = None,
     plan_only: bool = False,
 ):
     """c = epilogue(alpha * a @ b) for logical views a (..,M,K), b (..,K,N), c (..,M,N).
@@ -133,8 +134,14 @@ def gemm(
     if res is not None:
         args.res, args.res_dtype, args.ldres, args.res_scale = ptr(res), dt(res), res.stride(0), res_scale
     args.split_k = split_k
-    if split_k != 1:
-        need = 64 * z1 * z2 * M * Nn if split_k <= 0 else split_k * z1 * z2 * M * Nn
+    if rowsum is not None:
+        # fused bias gradient rowsum[m] += sum_k a[m, k] (fp32, a M-contiguous)
+        assert rowsum.dtype == torch.float32 and rowsum.is_contiguous() and rowsum.numel() == M
+        assert z1 * z2 == 1 and a_m == 1, "rowsum needs batch 1 and an M-contiguous A"
+        args.rowsum = ptr(rowsum)
+    if split_k != 1 or rowsum is not None:
+        ns = 64 if split_k <= 0 else split_k
+        need = ns * z1 * z2 * M * Nn + (ns + 128) * M if rowsum is not None else ns * z1 * z2 * M * Nn
         ws = WS.get(need, c.device)
         args.workspace, args.workspace_bytes = ptr(ws), ws.numel() * 4
     if plan_only:

@@ -71,12 +71,10 @@ def ffn_backward(gb, ln, z, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
     """gb: gradient of the FFN output (after the residual-branch dropout/scale)."""
     M = gb.shape[0]
     dev, adt = gb.device, gb.dtype
-    K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0)
-    K.colsum(gb, gb2)
+    K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0, rowsum=gb2)
     dz = _e((M, W1.shape[0]), adt, dev)
     K.gemm(gb, W2, dz, aux=z, aux_act=act, drop_p=p_ff, drop_seed=s_ff)
-    K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0)
-    K.colsum(dz, gb1)
+    K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
     dln = _e((M, W1.shape[1]), adt, dev)
     K.gemm(dz, W1, dln)
     return dln
@@ -135,8 +133,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     M = B * T
     scale = dk ** -0.5
     ldS = ld_scores(T)
-    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0)
-    K.colsum(gb, g.bo)
+    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo)
     dctx = _e((M, d), adt, dev)
     K.gemm(gb, w.Wo, dctx)
     dctx4 = _heads(dctx, B, T, H, dk)
@@ -164,8 +161,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     K.reduce_batch(dpb, B, H, T, dk, dp)
     K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
     K.gemm(dp.t(), pos, g.Wpos, beta=1.0)
-    K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0)
-    K.colsum(dqkv, g.bqkv)
+    K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv)
     dln = _e((M, d), adt, dev)
     K.gemm(dqkv, w.Wqkv, dln)
     return dln
@@ -215,8 +211,7 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
     R = B * Tq
     scale = dk ** -0.5
     ldS = ld_scores(Tk)
-    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0)
-    K.colsum(gb, g.bo)
+    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo)
     dctx = _e((R, d), adt, dev)
     K.gemm(gb, w.Wo, dctx)
     dctx4 = _heads(dctx, B, Tq, H, dk)
@@ -245,15 +240,12 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
     K.gemm(dS[..., :Tk].transpose(-1, -2), q4, dk4, alpha=scale)
     dln = _e((R, d), adt, dev)
     if mem is None:
-        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0)
-        K.colsum(dqkv, g.bqkv)
+        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv)
         K.gemm(dqkv, w.Wqkv, dln)
     else:
-        K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0)
-        K.colsum(dq, g.bq)
+        K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq)
         K.gemm(dq, w.Wq, dln)
-        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0)
-        K.colsum(dkv, g.bkv)
+        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv)
         K.gemm(dkv, w.Wkv, dmem, beta=1.0)
     return dln
 
@@ -283,16 +275,14 @@ def conv_backward(gb, ln, sv, w, g, env):
     B, T = env.B, env.T
     M, d = ln.shape
     dev, adt = ln.device, ln.dtype
-    K.gemm(gb.t(), sv.h3, g.Wpw2, beta=1.0, split_k=0)
-    K.colsum(gb, g.bpw2)
+    K.gemm(gb.t(), sv.h3, g.Wpw2, beta=1.0, split_k=0, rowsum=g.bpw2)
     dh3 = _e((M, d), adt, dev)
     K.gemm(gb, w.Wpw2, dh3)
     dy = _e((M, d), F32, dev)
     K.bn_swish_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy)
     dz1 = _e((M, 2 * d), adt, dev)
     K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
-    K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0)
-    K.colsum(dz1, g.bpw1)
+    K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0, rowsum=g.bpw1)
     dln = _e((M, d), adt, dev)
     K.gemm(dz1, w.Wpw1, dln)
     return dln
@@ -341,16 +331,14 @@ class EmbedFn(torch.autograd.Function):
         K.branch_grad(dx0.contiguous(), gb, math.sqrt(d), env.p_pos, env.seed + 1)
         y2f = sv.y2.view(M, F2 * C)
         dWo = _e((d, F2 * C), F32, dev)
-        K.gemm(gb.t(), y2f, dWo, split_k=0)
+        K.gemm(gb.t(), y2f, dWo, split_k=0, rowsum=g.bout)
         K.permute_last2(dWo, d, C, F2, g.out_w, reverse=True, accumulate=True)
-        K.colsum(gb, g.bout)
         dy2 = _e((M, F2 * C), adt, dev)
         K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
         dy2 = dy2.view(M * F2, C)
         dW2 = _e((C, 9 * C), F32, dev)
-        K.gemm(dy2.t(), sv.col, dW2, split_k=0)
+        K.gemm(dy2.t(), sv.col, dW2, split_k=0, rowsum=g.b2)
         K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
-        K.colsum(dy2, g.b2)
         dcol = _e((M * F2, 9 * C), adt, dev)
         K.gemm(dy2, w.W2p, dcol)
         dy1 = torch.empty_like(sv.y1)
@@ -513,8 +501,7 @@ class HeadsFn(torch.autograd.Function):
         wc, gc = model.ctc.weights(), model.ctc.grads()
         if g_ctc is not None:
             g_ctc = _rows2d(g_ctc, M)
-            K.gemm(g_ctc.t(), sv.hd, gc.W, beta=1.0, split_k=0)
-            K.colsum(g_ctc, gc.b)
+            K.gemm(g_ctc.t(), sv.hd, gc.W, beta=1.0, split_k=0, rowsum=gc.b)
             dhd = _e((M, d_enc), F32, dev)
             K.gemm(g_ctc, wc.W, dhd)
             K.branch_grad(dhd, dh, 1.0, env.p_ctc, env.seed + 2)
@@ -526,8 +513,7 @@ class HeadsFn(torch.autograd.Function):
         d = wd.d
         if g_attn is not None:
             g_attn = _rows2d(g_attn, R)
-            K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0)
-            K.colsum(g_attn, gd.bout)
+            K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0, rowsum=gd.bout)
             dyf = _e((R, d), adt, dev)
             K.gemm(g_attn, wd.Wout, dyf)
             dy = _e((R, d), F32, dev)

@@ -177,6 +177,35 @@ def test_gemm_splitk_and_batched(dtype):
     close(S[..., :T], q.double() @ p.double().transpose(-1, -2), 1e-5 if dtype == torch.float32 else 1e-2, "bcast")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("R,M,N,split", [(7968, 256, 2048, 0), (7968, 2048, 256, 0), (3001, 96, 160, 0),
+                                         (517, 64, 80, 1), (20000, 768, 256, 0), (333, 130, 40, 1)])
+def test_gemm_fused_rowsum(dtype, R, M, N, split):
+    """dW GEMM with the fused bias gradient: rowsum[m] += sum_k dY^T[m, k] (split-K
+    partials summed by the reduce kernel, or written directly without split; fallback
+    column sum on the non-LDS-DMA paths)."""
+    kn = K()
+    g = torch.Generator().manual_seed(R + M + N)
+    dy = torch.randn(R, M, generator=g).to(DEV, dtype)
+    x = torch.randn(R, N, generator=g).to(DEV, dtype)
+    dw = torch.randn(M, N, generator=g).to(DEV)
+    db = torch.randn(M, generator=g).to(DEV)
+    dw0, db0 = dw.double().cpu(), db.double().cpu()
+    kn.gemm(dy.t(), x, dw, beta=1.0, split_k=split, rowsum=db)
+    close(dw, dw0 + dy.double().cpu().t() @ x.double().cpu(), 1e-5 if dtype == torch.float32 else 1e-2, "dW")
+    ref_b = db0 + dy.double().cpu().sum(0)
+    close(db, ref_b, 1e-5, "db")
+    # padded-vocab view (row stride 4240 > M = 4233)
+    if R == 3001:
+        V = 4233
+        gl = torch.full((R, 4240), float("nan"), dtype=dtype, device=DEV)[:, :V]
+        gl.copy_(torch.randn(R, V, generator=g))
+        dW = torch.zeros(V, N, device=DEV)
+        bv = torch.zeros(V, device=DEV)
+        kn.gemm(gl.t(), x, dW, beta=1.0, split_k=0, rowsum=bv)
+        close(bv, gl.double().cpu().sum(0), 1e-5, "padded db")
+
+
 def test_gemm_dropout_matches_branch_grad():
     kn = K()
     M, N, Kd = 128, 256, 64

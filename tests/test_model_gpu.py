@@ -226,3 +226,96 @@ def test_dropout_train_step_runs_and_is_deterministic():
     assert math.isfinite(losses[0]) and losses[0] == losses[1]
     l3 = crit(model, xs, xlens, ys, ylens).item()  # counter advanced -> new masks
     assert l3 != losses[0]
+
+
+def _graph_setup(dropout):
+    from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+    from liteasr_amd.optims.noam import Noam, NoamConfig
+
+    params = O.init_params(TINY, seed=3)
+    model = build(TINY, "bf16", dropout=dropout)
+    model.load_state_dict({**params, **O.init_buffers(TINY)}, strict=False)
+    model = model.cuda().train()
+    crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=30, smoothing=0.1, ctc_weight=0.3))
+    opt = Noam(model.parameters(), NoamConfig(model_dim=64, warmup=10))
+    return model, crit, opt
+
+
+def test_graphed_step_matches_eager():
+    """liteasr_amd.graph_step: a replayed hipGraph step (fwd+loss+bwd+clip+Noam/Adam+zero_grad,
+    dropout on) is bit-identical to the same steps launched eagerly (deterministic
+    kernels, device-side dropout counter and optimizer state)."""
+    from liteasr_amd.graph_step import GraphedTrainStep
+
+    batches = [[t.cuda() for t in O.synthetic_batch(3, 120, 6, 30, seed=10 + i)] for i in range(4)]
+    m1, c1, o1 = _graph_setup(0.1)
+    eager = []
+    for b in batches:
+        l = c1(m1, *b)
+        l.backward()
+        o1.clip_and_step(5.0)
+        o1.zero_grad()
+        eager.append(l.item())
+    m2, c2, o2 = _graph_setup(0.1)
+    gs = GraphedTrainStep(m2, c2, o2, batches[0], clip=5.0, warmup=1)  # warm-up = eager step 1
+    graphed = [gs(b).item() for b in batches[1:]]
+    assert graphed == eager[1:], (graphed, eager)
+    assert torch.equal(m1.store.flat, m2.store.flat)
+    assert o1.device_state() == o2.device_state()
+
+
+def _ddp_graph_worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from liteasr_amd.distributed.ddp import DistributedDataParallel
+        from liteasr_amd.graph_step import GraphedTrainStep
+
+        out = {}
+        for mode in ("eager", "graph"):
+            m, c, o = _graph_setup(0.0)
+            net = DistributedDataParallel(m)
+            bs = [[t.cuda() for t in O.synthetic_batch(2, 100, 5, 30, seed=50 + 7 * rank + i)] for i in range(3)]
+            losses = []
+            if mode == "eager":
+                for b in bs:
+                    l = c(net, *b)
+                    l.backward()
+                    o.clip_and_step(5.0)
+                    o.zero_grad()
+                    losses.append(l.item())
+            else:
+                gs = GraphedTrainStep(net, c, o, bs[0], clip=5.0, warmup=1)
+                losses = [float("nan")] + [gs(b).item() for b in bs[1:]]
+            out[mode] = (losses, m.store.flat.double().cpu())
+        le, fe = out["eager"]
+        lg, fg = out["graph"]
+        ok = max(abs(a - b) / abs(a) for a, b in zip(le[1:], lg[1:])) < 1e-5 and \
+            (fe - fg).abs().max().item() <= 1e-6 * fe.abs().max().item()
+        q.put((rank, ok, le, lg))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, False, repr(e), None))
+
+
+def test_graphed_step_ddp_two_ranks_gloo():
+    """Split-graph DDP step (graph 1 fwd/bwd, eager bucketed all-reduce, graph 2 update) vs
+    the eager DDP step with hook-driven bucket all-reduce: 2 ranks sharing the one GPU,
+    gloo backend (RCCL cannot put two ranks on one device)."""
+    import multiprocessing as mp
+    import random
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    ps = [ctx.Process(target=_ddp_graph_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, ok, le, lg in res:
+        assert ok, (rank, le, lg)
