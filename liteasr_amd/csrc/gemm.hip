@@ -16,6 +16,12 @@
 // ctc.py:29, transformer_decoder.py:91 (and their autograd backward GEMMs).
 #include "common.h"
 
+// Ablation hooks for GEMM experiments (tools/gemm_exp.sh); 0 in every product build.
+// bit 1: skip the MFMAs, bit 2: skip the epilogue stores, bit 4: skip the glds loads.
+#ifndef LASR_EXP
+#define LASR_EXP 0
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -56,6 +62,7 @@ struct GemmP {
   // partials to rs_ws[s*M + m], summed in fixed order by splitk_reduce_kernel.
   float* rowsum;
   float* rs_ws;
+  int v4;  // direct epilogue: 4-wide C/zout/aux/res/bias/ws access allowed (host-checked)
 };
 
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
@@ -96,6 +103,7 @@ LASR_DEV void ld_any8(const void* base, int dt, int64_t idx, bool vec, int cnt, 
 }
 template <typename T>
 LASR_DEV void st_8(T* dst, const float* v, bool vec, int cnt) {
+  if ((LASR_EXP & 2) && v[0] != 1234.5f) return;
   if (vec && cnt == 8) st8(dst, v);
   else {
 #pragma unroll
@@ -291,7 +299,7 @@ LASR_DEV bf16x8 frag(const bf16_t* tile, int rbase, int lane) {
 // fp32) through LDS, then every thread finishes 8 contiguous columns of a row with 16-B
 // loads/stores (or writes its split-K partial).  The caller has passed a barrier after its
 // last LDS read of the main loop.
-template <int BM, int BN, typename TC>
+template <int BM, int BN, typename TC, bool TRANS = false>
 LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem_epi, int m0,
                             int n0, int s, int z, int z1, int z2) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
@@ -346,12 +354,21 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
     };
     prefetch(0);
     if (wr == h) {
+      if constexpr (TRANS) {
+        // C^T fragments: lane owns row cl, columns rq..rq+3 -> one 16-B LDS write each
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+          for (int j = 0; j < FN; ++j)
+            *(f32x4*)(cs + (i * 16 + cl) * LDC + wc * WN + j * 16 + rq) = acc[i][j];
+      } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) cs[(i * 16 + rq + e) * LDC + wc * WN + j * 16 + cl] = acc[i][j][e];
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cs[(i * 16 + rq + e) * LDC + wc * WN + j * 16 + cl] = acc[i][j][e];
+      }
     }
     __syncthreads();
     if (fast) {
@@ -462,6 +479,123 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
   }
 
   gemm_epilogue<BM, BN, TC>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
+}
+
+// Epilogue of 4 consecutive columns n..n+3 of row m (same order as epi_store8); cnt < 4 or
+// !vec -> element-wise tail.
+template <typename TC, bool VEC>
+LASR_DEV void epi_store4(const GemmP& p, int z1, int z2, int z, int m, int n, int cnt, const float* acc,
+                         float al) {
+  float v[4], t[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = acc[q] * al;
+  if (p.bias) {
+    if (VEC) {
+      ldv<4>(p.bias + n, t);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = q < cnt ? p.bias[n + q] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] += t[q];
+  }
+  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
+  auto st4 = [&](TC* dst, const float* x) {
+    if (VEC) stv<4>(dst, x);
+    else
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < cnt) dst[q] = from_f<TC>(x[q]);
+  };
+  auto ld4 = [&](const void* base, int dtp, int64_t idx, float* o) {
+    if (VEC) {
+      if (dtp == LASR_F32) ldv<4>((const float*)base + idx, o);
+      else ldv<4>((const bf16_t*)base + idx, o);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = q < cnt ? load_any(base, dtp, idx + q) : 0.f;
+    }
+  };
+  if (p.zout) st4((TC*)p.zout + cidx, v);
+  if (p.act == LASR_ACT_RELU) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+  } else if (p.act == LASR_ACT_SWISH) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = swishf(v[q]);
+  }
+  if (p.aux) {
+    ld4(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, t);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] *= (p.aux_act == LASR_ACT_RELU) ? (t[q] > 0.f ? 1.f : 0.f) : swish_grad(t[q]);
+  }
+  if (p.drop.p > 0.f) {
+    const uint64_t base = ((uint64_t)z * p.M + m) * (uint64_t)p.N + n;
+    const uint32_t key = drop_key(p.drop);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] *= drop_mul_k(p.drop, key, base + q);
+  }
+  if (p.res) {
+    ld4(p.res, p.res_dtype, (int64_t)m * p.ldres + n, t);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = t[q] + p.res_scale * v[q];
+  }
+  TC* C = (TC*)p.C + cidx;
+  if (p.beta != 0.f) {
+    ld4(C, sizeof(TC) == 4 ? LASR_F32 : LASR_BF16, 0, t);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] += p.beta * t[q];
+  }
+  if ((LASR_EXP & 2) && v[0] != 1234.5f) return;
+  st4(C, v);
+}
+
+// Epilogue straight from the accumulators, no LDS and no barrier.  The main loop issues
+// the MFMAs with the operands swapped (D = B-frag x A-frag), so acc[i][j] is a fragment of
+// C^T: lane l owns row m = mb + (l & 15) and the 4 consecutive columns nb + 4 (l >> 4) + e
+// -> one 8-B (bf16) / 16-B (fp32) access per 4 outputs (a wave instruction covers 16 rows
+// x 32 / 64 contiguous bytes; the L2 merges the row segments before write-back).
+template <int BM, int BN, typename TC>
+LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], int m0, int n0, int s,
+                                   int z, int z1, int z2) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const float al = alpha_of(p);
+  const int mr = m0 + wr * WM + (lane & 15), nc = n0 + wc * WN + 4 * (lane >> 4);
+  if (p.split_k > 1) {
+    float* wsp = p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = mr + i * 16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = nc + j * 16;
+        if (n >= p.N) continue;
+        float* dst = wsp + (int64_t)m * p.N + n;
+        const float a[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (p.v4 && n + 4 <= p.N) stv<4>(dst, a);
+        else
+          for (int q = 0; q < 4 && n + q < p.N; ++q) dst[q] = a[q];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = mr + i * 16;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nc + j * 16;
+      if (n >= p.N) continue;
+      const float a[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (p.v4 && n + 4 <= p.N) epi_store4<TC, true>(p, z1, z2, z, m, n, 4, a, al);
+      else epi_store4<TC, false>(p, z1, z2, z, m, n, min(4, p.N - n), a, al);
+    }
+  }
 }
 
 // ---------------- bf16 kernel, LDS-DMA pipeline (16-B aligned operands) ----------------
@@ -583,11 +717,11 @@ LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0,
 }
 
 template <int BM, int BN, bool AKC, bool BKC, typename TC, int S>
-__global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
+__global__ __launch_bounds__(256, 3) void gemm_bf16_glds_kernel(GemmP p) {
   constexpr int BK = 32;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int TILE = (BM + BN) * BK;  // elements per ring stage
-  constexpr int MAIN_BYTES = S * TILE * 2;
+  constexpr int MAIN_BYTES = S * TILE * 2;  // >= the rowsum combine slab (256/(BM/8) x BM floats)
   constexpr int EPI_BYTES = WM * (BN + 4) * 4;
   constexpr int GL = (BM + BN) * 4 / 256;  // glds per thread per k tile
   __shared__ __attribute__((aligned(16))) char smem_epi[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
@@ -625,6 +759,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
   auto issue = [&](int t) {
     bf16_t* dst = smem + (t % S) * TILE;
     const int k0 = kbeg + t * BK;
+    if (LASR_EXP & 4) return;
     glds_tile<BM, AKC>(A, lda, m0, p.M, k0, dst, tid);
     glds_tile<BN, BKC>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
   };
@@ -651,11 +786,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) bfr[j] = frag_from_raw(rb + 2 * j);
     }
+    if (LASR_EXP & 1) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) acc[i][0][0] += (float)af[i][0] + (float)bfr[0][i & 1];
+      return;
+    }
+    // swapped operands: acc[i][j] accumulates the C^T fragment (gemm_epilogue_direct)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
   };
 
   // fused bias gradient (rowsum of A) on the n-tile-0 blocks; uniform per block
@@ -714,7 +855,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmP p) {
       __syncthreads();
     }
   }
-  gemm_epilogue<BM, BN, TC>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
+  // split-K partials: fp32, 16-B per lane straight from the accumulators; final outputs:
+  // staged through LDS (full 256-B rows per wave store)
+  if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC>(p, acc, m0, n0, s, z, z1, z2);
+  else gemm_epilogue<BM, BN, TC, true>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
 }
 
 // ============================ fp32 MFMA kernel ===================================
@@ -872,9 +1016,10 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     BM = a->M >= 96 ? 128 : 64;
     BN = a->N >= 96 ? 128 : 64;
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
-    // >= 512 workgroups (2 per CU) with >= 8 k tiles per slice (in-model best: fewer
-    // slices starve the 4- and 12-tile dW GEMMs of the attention/conv projections)
-    while (nb * split < 512 && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
+    // >= 256 workgroups (one per CU; the 3-wave launch bound co-schedules the other
+    // GEMMs' blocks) with >= 8 k tiles per slice; fewer slices = less partial traffic
+    // (gemm_bench: dW fc1 split 8 29.6 us vs 16 35.4 us)
+    while (nb * split < 256 && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
   } else if (bf) {
     const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
     for (int c = 0; c < 4; ++c) {
@@ -943,6 +1088,19 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   p.res_vec = a->res && aligned16(a->res) && a->ldres % 8 == 0;
   p.ws_vec = a->N % 8 == 0;
   p.bias_vec = a->bias && aligned16(a->bias);
+  {
+    // 4-wide accesses of the direct epilogue: every row start 4-element aligned and the
+    // bases aligned to 4 elements' bytes (8 B bf16, 16 B fp32)
+    auto al4 = [](const void* q, int dtp) {
+      return ((uintptr_t)q & (dtp == LASR_F32 ? 15 : 7)) == 0;
+    };
+    const int cdt = a->c_dtype;
+    p.v4 = a->N % 4 == 0 && a->ldc % 4 == 0 && a->sc1 % 4 == 0 && a->sc2 % 4 == 0 && al4(a->C, cdt) &&
+           (!a->zout || al4(a->zout, cdt)) && (!a->bias || aligned16(a->bias)) &&
+           (!a->aux || (a->ldaux % 4 == 0 && al4(a->aux, a->aux_dtype))) &&
+           (!a->res || (a->ldres % 4 == 0 && al4(a->res, a->res_dtype))) &&
+           (!a->workspace || aligned16(a->workspace));
+  }
   {
     const int nsrc = (a->aux ? 1 : 0) + (a->res ? 1 : 0);
     const bool base_ok = p.c_vec && a->beta == 0.f;
