@@ -84,6 +84,9 @@ typedef struct lasr_gemm_args {
 } lasr_gemm_args;
 int lasr_gemm(const lasr_gemm_args* args, void* stream);
 int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k);
+/* Tuning hook: force the bf16 LDS-DMA tile (64/128/256 x 64/128/256) of every later
+ * lasr_gemm call in the process; (0, 0) restores the planner.  Benchmarks only. */
+int lasr_gemm_force_tile(int tile_m, int tile_n);
 
 /* Column sums: out[n] (+)= sum_m X[m,n]  (bias gradients; fp32 out).
  * Two-pass deterministic; workspace >= ceil(M/rows_per_block)*N floats (see impl). */

@@ -228,7 +228,7 @@ LASR_DEV uint4 load8(const bf16_t* src, int start, int lim, bool vec) {
 //     distinct 32-B bank groups (conflict-free); fragments read with 2 transposed reads.
 template <int R_TILE>
 LASR_DEV int htr(int k) {
-  return R_TILE == 128 ? ((k & 3) | ((k >> 1) & 4)) : (((k >> 1) & 1) | ((k >> 2) & 2));
+  return R_TILE >= 128 ? ((k & 3) | ((k >> 1) & 4)) : (((k >> 1) & 1) | ((k >> 2) & 2));
 }
 template <int R_TILE>
 LASR_DEV int tr_off(int k, int col) {  // element offset of (k, col), col % 4 == 0
@@ -617,6 +617,7 @@ LASR_DEV void wait_vmcnt() {
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else static_assert(N < 0, "unsupported vmcnt");
 }
 LASR_DEV void lds_barrier() {
@@ -647,6 +648,10 @@ LASR_DEV void tie_lgkm(v2i* r) {
   else if constexpr (N == 8)
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]),
                  "+v"(r[5]), "+v"(r[6]), "+v"(r[7]));
+  else if constexpr (N == 16)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]),
+                 "+v"(r[5]), "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]),
+                 "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15]));
   else
     static_assert(N < 0, "tie_lgkm: unsupported count");
 }
@@ -674,7 +679,8 @@ LASR_DEV void rowsum_tile(const bf16_t* tile, int tid, float* rs) {
 #pragma unroll
   for (int j = 0; j < KR; ++j) r[j] = ds_b128_asm(tile + tr_off<BM>(k0 + j * KG, 8 * c));
   if constexpr (KR == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]));
-  else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]));
+  else if constexpr (KR == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]));
+  else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]));
 #pragma unroll
   for (int j = 0; j < KR; ++j)
 #pragma unroll
@@ -716,8 +722,8 @@ LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0,
   }
 }
 
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S>
-__global__ __launch_bounds__(256, 3) void gemm_bf16_glds_kernel(GemmP p) {
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3>
+__global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
   constexpr int BK = 32;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int TILE = (BM + BN) * BK;  // elements per ring stage
@@ -964,7 +970,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
 template <bool AKC, bool BKC, typename TC>
 static void launch_bf16(const GemmP& p, int BM, int BN, bool glds, dim3 grid, hipStream_t st) {
   if (glds) {
-    if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
+    if (BM == 256 && BN == 256) gemm_bf16_glds_kernel<256, 256, AKC, BKC, TC, 3, 1><<<grid, 256, 0, st>>>(p);
+    else if (BM == 256) gemm_bf16_glds_kernel<256, 128, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
+    else if (BN == 256) gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
+    else if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
     else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
     else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
     else gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
@@ -1002,6 +1011,20 @@ static bool getenv_flag(const char* name) {
   return cached == 1;
 }
 
+// Tuning hook (tools/gemm_graph_bench.py): force the LDS-DMA tile of every later call;
+// 0 = the planner's choice.  Process-wide, not for product use.
+static int g_tile_m = 0, g_tile_n = 0;
+extern "C" int lasr_gemm_force_tile(int tile_m, int tile_n) {
+  const bool ok = (tile_m == 0 && tile_n == 0) ||
+                  ((tile_m == 64 || tile_m == 128 || tile_m == 256) &&
+                   (tile_n == 64 || tile_n == 128 || tile_n == 256) && (tile_m < 256 || tile_n >= 128) &&
+                   (tile_n < 256 || tile_m >= 128));
+  LASR_CHECK_ARG(ok, "lasr_gemm_force_tile: unsupported tile");
+  g_tile_m = tile_m;
+  g_tile_n = tile_n;
+  return LASR_OK;
+}
+
 // Tile and split-K choice for one call (shared by lasr_gemm and lasr_gemm_plan).
 static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) {
   const int batch = a->batch > 0 ? a->batch : 1;
@@ -1027,10 +1050,17 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
       BM = cfg[c][0]; BN = cfg[c][1];
       if (nb >= 512) break;
     }
+    // very large outputs with long K (subsampling conv2: M 151k, N 256, K 2304): the
+    // 128x256 tile halves the A re-reads (tile sweep: 237 vs 266 us)
+    if (BM == 128 && BN == 128 && a->N >= 256 && a->K >= 1024 && cdiv(a->M, 128) * batch >= 2048) BN = 256;
   }
   if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
     while (nb * split < 512 && split * 2 <= 32 && kt / (split * 2) >= 4) split *= 2;
+  }
+  if (bf && g_tile_m) {
+    BM = g_tile_m;
+    BN = g_tile_n;
   }
   const int64_t rs_floats = a->rowsum ? (int64_t)split * a->M : 0;
   if (split > 1 && (!plain || !a->workspace ||
@@ -1118,14 +1148,18 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   p.rs_ws = nullptr;
 
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM), (unsigned)(batch * split));
-  LASR_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lasr_gemm: grid too large");
   // LDS-DMA path: 16-B aligned rows/columns; for a non-K-contiguous operand the row stride
   // covers the extent rounded up to 8 (a 16-B chunk never leaves its row; the padding
   // columns only feed discarded outputs).
   const int64_t M8 = cdiv(a->M, 8) * 8, N8 = cdiv(a->N, 8) * 8;
   const bool glds = bf && p.a_vec && p.b_vec && (akc || a->lda_k >= M8) && (bkc || a->ldb_k >= N8) &&
-                    (int64_t)grid.x * grid.y < (1ll << 31) && !getenv_flag("LASR_GEMM_NO_GLDS");
+                    !getenv_flag("LASR_GEMM_NO_GLDS");
+  if (!glds) {  // 256-wide tiles exist only in the LDS-DMA kernel
+    BM = std::min(BM, 128);
+    BN = std::min(BN, 128);
+  }
+  dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM), (unsigned)(batch * split));
+  LASR_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lasr_gemm: grid too large");
   // fused bias gradient: in the LDS-DMA kernel when A is M-contiguous, else a column sum
   const bool rs_fused = a->rowsum && glds && !akc && a->split_k >= 0;
   if (rs_fused) {
