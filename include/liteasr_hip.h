@@ -184,6 +184,31 @@ int lasr_attn_softmax_bwd(const void* P, int pdt, const float* dPd, int B, int H
 /* Inverse of rel_shift: dBD[z,r,c] = dS[z,i,j] for the unique (i,j) that reads
  * BD[r,c] in attention.py:99-118, else 0. */
 int lasr_relshift_bwd(const void* dS, int dt, int Z, int T, int ldS, void* dBD, void* stream);
+/* Fused relative-position self-attention, bf16, d_k = 64, Tq = Tk = T, no attention
+ * dropout (liteasr/nets/attention.py:120-154 with rel_shift :99-118; replaces the
+ * materialised-score chain qu.k^T, qv.p^T, lasr_attn_softmax_fwd, P.V).
+ *   qu, qv   [B*T, ldq]  (q + pos_bias_u / v, lasr_qbias_fwd), head h at column h*64
+ *   k, v     [B*T, ldkv] (slots of the fused qkv projection)
+ *   pos      [T, ldp]    (linear_pos(pos_emb))
+ *   stats    [B*H*T][2]  out: row max and 1/row sum of exp (the backward recomputes P)
+ *   ctx      [B*T, ldc]  out: softmax(S) V, heads concatenated
+ * mask as lasr_attn_softmax_fwd.  Row strides multiples of 8 elements, 16-B aligned. */
+int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, const void* k, const void* v,
+                     int64_t ldkv, const void* pos, int64_t ldp, int B, int H, int T, int dk,
+                     const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                     float* stats, void* ctx, int64_t ldc, void* stream);
+/* Backward of lasr_relattn_fwd (recompute; deterministic).  Outputs:
+ *   Dbuf [B*H*T]        scratch: rowsum(dctx * ctx)
+ *   dqu  [B*T, ldq]     dL/d(q+u)
+ *   dbd  [B*H, T, ldS]  dL/d(bd) before rel_shift (unscaled), as lasr_relshift_bwd writes it:
+ *                       feeds dqv = scale dbd.p and dpos = scale sum_b dbd^T.qv
+ *   dk, dv [B*T, lddkv] dL/dk, dL/dv (may be the k / v slots of dqkv). */
+int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, const void* k, const void* v,
+                     int64_t ldkv, const void* pos, int64_t ldp, int B, int H, int T, int dk,
+                     const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                     const float* stats, const void* ctx, const void* dctx, int64_t ldc,
+                     float* Dbuf, void* dqu, void* dbd, int ldS, void* dk_out, void* dv_out,
+                     int64_t lddkv, void* stream);
 /* dst[t, h*dk + c] = sum_b src[b,h,t,c]  (pos-projection grad reduced over batch). */
 int lasr_reduce_batch(const float* src, int B, int H, int T, int dk, void* dst, int dt,
                       void* stream);

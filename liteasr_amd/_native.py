@@ -56,6 +56,9 @@ SIGNATURES = {
     "lasr_gemm": [C.POINTER(GemmArgs), _p],
     "lasr_gemm_plan": [C.POINTER(GemmArgs), _p, _p, _p],
     "lasr_gemm_force_tile": [C.c_int, C.c_int],
+    "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
+    "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
+                         _p, _p, _p, _i, _p, _p, _l, _p],
     "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
     "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],
     "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,

@@ -21,6 +21,7 @@ dtype ``adt`` (bf16, or fp32 for the parity build); attention scores fp32.
 from __future__ import annotations
 
 import math
+import os
 from types import SimpleNamespace
 
 import torch
@@ -92,6 +93,15 @@ def _slot(t, B, T, nslot, k, H, dk):
 
 
 # ============================================================ rel-pos MHSA ======
+FUSED_RELATTN = os.environ.get("LASR_FUSED_RELATTN", "1") != "0"
+
+
+def fused_relattn(adt, dk, p_att):
+    """The fused kernels (attn_fused.hip) cover bf16, d_k 64, no attention dropout (the
+    my_U2 preset); other shapes take the materialised-score kernels."""
+    return FUSED_RELATTN and adt == torch.bfloat16 and dk == 64 and p_att == 0.0
+
+
 def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res):
     B, T, H = env.B, env.T, env.H
     d = ln.shape[1]
@@ -106,6 +116,15 @@ def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res):
     qu = _e((M, d), adt, dev)
     qv = _e((M, d), adt, dev)
     K.qbias_fwd(qkv, B, T, H, dk, w.u, w.v, qu, qv)
+    if fused_relattn(adt, dk, p_att):
+        # scores never materialised (attn_fused.hip); row stats kept for the backward
+        stats = _e((B * H * T * 2,), F32, dev)
+        ctx = _e((M, d), adt, dev)
+        K.relattn_fwd(qu, qv, qkv[:, d:2 * d], qkv[:, 2 * d:], p, B, H, T, env.mask, env.msb, env.msq,
+                      scale, stats, ctx)
+        out = _e((M, d), F32, dev)
+        K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+        return out, SimpleNamespace(qkv=qkv, p=p, qu=qu, qv=qv, ctx=ctx, stats=stats)
     ldS = ld_scores(T)
     Sac = _e((B, H, T, ldS), F32, dev)
     Sbd = _e((B, H, T, ldS), F32, dev)
@@ -121,7 +140,7 @@ def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res):
     K.gemm(P[..., :T], v4, _heads(ctx, B, T, H, dk))
     out = _e((M, d), F32, dev)
     K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
-    saved = SimpleNamespace(qkv=qkv, p=p, qu=qu, qv=qv, P=P, Praw=Praw, ctx=ctx)
+    saved = SimpleNamespace(qkv=qkv, p=p, qu=qu, qv=qv, P=P, Praw=Praw, ctx=ctx, stats=None)
     return out, saved
 
 
@@ -136,22 +155,29 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo)
     dctx = _e((M, d), adt, dev)
     K.gemm(gb, w.Wo, dctx)
-    dctx4 = _heads(dctx, B, T, H, dk)
-    v4 = _slot(sv.qkv, B, T, 3, 2, H, dk)
-    k4 = _slot(sv.qkv, B, T, 3, 1, H, dk)
-    dPd = _e((B, H, T, ldS), F32, dev)
-    K.gemm(dctx4, v4.transpose(-1, -2), dPd[..., :T])
     dqkv = _e((M, 3 * d), adt, dev)
-    K.gemm(sv.P[..., :T].transpose(-1, -2), dctx4, _slot(dqkv, B, T, 3, 2, H, dk))
-    dS = _e((B, H, T, ldS), adt, dev)
-    K.attn_softmax_bwd(sv.Praw if sv.Praw is not None else sv.P, dPd, B, H, T, T, ldS, env.mask,
-                       env.msb, env.msq, dS, p_att, s_att)
-    dBD = _e((B, H, T, ldS), adt, dev)
-    K.relshift_bwd(dS.view(B * H, T, ldS), B * H, T, ldS, dBD)
     dqu = _e((M, d), adt, dev)
-    K.gemm(dS[..., :T], k4, _heads(dqu, B, T, H, dk), alpha=scale)
-    K.gemm(dS[..., :T].transpose(-1, -2), _heads(sv.qu, B, T, H, dk), _slot(dqkv, B, T, 3, 1, H, dk),
-           alpha=scale)
+    dBD = _e((B, H, T, ldS), adt, dev)
+    if sv.stats is not None:
+        # fused recompute backward: dqu, dk, dv and the pre-shift bd gradient
+        Dbuf = _e((B * H * T,), F32, dev)
+        K.relattn_bwd(sv.qu, sv.qv, sv.qkv[:, d:2 * d], sv.qkv[:, 2 * d:], sv.p, B, H, T, env.mask,
+                      env.msb, env.msq, scale, sv.stats, sv.ctx, dctx, Dbuf, dqu, dBD, ldS,
+                      dqkv[:, d:2 * d], dqkv[:, 2 * d:])
+    else:
+        dctx4 = _heads(dctx, B, T, H, dk)
+        v4 = _slot(sv.qkv, B, T, 3, 2, H, dk)
+        k4 = _slot(sv.qkv, B, T, 3, 1, H, dk)
+        dPd = _e((B, H, T, ldS), F32, dev)
+        K.gemm(dctx4, v4.transpose(-1, -2), dPd[..., :T])
+        K.gemm(sv.P[..., :T].transpose(-1, -2), dctx4, _slot(dqkv, B, T, 3, 2, H, dk))
+        dS = _e((B, H, T, ldS), adt, dev)
+        K.attn_softmax_bwd(sv.Praw if sv.Praw is not None else sv.P, dPd, B, H, T, T, ldS, env.mask,
+                           env.msb, env.msq, dS, p_att, s_att)
+        K.relshift_bwd(dS.view(B * H, T, ldS), B * H, T, ldS, dBD)
+        K.gemm(dS[..., :T], k4, _heads(dqu, B, T, H, dk), alpha=scale)
+        K.gemm(dS[..., :T].transpose(-1, -2), _heads(sv.qu, B, T, H, dk), _slot(dqkv, B, T, 3, 1, H, dk),
+               alpha=scale)
     p4 = sv.p.view(T, H, dk).permute(1, 0, 2).unsqueeze(0).expand(B, H, T, dk)
     dqv = _e((M, d), adt, dev)
     K.gemm(dBD[..., :T], p4, _heads(dqv, B, T, H, dk), alpha=scale)

@@ -416,6 +416,75 @@ def test_attn_softmax(relpos):
         close(dBD.view(B, H, T, ldS)[..., :T], gref, 1e-6, "relshift bwd")
 
 
+@pytest.mark.parametrize("B,H,T,masking", [(2, 2, 37, "pad"), (3, 4, 130, "pad"), (2, 4, 249, "pad"),
+                                            (2, 2, 100, "chunk"), (2, 1, 64, "none"), (1, 1, 1, "none")])
+def test_relattn_fused(B, H, T, masking):
+    """attn_fused.hip fwd + bwd vs the literal reference chain (attention.py:120-154) in fp64 on
+    the same bf16-rounded operands; one utterance fully masked when masking == "pad"."""
+    kn = K()
+    torch.manual_seed(T)
+    dk, d = 64, 64 * H
+    scale = dk ** -0.5
+    bf = torch.bfloat16
+    qkv = (torch.randn(B * T, 3 * d) * 0.5).to(bf)
+    qu = (torch.randn(B * T, d) * 0.5).to(bf)
+    qv = (torch.randn(B * T, d) * 0.5).to(bf)
+    pos = (torch.randn(T, d) * 0.5).to(bf)
+    dctx = torch.randn(B * T, d).to(bf)
+    if masking == "pad":
+        xl = torch.tensor([T, max(T // 3, 1), 0][:B])
+        mask = (torch.arange(T)[None, :] >= xl[:, None]).to(torch.uint8).contiguous()  # (B, T)
+        msb, msq, m4 = T, 0, mask.bool()[:, None, None, :]
+    elif masking == "chunk":
+        xl = torch.tensor([T, T - 17][:B])
+        pad = torch.arange(T)[None, :] >= xl[:, None]
+        tri = (torch.arange(T)[None, :] // 16) > (torch.arange(T)[:, None] // 16)
+        mask = (pad[:, None, :] | tri[None]).to(torch.uint8).contiguous()  # (B, T, T)
+        msb, msq, m4 = T * T, T, mask.bool()[:, None]
+    else:
+        mask, msb, msq, m4 = None, 0, 0, None
+
+    def heads(t):
+        return t.double().view(B, T, H, dk).permute(0, 2, 1, 3)
+
+    Qu = heads(qu).requires_grad_()
+    Qv = heads(qv).requires_grad_()
+    Kh = heads(qkv[:, d:2 * d]).requires_grad_()
+    Vh = heads(qkv[:, 2 * d:]).requires_grad_()
+    Pp = pos.double().view(T, H, dk).permute(1, 0, 2).unsqueeze(0).requires_grad_()
+    ac = Qu @ Kh.transpose(-1, -2)
+    bd = Qv @ Pp.transpose(-1, -2)
+    bd.retain_grad()
+    S = (ac + _rel_shift_ref(bd)) * scale
+    if m4 is not None:
+        S = S.masked_fill(m4, -1e38)
+    P = torch.softmax(S, -1)
+    ctx_ref = (P @ Vh).permute(0, 2, 1, 3).reshape(B * T, d)
+    ctx_ref.backward(dctx.double())
+
+    g = lambda t: t.to(DEV)
+    stats = torch.empty(B * H * T * 2, device=DEV)
+    ctx = torch.empty(B * T, d, dtype=bf, device=DEV)
+    qkv_d, mask_d = g(qkv), (g(mask) if mask is not None else None)
+    kn.relattn_fwd(g(qu), g(qv), qkv_d[:, d:2 * d], qkv_d[:, 2 * d:], g(pos), B, H, T, mask_d, msb, msq,
+                   scale, stats, ctx)
+    close(ctx, ctx_ref.detach(), 2e-2, "relattn ctx")
+
+    ldS = (T + 7) // 8 * 8
+    Dbuf = torch.empty(B * H * T, device=DEV)
+    dqu = torch.empty(B * T, d, dtype=bf, device=DEV)
+    dbd = torch.full((B, H, T, ldS), float("nan"), dtype=bf, device=DEV)
+    dqkv = torch.zeros(B * T, 3 * d, dtype=bf, device=DEV)
+    kn.relattn_bwd(g(qu), g(qv), qkv_d[:, d:2 * d], qkv_d[:, 2 * d:], g(pos), B, H, T, mask_d, msb, msq,
+                   scale, stats, ctx, g(dctx), Dbuf, dqu, dbd, ldS, dqkv[:, d:2 * d], dqkv[:, 2 * d:])
+    unh = lambda t: t.permute(0, 2, 1, 3).reshape(B * T, d)
+    close(dqu, unh(Qu.grad), 2e-2, "relattn dqu")
+    close(dqkv[:, d:2 * d], unh(Kh.grad), 2e-2, "relattn dk")
+    close(dqkv[:, 2 * d:], unh(Vh.grad), 2e-2, "relattn dv")
+    assert not dbd[..., :T].isnan().any(), "dbd entries left unwritten"
+    close(dbd[..., :T].float() * scale, bd.grad, 2e-2, "relattn dbd")
+
+
 def test_qbias_and_reduce():
     kn = K()
     B, T, H, dk = 2, 9, 4, 8
