@@ -87,6 +87,9 @@ int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* sp
 /* Tuning hook: force the bf16 LDS-DMA tile (64/128/256 x 64/128/256) of every later
  * lasr_gemm call in the process; (0, 0) restores the planner.  Benchmarks only. */
 int lasr_gemm_force_tile(int tile_m, int tile_n);
+/* Tuning hook: force the split-K factor of auto-split calls and the LDS ring depth (3..6)
+ * of split-K LDS-DMA launches; (0, 0) restores the planner.  Benchmarks only. */
+int lasr_gemm_force_split(int split_k, int stages);
 
 /* Column sums: out[n] (+)= sum_m X[m,n]  (bias gradients; fp32 out).
  * Two-pass deterministic; workspace >= ceil(M/rows_per_block)*N floats (see impl). */
@@ -131,13 +134,16 @@ int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_d
  * bwd: grad[b,t,:] = g * (softmax - gamma_t) for t < ilen[b], 0 otherwise, where
  *      g = gscale * (*gdev if gdev).  Uses beta[B*T*(2*Lmax+1)] scratch.
  * ---------------------------------------------------------------------- */
+/* beta (optional, [B][T][2*Lmax+1]): when given, the forward also runs the beta
+ * recursion, concurrently with alpha; pass beta_ready = 1 to lasr_ctc_bwd then.
+ * 2*Lmax+1 <= 1024 (one lattice state per thread). */
 int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, int64_t ld, const int32_t* targets,
                  int Lmax, const int32_t* ilen, const int32_t* tlen, float* lse, float* lp,
-                 float* alpha, float* nll, void* stream);
+                 float* alpha, float* beta, float* nll, void* stream);
 int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, int64_t ld, const int32_t* targets,
                  int Lmax, const int32_t* ilen, const int32_t* tlen, const float* lse,
                  const float* lp, const float* alpha, const float* nll, float* beta,
-                 void* grad, int gdt, float gscale, const float* gdev, void* stream);
+                 int beta_ready, void* grad, int gdt, float gscale, const float* gdev, void* stream);
 
 /* ------------------------------------------------------------------------
  * Label-smoothed KL (liteasr/criterions/hybrid_ctc_attn.py:49-64):

@@ -56,6 +56,7 @@ SIGNATURES = {
     "lasr_gemm": [C.POINTER(GemmArgs), _p],
     "lasr_gemm_plan": [C.POINTER(GemmArgs), _p, _p, _p],
     "lasr_gemm_force_tile": [C.c_int, C.c_int],
+    "lasr_gemm_force_split": [C.c_int, C.c_int],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
                          _p, _p, _p, _i, _p, _p, _l, _p],
@@ -64,8 +65,8 @@ SIGNATURES = {
     "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,
                            _p, _i, _f, _f, _u, _p],
     "lasr_branch_grad": [_p, _i, _l, _p, _i, _f, _f, _u, _p],
-    "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p],
-    "lasr_ctc_bwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p],
+    "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p],
+    "lasr_ctc_bwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _i, _p, _i, _f, _p, _p],
     "lasr_lsm_kl_fwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _p],
     "lasr_lsm_kl_bwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _i, _f, _p, _p],
     "lasr_loss_combine": [_p, _i, _f, _p, _i, _f, _p, _p],

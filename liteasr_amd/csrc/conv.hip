@@ -272,51 +272,98 @@ constexpr int DW_K = 15;
 constexpr int DW_P = (DW_K - 1) / 2;
 constexpr int DW_WIN = DW_TT + 2 * DW_P;
 
+// Thread layout of the GLU/depthwise kernels: 256 threads = DW_G time groups of DW_R rows
+// x 64 channel pairs (128 channels, 2 per thread with 4-B / 8-B loads); a block covers
+// DW_TT = DW_G * DW_R rows, its per-channel partials are combined across the groups in LDS
+// in a fixed order (one partial per block, as lasr_dwconv_nparts counts them).
+constexpr int DW_G = 4, DW_R = DW_TT / DW_G, DW_CP = 64;
+constexpr int DW_RW = DW_R + 2 * DW_P;  // rows a thread reads (window + halo)
+
+template <typename T>
+LASR_DEV float2 glu2(const T* zr, int C, int c) {  // a * sigmoid(gate) for channels c, c+1
+  float a[2], gt[2];
+  ldv<2>(zr + c, a);
+  ldv<2>(zr + C + c, gt);
+  return make_float2(a[0] * sigmoidf_(gt[0]), a[1] * sigmoidf_(gt[1]));
+}
+
 template <typename T, typename TY>
 __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const T* __restrict__ z1, int T_,
                                                              int C, const float* w,
                                                              const float* bias, TY* y,
                                                              float* stats) {
-  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  __shared__ float sst[DW_G][3][2 * DW_CP];
+  const int cp = threadIdx.x % DW_CP, grp = threadIdx.x / DW_CP;
+  const int c = (blockIdx.y * DW_CP + cp) * 2;
   const int nchunk = (T_ + DW_TT - 1) / DW_TT;
-  const int b = blockIdx.x / nchunk, t0 = (blockIdx.x - b * nchunk) * DW_TT;
-  if (c >= C) return;
-  float g[DW_WIN];
-#pragma unroll
-  for (int i = 0; i < DW_WIN; ++i) {
-    const int t = t0 - DW_P + i;
-    float v = 0.f;
-    if (t >= 0 && t < T_) {
-      const T* zr = z1 + ((int64_t)b * T_ + t) * 2 * C;
-      v = to_f(zr[c]) * sigmoidf_(to_f(zr[C + c]));
-    }
-    g[i] = v;
+  const int b = blockIdx.x / nchunk, t0 = (blockIdx.x - b * nchunk) * DW_TT + grp * DW_R;
+  const bool live = c < C;
+  // the block's GLU window (DW_TT + halo rows x 128 channels), each row computed once
+  __shared__ float2 win[DW_WIN][DW_CP];
+  const int tb = t0 - grp * DW_R;
+  for (int e = threadIdx.x; e < DW_WIN * DW_CP; e += 256) {
+    const int rr = e / DW_CP, cq = e % DW_CP, t = tb - DW_P + rr, ce = (blockIdx.y * DW_CP + cq) * 2;
+    win[rr][cq] = (ce < C && t >= 0 && t < T_) ? glu2(z1 + ((int64_t)b * T_ + t) * 2 * C, C, ce)
+                                              : make_float2(0.f, 0.f);
   }
-  float wk[DW_K];
+  __syncthreads();
+  float2 g[DW_RW];
 #pragma unroll
-  for (int k = 0; k < DW_K; ++k) wk[k] = w[c * DW_K + k];
-  const float bs = bias[c];
-  int cnt = 0;
-  float mean = 0.f, m2 = 0.f;
+  for (int i = 0; i < DW_RW; ++i) g[i] = win[grp * DW_R + i][cp];
+  float cnt = 0.f, mean[2] = {0.f, 0.f}, m2[2] = {0.f, 0.f};
+  if (live) {
+    float w0[DW_K], w1[DW_K];
 #pragma unroll
-  for (int i = 0; i < DW_TT; ++i) {
-    const int t = t0 + i;
-    if (t < T_) {
-      float acc = bs;
+    for (int k = 0; k < DW_K; ++k) { w0[k] = w[c * DW_K + k]; w1[k] = w[(c + 1) * DW_K + k]; }
+    const float b0 = bias[c], b1 = bias[c + 1];
 #pragma unroll
-      for (int k = 0; k < DW_K; ++k) acc += wk[k] * g[i + k];
-      y[((int64_t)b * T_ + t) * C + c] = from_f<TY>(acc);
-      const float yv = to_f(from_f<TY>(acc));  // stats on the stored value
-      ++cnt;
-      const float dlt = yv - mean;
-      mean += dlt / cnt;
-      m2 += dlt * (yv - mean);
+    for (int i = 0; i < DW_R; ++i) {
+      const int t = t0 + i;
+      if (t < T_) {
+        float acc[2] = {b0, b1};
+#pragma unroll
+        for (int k = 0; k < DW_K; ++k) {
+          acc[0] += w0[k] * g[i + k].x;
+          acc[1] += w1[k] * g[i + k].y;
+        }
+        TY* yr = y + ((int64_t)b * T_ + t) * C + c;
+        stv<2>(yr, acc);
+        cnt += 1.f;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float yv = to_f(from_f<TY>(acc[q]));  // stats on the stored value
+          const float dlt = yv - mean[q];
+          mean[q] += dlt / cnt;
+          m2[q] += dlt * (yv - mean[q]);
+        }
+      }
     }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    sst[grp][0][2 * cp + q] = cnt;
+    sst[grp][1][2 * cp + q] = mean[q];
+    sst[grp][2][2 * cp + q] = m2[q];
+  }
+  __syncthreads();
+  if (threadIdx.x >= 2 * DW_CP) return;
+  const int cl = threadIdx.x, cc = blockIdx.y * 2 * DW_CP + cl;
+  if (cc >= C) return;
+  // Chan et al. pairwise combine of the time groups, fixed order
+  float n = sst[0][0][cl], mu = sst[0][1][cl], M2 = sst[0][2][cl];
+#pragma unroll
+  for (int k = 1; k < DW_G; ++k) {
+    const float nb = sst[k][0][cl];
+    if (nb == 0.f) continue;
+    const float nt = n + nb, dl = sst[k][1][cl] - mu;
+    mu += dl * (nb / nt);
+    M2 += sst[k][2][cl] + dl * dl * (n * nb / nt);
+    n = nt;
   }
   float* st = stats + (int64_t)blockIdx.x * 3 * C;
-  st[c] = (float)cnt;
-  st[C + c] = mean;
-  st[2 * C + c] = m2;
+  st[cc] = n;
+  st[C + cc] = mu;
+  st[2 * C + cc] = M2;
 }
 
 template <typename T, typename TD>
@@ -324,50 +371,87 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
                                                              const TD* __restrict__ dy, int T_,
                                                              int C, const float* w, T* dz1,
                                                              float* part) {
-  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  __shared__ float sp[DW_G][DW_K + 1][2 * DW_CP];
+  const int cp = threadIdx.x % DW_CP, grp = threadIdx.x / DW_CP;
+  const int c = (blockIdx.y * DW_CP + cp) * 2;
   const int nchunk = (T_ + DW_TT - 1) / DW_TT;
-  const int b = blockIdx.x / nchunk, t0 = (blockIdx.x - b * nchunk) * DW_TT;
-  if (c >= C) return;
-  float g[DW_WIN], d[DW_WIN];
-#pragma unroll
-  for (int i = 0; i < DW_WIN; ++i) {
-    const int t = t0 - DW_P + i;
-    float gv = 0.f, dv = 0.f;
-    if (t >= 0 && t < T_) {
+  const int b = blockIdx.x / nchunk, t0 = (blockIdx.x - b * nchunk) * DW_TT + grp * DW_R;
+  const bool live = c < C;
+  // the block's GLU and dy windows (DW_TT + halo rows x 128 channels), loaded once
+  __shared__ float2 wg[DW_WIN][DW_CP], wd[DW_WIN][DW_CP];
+  const int tb = t0 - grp * DW_R;
+  for (int e = threadIdx.x; e < DW_WIN * DW_CP; e += 256) {
+    const int rr = e / DW_CP, cq = e % DW_CP, t = tb - DW_P + rr, ce = (blockIdx.y * DW_CP + cq) * 2;
+    float2 gv = make_float2(0.f, 0.f), dv2 = make_float2(0.f, 0.f);
+    if (ce < C && t >= 0 && t < T_) {
       const int64_t r = (int64_t)b * T_ + t;
-      gv = to_f(z1[r * 2 * C + c]) * sigmoidf_(to_f(z1[r * 2 * C + C + c]));
-      dv = to_f(dy[r * C + c]);
+      gv = glu2(z1 + r * 2 * C, C, ce);
+      float dv[2];
+      ldv<2>(dy + r * C + ce, dv);
+      dv2 = make_float2(dv[0], dv[1]);
     }
-    g[i] = gv;
-    d[i] = dv;
+    wg[rr][cq] = gv;
+    wd[rr][cq] = dv2;
   }
-  float wk[DW_K], dw[DW_K];
+  __syncthreads();
+  float2 g[DW_RW], d[DW_RW];
 #pragma unroll
-  for (int k = 0; k < DW_K; ++k) { wk[k] = w[c * DW_K + k]; dw[k] = 0.f; }
-  float db = 0.f;
+  for (int i = 0; i < DW_RW; ++i) {
+    g[i] = wg[grp * DW_R + i][cp];
+    d[i] = wd[grp * DW_R + i][cp];
+  }
+  float dw0[DW_K], dw1[DW_K], db0 = 0.f, db1 = 0.f;
 #pragma unroll
-  for (int i = 0; i < DW_TT; ++i) {
-    const int t = t0 + i;
-    if (t < T_) {
-      const float dyt = d[i + DW_P];
-      db += dyt;
+  for (int k = 0; k < DW_K; ++k) { dw0[k] = 0.f; dw1[k] = 0.f; }
+  if (live) {
+    float w0[DW_K], w1[DW_K];
 #pragma unroll
-      for (int k = 0; k < DW_K; ++k) dw[k] += dyt * g[i + k];
-      // dg[t] = sum_k w[k] * dy[t - k + P]
-      float dg = 0.f;
+    for (int k = 0; k < DW_K; ++k) { w0[k] = w[c * DW_K + k]; w1[k] = w[(c + 1) * DW_K + k]; }
 #pragma unroll
-      for (int k = 0; k < DW_K; ++k) dg += wk[k] * d[i + 2 * DW_P - k];
-      const int64_t r = (int64_t)b * T_ + t;
-      const float a = to_f(z1[r * 2 * C + c]);
-      const float s = sigmoidf_(to_f(z1[r * 2 * C + C + c]));
-      dz1[r * 2 * C + c] = from_f<T>(dg * s);
-      dz1[r * 2 * C + C + c] = from_f<T>(dg * a * s * (1.f - s));
+    for (int i = 0; i < DW_R; ++i) {
+      const int t = t0 + i;
+      if (t < T_) {
+        const float2 dyt = d[i + DW_P];
+        db0 += dyt.x;
+        db1 += dyt.y;
+        float dg0 = 0.f, dg1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < DW_K; ++k) {
+          dw0[k] += dyt.x * g[i + k].x;
+          dw1[k] += dyt.y * g[i + k].y;
+          // dg[t] = sum_k w[k] * dy[t - k + P]
+          dg0 += w0[k] * d[i + 2 * DW_P - k].x;
+          dg1 += w1[k] * d[i + 2 * DW_P - k].y;
+        }
+        const int64_t r = (int64_t)b * T_ + t;
+        float a[2], gt[2];
+        ldv<2>(z1 + r * 2 * C + c, a);
+        ldv<2>(z1 + r * 2 * C + C + c, gt);
+        const float s0 = sigmoidf_(gt[0]), s1 = sigmoidf_(gt[1]);
+        const float da[2] = {dg0 * s0, dg1 * s1};
+        const float dgt[2] = {dg0 * a[0] * s0 * (1.f - s0), dg1 * a[1] * s1 * (1.f - s1)};
+        stv<2>(dz1 + r * 2 * C + c, da);
+        stv<2>(dz1 + r * 2 * C + C + c, dgt);
+      }
     }
   }
-  float* pp = part + (int64_t)blockIdx.x * (DW_K + 1) * C;
 #pragma unroll
-  for (int k = 0; k < DW_K; ++k) pp[k * C + c] = dw[k];
-  pp[DW_K * C + c] = db;
+  for (int k = 0; k < DW_K; ++k) {
+    sp[grp][k][2 * cp] = dw0[k];
+    sp[grp][k][2 * cp + 1] = dw1[k];
+  }
+  sp[grp][DW_K][2 * cp] = db0;
+  sp[grp][DW_K][2 * cp + 1] = db1;
+  __syncthreads();
+  float* pp = part + (int64_t)blockIdx.x * (DW_K + 1) * C + blockIdx.y * 2 * DW_CP;
+  for (int e = threadIdx.x; e < (DW_K + 1) * 2 * DW_CP; e += 256) {
+    const int k = e / (2 * DW_CP), cl = e % (2 * DW_CP);
+    if (blockIdx.y * 2 * DW_CP + cl >= C) continue;
+    float v = sp[0][k][cl];
+#pragma unroll
+    for (int q = 1; q < DW_G; ++q) v += sp[q][k][cl];
+    pp[(int64_t)k * C + cl] = v;
+  }
 }
 
 __global__ void dw_reduce_kernel(const float* part, int nparts, int C, float* dw, float* db) {
@@ -448,35 +532,66 @@ __global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
   }
 }
 
+// Elementwise BN + Swish, 8 channels per thread (C % 8 == 0; the host checks).
 template <typename TY, typename TH>
 __global__ void bn_swish_fwd_kernel(const TY* y, int64_t rows, int C, const float* scale,
                                     const float* shift, TH* h) {
-  const int64_t n = rows * C;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    h[e] = from_f<TH>(swishf(to_f(y[e]) * scale[c] + shift[c]));
+  const int64_t n8 = rows * C / 8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)((e * 8) % C);
+    float v[8], sc[8], sf[8];
+    ldv<8>(y + e * 8, v);
+    ldv<8>(scale + c, sc);
+    ldv<8>(shift + c, sf);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = swishf(v[q] * sc[q] + sf[q]);
+    stv<8>(h + e * 8, v);
   }
 }
 
 constexpr int BN_ROWS = 64;
+// 256 threads = BN_G row groups x BN_CP channel pairs; a block reduces BN_ROWS rows of
+// 2*BN_CP channels and combines its row groups in LDS (fixed order).
+constexpr int BN_G = 8, BN_CP = 32;
 template <typename TY, typename TH>
-__global__ void bn_swish_bwd_reduce_kernel(const TY* y, const TH* dh, int64_t rows, int C,
-                                           const float* scale, const float* shift,
-                                           const float* mean, const float* rstd, float* part) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
-  const float sc = scale[c], sf = shift[c], mu = mean[c], rs = rstd[c];
-  float s1 = 0.f, s2 = 0.f;
-  for (int64_t r = r0; r < r1; ++r) {
-    const float yv = to_f(y[r * C + c]);
-    const float du = to_f(dh[r * C + c]) * swish_grad(yv * sc + sf);
-    s1 += du;
-    s2 += du * (yv - mu) * rs;
+__global__ __launch_bounds__(256) void bn_swish_bwd_reduce_kernel(const TY* y, const TH* dh, int64_t rows, int C,
+                                                                  const float* scale, const float* shift,
+                                                                  const float* mean, const float* rstd, float* part) {
+  __shared__ float sp[BN_G][2][2 * BN_CP];
+  const int cp = threadIdx.x % BN_CP, grp = threadIdx.x / BN_CP;
+  const int c = (blockIdx.x * BN_CP + cp) * 2;
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  if (c < C) {
+    const float sc[2] = {scale[c], scale[c + 1]}, sf[2] = {shift[c], shift[c + 1]};
+    const float mu[2] = {mean[c], mean[c + 1]}, rs[2] = {rstd[c], rstd[c + 1]};
+    const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
+    const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
+    for (int64_t r = r0 + grp; r < r1; r += BN_G) {
+      float yv[2], gv[2];
+      ldv<2>(y + r * C + c, yv);
+      ldv<2>(dh + r * C + c, gv);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float du = gv[q] * swish_grad(yv[q] * sc[q] + sf[q]);
+        s1[q] += du;
+        s2[q] += du * (yv[q] - mu[q]) * rs[q];
+      }
+    }
   }
-  part[(int64_t)blockIdx.y * 2 * C + c] = s1;
-  part[(int64_t)blockIdx.y * 2 * C + C + c] = s2;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    sp[grp][0][2 * cp + q] = s1[q];
+    sp[grp][1][2 * cp + q] = s2[q];
+  }
+  __syncthreads();
+  if (threadIdx.x >= 2 * 2 * BN_CP) return;
+  const int which = threadIdx.x / (2 * BN_CP), cl = threadIdx.x % (2 * BN_CP);
+  const int cc = blockIdx.x * 2 * BN_CP + cl;
+  if (cc >= C) return;
+  float v = sp[0][which][cl];
+#pragma unroll
+  for (int q = 1; q < BN_G; ++q) v += sp[q][which][cl];
+  part[(int64_t)blockIdx.y * 2 * C + (int64_t)which * C + cc] = v;
 }
 __global__ void bn_bwd_total_kernel(const float* part, int nparts, int C, float* tot,
                                     float* dgamma, float* dbeta) {
@@ -504,14 +619,21 @@ __global__ void bn_swish_bwd_apply_kernel(const TY* y, const TH* dh, int64_t row
                                           const float* scale, const float* shift,
                                           const float* mean, const float* rstd,
                                           const float* gamma, const float* tot, TD* dy) {
-  const int64_t n = rows * C;
+  const int64_t n8 = rows * C / 8;
   const float inv_n = 1.f / (float)rows;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    const float yv = to_f(y[e]);
-    const float du = to_f(dh[e]) * swish_grad(yv * scale[c] + shift[c]);
-    const float xh = (yv - mean[c]) * rstd[c];
-    dy[e] = from_f<TD>(gamma[c] * rstd[c] * (du - tot[c] * inv_n - xh * tot[C + c] * inv_n));
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)((e * 8) % C);
+    float yv[8], gv[8], o[8];
+    ldv<8>(y + e * 8, yv);
+    ldv<8>(dh + e * 8, gv);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = c0 + q;
+      const float du = gv[q] * swish_grad(yv[q] * scale[c] + shift[c]);
+      const float xh = (yv[q] - mean[c]) * rstd[c];
+      o[q] = gamma[c] * rstd[c] * (du - tot[c] * inv_n - xh * tot[C + c] * inv_n);
+    }
+    stv<8>(dy + e * 8, o);
   }
 }
 
@@ -603,8 +725,9 @@ extern "C" int lasr_glu_dwconv_fwd(const void* z1, int dt, int B, int T, int C, 
                                    const float* w, const float* bias, void* y, int ydt,
                                    float* stats_ws, void* stream) {
   LASR_CHECK_ARG(K == DW_K, "lasr_glu_dwconv_fwd: only kernel size %d is built (got %d)", DW_K, K);
+  LASR_CHECK_ARG(C % 2 == 0, "lasr_glu_dwconv_fwd: C must be even");
   const int nchunk = (int)cdiv(T, DW_TT);
-  dim3 g((unsigned)(B * nchunk), (unsigned)cdiv(C, 256));
+  dim3 g((unsigned)(B * nchunk), (unsigned)cdiv(C, 2 * DW_CP));
   hipStream_t st = (hipStream_t)stream;
 #define GF(TT, TY) glu_dwconv_fwd_kernel<TT, TY><<<g, 256, 0, st>>>((const TT*)z1, T, C, w, bias, (TY*)y, stats_ws)
   if (dt == LASR_F32 && ydt == LASR_F32) GF(float, float);
@@ -630,7 +753,8 @@ extern "C" int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float 
 
 extern "C" int lasr_bn_swish_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
                                  const float* shift, void* h, int hdt, void* stream) {
-  const int64_t n = rows * C;
+  LASR_CHECK_ARG(C % 8 == 0, "lasr_bn_swish_fwd: C must be a multiple of 8");
+  const int64_t n = rows * C / 8;
   if (n == 0) return LASR_OK;
   hipStream_t st = (hipStream_t)stream;
 #define BF(TY, TH) bn_swish_fwd_kernel<TY, TH><<<gridn(n), 256, 0, st>>>((const TY*)y, rows, C, scale, shift, (TH*)h)
@@ -652,8 +776,9 @@ extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt
   LASR_CHECK_ARG(nparts <= 65535, "lasr_bn_swish_bwd: too many rows");
   if (rows == 0) return LASR_OK;
   hipStream_t st = (hipStream_t)stream;
+  LASR_CHECK_ARG(C % 8 == 0, "lasr_bn_swish_bwd: C must be a multiple of 8");
   float* tot = ws + nparts * 2 * C;
-  dim3 g((unsigned)cdiv(C, 256), (unsigned)nparts);
+  dim3 g((unsigned)cdiv(C, 2 * BN_CP), (unsigned)nparts);
 #define BR(TY, TH) bn_swish_bwd_reduce_kernel<TY, TH><<<g, 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, ws)
   if (ydt == LASR_F32 && hdt == LASR_F32) BR(float, float);
   else if (ydt == LASR_F32) BR(float, bf16_t);
@@ -667,7 +792,7 @@ extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt
   bn_bwd_accum_kernel<<<(unsigned)cdiv(C, 256), 256, 0, st>>>(tot, C, dgamma, dbeta);
   rc = lasr_check_launch("bn_swish_bwd/accum");
   if (rc) return rc;
-  const int64_t n = rows * C;
+  const int64_t n = rows * C / 8;
 #define BA(TY, TH, TD) bn_swish_bwd_apply_kernel<TY, TH, TD><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy)
   const bool yf = ydt == LASR_F32, hf = hdt == LASR_F32, df = dydt == LASR_F32;
   if (yf && hf && df) BA(float, float, float);
@@ -689,7 +814,8 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
   const int nchunk = (int)cdiv(T, DW_TT);
   const int nparts = B * nchunk;
   LASR_CHECK_ARG(ws_floats >= (int64_t)(nparts + 1) * (DW_K + 1) * C, "lasr_glu_dwconv_bwd: workspace too small");
-  dim3 g((unsigned)nparts, (unsigned)cdiv(C, 256));
+  LASR_CHECK_ARG(C % 2 == 0, "lasr_glu_dwconv_bwd: C must be even");
+  dim3 g((unsigned)nparts, (unsigned)cdiv(C, 2 * DW_CP));
   hipStream_t st = (hipStream_t)stream;
 #define GB(TT, TD) glu_dwconv_bwd_kernel<TT, TD><<<g, 256, 0, st>>>((const TT*)z1, (const TD*)dy, T, C, w, (TT*)dz1, ws)
   if (dt == LASR_F32 && dydt == LASR_F32) GB(float, float);

@@ -68,11 +68,15 @@ LASR_DEV float lse2(float a, float b) {
 // label id of extended state s (blank for even s)
 LASR_DEV int ext_label(const int32_t* tg, int s) { return (s & 1) ? tg[s >> 1] : 0; }
 
-__global__ void ctc_alpha_kernel(int T_, int Lmax, const int32_t* __restrict__ targets,
-                                 const int32_t* ilen, const int32_t* tlen, const float* lp,
-                                 float* alpha, float* nll) {
+// The recursions run one state per thread (S <= blockDim <= 1024).  Everything a step
+// needs from HBM is off the serial chain: the skip rule is decided once, and each
+// thread's emission log-probs are prefetched CTC_PF steps ahead into a register ring.
+constexpr int CTC_PF = 8;
+
+LASR_DEV void ctc_alpha(int b, int T_, int Lmax, const int32_t* __restrict__ targets,
+                        const int32_t* ilen, const int32_t* tlen, const float* lp, float* alpha,
+                        float* nll) {
   extern __shared__ float sh[];
-  const int b = blockIdx.x;
   const int Tb = ilen[b], Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
   const int32_t* tg = targets + (int64_t)b * Lmax;
   float* buf0 = sh;
@@ -81,30 +85,42 @@ __global__ void ctc_alpha_kernel(int T_, int Lmax, const int32_t* __restrict__ t
     if (threadIdx.x == 0) nll[b] = (Lb == 0) ? 0.f : INFINITY;
     return;
   }
-  const float* lpb = lp + (int64_t)b * T_ * (Lmax + 1);
+  const int s = threadIdx.x;
+  const bool act = s < S;
+  const bool skip = act && s >= 2 && (s & 1) && ext_label(tg, s) != ext_label(tg, s - 2);
+  const int eix = (s & 1) ? 1 + (s >> 1) : 0;
+  const int64_t ld = Lmax + 1;
+  const float* lpb = lp + (int64_t)b * T_ * ld + eix;
   float* al = alpha + (int64_t)b * T_ * Smax;
-  for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    const float v = (s == 0) ? lpb[0] : (s == 1) ? lpb[1] : -INFINITY;
+  if (act) {
+    const float v = (s == 0) ? lpb[0] : (s == 1) ? lpb[0] : -INFINITY;
     buf0[s] = v;
     al[s] = v;
   }
+  float epf[CTC_PF];
+#pragma unroll
+  for (int k = 0; k < CTC_PF; ++k) epf[k] = (act && 1 + k < Tb) ? lpb[(1 + k) * ld] : 0.f;
   __syncthreads();
   float* prev = buf0;
   float* cur = buf1;
-  for (int t = 1; t < Tb; ++t) {
-    const float* lpt = lpb + (int64_t)t * (Lmax + 1);
-    for (int s = threadIdx.x; s < S; s += blockDim.x) {
-      const float a0 = prev[s];
-      const float a1 = s >= 1 ? prev[s - 1] : -INFINITY;
-      float a2 = -INFINITY;
-      if (s >= 2 && (s & 1) && ext_label(tg, s) != ext_label(tg, s - 2)) a2 = prev[s - 2];
-      const float e = (s & 1) ? lpt[1 + (s >> 1)] : lpt[0];
-      const float v = lse3(a0, a1, a2) + e;
-      cur[s] = v;
-      al[(int64_t)t * Smax + s] = v;
+  for (int t0 = 1; t0 < Tb; t0 += CTC_PF) {
+#pragma unroll
+    for (int k = 0; k < CTC_PF; ++k) {
+      const int t = t0 + k;
+      if (t >= Tb) break;  // uniform
+      const float e = epf[k];
+      epf[k] = (act && t + CTC_PF < Tb) ? lpb[(t + CTC_PF) * ld] : 0.f;
+      if (act) {
+        const float a0 = prev[s];
+        const float a1 = s >= 1 ? prev[s - 1] : -INFINITY;
+        const float a2 = skip ? prev[s - 2] : -INFINITY;
+        const float v = lse3(a0, a1, a2) + e;
+        cur[s] = v;
+        al[(int64_t)t * Smax + s] = v;
+      }
+      __syncthreads();
+      float* tmp = prev; prev = cur; cur = tmp;
     }
-    __syncthreads();
-    float* tmp = prev; prev = cur; cur = tmp;
   }
   if (threadIdx.x == 0) {
     const float ll = (S >= 2) ? lse2(prev[S - 1], prev[S - 2]) : prev[0];
@@ -112,45 +128,66 @@ __global__ void ctc_alpha_kernel(int T_, int Lmax, const int32_t* __restrict__ t
   }
 }
 
-__global__ void ctc_beta_kernel(int T_, int Lmax, const int32_t* __restrict__ targets,
-                                const int32_t* ilen, const int32_t* tlen, const float* lp,
-                                float* beta) {
+LASR_DEV void ctc_beta(int b, int T_, int Lmax, const int32_t* __restrict__ targets,
+                       const int32_t* ilen, const int32_t* tlen, const float* lp, float* beta) {
   extern __shared__ float sh[];
-  const int b = blockIdx.x;
   const int Tb = ilen[b], Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
   if (Tb <= 0) return;
   const int32_t* tg = targets + (int64_t)b * Lmax;
   float* buf0 = sh;
   float* buf1 = sh + Smax;
-  const float* lpb = lp + (int64_t)b * T_ * (Lmax + 1);
+  const int s = threadIdx.x;
+  const bool act = s < S;
+  const bool skip = act && s + 2 < S && (s & 1) && ext_label(tg, s) != ext_label(tg, s + 2);
+  const int eix = (s & 1) ? 1 + (s >> 1) : 0;
+  const int64_t ld = Lmax + 1;
+  const float* lpb = lp + (int64_t)b * T_ * ld + eix;
   float* be = beta + (int64_t)b * T_ * Smax;
-  {
-    const float* lpt = lpb + (int64_t)(Tb - 1) * (Lmax + 1);
-    for (int s = threadIdx.x; s < S; s += blockDim.x) {
-      const float e = (s & 1) ? lpt[1 + (s >> 1)] : lpt[0];
-      const float v = (s >= S - 2) ? e : -INFINITY;
-      buf0[s] = v;
-      be[(int64_t)(Tb - 1) * Smax + s] = v;
-    }
+  if (act) {
+    const float e = lpb[(int64_t)(Tb - 1) * ld];
+    const float v = (s >= S - 2) ? e : -INFINITY;
+    buf0[s] = v;
+    be[(int64_t)(Tb - 1) * Smax + s] = v;
   }
+  float epf[CTC_PF];
+#pragma unroll
+  for (int k = 0; k < CTC_PF; ++k) epf[k] = (act && Tb - 2 - k >= 0) ? lpb[(int64_t)(Tb - 2 - k) * ld] : 0.f;
   __syncthreads();
   float* nxt = buf0;
   float* cur = buf1;
-  for (int t = Tb - 2; t >= 0; --t) {
-    const float* lpt = lpb + (int64_t)t * (Lmax + 1);
-    for (int s = threadIdx.x; s < S; s += blockDim.x) {
-      const float b0 = nxt[s];
-      const float b1 = (s + 1 < S) ? nxt[s + 1] : -INFINITY;
-      float b2 = -INFINITY;
-      if (s + 2 < S && (s & 1) && ext_label(tg, s) != ext_label(tg, s + 2)) b2 = nxt[s + 2];
-      const float e = (s & 1) ? lpt[1 + (s >> 1)] : lpt[0];
-      const float v = lse3(b0, b1, b2) + e;
-      cur[s] = v;
-      be[(int64_t)t * Smax + s] = v;
+  for (int t0 = Tb - 2; t0 >= 0; t0 -= CTC_PF) {
+#pragma unroll
+    for (int k = 0; k < CTC_PF; ++k) {
+      const int t = t0 - k;
+      if (t < 0) break;  // uniform
+      const float e = epf[k];
+      epf[k] = (act && t - CTC_PF >= 0) ? lpb[(int64_t)(t - CTC_PF) * ld] : 0.f;
+      if (act) {
+        const float b0 = nxt[s];
+        const float b1 = (s + 1 < S) ? nxt[s + 1] : -INFINITY;
+        const float b2 = skip ? nxt[s + 2] : -INFINITY;
+        const float v = lse3(b0, b1, b2) + e;
+        cur[s] = v;
+        be[(int64_t)t * Smax + s] = v;
+      }
+      __syncthreads();
+      float* tmp = nxt; nxt = cur; cur = tmp;
     }
-    __syncthreads();
-    float* tmp = nxt; nxt = cur; cur = tmp;
   }
+}
+
+// blocks [0, B): alpha (+ nll); blocks [B, 2B) when beta != nullptr: beta.  The two
+// recursions are independent, so the forward runs them side by side.
+__global__ void ctc_alpha_beta_kernel(int B, int T_, int Lmax, const int32_t* __restrict__ targets,
+                                      const int32_t* ilen, const int32_t* tlen, const float* lp,
+                                      float* alpha, float* nll, float* beta) {
+  if ((int)blockIdx.x < B) ctc_alpha(blockIdx.x, T_, Lmax, targets, ilen, tlen, lp, alpha, nll);
+  else ctc_beta(blockIdx.x - B, T_, Lmax, targets, ilen, tlen, lp, beta);
+}
+__global__ void ctc_beta_kernel(int T_, int Lmax, const int32_t* __restrict__ targets,
+                                const int32_t* ilen, const int32_t* tlen, const float* lp,
+                                float* beta) {
+  ctc_beta(blockIdx.x, T_, Lmax, targets, ilen, tlen, lp, beta);
 }
 
 template <typename T, typename TG>
@@ -215,11 +252,11 @@ static int ctc_block(int S) {
 
 extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, int64_t ld,
                             const int32_t* targets, int Lmax, const int32_t* ilen,
-                            const int32_t* tlen, float* lse, float* lp, float* alpha, float* nll,
-                            void* stream) {
+                            const int32_t* tlen, float* lse, float* lp, float* alpha, float* beta,
+                            float* nll, void* stream) {
   LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0 && ld >= V, "lasr_ctc_fwd: bad sizes");
   LASR_CHECK_ARG(ldt == LASR_F32 || ldt == LASR_BF16, "lasr_ctc_fwd: bad dtype");
-  LASR_CHECK_ARG(2 * (2 * Lmax + 1) * 4 <= 160 * 1024, "lasr_ctc_fwd: Lmax too large");
+  LASR_CHECK_ARG(2 * Lmax + 1 <= 1024, "lasr_ctc_fwd: Lmax=%d too large (one lattice state per thread)", Lmax);
   hipStream_t st = (hipStream_t)stream;
   if (ldt == LASR_F32)
     ctc_lse_gather_kernel<float><<<B * T, 256, 0, st>>>((const float*)logits, B, T, V, ld, targets, Lmax, ilen, tlen, lse, lp);
@@ -228,21 +265,25 @@ extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, in
   int rc = lasr_check_launch("ctc_lse_gather");
   if (rc) return rc;
   const int Smax = 2 * Lmax + 1;
-  ctc_alpha_kernel<<<B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(T, Lmax, targets, ilen, tlen, lp, alpha, nll);
-  return lasr_check_launch("ctc_alpha");
+  ctc_alpha_beta_kernel<<<beta ? 2 * B : B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(
+      B, T, Lmax, targets, ilen, tlen, lp, alpha, nll, beta);
+  return lasr_check_launch("ctc_alpha_beta");
 }
 
 extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, int64_t ld,
                             const int32_t* targets, int Lmax, const int32_t* ilen,
                             const int32_t* tlen, const float* lse, const float* lp,
-                            const float* alpha, const float* nll, float* beta, void* grad, int gdt,
-                            float gscale, const float* gdev, void* stream) {
+                            const float* alpha, const float* nll, float* beta, int beta_ready,
+                            void* grad, int gdt, float gscale, const float* gdev, void* stream) {
   LASR_CHECK_ARG(B > 0 && T > 0 && V > 0 && Lmax >= 0 && ld >= V, "lasr_ctc_bwd: bad sizes");
+  LASR_CHECK_ARG(2 * Lmax + 1 <= 1024, "lasr_ctc_bwd: Lmax=%d too large", Lmax);
   hipStream_t st = (hipStream_t)stream;
   const int Smax = 2 * Lmax + 1;
-  ctc_beta_kernel<<<B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(T, Lmax, targets, ilen, tlen, lp, beta);
-  int rc = lasr_check_launch("ctc_beta");
-  if (rc) return rc;
+  if (!beta_ready) {
+    ctc_beta_kernel<<<B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(T, Lmax, targets, ilen, tlen, lp, beta);
+    const int rc = lasr_check_launch("ctc_beta");
+    if (rc) return rc;
+  }
   const size_t shm = ((size_t)2 * (Lmax > 0 ? Lmax : 1) + (V + 31) / 32) * sizeof(float);
   LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_ctc_bwd: vocab/labels too large for LDS");
 #define CTC_G(TT, TGG)                                                                      \

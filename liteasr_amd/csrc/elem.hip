@@ -46,25 +46,60 @@ __global__ void embed_pe_fwd_kernel(const int32_t* ids, int R, int L, int D, con
 }
 
 // Deterministic embedding backward: the workgroup of the first row holding an id sums
-// every row with that id in row order and adds it to dE[id].
+// every row with that id and adds it to dE[id].  The rows holding the id are found in
+// parallel (ballot compaction, row order kept); the sum runs over 4 row groups x 8
+// accumulators per column and is combined in a fixed order (run-to-run identical).
 template <typename TD>
-__global__ void embed_bwd_kernel(const int32_t* ids, int R, int D, const TD* dy, float xscale,
-                                 DropCfg d, float* dE) {
-  extern __shared__ int sid[];
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int R, int D, const TD* dy,
+                                                        float xscale, DropCfg d, float* dE) {
+  extern __shared__ int sid[];  // R ids, up to R matching rows, 256 partial sums
+  __shared__ int wcnt[4];
+  int* rows = sid + R;
   for (int i = threadIdx.x; i < R; i += blockDim.x) sid[i] = ids[i];
   __syncthreads();
-  const int r = blockIdx.x;
-  const int id = sid[r];
-  for (int k = 0; k < r; ++k)
-    if (sid[k] == id) return;  // not the first occurrence (uniform across the block)
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float acc = 0.f;
-    for (int k = r; k < R; ++k)
-      if (sid[k] == id) {
-        const int64_t e = (int64_t)k * D + c;
-        acc += to_f(dy[e]) * drop_mul(d, (uint64_t)e);
+  const int r = blockIdx.x, id = sid[r];
+  int earlier = 0;
+  for (int k = threadIdx.x; k < r; k += blockDim.x) earlier |= sid[k] == id;
+  if (__syncthreads_or(earlier)) return;  // not the first occurrence (uniform)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int n = 0;
+  for (int base = r; base < R; base += 256) {
+    const int k = base + threadIdx.x;
+    const bool m = k < R && sid[k] == id;
+    const uint64_t bal = __ballot(m);
+    if (lane == 0) wcnt[w] = __popcll(bal);
+    __syncthreads();
+    int off = n;
+    for (int q = 0; q < w; ++q) off += wcnt[q];
+    if (m) rows[off + __popcll(bal & ((1ull << lane) - 1))] = k;
+    n += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+  }
+  // 4 row groups x 64 columns per pass, fixed-order combine
+  const uint32_t key = d.p > 0.f ? drop_key(d) : 0u;
+  float* part = reinterpret_cast<float*>(rows + R);  // [4][64]
+  for (int c0 = 0; c0 < D; c0 += 64) {
+    const int c = c0 + lane;
+    // 8 independent loads in flight per step (a frequent id, e.g. the eos padding, has
+    // hundreds of rows: the latency chain, not bandwidth, bounds this block)
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (c < D) {
+      for (int q0 = w; q0 < n; q0 += 32) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int q = q0 + 4 * u;
+          if (q < n) {
+            const int64_t e = (int64_t)rows[q] * D + c;
+            a[u] += to_f(dy[e]) * drop_mul_k(d, key, (uint64_t)e);
+          }
+        }
       }
-    dE[(int64_t)id * D + c] += acc * xscale;
+    }
+    part[w * 64 + lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (w == 0 && c < D)
+      dE[(int64_t)id * D + c] += (((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane]) * xscale;
+    __syncthreads();
   }
 }
 
@@ -133,10 +168,10 @@ extern "C" int lasr_embed_pe_fwd(const int32_t* ids, int R, int L, int D, const 
 extern "C" int lasr_embed_bwd(const int32_t* ids, int R, int D, const void* dy, int dydt,
                               float xscale, float p, uint64_t seed, float* dE, void* stream) {
   if (R <= 0) return LASR_OK;
-  LASR_CHECK_ARG(R <= 16384, "lasr_embed_bwd: R=%d > 16384", R);
+  LASR_CHECK_ARG(R <= 16384, "lasr_embed_bwd: R=%d > 16384", R);  // 2 R ints of LDS
   DropCfg d = mkdrop(p, seed);
   hipStream_t st = (hipStream_t)stream;
-  const size_t shm = (size_t)R * sizeof(int);
+  const size_t shm = ((size_t)2 * R + 256) * sizeof(int);
   if (dydt == LASR_F32) embed_bwd_kernel<float><<<R, 256, shm, st>>>(ids, R, D, (const float*)dy, xscale, d, dE);
   else embed_bwd_kernel<bf16_t><<<R, 256, shm, st>>>(ids, R, D, (const bf16_t*)dy, xscale, d, dE);
   return lasr_check_launch("embed_bwd");

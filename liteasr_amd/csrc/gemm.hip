@@ -16,6 +16,8 @@
 // ctc.py:29, transformer_decoder.py:91 (and their autograd backward GEMMs).
 #include "common.h"
 
+#include <type_traits>
+
 // Ablation hooks for GEMM experiments (tools/gemm_exp.sh); 0 in every product build.
 // bit 1: skip the MFMAs, bit 2: skip the epilogue stores, bit 4: skip the glds loads.
 #ifndef LASR_EXP
@@ -609,16 +611,17 @@ LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32
 // outputs.  Blocks are remapped so consecutive tiles share an XCD (and its L2).
 template <int N>
 LASR_DEV void wait_vmcnt() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else static_assert(N < 0, "unsupported vmcnt");
+  static_assert(N >= 0 && N < 64, "vmcnt out of range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// Retire ring tile kt when `after` (<= S-2) later tiles of GL glds each are still in flight.
+template <int S, int GL>
+LASR_DEV void wait_ring(int after) {
+  if constexpr (S >= 6) if (after >= 4) { wait_vmcnt<4 * GL>(); return; }
+  if constexpr (S >= 5) if (after >= 3) { wait_vmcnt<3 * GL>(); return; }
+  if constexpr (S >= 4) if (after >= 2) { wait_vmcnt<2 * GL>(); return; }
+  if (after >= 1) wait_vmcnt<GL>();
+  else wait_vmcnt<0>();
 }
 LASR_DEV void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -817,9 +820,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
 
   for (int kt = 0; kt < nfull; ++kt) {
     const int after = min(S - 2, nfull - 1 - kt);  // tiles issued after kt (still in flight)
-    if (S >= 4 && after >= 2) wait_vmcnt<2 * GL>();
-    else if (after >= 1) wait_vmcnt<GL>();
-    else wait_vmcnt<0>();
+    wait_ring<S, GL>(after);
     lds_barrier();
     if (kt + S - 1 < nfull) issue(kt + S - 1);
     compute(smem + (kt % S) * TILE);
@@ -967,8 +968,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
 }
 
 // ================================ host launcher ==================================
+static int g_stages = 0;  // lasr_gemm_force_split (tuning hook)
+
 template <bool AKC, bool BKC, typename TC>
 static void launch_bf16(const GemmP& p, int BM, int BN, bool glds, dim3 grid, hipStream_t st) {
+  if constexpr (!AKC && !BKC && std::is_same<TC, float>::value) {
+    // split-K weight-gradient GEMMs: one block per CU, so a deeper ring hides the latency
+    const int S = g_stages;
+    if (glds && p.split_k > 1 && S >= 4) {
+#define DWL(bm, bn, s, mb) gemm_bf16_glds_kernel<bm, bn, false, false, float, s, mb><<<grid, 256, 0, st>>>(p)
+      if (BM == 128 && BN == 128) { if (S == 4) DWL(128, 128, 4, 2); else if (S == 5) DWL(128, 128, 5, 1); else DWL(128, 128, 6, 1); return; }
+      if (BM == 64 && BN == 128) { if (S == 4) DWL(64, 128, 4, 3); else if (S == 5) DWL(64, 128, 5, 2); else DWL(64, 128, 6, 2); return; }
+      if (BM == 128 && BN == 64) { if (S == 4) DWL(128, 64, 4, 3); else if (S == 5) DWL(128, 64, 5, 2); else DWL(128, 64, 6, 2); return; }
+      if (BM == 64 && BN == 64) { if (S == 4) DWL(64, 64, 4, 4); else if (S == 5) DWL(64, 64, 5, 3); else DWL(64, 64, 6, 3); return; }
+#undef DWL
+    }
+  }
   if (glds) {
     if (BM == 256 && BN == 256) gemm_bf16_glds_kernel<256, 256, AKC, BKC, TC, 3, 1><<<grid, 256, 0, st>>>(p);
     else if (BM == 256) gemm_bf16_glds_kernel<256, 128, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
@@ -1013,7 +1028,7 @@ static bool getenv_flag(const char* name) {
 
 // Tuning hook (tools/gemm_graph_bench.py): force the LDS-DMA tile of every later call;
 // 0 = the planner's choice.  Process-wide, not for product use.
-static int g_tile_m = 0, g_tile_n = 0;
+static int g_tile_m = 0, g_tile_n = 0, g_split = 0;
 extern "C" int lasr_gemm_force_tile(int tile_m, int tile_n) {
   const bool ok = (tile_m == 0 && tile_n == 0) ||
                   ((tile_m == 64 || tile_m == 128 || tile_m == 256) &&
@@ -1022,6 +1037,16 @@ extern "C" int lasr_gemm_force_tile(int tile_m, int tile_n) {
   LASR_CHECK_ARG(ok, "lasr_gemm_force_tile: unsupported tile");
   g_tile_m = tile_m;
   g_tile_n = tile_n;
+  return LASR_OK;
+}
+
+// Tuning hook: force the split-K factor of autosplit calls and the ring depth of split-K
+// LDS-DMA launches (0 = planner).  Benchmarks only.
+extern "C" int lasr_gemm_force_split(int split_k, int stages) {
+  LASR_CHECK_ARG(split_k >= 0 && split_k <= 64 && (stages == 0 || (stages >= 3 && stages <= 6)),
+                 "lasr_gemm_force_split: bad arguments");
+  g_split = split_k;
+  g_stages = stages;
   return LASR_OK;
 }
 
@@ -1036,13 +1061,22 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
   const int kt = (int)cdiv(a->K, 32);
   if (bf && autosplit && kt >= 16) {
     // long-K (weight-gradient) GEMMs: big tiles, fill the chip with K slices instead
-    BM = a->M >= 96 ? 128 : 64;
-    BN = a->N >= 96 ? 128 : 64;
+    // dW shapes of the step (K = B*T' ~ 8k): 64-wide tiles and >= 512 workgroups
+    // (tools/dw_sweep.py: 15-25 % faster than 128 x 128 at 256 blocks); 64 x 64 up to
+    // 768 x 256 outputs, else 64 along the longer side.  Very long K (the subsampling
+    // conv2 weight gradient, K ~ 151k) keeps 128 x 128 and 256 workgroups.
+    const bool very_long = kt >= 2048;
+    BM = BN = 64;
+    if (very_long) {
+      BM = a->M >= 96 ? 128 : 64;
+      BN = a->N >= 96 ? 128 : 64;
+    } else if ((int64_t)a->M * a->N > 768 * 256) {
+      BM = a->M >= a->N ? 64 : 128;
+      BN = a->M >= a->N ? 128 : 64;
+    }
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
-    // >= 256 workgroups (one per CU; the 3-wave launch bound co-schedules the other
-    // GEMMs' blocks) with >= 8 k tiles per slice; fewer slices = less partial traffic
-    // (gemm_bench: dW fc1 split 8 29.6 us vs 16 35.4 us)
-    while (nb * split < 256 && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
+    const int64_t target = very_long ? 256 : 512;
+    while (nb * split < target && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
   } else if (bf) {
     const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
     for (int c = 0; c < 4; ++c) {
@@ -1052,7 +1086,7 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     }
     // very large outputs with long K (subsampling conv2: M 151k, N 256, K 2304): the
     // 128x256 tile halves the A re-reads (tile sweep: 237 vs 266 us)
-    if (BM == 128 && BN == 128 && a->N >= 256 && a->K >= 1024 && cdiv(a->M, 128) * batch >= 2048) BN = 256;
+    if (BM == 128 && BN == 128 && a->N >= 256 && a->K >= 1024 && cdiv(a->M, 128) * batch >= 1024) BN = 256;
   }
   if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
@@ -1062,6 +1096,7 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     BM = g_tile_m;
     BN = g_tile_n;
   }
+  if (autosplit && g_split) split = g_split;
   const int64_t rs_floats = a->rowsum ? (int64_t)split * a->M : 0;
   if (split > 1 && (!plain || !a->workspace ||
                     a->workspace_bytes < ((int64_t)split * batch * a->M * a->N + rs_floats) * 4))

@@ -59,6 +59,7 @@ class _Workspace:
 WS = _Workspace()
 
 
+
 # ----------------------------------------------------------------------- GEMM ---
 def _split(t: torch.Tensor):
     """(batch strides (s1, s2), batch shape (z1, z2), row stride, col stride)."""
@@ -204,21 +205,24 @@ def _rows_ld(x, lead):
     return ld
 
 
-def ctc_fwd(logits, targets, ilen, tlen, lse, lp, alpha, nll):
+def ctc_fwd(logits, targets, ilen, tlen, lse, lp, alpha, nll, beta=None):
+    """beta given: the beta recursion runs in the forward launch too (then ctc_bwd with
+    beta_ready=True)."""
     B, T, V = logits.shape
     Lmax = targets.shape[1]
     N.call("lasr_ctc_fwd", ptr(logits), dt(logits), B, T, V, _rows_ld(logits, 1), ptr(targets), Lmax,
-           ptr(ilen), ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), stream())
+           ptr(ilen), ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(beta), ptr(nll), stream())
 
 
-def ctc_bwd(logits, targets, ilen, tlen, lse, lp, alpha, nll, beta, grad, gscale, gdev=None):
+def ctc_bwd(logits, targets, ilen, tlen, lse, lp, alpha, nll, beta, grad, gscale, gdev=None,
+            beta_ready=False):
     B, T, V = logits.shape
     Lmax = targets.shape[1]
     ld = _rows_ld(logits, 1)
     assert grad.shape == logits.shape and _rows_ld(grad, 1) == ld
     N.call("lasr_ctc_bwd", ptr(logits), dt(logits), B, T, V, ld, ptr(targets), Lmax, ptr(ilen),
-           ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), ptr(beta), ptr(grad), dt(grad),
-           gscale, ptr(gdev), stream())
+           ptr(tlen), ptr(lse), ptr(lp), ptr(alpha), ptr(nll), ptr(beta), int(beta_ready), ptr(grad),
+           dt(grad), gscale, ptr(gdev), stream())
 
 
 def lsm_kl_fwd(logits, target, ignore, smoothing, lse, loss_rows):

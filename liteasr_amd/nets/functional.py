@@ -601,12 +601,13 @@ class HybridLossFn(torch.autograd.Function):
         lse = _e(B * Tp, F32, dev)
         lp = _e(B * Tp * (L + 1), F32, dev)
         alpha = _e(B * Tp * S, F32, dev)
+        beta = _e(B * Tp * S, F32, dev)  # computed alongside alpha (one launch)
         nll = _e(B, F32, dev)
-        K.ctc_fwd(hc, prep.tgt_ctc, prep.pred_len, prep.ylen, lse, lp, alpha, nll)
+        K.ctc_fwd(hc, prep.tgt_ctc, prep.pred_len, prep.ylen, lse, lp, alpha, nll, beta=beta)
         loss = _e(1, F32, dev)
         K.loss_combine(nll, ctc_weight / B, rows, (1.0 - ctc_weight) / B, loss)
         ctx.sv = SimpleNamespace(ha=ha, hc=hc, prep=prep, lse_a=lse_a, lse=lse, lp=lp, alpha=alpha,
-                                 nll=nll, w=ctc_weight, s=smoothing, ign=ignore, B=B,
+                                 beta=beta, nll=nll, w=ctc_weight, s=smoothing, ign=ignore, B=B,
                                  shapes=(h_attn.shape, h_ctc.shape))
         ctx.parts = (nll, rows)
         return loss.view(())
@@ -621,8 +622,7 @@ class HybridLossFn(torch.autograd.Function):
         K.lsm_kl_bwd(sv.ha, sv.prep.tgt, sv.ign, sv.s, sv.lse_a, ga, (1.0 - sv.w) / B, gdev=g)
         gc = K.padded_rows(sv.hc.shape[0] * sv.hc.shape[1], sv.hc.shape[2], sv.hc.dtype, dev).view(sv.hc.shape)
         L = sv.prep.tgt_ctc.shape[1]
-        beta = _e(sv.alpha.numel(), F32, dev)
         K.ctc_bwd(sv.hc, sv.prep.tgt_ctc, sv.prep.pred_len, sv.prep.ylen, sv.lse, sv.lp, sv.alpha,
-                  sv.nll, beta, gc, sv.w / B, gdev=g)
+                  sv.nll, sv.beta, gc, sv.w / B, gdev=g, beta_ready=True)
         ctx.sv = None
         return ga.view(sv.shapes[0]), gc.view(sv.shapes[1]), None, None, None, None

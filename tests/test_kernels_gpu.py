@@ -315,6 +315,13 @@ def test_ctc(B, T, V, L, dtype):
     # torch's own fp32 ctc_loss is 5.8e-4 (max-abs) off its fp64 result on the 249x4233
     # case (the lattice sums ~600-nat log terms in fp32); allow 2e-3.
     close(gg[fin], gref[fin], 2e-3, "ctc grad")
+    # beta computed in the forward launch (alongside alpha): identical results
+    alpha2, beta2, nll2 = torch.empty_like(alpha), torch.empty_like(beta), torch.empty_like(nll)
+    kn.ctc_fwd(d_log, tg32, il, tl, lse, lpb, alpha2, nll2, beta=beta2)
+    grad2 = torch.empty_like(grad)
+    kn.ctc_bwd(d_log, tg32, il, tl, lse, lpb, alpha2, nll2, beta2, grad2, 1.0, beta_ready=True)
+    assert torch.equal(nll2.isfinite(), nll.isfinite()) and torch.equal(nll2[nll.isfinite()], nll[nll.isfinite()])
+    torch.testing.assert_close(grad2, grad, rtol=0, atol=0, equal_nan=True)  # infeasible rows: nan
 
 
 # ----------------------------------------------------------- label-smoothed KL
@@ -563,9 +570,10 @@ def test_subsampling_convs(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_conformer_conv_module_pieces(dtype):
+@pytest.mark.parametrize("Cc,T", [(64, 70), (200, 133)])
+def test_conformer_conv_module_pieces(dtype, Cc, T):
     kn = K()
-    B, T, Cc, Kk = 3, 70, 64, 15
+    B, Kk = 3, 15
     z1 = torch.randn(B, T, 2 * Cc, device=DEV).to(dtype)
     w = torch.randn(Cc, Kk, device=DEV) * 0.2
     bias = torch.randn(Cc, device=DEV) * 0.1
@@ -638,6 +646,16 @@ def test_embed_pe_and_prep():
     kn.embed_bwd(ids, dy, 4.0, dE)
     ref = torch.zeros(V, D, device=DEV, dtype=torch.float64).index_add_(0, ids.view(-1).long(), dy.double() * 4)
     close(dE, ref, 1e-6, "embed bwd")
+    # decoder-sized: 1312 rows (several ballot chunks), a frequent id (eos padding) and
+    # rare ones, against an fp64 index_add
+    R, D2, V2 = 1312, 256, 4233
+    ids2 = torch.randint(0, V2, (R,), device=DEV, dtype=torch.int32)
+    ids2[::3] = V2 - 1
+    dy2 = torch.randn(R, D2, device=DEV)
+    dE2 = torch.zeros(V2, D2, device=DEV)
+    kn.embed_bwd(ids2, dy2, 1.0, dE2)
+    ref2 = torch.zeros(V2, D2, device=DEV, dtype=torch.float64).index_add_(0, ids2.long(), dy2.double())
+    close(dE2, ref2, 1e-6, "embed bwd R=1312")
     # u2 bookkeeping vs literal python restatement
     xlens = torch.tensor([100, 97, 3], device=DEV)
     ys = torch.tensor([[5, 6, 7, 8], [2, 2, -1, -1], [-1, -1, -1, -1]], device=DEV)
