@@ -950,13 +950,43 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
   const int64_t MN = (int64_t)p.M * p.N;
   const int64_t total = MN * p.batch;
   const float al = alpha_of(p);
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int z = (int)(i / MN);
-    const int64_t r = i - (int64_t)z * MN;
-    float acc = 0.f;
-    for (int s = 0; s < p.split_k; ++s) acc += p.ws[((int64_t)s * p.batch + z) * MN + r];
-    const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
-    epi_store<TC>(p, z / p.batch_div, z % p.batch_div, z, m, n, acc, al);
+  if (p.v4) {
+    // 4 consecutive columns per thread (N % 4 == 0): 16-B partial loads, 4 slices in
+    // flight, summed in slice order
+    const int64_t sstride = (int64_t)p.batch * MN;
+    for (int64_t i4 = blockIdx.x * 256 + threadIdx.x; i4 < total / 4; i4 += (int64_t)gridDim.x * 256) {
+      const int64_t i = i4 * 4;
+      const int z = (int)(i / MN);
+      const int64_t r = i - (int64_t)z * MN;
+      const float* src = p.ws + (int64_t)z * MN + r;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      int sl = 0;
+      for (; sl + 4 <= p.split_k; sl += 4) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const f32x4*)(src + (int64_t)(sl + u) * sstride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] += v[u][e];
+      }
+      for (; sl < p.split_k; ++sl) {
+        const f32x4 v = *(const f32x4*)(src + (int64_t)sl * sstride);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += v[e];
+      }
+      const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
+      epi_store4<TC, true>(p, z / p.batch_div, z % p.batch_div, z, m, n, 4, acc, al);
+    }
+  } else {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+      const int z = (int)(i / MN);
+      const int64_t r = i - (int64_t)z * MN;
+      float acc = 0.f;
+      for (int s = 0; s < p.split_k; ++s) acc += p.ws[((int64_t)s * p.batch + z) * MN + r];
+      const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
+      epi_store<TC>(p, z / p.batch_div, z % p.batch_div, z, m, n, acc, al);
+    }
   }
   if (p.rs_ws) {  // bias-gradient partials (batch == 1)
     for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < p.M; m += (int64_t)gridDim.x * 256) {
@@ -1206,7 +1236,7 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   int rc = lasr_check_launch("lasr_gemm");
   if (!rc && split > 1 && a->split_k >= 0) {
     const int64_t total = (int64_t)a->M * a->N * batch;
-    const int nblk = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+    const int nblk = (int)std::min<int64_t>(cdiv(p.v4 ? total / 4 : total, 256), 4096);
     if (a->c_dtype == LASR_F32) splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);
     else splitk_reduce_kernel<bf16_t><<<nblk, 256, 0, st>>>(p);
     rc = lasr_check_launch("lasr_gemm/splitk_reduce");

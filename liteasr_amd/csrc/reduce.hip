@@ -1,12 +1,12 @@
 // Deterministic reduction of per-block partial sums: out[n] (+)= sum_p part[p*N + n].
-// 256-thread blocks cover 32 columns x 8 partial-groups (coalesced 128-B reads per
+// 256-thread blocks cover 16 columns x 16 partial-groups (coalesced 64-B reads per
 // group row); each thread sums its strided partials, then a fixed-order LDS combine.
 // Used by every "partials -> parameter gradient" epilogue (LayerNorm, bias colsums,
 // BatchNorm, depthwise conv, conv1, positional biases).
 #include "common.h"
 
-constexpr int RC_COLS = 32;
-constexpr int RC_GROUPS = 8;
+constexpr int RC_COLS = 16;
+constexpr int RC_GROUPS = 16;
 
 __global__ __launch_bounds__(256) void reduce_cols_kernel(const float* __restrict__ part, int P,
                                                           int64_t N, float* out0, float* out1,
