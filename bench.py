@@ -66,17 +66,22 @@ def synthetic(cfgd, rank, dev):
 
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
-ROOFLINE_KERNEL = "gemm_bf16_glds_kernel<128, 128, false, false, float, 3>"
+# template instance lasr_gemm launches for a split-K weight-gradient tile (gemm.hip
+# launch_bf16): ring depth and launch bound per tile
+_DW_INSTANCE = {(128, 128): (3, 3), (64, 128): (4, 3), (128, 64): (4, 3), (64, 64): (4, 3)}
 
 
 def roofline_case(cfgd, dev):
-    """The dominant kernel of the step (rocprof, profiles/r01): the weight-gradient GEMM
-    gemm_bf16_glds_kernel<128,128,false,false,float,3> (both operands M/N-contiguous, LDS
-    transposed reads, split-K fp32 partials).  Representative launch: the FFN fc1 dW,
-    dW1[ff, d] = dZ^T[ff, rows] @ LN[rows, d] with rows = B*T' — the largest and most frequent
-    shape of the family (4 of its 11 launches per Conformer layer).  Run in the library's
-    partials-only mode (split_k=-1) so the timed launches are that kernel alone; the
-    fixed-order split-K reduction is a separate kernel (splitk_reduce_kernel)."""
+    """The dominant kernel family of the step (rocprof, profiles/r01): the weight-gradient
+    GEMMs (both operands M/N-contiguous, LDS transposed reads, split-K fp32 partials; ~25 %
+    of the step).  Representative launch: the FFN fc1 dW, dW1[ff, d] = dZ^T[ff, rows] @
+    LN[rows, d] with rows = B*T' -- the largest and most frequent shape (4 of the 11 dW
+    launches of a Conformer layer).  Run in the library's partials-only mode (split_k=-1)
+    so the timed launches are that kernel alone; the fixed-order split-K reduction is a
+    separate kernel (splitk_reduce_kernel).
+    Algorithmic bytes: each bf16 operand read once + the fp32 result written once.  The
+    split-K partial slabs are NOT counted: they are traffic this design adds, so they
+    show up as PMC traffic above the algorithmic bytes."""
     import torch
 
     from liteasr_amd import kernels as K
@@ -87,16 +92,17 @@ def roofline_case(cfgd, dev):
     dz = torch.randn(rows, M, device=dev).bfloat16()
     ln = torch.randn(rows, N, device=dev).bfloat16()
     dw = torch.zeros(M, N, device=dev)
-    _, _, split = K.gemm_plan(dz.t(), ln, dw, beta=1.0, split_k=-1)
+    tm, tn, split = K.gemm_plan(dz.t(), ln, dw, beta=1.0, split_k=-1)
 
     def launch():
         K.gemm(dz.t(), ln, dw, beta=1.0, split_k=-1)
 
     flops = 2.0 * M * N * Kd
-    # algorithmic bytes of one launch: each bf16 operand read once + the fp32 partial slabs
-    bytes_ = 2.0 * (Kd * M + Kd * N) + 4.0 * split * M * N
-    meta = {"kernel": ROOFLINE_KERNEL, "shape": f"M={M} N={N} K={Kd} split_k={split}",
-            "grid": [-(-N // 128), -(-M // 128), split]}
+    bytes_ = 2.0 * (Kd * M + Kd * N) + 4.0 * M * N
+    S, minb = _DW_INSTANCE[(tm, tn)]
+    meta = {"kernel": f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}>",
+            "shape": f"M={M} N={N} K={Kd} split_k={split}",
+            "grid": [-(-N // tn), -(-M // tm), split]}
     return launch, flops, bytes_, meta
 
 
@@ -186,11 +192,12 @@ def cpu_baseline(cfgd_name, budget_s=25.0):
                                            model_dim=cfgd["d"])
         steps += 1
         el = time.perf_counter() - t0
-        if el + el / steps > budget_s or steps >= 3:
+        # ~10-25 s of timed CPU work (at least 3 steps), bounded so the bench stays short
+        if el + el / steps > budget_s or (steps >= 3 and el >= 10.0):
             break
     return {"value": round(Bs * steps / el, 3), "unit": "utterances/sec", "cores": n, "kind": "port",
             "sample": f"oracle (torch CPU fp32) {cfgd_name} U2, B={Bs} T={cfgd['T']} L={cfgd['L']}, dropout 0.1, "
-                      f"{steps} timed step(s) after 1 warm-up ({warm:.1f}s)"}
+                      f"{steps} timed step(s) = {el:.1f} s after 1 warm-up ({warm:.1f} s)"}
 
 
 def main():

@@ -13,7 +13,11 @@ from tools.gemm_graph_bench import graph_time, make  # noqa: E402
 
 SHAPES = [("ffn W1 2048x256", 2048, 256, 7968), ("ffn W2 256x2048", 256, 2048, 7968),
           ("Wo 256x256", 256, 256, 7968), ("pw1 512x256", 512, 256, 7968), ("qkv 768x256", 768, 256, 7968)]
-TILES = [(0, 0), (64, 64), (64, 128), (128, 64), (128, 128)]
+TILES = [(0, 0), (64, 64), (64, 128), (128, 64), (128, 128), (128, 256), (256, 128)]
+
+
+SPLITS = (0, 8, 16, 32)
+STAGES = (0,)
 
 
 def main():
@@ -23,9 +27,11 @@ def main():
         flops = 2.0 * M * N_ * Kd
         rows = []
         for tm, tn in TILES:
+            if tm > 2 * M or tn > 2 * N_:
+                continue
             N.call("lasr_gemm_force_tile", tm, tn)
-            for split in (0, 4, 8, 16):
-                for stages in (0, 4, 6):
+            for split in SPLITS:
+                for stages in STAGES:
                     N.call("lasr_gemm_force_split", split, stages)
                     plan = K.gemm_plan(a, b, c, **extra)
                     us = graph_time(lambda: K.gemm(a, b, c, **extra))
