@@ -76,20 +76,38 @@ typedef struct lasr_gemm_args {
   const void* aux; int aux_dtype; int64_t ldaux; int aux_act;
   float drop_p; uint64_t drop_seed;
   const void* res; int res_dtype; int64_t ldres; float res_scale;
-  int split_k; void* workspace; int64_t workspace_bytes;
+  int split_k;  /* 1: none, > 1: forced, 0: auto (fills the chip; needs workspace), -1: auto,
+                 fp32 partials only (no reduction; the caller sums the [split] slabs) */
+  void* workspace; int64_t workspace_bytes;
   /* optional fused bias gradient: rowsum[m] += sum_k A[m,k] (fp32, batch == 1, A
    * M-contiguous i.e. lda_m == 1: the dW = dY^T X GEMMs, rowsum = dbias).  Replaces the
    * separate column sum of dY (aten sum over rows in Linear's backward). */
   float* rowsum;
 } lasr_gemm_args;
 int lasr_gemm(const lasr_gemm_args* args, void* stream);
-int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k);
+/* Tile and split-K lasr_gemm would use; flags (nullable): LASR_PLAN_GLDS (LDS-DMA
+ * kernel), LASR_PLAN_ROWSUM_FUSED (rowsum computed in the GEMM; with split_k = -1 and a
+ * split > 1 its [split][M] partials follow the [split][batch][M][N] C partials in the
+ * workspace, else it is written to rowsum directly). */
+#define LASR_PLAN_GLDS 1
+#define LASR_PLAN_ROWSUM_FUSED 2
+int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k, int* flags);
 /* Tuning hook: force the bf16 LDS-DMA tile (64/128/256 x 64/128/256) of every later
  * lasr_gemm call in the process; (0, 0) restores the planner.  Benchmarks only. */
 int lasr_gemm_force_tile(int tile_m, int tile_n);
 /* Tuning hook: force the split-K factor of auto-split calls and the LDS ring depth (3..6)
  * of split-K LDS-DMA launches; (0, 0) restores the planner.  Benchmarks only. */
 int lasr_gemm_force_split(int split_k, int stages);
+
+/* Batched partial reductions (one launch for a backward node's deferred parameter
+ * gradients): out[n] (+)= sum_p part[p*N + n], n < split -> out0[n], else out1[n-split].
+ * Summation order per segment as the single-launch kernels (lasr_reduce_cols for P > 64,
+ * the split-K reduce for P <= 64 with N % 4 == 0), so results are bit-identical. */
+typedef struct lasr_reduce_seg {
+  const float* part; int64_t N; int P; int accumulate;
+  float* out0; float* out1; int64_t split;
+} lasr_reduce_seg;
+int lasr_reduce_multi(const lasr_reduce_seg* segs, int nseg, void* stream);
 
 /* Column sums: out[n] (+)= sum_m X[m,n]  (bias gradients; fp32 out).
  * Two-pass deterministic; workspace >= ceil(M/rows_per_block)*N floats (see impl). */
@@ -176,6 +194,7 @@ int lasr_qbias_fwd(const void* qkv, int dt, int B, int T, int H, int dk, int64_t
 int lasr_qbias_bwd(const void* dqu, const void* dqv, int dt, int B, int T, int H, int dk,
                    void* dqkv, int64_t ld_dqkv, float* dbias_u, float* dbias_v,
                    float* workspace, int64_t ws_floats, void* stream);
+/* (dbias_u = dbias_v = NULL: the [ceil(B*T/64)][2*H*dk] partials stay in workspace.) */
 int lasr_attn_softmax_fwd(const float* s_ac, const float* s_bd, int relpos, int B, int H,
                           int Tq, int Tk, int ldS, const uint8_t* mask, int64_t mask_sb,
                           int64_t mask_sq, void* P, int pdt, float drop_p, uint64_t seed,

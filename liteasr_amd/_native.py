@@ -47,6 +47,13 @@ class GemmArgs(C.Structure):
     ]
 
 
+class ReduceSeg(C.Structure):
+    """Mirror of ``lasr_reduce_seg``."""
+
+    _fields_ = [("part", _p), ("N", _l), ("P", _i), ("accumulate", _i), ("out0", _p), ("out1", _p),
+                ("split", _l)]
+
+
 # name -> argtypes (all return int unless listed in _RESTYPES)
 SIGNATURES = {
     "lasr_version": [],
@@ -54,12 +61,13 @@ SIGNATURES = {
     "lasr_set_dropout_counter": [_p],
     "lasr_counter_add": [_p, _u, _p],
     "lasr_gemm": [C.POINTER(GemmArgs), _p],
-    "lasr_gemm_plan": [C.POINTER(GemmArgs), _p, _p, _p],
+    "lasr_gemm_plan": [C.POINTER(GemmArgs), _p, _p, _p, _p],
     "lasr_gemm_force_tile": [C.c_int, C.c_int],
     "lasr_gemm_force_split": [C.c_int, C.c_int],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
                          _p, _p, _p, _i, _p, _p, _l, _p],
+    "lasr_reduce_multi": [C.POINTER(ReduceSeg), _i, _p],
     "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
     "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],
     "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,

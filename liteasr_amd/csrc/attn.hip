@@ -243,7 +243,7 @@ extern "C" int lasr_qbias_bwd(const void* dqu, const void* dqv, int dt, int B, i
   if (dt == LASR_F32) qbias_bwd_kernel<float><<<g, 256, 0, st>>>((const float*)dqu, (const float*)dqv, rows, D, (float*)dqkv, ld, ws);
   else qbias_bwd_kernel<bf16_t><<<g, 256, 0, st>>>((const bf16_t*)dqu, (const bf16_t*)dqv, rows, D, (bf16_t*)dqkv, ld, ws);
   int rc = lasr_check_launch("qbias_bwd");
-  if (rc) return rc;
+  if (rc || (!du && !dv)) return rc;  // no outputs: partials left in ws (deferred reduction)
   return lasr_reduce_cols(ws, (int)nchunk, 2 * D, du, dv, D, 1, st);
 }
 

@@ -8,6 +8,7 @@ no CPU path (the CPU restatement lives in ``oracle/`` and is test-only).
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 from typing import Optional
@@ -57,6 +58,52 @@ class _Workspace:
 
 
 WS = _Workspace()
+
+
+# --------------------------------------------------------- deferred reductions ---
+class _Deferred:
+    """Parameter-gradient reductions parked until the end of a backward node: the
+    partial-sum buffers of LayerNorm gamma/beta, the positional biases and the split-K
+    weight gradients (+ their bias rowsums) are collected and finished by ONE
+    lasr_reduce_multi launch, with each reduction's usual summation order."""
+
+    def __init__(self):
+        self.depth = 0
+        self.segs = []
+
+
+_DEFER = _Deferred()
+
+
+@contextlib.contextmanager
+def deferred_reductions():
+    """Within the block, gradient outputs of layernorm_bwd / qbias_bwd / split-K weight
+    GEMMs (split_k=0, beta 0 or 1, fp32 contiguous C) are only complete after the block
+    exits; nothing inside may read them."""
+    _DEFER.depth += 1
+    try:
+        yield
+    finally:
+        _DEFER.depth -= 1
+        if _DEFER.depth == 0:
+            flush_reductions()
+
+
+def _defer(part, P, Ncols, out0, out1=None, split=None, accumulate=True):
+    _DEFER.segs.append((part, int(P), int(Ncols), out0, out1, int(split if split is not None else Ncols),
+                        int(accumulate)))
+
+
+def flush_reductions():
+    segs, _DEFER.segs = _DEFER.segs, []
+    if not segs:
+        return
+    arr = (N.ReduceSeg * len(segs))()
+    for i, (part, P, Ncols, o0, o1, split, acc) in enumerate(segs):
+        arr[i] = N.ReduceSeg(ptr(part), Ncols, P, acc, ptr(o0), ptr(o1), split)
+    N.call("lasr_reduce_multi", arr, len(segs), stream())
+    # the partial buffers are released here; the caching allocator hands their memory only
+    # to work stream-ordered after the reduction
 
 
 
@@ -147,8 +194,25 @@ def gemm(
         args.workspace, args.workspace_bytes = ptr(ws), ws.numel() * 4
     if plan_only:
         tm, tn, sp = C.c_int(), C.c_int(), C.c_int()
-        N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp))
+        N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp), None)
         return tm.value, tn.value, sp.value
+    if (_DEFER.depth and split_k == 0 and beta in (0.0, 1.0) and alpha == 1.0 and alpha_dev is None
+            and bias is None and act == N.ACT_NONE and zout is None and aux is None and res is None
+            and drop_p <= 0.0 and z1 * z2 == 1 and c.dtype == torch.float32 and c.is_contiguous()):
+        tm, tn, sp, fl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp), C.byref(fl))
+        sp = sp.value
+        if sp > 1:
+            # partials-only launch (split_k = -1) into a buffer that lives until the flush
+            nrs = sp * M if rowsum is not None else 0
+            part = torch.empty(sp * M * Nn + nrs, dtype=torch.float32, device=c.device)
+            args.split_k = -1
+            args.workspace, args.workspace_bytes = ptr(part), part.numel() * 4
+            N.call("lasr_gemm", C.byref(args), stream())
+            _defer(part, sp, M * Nn, c, accumulate=beta == 1.0)
+            if rowsum is not None and fl.value & 2:  # LASR_PLAN_ROWSUM_FUSED: partials follow C's
+                _defer(part[sp * M * Nn:], sp, M, rowsum)
+            return c
     N.call("lasr_gemm", C.byref(args), stream())
     return c
 
@@ -182,12 +246,20 @@ def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd, y2=None, p2=0.0, seed2=0):
 def layernorm_bwd(x, dy, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, gb=None,
                   bscale=1.0, bp=0.0, bseed=0):
     rows, D = x.shape
-    nblk = (rows + 31) // 32
-    ws = WS.get(nblk * 2 * D, x.device)
+    nblk = (rows + 31) // 32  # LN_ROWS_PER_BLOCK (norm.hip)
+    defer = _DEFER.depth and dgamma is not None and dbeta is not None
+    if defer:
+        ws = torch.empty(nblk * 2 * D, dtype=torch.float32, device=x.device)
+        og, ob = None, None
+    else:
+        ws = WS.get(nblk * 2 * D, x.device)
+        og, ob = dgamma, dbeta
     N.call("lasr_layernorm_bwd", ptr(x), dt(x), ptr(dy), dt(dy), rows, D, ptr(gamma), ptr(mean),
            ptr(rstd), ptr(dres), dt(dres) if dres is not None else 0, ptr(dx), dt(dx),
-           ptr(dgamma), ptr(dbeta), ptr(ws), ws.numel(), ptr(gb),
+           ptr(og), ptr(ob), ptr(ws), ws.numel(), ptr(gb),
            dt(gb) if gb is not None else 0, bscale, bp, bseed, stream())
+    if defer:
+        _defer(ws, nblk, 2 * D, dgamma, dbeta, split=D)
 
 
 def branch_grad(dx, gb, scale, p=0.0, seed=0):
@@ -259,7 +331,14 @@ def qbias_fwd(qkv, B, T, H, dk, bu, bv, qu, qv):
 def qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, du, dv):
     rows = B * T
     D = H * dk
-    ws = WS.get(((rows + 63) // 64) * 2 * D, dqu.device)
+    nchunk = (rows + 63) // 64  # QB_ROWS (attn.hip)
+    if _DEFER.depth:
+        ws = torch.empty(nchunk * 2 * D, dtype=torch.float32, device=dqu.device)
+        N.call("lasr_qbias_bwd", ptr(dqu), ptr(dqv), dt(dqu), B, T, H, dk, ptr(dqkv), dqkv.stride(0),
+               None, None, ptr(ws), ws.numel(), stream())
+        _defer(ws, nchunk, 2 * D, du, dv, split=D)
+        return
+    ws = WS.get(nchunk * 2 * D, dqu.device)
     N.call("lasr_qbias_bwd", ptr(dqu), ptr(dqv), dt(dqu), B, T, H, dk, ptr(dqkv), dqkv.stride(0),
            ptr(du), ptr(dv), ptr(ws), ws.numel(), stream())
 

@@ -426,28 +426,30 @@ class ConformerLayerFn(torch.autograd.Function):
         dev, adt = dx5.device, env.adt
         M, d = x4.shape
         dx5 = dx5.contiguous()
-        # final LN; emits the (d)-branch gradient 0.5*drop(dx4)
-        dx4 = _e((M, d), F32, dev)
-        gb = _e((M, d), adt, dev)
-        K.layernorm_bwd(x4, dx5, w.ln_f.g, mf, rf, dx4, g.ln_f.g, g.ln_f.b, gb=gb, bscale=0.5,
-                        bp=pd, bseed=_seed(s, 7))
-        dln = ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2,
-                           g.ff.b2, ACT_SWISH, pff, _seed(s, 6))
-        dx3 = _e((M, d), F32, dev)
-        K.layernorm_bwd(x3, dln, w.ln_d.g, md, rd, dx3, g.ln_d.g, g.ln_d.b, dres=dx4, gb=gb,
-                        bscale=1.0, bp=pd, bseed=_seed(s, 5))
-        dln = conv_backward(gb, ln_c, sv.svc, w.conv, g.conv, env)
-        dx2 = _e((M, d), F32, dev)
-        K.layernorm_bwd(x2, dln, w.ln_c.g, mc, rc, dx2, g.ln_c.g, g.ln_c.b, dres=dx3, gb=gb,
-                        bscale=1.0, bp=pd, bseed=_seed(s, 4))
-        dln = relmha_backward(gb, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3))
-        dx1 = _e((M, d), F32, dev)
-        K.layernorm_bwd(x1, dln, w.ln_b.g, mb, rb, dx1, g.ln_b.g, g.ln_b.b, dres=dx2, gb=gb,
-                        bscale=0.5, bp=pd, bseed=_seed(s, 2))
-        dln = ffn_backward(gb, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1,
-                           g.ffm.W2, g.ffm.b2, ACT_SWISH, pff, _seed(s, 1))
-        dx0 = _e((M, d), F32, dev)
-        K.layernorm_bwd(x0, dln, w.ln_a.g, ma, ra, dx0, g.ln_a.g, g.ln_a.b, dres=dx1)
+        # parameter-gradient reductions of the whole layer finish in one launch at the end
+        with K.deferred_reductions():
+            # final LN; emits the (d)-branch gradient 0.5*drop(dx4)
+            dx4 = _e((M, d), F32, dev)
+            gb = _e((M, d), adt, dev)
+            K.layernorm_bwd(x4, dx5, w.ln_f.g, mf, rf, dx4, g.ln_f.g, g.ln_f.b, gb=gb, bscale=0.5,
+                            bp=pd, bseed=_seed(s, 7))
+            dln = ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2,
+                               g.ff.b2, ACT_SWISH, pff, _seed(s, 6))
+            dx3 = _e((M, d), F32, dev)
+            K.layernorm_bwd(x3, dln, w.ln_d.g, md, rd, dx3, g.ln_d.g, g.ln_d.b, dres=dx4, gb=gb,
+                            bscale=1.0, bp=pd, bseed=_seed(s, 5))
+            dln = conv_backward(gb, ln_c, sv.svc, w.conv, g.conv, env)
+            dx2 = _e((M, d), F32, dev)
+            K.layernorm_bwd(x2, dln, w.ln_c.g, mc, rc, dx2, g.ln_c.g, g.ln_c.b, dres=dx3, gb=gb,
+                            bscale=1.0, bp=pd, bseed=_seed(s, 4))
+            dln = relmha_backward(gb, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3))
+            dx1 = _e((M, d), F32, dev)
+            K.layernorm_bwd(x1, dln, w.ln_b.g, mb, rb, dx1, g.ln_b.g, g.ln_b.b, dres=dx2, gb=gb,
+                            bscale=0.5, bp=pd, bseed=_seed(s, 2))
+            dln = ffn_backward(gb, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1,
+                               g.ffm.W2, g.ffm.b2, ACT_SWISH, pff, _seed(s, 1))
+            dx0 = _e((M, d), F32, dev)
+            K.layernorm_bwd(x0, dln, w.ln_a.g, ma, ra, dx0, g.ln_a.g, g.ln_a.b, dres=dx1)
         ctx.sv = None
         layer.on_grads_ready()
         return dx0, None, None, None, None
@@ -537,38 +539,39 @@ class HeadsFn(torch.autograd.Function):
         # ---- decoder
         wd, gd = dec.weights(), dec.grads()
         d = wd.d
-        if g_attn is not None:
-            g_attn = _rows2d(g_attn, R)
-            K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0, rowsum=gd.bout)
-            dyf = _e((R, d), adt, dev)
-            K.gemm(g_attn, wd.Wout, dyf)
-            dy = _e((R, d), F32, dev)
-            K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
-            gb = _e((R, d), adt, dev)
-            for i in range(len(wd.layers) - 1, -1, -1):
-                lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
-                s = dec.dec_layers[i].seed
-                y0, y1, y2 = ls.y
-                l1, l2, l3 = ls.ln
-                (m1, r1), (m2, r2), (m3, r3) = ls.st
-                K.branch_grad(dy, gb, 1.0, pd, _seed(s, 6))
-                dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1,
-                                   lg.ff.W2, lg.ff.b2, ACT_RELU, pff, _seed(s, 5))
-                dy2 = _e((R, d), F32, dev)
-                K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb,
-                                bscale=1.0, bp=pd, bseed=_seed(s, 4))
-                dln = mha_backward(gb, l2, sv.h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, env.mask_k, T,
-                                   0, pca, _seed(s, 3), dh)
-                dy1 = _e((R, d), F32, dev)
-                K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb,
-                                bscale=1.0, bp=pd, bseed=_seed(s, 2))
-                dln = mha_backward(gb, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, env.dec_mask,
-                                   L1 * L1, L1, pat, _seed(s, 1), None)
-                dy0 = _e((R, d), F32, dev)
-                K.layernorm_bwd(y0, dln, lw.ln1.g, m1, r1, dy0, lg.ln1.g, lg.ln1.b, dres=dy1)
-                dy = dy0
-            K.embed_bwd(env.ys_in, dy, math.sqrt(d), gd.E, env.p_dec_pos if env.training else 0.0,
-                        env.seed + 3)
+        with K.deferred_reductions():  # decoder parameter-gradient reductions: one launch
+            if g_attn is not None:
+                g_attn = _rows2d(g_attn, R)
+                K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0, rowsum=gd.bout)
+                dyf = _e((R, d), adt, dev)
+                K.gemm(g_attn, wd.Wout, dyf)
+                dy = _e((R, d), F32, dev)
+                K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
+                gb = _e((R, d), adt, dev)
+                for i in range(len(wd.layers) - 1, -1, -1):
+                    lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
+                    s = dec.dec_layers[i].seed
+                    y0, y1, y2 = ls.y
+                    l1, l2, l3 = ls.ln
+                    (m1, r1), (m2, r2), (m3, r3) = ls.st
+                    K.branch_grad(dy, gb, 1.0, pd, _seed(s, 6))
+                    dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1,
+                                       lg.ff.W2, lg.ff.b2, ACT_RELU, pff, _seed(s, 5))
+                    dy2 = _e((R, d), F32, dev)
+                    K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb,
+                                    bscale=1.0, bp=pd, bseed=_seed(s, 4))
+                    dln = mha_backward(gb, l2, sv.h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, env.mask_k, T,
+                                       0, pca, _seed(s, 3), dh)
+                    dy1 = _e((R, d), F32, dev)
+                    K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb,
+                                    bscale=1.0, bp=pd, bseed=_seed(s, 2))
+                    dln = mha_backward(gb, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, env.dec_mask,
+                                       L1 * L1, L1, pat, _seed(s, 1), None)
+                    dy0 = _e((R, d), F32, dev)
+                    K.layernorm_bwd(y0, dln, lw.ln1.g, m1, r1, dy0, lg.ln1.g, lg.ln1.b, dres=dy1)
+                    dy = dy0
+                K.embed_bwd(env.ys_in, dy, math.sqrt(d), gd.E, env.p_dec_pos if env.training else 0.0,
+                            env.seed + 3)
         dec.on_grads_ready()
         # ---- encoder after_norm
         we, ge = enc.after_norm_weights(), enc.after_norm_grads()

@@ -205,6 +205,31 @@ def test_eval_forward_uses_running_stats():
     assert rel(hc, hc_o) < 2e-4
 
 
+def test_deferred_reductions_bit_exact(monkeypatch):
+    """kernels.deferred_reductions (one lasr_reduce_multi launch per backward node) gives
+    the same gradients, bit for bit, as the immediate per-call reductions."""
+    import contextlib
+
+    from liteasr_amd import kernels as Kn
+    from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+
+    params = O.init_params(SMALL, seed=5)
+    xs, xlens, ys, ylens = [t.cuda() for t in O.synthetic_batch(2, 300, 9, SMALL["vocab_size"], seed=4)]
+    grads = []
+    for defer in (True, False):
+        if not defer:
+            monkeypatch.setattr(Kn, "deferred_reductions", contextlib.nullcontext)
+        model = build(SMALL, "bf16")
+        model.load_state_dict({**params, **O.init_buffers(SMALL)}, strict=False)
+        model = model.cuda().train()
+        crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=SMALL["vocab_size"], smoothing=0.1, ctc_weight=0.3))
+        crit(model, xs, xlens, ys, ylens).backward()
+        grads.append({n: p.grad.detach().clone() for n, p in model.named_parameters()})
+    assert not Kn._DEFER.segs and Kn._DEFER.depth == 0
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+
+
 def test_dropout_train_step_runs_and_is_deterministic():
     """Dropout cannot match torch's RNG bit-for-bit; check the step is finite, that the
     same device counter reproduces the same loss, and that the keep rate is right
