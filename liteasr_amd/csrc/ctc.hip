@@ -36,10 +36,29 @@ __global__ __launch_bounds__(256) void ctc_lse_gather_kernel(const T* __restrict
   }
   const T* x = logits + (int64_t)row * ld;
   float m = -INFINITY, s = 0.f;
-  for (int c = threadIdx.x; c < V; c += blockDim.x) {
-    const float v = to_f(x[c]);
+  auto acc = [&](float v) {
     if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
     else s += __expf(v - m);
+  };
+  if (ld % 8 == 0 && ((uintptr_t)logits & 15) == 0) {  // 16-B loads, 8 columns per thread
+    for (int c0 = threadIdx.x * 8; c0 < V; c0 += blockDim.x * 8) {
+      if (c0 + 8 <= V) {
+        float v[8];
+        ldv<8>(x + c0, v);
+        float mx = v[0];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) mx = fmaxf(mx, v[q]);
+        float e = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) e += __expf(v[q] - mx);
+        if (mx > m) { s = s * __expf(m - mx) + e; m = mx; }
+        else s += e * __expf(mx - m);
+      } else {
+        for (int c = c0; c < V; ++c) acc(to_f(x[c]));
+      }
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += blockDim.x) acc(to_f(x[c]));
   }
   const float M = block_max(m, red);
   const float S = block_sum(m == -INFINITY ? 0.f : s * __expf(m - M), red + 16);
@@ -209,8 +228,18 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
   const int b = row / T_, t = row - b * T_;
   TG* g = grad + (int64_t)row * ld;
   const int Tb = ilen[b];
+  // 8 columns per thread with 16-B accesses when the rows allow it (ld % 8, aligned base)
+  const bool vec = ld % 8 == 0 && ((uintptr_t)logits & 15) == 0 && ((uintptr_t)grad & 15) == 0;
   if (t >= Tb) {
-    for (int c = threadIdx.x; c < V; c += blockDim.x) g[c] = from_f<TG>(0.f);
+    if (vec) {
+      const float z8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int c0 = threadIdx.x * 8; c0 < V; c0 += blockDim.x * 8) {
+        if (c0 + 8 <= V) stv<8>(g + c0, z8);
+        else for (int c = c0; c < V; ++c) g[c] = from_f<TG>(0.f);
+      }
+    } else {
+      for (int c = threadIdx.x; c < V; c += blockDim.x) g[c] = from_f<TG>(0.f);
+    }
     return;
   }
   const int Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
@@ -235,14 +264,30 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
   const float gs = gscale * (gdev ? gdev[0] : 1.f);
   const T* x = logits + (int64_t)row * ld;
   const float l = lse[row];
-  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+  auto gamma_of = [&](int c) {
     float sub = (c == 0) ? gb : 0.f;
     if (c != 0 && ((bits[c >> 5] >> (c & 31)) & 1u)) {
       for (int j = 0; j < Lb; ++j)
         if (lab[j] == c) sub += glab[j];
     }
-    g[c] = from_f<TG>(gs * (__expf(to_f(x[c]) - l) - sub));
+    return sub;
+  };
+  if (vec) {
+    for (int c0 = threadIdx.x * 8; c0 < V; c0 += blockDim.x * 8) {
+      if (c0 + 8 <= V) {
+        float v[8];
+        ldv<8>(x + c0, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = gs * (__expf(v[q] - l) - gamma_of(c0 + q));
+        stv<8>(g + c0, v);
+      } else {
+        for (int c = c0; c < V; ++c) g[c] = from_f<TG>(gs * (__expf(to_f(x[c]) - l) - gamma_of(c)));
+      }
+    }
+    return;
   }
+  for (int c = threadIdx.x; c < V; c += blockDim.x)
+    g[c] = from_f<TG>(gs * (__expf(to_f(x[c]) - l) - gamma_of(c)));
 }
 
 static int ctc_block(int S) {
