@@ -1,4 +1,4 @@
-// Fused relative-position self-attention (encoder MHSA), bf16 operands, d_k = 64.
+// Fused relative-position self-attention (encoder MHSA), bf16 operands, d_k = 64 or 32.
 // Reference: liteasr/nets/attention.py RelativeMultiHeadAttention.forward :120-154
 // (ac = (q+u) k^T, bd = rel_shift((q+v) p^T), (ac+bd)/sqrt(d_k), masked_fill(-1e38),
 // softmax, attn @ v), legacy rel_shift :99-118.
@@ -33,8 +33,8 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 namespace {
 
-constexpr int DK = 64;
-constexpr int KS = DK / 32;   // k steps of v_mfma_f32_16x16x32_bf16 over d_k
+// d_k (DK) is a template parameter: 64 (small / long configs) or 32 (large, 16 heads).  The
+// LDS images stay 64 columns wide; with DK = 32 only their first 32 columns are filled/read.
 constexpr int GLD = 84;       // fp32 row stride of a wave's G window (80 + 4)
 constexpr int PLD = 72;       // bf16 row stride of a wave's P / dS tile (64 + 8)
 
@@ -94,16 +94,21 @@ LASR_DEV bf16x8 frag_tr(const bf16_t* img, int cbase, int lane) {
 struct Blk {
   uint4 x0, x1;
 };
+template <int DK>
 LASR_DEV Blk blk_fetch(const bf16_t* src, int64_t ld, int row0, int nrows, int tid) {
+  constexpr int SH = DK == 64 ? 3 : 2;  // log2(16-B chunks per row)
   Blk r;
-  r.x0 = *(const uint4*)(src + (int64_t)min(row0 + (tid >> 3), nrows - 1) * ld + (tid & 7) * 8);
-  r.x1 = *(const uint4*)(src + (int64_t)min(row0 + 32 + (tid >> 3), nrows - 1) * ld + (tid & 7) * 8);
+  r.x0 = *(const uint4*)(src + (int64_t)min(row0 + (tid >> SH), nrows - 1) * ld + (tid & ((1 << SH) - 1)) * 8);
+  if constexpr (DK == 64)
+    r.x1 = *(const uint4*)(src + (int64_t)min(row0 + 32 + (tid >> 3), nrows - 1) * ld + (tid & 7) * 8);
   return r;
 }
 // ... registers -> LDS image
+template <int DK>
 LASR_DEV void blk_store(bf16_t* img, const Blk& r, int tid) {
-  *(uint4*)(img + img_off(tid >> 3, (tid & 7) * 8)) = r.x0;
-  *(uint4*)(img + img_off(32 + (tid >> 3), (tid & 7) * 8)) = r.x1;
+  constexpr int SH = DK == 64 ? 3 : 2;
+  *(uint4*)(img + img_off(tid >> SH, (tid & ((1 << SH) - 1)) * 8)) = r.x0;
+  if constexpr (DK == 64) *(uint4*)(img + img_off(32 + (tid >> 3), (tid & 7) * 8)) = r.x1;
 }
 
 // Relative-position window of a (64-query, 64-key) block pair: row r <-> m = mlo + r,
@@ -116,27 +121,30 @@ struct PeWin {
   uint4 x[4];
   uint32_t valid;
 };
+template <int DK>
 LASR_DEV uint4 pe_chunk(const bf16_t* ph, int64_t ldp, int T, int mlo, int u, uint32_t& valid, int it) {
-  const int m = mlo + (u >> 3);
+  constexpr int CPR = DK / 8;  // 16-B chunks per row
+  const int m = mlo + u / CPR;
   const bool v1 = m >= 0 && m <= T - 1, v2 = m >= T + 1 && m <= 2 * T;
   const int src = v1 ? m : (v2 ? m - T - 1 : 0);
   valid |= (v1 || v2 ? 1u : 0u) << it;
-  return *(const uint4*)(ph + (int64_t)src * ldp + (u & 7) * 8);
+  return *(const uint4*)(ph + (int64_t)src * ldp + (u % CPR) * 8);
 }
+template <int DK>
 LASR_DEV PeWin pe_fetch(const bf16_t* ph, int64_t ldp, int T, int mlo, int tid) {
   PeWin r;
   r.valid = 0;
-  r.x[0] = pe_chunk(ph, ldp, T, mlo, tid, r.valid, 0);
-  r.x[1] = pe_chunk(ph, ldp, T, mlo, 256 + tid, r.valid, 1);
-  r.x[2] = pe_chunk(ph, ldp, T, mlo, 512 + tid, r.valid, 2);
-  r.x[3] = pe_chunk(ph, ldp, T, mlo, 768 + tid, r.valid, 3);
+#pragma unroll
+  for (int it = 0; it < DK / 16; ++it) r.x[it] = pe_chunk<DK>(ph, ldp, T, mlo, it * 256 + tid, r.valid, it);
   return r;
 }
+template <int DK>
 LASR_DEV void pe_store(bf16_t* img, const PeWin& r, int tid) {
+  constexpr int CPR = DK / 8;
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < DK / 16; ++it) {
     const int u = it * 256 + tid;
-    *(uint4*)(img + (u >> 3) * PELD + (u & 7) * 8) = ((r.valid >> it) & 1u) ? r.x[it] : make_uint4(0, 0, 0, 0);
+    *(uint4*)(img + (u / CPR) * PELD + (u % CPR) * 8) = ((r.valid >> it) & 1u) ? r.x[it] : make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -163,9 +171,11 @@ LASR_DEV uint32_t keymask_bits(const KeyMask& km) {
 // Scaled, masked scores of wave w's 16 query rows (iw = i0 + 16w ..) x the 64 keys j0 ..
 // from the staged K image and relative-position window.
 // s[c][q]: row iw + 4*(lane/16) + q, key j0 + 16c + lane%16.  -inf past T, -1e38 masked.
-LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* peimg, const bf16x8 (&qu)[KS],
-                         const bf16x8 (&qv)[KS], const bf16x8 (&qv1)[KS], int b, int w, int iw, int j0,
+template <int DK>
+LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* peimg, const bf16x8 (&qu)[DK / 32],
+                         const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int b, int w, int iw, int j0,
                          uint32_t mbits, float* gw, f32x4 (&s)[4], int lane) {
+  constexpr int KS = DK / 32;
   const int T = a.T, col = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -224,8 +234,10 @@ LASR_DEV float rsum16(float v) {
 }
 
 // Query-side fragments of 16 rows from global (A operands: row = lane%16, k = 8*(lane/16)).
-LASR_DEV void load_qfrags(const RelAttnP& a, int b, int h, int iw, int lane, bf16x8 (&qu)[KS],
-                          bf16x8 (&qv)[KS], bf16x8 (&qv1)[KS]) {
+template <int DK>
+LASR_DEV void load_qfrags(const RelAttnP& a, int b, int h, int iw, int lane, bf16x8 (&qu)[DK / 32],
+                          bf16x8 (&qv)[DK / 32], bf16x8 (&qv1)[DK / 32]) {
+  constexpr int KS = DK / 32;
   const int T = a.T, col = lane & 15, g = lane >> 4;
   const int r = min(iw + col, T - 1), r1 = min(iw + col + 1, T - 1);
   const int64_t base = (int64_t)b * T;
@@ -243,7 +255,9 @@ LASR_DEV void load_qfrags(const RelAttnP& a, int b, int h, int iw, int lane, bf1
 // Forward, one pass with the online softmax: per key block, stage K / V / the position
 // window (the next block's global loads in flight while this one computes), S on MFMA,
 // running max / sum, O = O * exp(m_old - m_new) + P V.
+template <int DK>
 __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
+  constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
   __shared__ __attribute__((aligned(16))) bf16_t psh[4][16 * PLD];
   __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
@@ -260,9 +274,9 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   bf16_t* pw = psh[w];
 
   bf16x8 qu[KS], qv[KS], qv1[KS];
-  load_qfrags(a, b, h, iw, lane, qu, qv, qv1);
-    Blk rk = blk_fetch(kh, a.ldkv, 0, T, tid), rv = blk_fetch(vh, a.ldkv, 0, T, tid);
-  PeWin rp = pe_fetch(ph, a.ldp, T, -i0 + T - 64, tid);
+  load_qfrags<DK>(a, b, h, iw, lane, qu, qv, qv1);
+    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, T, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, T, tid);
+  PeWin rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
   KeyMask km;
   keymask_fetch(a, b, 0, lane, km);
 
@@ -274,18 +288,18 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   for (int t = 0; t < DK / 16; ++t) o[t] = zero4();
   for (int j0 = 0; j0 < T; j0 += 64) {
     __syncthreads();  // previous block's images consumed
-    blk_store(ksh, rk, tid);
-    blk_store(vsh, rv, tid);
-    pe_store(pesh, rp, tid);
+    blk_store<DK>(ksh, rk, tid);
+    blk_store<DK>(vsh, rv, tid);
+    pe_store<DK>(pesh, rp, tid);
     const uint32_t mb_cur = keymask_bits(km);
     __syncthreads();
     // prefetch the next key block (unconditional: clamped rows keep the last one in
     // bounds, and no branch merge forces a wait on the loads)
-    rk = blk_fetch(kh, a.ldkv, j0 + 64, T, tid);
-    rv = blk_fetch(vh, a.ldkv, j0 + 64, T, tid);
-    rp = pe_fetch(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
+    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, T, tid);
+    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, T, tid);
+    rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
     keymask_fetch(a, b, j0 + 64, lane, km);
-    score_tile(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, gw, s, lane);
+    score_tile<DK>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, gw, s, lane);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float bm = rmax16(fmaxf(fmaxf(s[0][q], s[1][q]), fmaxf(s[2][q], s[3][q])));
@@ -332,9 +346,11 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
 // P and dS of one (16 x 64) tile: P as the forward normalised it (a fully masked row is
 // uniform, attention.py:54-55), dS = P (dP - D), zero where masked (masked_fill backward),
 // past T or past the rows.  dP = dO V^T with V from its staged image.
-LASR_DEV void dscore_tile(const RelAttnP& a, const bf16_t* vimg, const bf16x8 (&dof)[KS], const f32x4 (&s)[4],
+template <int DK>
+LASR_DEV void dscore_tile(const RelAttnP& a, const bf16_t* vimg, const bf16x8 (&dof)[DK / 32], const f32x4 (&s)[4],
                           const float (&mx)[4], const float (&il)[4], const float (&D)[4], int iw,
                           int lane, f32x4 (&p)[4], f32x4 (&ds)[4]) {
+  constexpr int KS = DK / 32;
   const int T = a.T, g = lane >> 4;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -351,7 +367,9 @@ LASR_DEV void dscore_tile(const RelAttnP& a, const bf16_t* vimg, const bf16x8 (&
   }
 }
 
+template <int DK>
 __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
+  constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
   __shared__ __attribute__((aligned(16))) bf16_t psh[4][16 * PLD];
   __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
@@ -367,12 +385,12 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   float* gw = gsh[w];
   bf16_t* pw = psh[w];
 
-    Blk rk = blk_fetch(kh, a.ldkv, 0, T, tid), rv = blk_fetch(vh, a.ldkv, 0, T, tid);
-  PeWin rp = pe_fetch(ph, a.ldp, T, -i0 + T - 64, tid);
+    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, T, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, T, tid);
+  PeWin rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
   KeyMask km;
   keymask_fetch(a, b, 0, lane, km);
   bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
-  load_qfrags(a, b, h, iw, lane, qu, qv, qv1);
+  load_qfrags<DK>(a, b, h, iw, lane, qu, qv, qv1);
   {
     const bf16_t* pd = a.dctx + (base + min(iw + col, T - 1)) * a.ldc + h * DK + 8 * g;
 #pragma unroll
@@ -384,14 +402,15 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
     const int i = min(iw + 4 * g + q, T - 1);
     mx[q] = a.stats[2 * (zrow + i)];
     il[q] = a.stats[2 * (zrow + i) + 1];
-    // D_i = sum_c dO[i,c] O[i,c]: the 16 lanes of the row group take 4 columns each
-    const bf16_t* pd = a.dctx + (base + i) * a.ldc + h * DK + 4 * col;
-    const bf16_t* po = a.ctx_in + (base + i) * a.ldc + h * DK + 4 * col;
-    const uint2 ud = *(const uint2*)pd, uo = *(const uint2*)po;
-    float acc = __uint_as_float(ud.x << 16) * __uint_as_float(uo.x << 16) +
-                __uint_as_float(ud.x & 0xffff0000u) * __uint_as_float(uo.x & 0xffff0000u) +
-                __uint_as_float(ud.y << 16) * __uint_as_float(uo.y << 16) +
-                __uint_as_float(ud.y & 0xffff0000u) * __uint_as_float(uo.y & 0xffff0000u);
+    // D_i = sum_c dO[i,c] O[i,c]: the 16 lanes of the row group take DK/16 columns each
+    const bf16_t* pd = a.dctx + (base + i) * a.ldc + h * DK + (DK / 16) * col;
+    const bf16_t* po = a.ctx_in + (base + i) * a.ldc + h * DK + (DK / 16) * col;
+    float vd[DK / 16], vo[DK / 16];
+    ldv<DK / 16>(pd, vd);
+    ldv<DK / 16>(po, vo);
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < DK / 16; ++e) acc += vd[e] * vo[e];
     D[q] = rsum16(acc);
     if (col == 0 && iw + 4 * g + q < T) a.Dbuf[zrow + iw + 4 * g + q] = D[q];
   }
@@ -403,17 +422,17 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   f32x4 s[4], p[4], ds[4];
   for (int j0 = 0; j0 < T; j0 += 64) {
     __syncthreads();
-    blk_store(ksh, rk, tid);
-    blk_store(vsh, rv, tid);
-    pe_store(pesh, rp, tid);
+    blk_store<DK>(ksh, rk, tid);
+    blk_store<DK>(vsh, rv, tid);
+    pe_store<DK>(pesh, rp, tid);
     const uint32_t mb_cur = keymask_bits(km);
     __syncthreads();
-    rk = blk_fetch(kh, a.ldkv, j0 + 64, T, tid);  // next block (unconditional, clamped)
-    rv = blk_fetch(vh, a.ldkv, j0 + 64, T, tid);
-    rp = pe_fetch(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
+    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, T, tid);  // next block (unconditional, clamped)
+    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, T, tid);
+    rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
     keymask_fetch(a, b, j0 + 64, lane, km);
-    score_tile(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, gw, s, lane);
-    dscore_tile(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
+    score_tile<DK>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, gw, s, lane);
+    dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -451,7 +470,9 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
 // dK, dV of one key block: loops over the query blocks; per block the Qu / dO images (A of
 // the scores, B of dK / dV), query stats and the position window are staged (next block
 // prefetched), the K / V fragments of the block stay in registers.
+template <int DK>
 __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
+  constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
   __shared__ __attribute__((aligned(16))) bf16_t pimg[64 * 64];  // P  [i][j]
   __shared__ __attribute__((aligned(16))) bf16_t simg[64 * 64];  // dS [i][j]
@@ -471,10 +492,10 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
   KeyMask km;
   keymask_fetch(a, b, j0, lane, km);
   const uint32_t mbits = keymask_bits(km);
-  blk_store(ksh, blk_fetch(a.k + base * a.ldkv + h * DK, a.ldkv, j0, T, tid), tid);
-  blk_store(vsh, blk_fetch(a.v + base * a.ldkv + h * DK, a.ldkv, j0, T, tid), tid);
-  Blk rq = blk_fetch(quh, a.ldq, 0, T, tid), ro = blk_fetch(doh, a.ldc, 0, T, tid);
-  PeWin rp = pe_fetch(ph, a.ldp, T, j0 + T - 64, tid);
+  blk_store<DK>(ksh, blk_fetch<DK>(a.k + base * a.ldkv + h * DK, a.ldkv, j0, T, tid), tid);
+  blk_store<DK>(vsh, blk_fetch<DK>(a.v + base * a.ldkv + h * DK, a.ldkv, j0, T, tid), tid);
+  Blk rq = blk_fetch<DK>(quh, a.ldq, 0, T, tid), ro = blk_fetch<DK>(doh, a.ldc, 0, T, tid);
+  PeWin rp = pe_fetch<DK>(ph, a.ldp, T, j0 + T - 64, tid);
 
   f32x4 dk[DK / 16], dv[DK / 16];
 #pragma unroll
@@ -483,9 +504,9 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
   for (int i0 = 0; i0 < T; i0 += 64) {
     const int iw = i0 + 16 * w;
     __syncthreads();  // images of the previous query block consumed
-    blk_store(qimg, rq, tid);
-    blk_store(oimg, ro, tid);
-    pe_store(pesh, rp, tid);
+    blk_store<DK>(qimg, rq, tid);
+    blk_store<DK>(oimg, ro, tid);
+    pe_store<DK>(pesh, rp, tid);
     // per-row operands of this wave's 16 queries (global; qv / qv1 are not staged)
     bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
     {
@@ -507,16 +528,16 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
       D[q] = a.Dbuf[zrow + i];
     }
     __syncthreads();
-    rq = blk_fetch(quh, a.ldq, i0 + 64, T, tid);  // next block (unconditional, clamped)
-    ro = blk_fetch(doh, a.ldc, i0 + 64, T, tid);
-    rp = pe_fetch(ph, a.ldp, T, j0 - (i0 + 64) + T - 64, tid);
+    rq = blk_fetch<DK>(quh, a.ldq, i0 + 64, T, tid);  // next block (unconditional, clamped)
+    ro = blk_fetch<DK>(doh, a.ldc, i0 + 64, T, tid);
+    rp = pe_fetch<DK>(ph, a.ldp, T, j0 - (i0 + 64) + T - 64, tid);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       qu[ks] = frag_row(qimg, 16 * w, 32 * ks, lane);
       dof[ks] = frag_row(oimg, 16 * w, 32 * ks, lane);
     }
-    score_tile(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mbits, gw, s, lane);
-    dscore_tile(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
+    score_tile<DK>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mbits, gw, s, lane);
+    dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -561,7 +582,7 @@ extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, con
                                 int H, int T, int dk, const uint8_t* mask, int64_t mask_sb,
                                 int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc,
                                 void* stream) {
-  LASR_CHECK_ARG(dk == DK, "lasr_relattn_fwd: d_k=%d (only 64)", dk);
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_fwd: d_k=%d (32 or 64)", dk);
   LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_fwd: bad B/H/T");
   LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc >= H * dk,
                  "lasr_relattn_fwd: row strides must be multiples of 8");
@@ -575,7 +596,8 @@ extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, con
   a.B = B; a.H = H; a.T = T; a.scale = scale;
   a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
   dim3 grid((unsigned)cdiv(T, 64), (unsigned)H, (unsigned)B);
-  relattn_fwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  if (dk == 64) relattn_fwd_kernel<64><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  else relattn_fwd_kernel<32><<<grid, 256, 0, (hipStream_t)stream>>>(a);
   return lasr_check_launch("relattn_fwd");
 }
 
@@ -585,7 +607,7 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
                                 int64_t mask_sq, float scale, const float* stats, const void* ctx,
                                 const void* dctx, int64_t ldc, float* Dbuf, void* dqu, void* dbd,
                                 int ldS, void* dk_out, void* dv_out, int64_t lddkv, void* stream) {
-  LASR_CHECK_ARG(dk == DK, "lasr_relattn_bwd: d_k=%d (only 64)", dk);
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_bwd: d_k=%d (32 or 64)", dk);
   LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_bwd: bad B/H/T");
   LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
                  "lasr_relattn_bwd: row strides must be multiples of 8");
@@ -605,9 +627,11 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)cdiv(T, 64), (unsigned)H, (unsigned)B);
-  relattn_bwd_q_kernel<<<grid, 256, 0, st>>>(a);
+  if (dk == 64) relattn_bwd_q_kernel<64><<<grid, 256, 0, st>>>(a);
+  else relattn_bwd_q_kernel<32><<<grid, 256, 0, st>>>(a);
   int rc = lasr_check_launch("relattn_bwd_q");
   if (rc) return rc;
-  relattn_bwd_kv_kernel<<<grid, 256, 0, st>>>(a);
+  if (dk == 64) relattn_bwd_kv_kernel<64><<<grid, 256, 0, st>>>(a);
+  else relattn_bwd_kv_kernel<32><<<grid, 256, 0, st>>>(a);
   return lasr_check_launch("relattn_bwd_kv");
 }

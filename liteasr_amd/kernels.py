@@ -359,11 +359,11 @@ def relshift_bwd(dS, Z, T, ldS, dBD):
 
 
 def relattn_fwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx):
-    """Fused rel-pos self-attention (bf16, d_k 64); 2-D row-major operands (row strides
-    read from the tensors), stats [B*H*T*2] fp32 out, ctx [B*T, H*64] out."""
+    """Fused rel-pos self-attention (bf16, d_k 32 or 64); 2-D row-major operands (row
+    strides read from the tensors), stats [B*H*T*2] fp32 out, ctx [B*T, H*d_k] out."""
     N.call("lasr_relattn_fwd", ptr(qu), ptr(qv), qu.stride(0), ptr(k), ptr(v), k.stride(0), ptr(pos),
-           pos.stride(0), B, H, T, 64, ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ctx.stride(0),
-           stream())
+           pos.stride(0), B, H, T, qu.shape[1] // H, ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx),
+           ctx.stride(0), stream())
 
 
 def relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dqu,
@@ -371,7 +371,7 @@ def relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, d
     assert qv.stride(0) == qu.stride(0) and dqu.stride(0) == qu.stride(0)
     assert v.stride(0) == k.stride(0) and dv.stride(0) == dk.stride(0) and dctx.stride(0) == ctx.stride(0)
     N.call("lasr_relattn_bwd", ptr(qu), ptr(qv), qu.stride(0), ptr(k), ptr(v), k.stride(0), ptr(pos),
-           pos.stride(0), B, H, T, 64, ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx),
+           pos.stride(0), B, H, T, qu.shape[1] // H, ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx),
            ctx.stride(0), ptr(Dbuf), ptr(dqu), ptr(dbd), ldS, ptr(dk), ptr(dv), dk.stride(0), stream())
 
 

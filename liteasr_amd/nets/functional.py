@@ -97,9 +97,9 @@ FUSED_RELATTN = os.environ.get("LASR_FUSED_RELATTN", "1") != "0"
 
 
 def fused_relattn(adt, dk, p_att):
-    """The fused kernels (attn_fused.hip) cover bf16, d_k 64, no attention dropout (the
-    my_U2 preset); other shapes take the materialised-score kernels."""
-    return FUSED_RELATTN and adt == torch.bfloat16 and dk == 64 and p_att == 0.0
+    """The fused kernels (attn_fused.hip) cover bf16, d_k 32 or 64, no attention dropout
+    (the my_U2 preset); other shapes take the materialised-score kernels."""
+    return FUSED_RELATTN and adt == torch.bfloat16 and dk in (32, 64) and p_att == 0.0
 
 
 def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res):

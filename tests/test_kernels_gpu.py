@@ -423,14 +423,15 @@ def test_attn_softmax(relpos):
         close(dBD.view(B, H, T, ldS)[..., :T], gref, 1e-6, "relshift bwd")
 
 
-@pytest.mark.parametrize("B,H,T,masking", [(2, 2, 37, "pad"), (3, 4, 130, "pad"), (2, 4, 249, "pad"),
-                                            (2, 2, 100, "chunk"), (2, 1, 64, "none"), (1, 1, 1, "none")])
-def test_relattn_fused(B, H, T, masking):
+@pytest.mark.parametrize("B,H,T,masking,dk", [(2, 2, 37, "pad", 64), (3, 4, 130, "pad", 64), (2, 4, 249, "pad", 64),
+                                               (2, 2, 100, "chunk", 64), (2, 1, 64, "none", 64), (1, 1, 1, "none", 64),
+                                               (2, 16, 249, "chunk", 32), (3, 3, 70, "pad", 32)])
+def test_relattn_fused(B, H, T, masking, dk):
     """attn_fused.hip fwd + bwd vs the literal reference chain (attention.py:120-154) in fp64 on
     the same bf16-rounded operands; one utterance fully masked when masking == "pad"."""
     kn = K()
     torch.manual_seed(T)
-    dk, d = 64, 64 * H
+    d = dk * H
     scale = dk ** -0.5
     bf = torch.bfloat16
     qkv = (torch.randn(B * T, 3 * d) * 0.5).to(bf)

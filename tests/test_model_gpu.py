@@ -157,6 +157,24 @@ def test_parity_bf16(cfg, B, T, L):
         assert errs[k] < 2.5e-1, (k, errs[k])
 
 
+# d_k 32 with the streaming chunk mask (config 4's attention shape) through the fused kernels
+LARGE_HEADS = O.default_cfg(enc_dim=128, enc_heads=4, enc_ff=256, enc_layers=2, dec_dim=128, dec_heads=4,
+                            dec_ff=256, dec_layers=1, vocab_size=30)
+
+
+def test_parity_bf16_dk32_chunk_mask():
+    r = run_case(LARGE_HEADS, 2, 150, 6, "bf16", chunk=8)
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 5e-3 * abs(lo), r["loss"]
+    assert rel(*r["h_ctc"]) < 5e-2
+    g, go = r["grads"]
+    errs, floor = grad_errs(g, go)
+    for k in go:
+        if go[k].abs().max().item() > floor:
+            assert cos(g[k], go[k]) > 0.995, (k, cos(g[k], go[k]))
+        assert errs[k] < 2.5e-1, (k, errs[k])
+
+
 def test_parity_chunk_mask_fp32():
     r = run_case(TINY, 2, 150, 6, "fp32", chunk=8)
     lg, lo = r["loss"]
