@@ -168,13 +168,32 @@ LASR_DEV uint32_t keymask_bits(const KeyMask& km) {
   return (km.r0 ? 1u : 0u) | (km.r1 ? 2u : 0u) | (km.r2 ? 4u : 0u) | (km.r3 ? 8u : 0u);
 }
 
+// Query-dependent masks (msq != 0, e.g. the streaming chunk mask): the (64 x 64) byte tile
+// of a block pair is prefetched like the operands (16 B per thread, clamped, unconditional)
+// and read from LDS by the score tile.
+constexpr int MLD = 80;  // LDS row stride of the mask tile (16-B aligned)
+struct MaskBlk {
+  uint32_t w0, w1, w2, w3;
+};
+LASR_DEV MaskBlk mask_fetch(const RelAttnP& a, int b, int i0, int j0, int tid) {
+  const int r = tid >> 2, c16 = (tid & 3) * 16, jm = a.T - 1;
+  const uint8_t* mr = a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + r, jm) * a.msq;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int e = 0; e < 16; ++e) w[e >> 2] |= (mr[min(j0 + c16 + e, jm)] ? 1u : 0u) << (8 * (e & 3));
+  return MaskBlk{w[0], w[1], w[2], w[3]};
+}
+LASR_DEV void mask_store(uint8_t* msh, const MaskBlk& m, int tid) {
+  *(uint4*)(msh + (tid >> 2) * MLD + (tid & 3) * 16) = make_uint4(m.w0, m.w1, m.w2, m.w3);
+}
+
 // Scaled, masked scores of wave w's 16 query rows (iw = i0 + 16w ..) x the 64 keys j0 ..
 // from the staged K image and relative-position window.
 // s[c][q]: row iw + 4*(lane/16) + q, key j0 + 16c + lane%16.  -inf past T, -1e38 masked.
-template <int DK>
+template <int DK, bool RM>
 LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* peimg, const bf16x8 (&qu)[DK / 32],
                          const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int b, int w, int iw, int j0,
-                         uint32_t mbits, float* gw, f32x4 (&s)[4], int lane) {
+                         uint32_t mbits, const uint8_t* mtile, float* gw, f32x4 (&s)[4], int lane) {
   constexpr int KS = DK / 32;
   const int T = a.T, col = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -205,8 +224,6 @@ LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* pe
     for (int q = 0; q < 4; ++q) gw[(4 * g + q) * GLD + 16 * t + col] = v1 ? g1[q] : g2[q];
   }
   lds_fence();
-  const bool rowmask = a.mask && a.msq != 0;
-  const uint8_t* mrow = a.mask + (int64_t)b * a.msb;
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -214,7 +231,7 @@ LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* pe
       const int r = 4 * g + q, i = iw + r, j = j0 + 16 * c + col;
       float v = (s[c][q] + gw[r * GLD + 16 * c + col - r + 15]) * a.scale;
       bool masked = (mbits >> c) & 1u;
-      if (rowmask && i < T && j < T) masked = mrow[(int64_t)i * a.msq + j] != 0;
+      if constexpr (RM) masked = mtile[(16 * w + r) * MLD + 16 * c + col] != 0;
       if (j >= T) v = -INFINITY;
       else if (masked) v = -1e38f;
       s[c][q] = v;
@@ -255,7 +272,7 @@ LASR_DEV void load_qfrags(const RelAttnP& a, int b, int h, int iw, int lane, bf1
 // Forward, one pass with the online softmax: per key block, stage K / V / the position
 // window (the next block's global loads in flight while this one computes), S on MFMA,
 // running max / sum, O = O * exp(m_old - m_new) + P V.
-template <int DK>
+template <int DK, bool RM>
 __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
@@ -263,6 +280,7 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
   __shared__ __attribute__((aligned(16))) bf16_t vsh[64 * 64];
   __shared__ __attribute__((aligned(16))) bf16_t pesh[PE_ROWS * PELD];
+  __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T;
   const int i0 = blockIdx.x * 64, iw = i0 + 16 * w;
@@ -279,6 +297,8 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   PeWin rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
   KeyMask km;
   keymask_fetch(a, b, 0, lane, km);
+  MaskBlk mk{};
+  if constexpr (RM) mk = mask_fetch(a, b, i0, 0, tid);
 
   float mrun[4], lrun[4];
   f32x4 o[DK / 16], s[4];
@@ -292,6 +312,7 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
     blk_store<DK>(vsh, rv, tid);
     pe_store<DK>(pesh, rp, tid);
     const uint32_t mb_cur = keymask_bits(km);
+    if constexpr (RM) mask_store(msh, mk, tid);
     __syncthreads();
     // prefetch the next key block (unconditional: clamped rows keep the last one in
     // bounds, and no branch merge forces a wait on the loads)
@@ -299,7 +320,8 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
     rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, T, tid);
     rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
     keymask_fetch(a, b, j0 + 64, lane, km);
-    score_tile<DK>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, gw, s, lane);
+    if constexpr (RM) mk = mask_fetch(a, b, i0, j0 + 64, tid);
+    score_tile<DK, RM>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float bm = rmax16(fmaxf(fmaxf(s[0][q], s[1][q]), fmaxf(s[2][q], s[3][q])));
@@ -367,7 +389,7 @@ LASR_DEV void dscore_tile(const RelAttnP& a, const bf16_t* vimg, const bf16x8 (&
   }
 }
 
-template <int DK>
+template <int DK, bool RM>
 __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
@@ -375,6 +397,7 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
   __shared__ __attribute__((aligned(16))) bf16_t vsh[64 * 64];
   __shared__ __attribute__((aligned(16))) bf16_t pesh[PE_ROWS * PELD];
+  __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T;
   const int i0 = blockIdx.x * 64, iw = i0 + 16 * w;
@@ -389,6 +412,8 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   PeWin rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
   KeyMask km;
   keymask_fetch(a, b, 0, lane, km);
+  MaskBlk mk{};
+  if constexpr (RM) mk = mask_fetch(a, b, i0, 0, tid);
   bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
   load_qfrags<DK>(a, b, h, iw, lane, qu, qv, qv1);
   {
@@ -426,12 +451,14 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
     blk_store<DK>(vsh, rv, tid);
     pe_store<DK>(pesh, rp, tid);
     const uint32_t mb_cur = keymask_bits(km);
+    if constexpr (RM) mask_store(msh, mk, tid);
     __syncthreads();
     rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, T, tid);  // next block (unconditional, clamped)
     rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, T, tid);
     rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
     keymask_fetch(a, b, j0 + 64, lane, km);
-    score_tile<DK>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, gw, s, lane);
+    if constexpr (RM) mk = mask_fetch(a, b, i0, j0 + 64, tid);
+    score_tile<DK, RM>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
     dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -470,7 +497,7 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
 // dK, dV of one key block: loops over the query blocks; per block the Qu / dO images (A of
 // the scores, B of dK / dV), query stats and the position window are staged (next block
 // prefetched), the K / V fragments of the block stay in registers.
-template <int DK>
+template <int DK, bool RM>
 __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
   constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
@@ -481,6 +508,7 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
   __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
   __shared__ __attribute__((aligned(16))) bf16_t vsh[64 * 64];
   __shared__ __attribute__((aligned(16))) bf16_t pesh[PE_ROWS * PELD];
+  __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T;
   const int j0 = blockIdx.x * 64;
@@ -496,6 +524,8 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
   blk_store<DK>(vsh, blk_fetch<DK>(a.v + base * a.ldkv + h * DK, a.ldkv, j0, T, tid), tid);
   Blk rq = blk_fetch<DK>(quh, a.ldq, 0, T, tid), ro = blk_fetch<DK>(doh, a.ldc, 0, T, tid);
   PeWin rp = pe_fetch<DK>(ph, a.ldp, T, j0 + T - 64, tid);
+  MaskBlk mk{};
+  if constexpr (RM) mk = mask_fetch(a, b, 0, j0, tid);
 
   f32x4 dk[DK / 16], dv[DK / 16];
 #pragma unroll
@@ -507,6 +537,7 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
     blk_store<DK>(qimg, rq, tid);
     blk_store<DK>(oimg, ro, tid);
     pe_store<DK>(pesh, rp, tid);
+    if constexpr (RM) mask_store(msh, mk, tid);
     // per-row operands of this wave's 16 queries (global; qv / qv1 are not staged)
     bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
     {
@@ -531,12 +562,13 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
     rq = blk_fetch<DK>(quh, a.ldq, i0 + 64, T, tid);  // next block (unconditional, clamped)
     ro = blk_fetch<DK>(doh, a.ldc, i0 + 64, T, tid);
     rp = pe_fetch<DK>(ph, a.ldp, T, j0 - (i0 + 64) + T - 64, tid);
+    if constexpr (RM) mk = mask_fetch(a, b, i0 + 64, j0, tid);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       qu[ks] = frag_row(qimg, 16 * w, 32 * ks, lane);
       dof[ks] = frag_row(oimg, 16 * w, 32 * ks, lane);
     }
-    score_tile<DK>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mbits, gw, s, lane);
+    score_tile<DK, RM>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mbits, msh, gw, s, lane);
     dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -596,8 +628,11 @@ extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, con
   a.B = B; a.H = H; a.T = T; a.scale = scale;
   a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
   dim3 grid((unsigned)cdiv(T, 64), (unsigned)H, (unsigned)B);
-  if (dk == 64) relattn_fwd_kernel<64><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-  else relattn_fwd_kernel<32><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  const bool rm = a.mask && a.msq != 0;
+  if (dk == 64 && rm) relattn_fwd_kernel<64, true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  else if (dk == 64) relattn_fwd_kernel<64, false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  else if (rm) relattn_fwd_kernel<32, true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  else relattn_fwd_kernel<32, false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
   return lasr_check_launch("relattn_fwd");
 }
 
@@ -627,11 +662,16 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)cdiv(T, 64), (unsigned)H, (unsigned)B);
-  if (dk == 64) relattn_bwd_q_kernel<64><<<grid, 256, 0, st>>>(a);
-  else relattn_bwd_q_kernel<32><<<grid, 256, 0, st>>>(a);
+  const bool rm = a.mask && a.msq != 0;
+  if (dk == 64 && rm) relattn_bwd_q_kernel<64, true><<<grid, 256, 0, st>>>(a);
+  else if (dk == 64) relattn_bwd_q_kernel<64, false><<<grid, 256, 0, st>>>(a);
+  else if (rm) relattn_bwd_q_kernel<32, true><<<grid, 256, 0, st>>>(a);
+  else relattn_bwd_q_kernel<32, false><<<grid, 256, 0, st>>>(a);
   int rc = lasr_check_launch("relattn_bwd_q");
   if (rc) return rc;
-  if (dk == 64) relattn_bwd_kv_kernel<64><<<grid, 256, 0, st>>>(a);
-  else relattn_bwd_kv_kernel<32><<<grid, 256, 0, st>>>(a);
+  if (dk == 64 && rm) relattn_bwd_kv_kernel<64, true><<<grid, 256, 0, st>>>(a);
+  else if (dk == 64) relattn_bwd_kv_kernel<64, false><<<grid, 256, 0, st>>>(a);
+  else if (rm) relattn_bwd_kv_kernel<32, true><<<grid, 256, 0, st>>>(a);
+  else relattn_bwd_kv_kernel<32, false><<<grid, 256, 0, st>>>(a);
   return lasr_check_launch("relattn_bwd_kv");
 }
