@@ -189,16 +189,19 @@ template <typename T>
 __global__ void im2col_kernel(const T* __restrict__ y1, int B, int T1, int F1, int C, int T2,
                               int F2, T* col) {
   const int64_t n8 = (int64_t)B * T2 * F2 * 9 * C / 8;  // C % 8 == 0
+  // 32-bit index arithmetic (host-checked: B*T2*F2*9*C < 2^31): the 64-bit divisions
+  // otherwise dominate this copy
+  const uint32_t KC = 9u * (uint32_t)C, P2 = (uint32_t)(T2 * F2);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t el = e * 8;
-    const int64_t m = el / (9 * C);
-    const int k = (int)(el - m * 9 * C);
-    const int tap = k / C, cin = k - tap * C;
-    const int kh = tap / 3, kw = tap - kh * 3;
-    const int64_t b = m / (T2 * F2);
-    const int rem = (int)(m - b * T2 * F2);
-    const int t2 = rem / F2, f2 = rem - t2 * F2;
-    const T* src = y1 + ((b * T1 + 2 * t2 + kh) * F1 + 2 * f2 + kw) * C + cin;
+    const uint32_t el = (uint32_t)e * 8u;
+    const uint32_t m = el / KC;
+    const uint32_t k = el - m * KC;
+    const uint32_t tap = k / (uint32_t)C, cin = k - tap * (uint32_t)C;
+    const uint32_t kh = tap / 3u, kw = tap - kh * 3u;
+    const uint32_t b = m / P2;
+    const uint32_t rem = m - b * P2;
+    const uint32_t t2 = rem / (uint32_t)F2, f2 = rem - t2 * (uint32_t)F2;
+    const T* src = y1 + ((int64_t)((b * T1 + 2 * t2 + kh) * F1 + 2 * f2 + kw)) * C + cin;
     if (sizeof(T) == 2) *(uint4*)(col + el) = *(const uint4*)src;
     else {
       *(float4*)(col + el) = *(const float4*)src;
@@ -206,7 +209,6 @@ __global__ void im2col_kernel(const T* __restrict__ y1, int B, int T1, int F1, i
     }
   }
 }
-
 template <typename T>
 __global__ void col2im_kernel(const T* __restrict__ dcol, int B, int T1, int F1, int C, int T2,
                               int F2, const T* __restrict__ y1, T* dy1) {
@@ -214,12 +216,15 @@ __global__ void col2im_kernel(const T* __restrict__ dcol, int B, int T1, int F1,
   const int C8 = C / 8;
   const int64_t n = (int64_t)B * T1 * F1 * C8;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int cin = (int)(e % C8) * 8;
-    const int64_t pix = e / C8;
-    const int fi = (int)(pix % F1);
-    const int64_t bt = pix / F1;
-    const int ti = (int)(bt % T1);
-    const int64_t b = bt / T1;
+    // 32-bit index arithmetic (host-checked: B*T1*F1*C/8 < 2^31)
+    const uint32_t e32 = (uint32_t)e, pix32 = e32 / (uint32_t)C8;
+    const int cin = (int)(e32 - pix32 * (uint32_t)C8) * 8;
+    const int64_t pix = pix32;
+    const uint32_t bt = pix32 / (uint32_t)F1;
+    const int fi = (int)(pix32 - bt * (uint32_t)F1);
+    const uint32_t b32 = bt / (uint32_t)T1;
+    const int ti = (int)(bt - b32 * (uint32_t)T1);
+    const int64_t b = b32;
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t[8], yv[8];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
@@ -690,6 +695,7 @@ extern "C" int lasr_im2col3x3s2(const void* y1, int dt, int B, int T1, int F1, i
   LASR_CHECK_ARG(C % 8 == 0, "lasr_im2col3x3s2: C %% 8 != 0");
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const int64_t n8 = (int64_t)B * T2 * F2 * 9 * C / 8;
+  LASR_CHECK_ARG(n8 * 8 < (1ll << 31), "lasr_im2col3x3s2: column matrix too large");
   hipStream_t st = (hipStream_t)stream;
   if (dt == LASR_F32) im2col_kernel<float><<<gridn(n8), 256, 0, st>>>((const float*)y1, B, T1, F1, C, T2, F2, (float*)col);
   else im2col_kernel<bf16_t><<<gridn(n8), 256, 0, st>>>((const bf16_t*)y1, B, T1, F1, C, T2, F2, (bf16_t*)col);
@@ -701,6 +707,7 @@ extern "C" int lasr_col2im3x3s2(const void* dcol, int dt, int B, int T1, int F1,
   LASR_CHECK_ARG(C % 8 == 0, "lasr_col2im3x3s2: C %% 8 != 0");
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const int64_t n = (int64_t)B * T1 * F1 * (C / 8);
+  LASR_CHECK_ARG((int64_t)B * T2 * F2 * 9 * C < (1ll << 31), "lasr_col2im3x3s2: column matrix too large");
   hipStream_t st = (hipStream_t)stream;
   if (dt == LASR_F32) col2im_kernel<float><<<gridn(n), 256, 0, st>>>((const float*)dcol, B, T1, F1, C, T2, F2, (const float*)y1, (float*)dy1);
   else col2im_kernel<bf16_t><<<gridn(n), 256, 0, st>>>((const bf16_t*)dcol, B, T1, F1, C, T2, F2, (const bf16_t*)y1, (bf16_t*)dy1);
