@@ -225,15 +225,16 @@ int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, const void* k,
 /* Backward of lasr_relattn_fwd (recompute; deterministic).  Outputs:
  *   Dbuf [B*H*T]        scratch: rowsum(dctx * ctx)
  *   dqu  [B*T, ldq]     dL/d(q+u)
- *   dbd  [B*H, T, ldS]  dL/d(bd) before rel_shift (unscaled), as lasr_relshift_bwd writes it:
- *                       feeds dqv = scale dbd.p and dpos = scale sum_b dbd^T.qv
+ *   dbd  [B][H][T][ldS] dL/d(bd) before rel_shift (unscaled), as lasr_relshift_bwd writes it
+ *                       ([H][B][T][ldS] when dbd_head_major: then dpos = scale sum_b dbd^T.qv
+ *                       is one K = B*T GEMM per head); feeds dqv = scale dbd.p
  *   dk, dv [B*T, lddkv] dL/dk, dL/dv (may be the k / v slots of dqkv). */
 int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, const void* k, const void* v,
                      int64_t ldkv, const void* pos, int64_t ldp, int B, int H, int T, int dk,
                      const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
                      const float* stats, const void* ctx, const void* dctx, int64_t ldc,
-                     float* Dbuf, void* dqu, void* dbd, int ldS, void* dk_out, void* dv_out,
-                     int64_t lddkv, void* stream);
+                     float* Dbuf, void* dqu, void* dbd, int ldS, int dbd_head_major, void* dk_out,
+                     void* dv_out, int64_t lddkv, void* stream);
 /* dst[t, h*dk + c] = sum_b src[b,h,t,c]  (pos-projection grad reduced over batch). */
 int lasr_reduce_batch(const float* src, int B, int H, int T, int dk, void* dst, int dt,
                       void* stream);

@@ -66,7 +66,7 @@ SIGNATURES = {
     "lasr_gemm_force_split": [C.c_int, C.c_int],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
-                         _p, _p, _p, _i, _p, _p, _l, _p],
+                         _p, _p, _p, _i, _i, _p, _p, _l, _p],
     "lasr_reduce_multi": [C.POINTER(ReduceSeg), _i, _p],
     "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
     "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],

@@ -53,8 +53,8 @@ struct RelAttnP {
   const bf16_t* ctx_in;                 // forward ctx (for D)
   float* Dbuf;                          // [B*H*T]
   bf16_t* dqu;                          // [B*T, ldq]
-  bf16_t* dbd;                          // [B*H, T, ldS]
-  int ldS;
+  bf16_t* dbd;                          // [B][H] (or [H][B] if dbd_hb) x [T, ldS]
+  int ldS, dbd_hb;
   bf16_t *dk, *dv;                      // [B*T, lddkv]
   int64_t lddkv;
 };
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   f32x4 dq[DK / 16];
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) dq[t] = zero4();
-  bf16_t* dbd = a.dbd + zrow * a.ldS;
+  bf16_t* dbd = a.dbd + (a.dbd_hb ? ((int64_t)h * a.B + b) * T : zrow) * a.ldS;
   f32x4 s[4], p[4], ds[4];
   for (int j0 = 0; j0 < T; j0 += 64) {
     __syncthreads();
@@ -641,7 +641,8 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
                                 int H, int T, int dk, const uint8_t* mask, int64_t mask_sb,
                                 int64_t mask_sq, float scale, const float* stats, const void* ctx,
                                 const void* dctx, int64_t ldc, float* Dbuf, void* dqu, void* dbd,
-                                int ldS, void* dk_out, void* dv_out, int64_t lddkv, void* stream) {
+                                int ldS, int dbd_head_major, void* dk_out, void* dv_out, int64_t lddkv,
+                                void* stream) {
   LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_bwd: d_k=%d (32 or 64)", dk);
   LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_bwd: bad B/H/T");
   LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
@@ -658,7 +659,7 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   a.B = B; a.H = H; a.T = T; a.scale = scale;
   a.stats = (float*)stats; a.ldc = ldc;
   a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
-  a.dqu = (bf16_t*)dqu; a.dbd = (bf16_t*)dbd; a.ldS = ldS;
+  a.dqu = (bf16_t*)dqu; a.dbd = (bf16_t*)dbd; a.ldS = ldS; a.dbd_hb = dbd_head_major;
   a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)cdiv(T, 64), (unsigned)H, (unsigned)B);

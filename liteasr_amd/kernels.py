@@ -367,12 +367,13 @@ def relattn_fwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx):
 
 
 def relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dqu,
-                dbd, ldS, dk, dv):
+                dbd, ldS, dk, dv, dbd_head_major=False):
     assert qv.stride(0) == qu.stride(0) and dqu.stride(0) == qu.stride(0)
     assert v.stride(0) == k.stride(0) and dv.stride(0) == dk.stride(0) and dctx.stride(0) == ctx.stride(0)
     N.call("lasr_relattn_bwd", ptr(qu), ptr(qv), qu.stride(0), ptr(k), ptr(v), k.stride(0), ptr(pos),
            pos.stride(0), B, H, T, qu.shape[1] // H, ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx),
-           ctx.stride(0), ptr(Dbuf), ptr(dqu), ptr(dbd), ldS, ptr(dk), ptr(dv), dk.stride(0), stream())
+           ctx.stride(0), ptr(Dbuf), ptr(dqu), ptr(dbd), ldS, int(dbd_head_major), ptr(dk), ptr(dv), dk.stride(0),
+           stream())
 
 
 def reduce_batch(src, B, H, T, dk, dst):

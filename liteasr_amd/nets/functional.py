@@ -157,27 +157,41 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     K.gemm(gb, w.Wo, dctx)
     dqkv = _e((M, 3 * d), adt, dev)
     dqu = _e((M, d), adt, dev)
-    dBD = _e((B, H, T, ldS), adt, dev)
     if sv.stats is not None:
-        # fused recompute backward: dqu, dk, dv and the pre-shift bd gradient
+        # fused recompute backward: dqu, dk, dv and the pre-shift bd gradient, head-major
+        # ([H][B][T][ldS]) so the positional gradient is one K = B*T GEMM per head
+        dBDh = _e((H, B, T, ldS), adt, dev)
         Dbuf = _e((B * H * T,), F32, dev)
         K.relattn_bwd(sv.qu, sv.qv, sv.qkv[:, d:2 * d], sv.qkv[:, 2 * d:], sv.p, B, H, T, env.mask,
-                      env.msb, env.msq, scale, sv.stats, sv.ctx, dctx, Dbuf, dqu, dBD, ldS,
-                      dqkv[:, d:2 * d], dqkv[:, 2 * d:])
-    else:
-        dctx4 = _heads(dctx, B, T, H, dk)
-        v4 = _slot(sv.qkv, B, T, 3, 2, H, dk)
-        k4 = _slot(sv.qkv, B, T, 3, 1, H, dk)
-        dPd = _e((B, H, T, ldS), F32, dev)
-        K.gemm(dctx4, v4.transpose(-1, -2), dPd[..., :T])
-        K.gemm(sv.P[..., :T].transpose(-1, -2), dctx4, _slot(dqkv, B, T, 3, 2, H, dk))
-        dS = _e((B, H, T, ldS), adt, dev)
-        K.attn_softmax_bwd(sv.Praw if sv.Praw is not None else sv.P, dPd, B, H, T, T, ldS, env.mask,
-                           env.msb, env.msq, dS, p_att, s_att)
-        K.relshift_bwd(dS.view(B * H, T, ldS), B * H, T, ldS, dBD)
-        K.gemm(dS[..., :T], k4, _heads(dqu, B, T, H, dk), alpha=scale)
-        K.gemm(dS[..., :T].transpose(-1, -2), _heads(sv.qu, B, T, H, dk), _slot(dqkv, B, T, 3, 1, H, dk),
-               alpha=scale)
+                      env.msb, env.msq, scale, sv.stats, sv.ctx, dctx, Dbuf, dqu, dBDh, ldS,
+                      dqkv[:, d:2 * d], dqkv[:, 2 * d:], dbd_head_major=True)
+        p4 = sv.p.view(T, H, dk).permute(1, 0, 2).unsqueeze(0).expand(B, H, T, dk)
+        dqv = _e((M, d), adt, dev)
+        K.gemm(dBDh.permute(1, 0, 2, 3)[..., :T], p4, _heads(dqv, B, T, H, dk), alpha=scale)
+        dp = _e((T, d), adt, dev)
+        K.gemm(dBDh.view(H, B * T, ldS)[..., :T].transpose(-1, -2), sv.qv.view(M, H, dk).permute(1, 0, 2),
+               dp.view(T, H, dk).permute(1, 0, 2), alpha=scale, split_k=0)
+        K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
+        K.gemm(dp.t(), pos, g.Wpos, beta=1.0)
+        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv)
+        dln = _e((M, d), adt, dev)
+        K.gemm(dqkv, w.Wqkv, dln)
+        return dln
+    dBD = _e((B, H, T, ldS), adt, dev)
+    # materialised-score backward (fp32 build, attention dropout, other d_k)
+    dctx4 = _heads(dctx, B, T, H, dk)
+    v4 = _slot(sv.qkv, B, T, 3, 2, H, dk)
+    k4 = _slot(sv.qkv, B, T, 3, 1, H, dk)
+    dPd = _e((B, H, T, ldS), F32, dev)
+    K.gemm(dctx4, v4.transpose(-1, -2), dPd[..., :T])
+    K.gemm(sv.P[..., :T].transpose(-1, -2), dctx4, _slot(dqkv, B, T, 3, 2, H, dk))
+    dS = _e((B, H, T, ldS), adt, dev)
+    K.attn_softmax_bwd(sv.Praw if sv.Praw is not None else sv.P, dPd, B, H, T, T, ldS, env.mask,
+                       env.msb, env.msq, dS, p_att, s_att)
+    K.relshift_bwd(dS.view(B * H, T, ldS), B * H, T, ldS, dBD)
+    K.gemm(dS[..., :T], k4, _heads(dqu, B, T, H, dk), alpha=scale)
+    K.gemm(dS[..., :T].transpose(-1, -2), _heads(sv.qu, B, T, H, dk), _slot(dqkv, B, T, 3, 1, H, dk),
+           alpha=scale)
     p4 = sv.p.view(T, H, dk).permute(1, 0, 2).unsqueeze(0).expand(B, H, T, dk)
     dqv = _e((M, d), adt, dev)
     K.gemm(dBD[..., :T], p4, _heads(dqv, B, T, H, dk), alpha=scale)

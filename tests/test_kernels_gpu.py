@@ -491,6 +491,13 @@ def test_relattn_fused(B, H, T, masking, dk):
     close(dqkv[:, 2 * d:], unh(Vh.grad), 2e-2, "relattn dv")
     assert not dbd[..., :T].isnan().any(), "dbd entries left unwritten"
     close(dbd[..., :T].float() * scale, bd.grad, 2e-2, "relattn dbd")
+    # head-major dBD ([H][B][T][ldS], the positional-gradient GEMM layout): same values
+    dbdh = torch.full((H, B, T, ldS), float("nan"), dtype=bf, device=DEV)
+    dqkv2 = torch.zeros_like(dqkv)
+    kn.relattn_bwd(g(qu), g(qv), qkv_d[:, d:2 * d], qkv_d[:, 2 * d:], g(pos), B, H, T, mask_d, msb, msq,
+                   scale, stats, ctx, g(dctx), Dbuf, torch.empty_like(dqu), dbdh, ldS, dqkv2[:, d:2 * d],
+                   dqkv2[:, 2 * d:], dbd_head_major=True)
+    assert torch.equal(dbdh.permute(1, 0, 2, 3)[..., :T], dbd[..., :T])
 
 
 def test_qbias_and_reduce():
