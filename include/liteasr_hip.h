@@ -284,6 +284,8 @@ int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt, int64_t r
 int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int dydt, int B, int T, int C,
                         int K, const float* w, void* dz1, float* dw, float* db, float* ws,
                         int64_t ws_floats, void* stream);
+/* dw [C][K] and db [C] accumulate; with dw = db = NULL the [nparts][C*K + C] partials
+ * (lasr_dwconv_nparts) stay in ws for a deferred lasr_reduce_multi. */
 
 /* ------------------------------------------------------------------------
  * Elementwise / embedding / positional encoding

@@ -448,25 +448,18 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
   sp[grp][DW_K][2 * cp] = db0;
   sp[grp][DW_K][2 * cp + 1] = db1;
   __syncthreads();
-  float* pp = part + (int64_t)blockIdx.x * (DW_K + 1) * C + blockIdx.y * 2 * DW_CP;
+  // partial row of this block in the parameters' own layout: [C][K] weight taps, then [C]
+  // bias, so the reduction writes dw / db directly (or is deferred as one segment)
+  float* pp = part + (int64_t)blockIdx.x * (DW_K + 1) * C;
   for (int e = threadIdx.x; e < (DW_K + 1) * 2 * DW_CP; e += 256) {
-    const int k = e / (2 * DW_CP), cl = e % (2 * DW_CP);
-    if (blockIdx.y * 2 * DW_CP + cl >= C) continue;
+    const int cl = e / (DW_K + 1), k = e % (DW_K + 1);
+    const int cg = blockIdx.y * 2 * DW_CP + cl;
+    if (cg >= C) continue;
     float v = sp[0][k][cl];
 #pragma unroll
     for (int q = 1; q < DW_G; ++q) v += sp[q][k][cl];
-    pp[(int64_t)k * C + cl] = v;
+    pp[k < DW_K ? (int64_t)cg * DW_K + k : (int64_t)DW_K * C + cg] = v;
   }
-}
-
-__global__ void dw_reduce_kernel(const float* part, int nparts, int C, float* dw, float* db) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // e = c*(K+1) + k
-  if (e >= C * (DW_K + 1)) return;
-  const int c = e / (DW_K + 1), k = e - c * (DW_K + 1);
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[((int64_t)p * (DW_K + 1) + k) * C + c];
-  if (k < DW_K) dw[c * DW_K + k] += s;
-  else db[c] += s;
 }
 
 // ------------------------------- BatchNorm ---------------------------------------
@@ -612,18 +605,17 @@ __global__ void bn_bwd_total_kernel(const float* part, int nparts, int C, float*
   dbeta[c] += s1;
   dgamma[c] += s2;
 }
-__global__ void bn_bwd_accum_kernel(const float* tot, int C, float* dgamma, float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  dbeta[c] += tot[c];
-  dgamma[c] += tot[C + c];
-}
-
 template <typename TY, typename TH, typename TD>
 __global__ void bn_swish_bwd_apply_kernel(const TY* y, const TH* dh, int64_t rows, int C,
                                           const float* scale, const float* shift,
                                           const float* mean, const float* rstd,
-                                          const float* gamma, const float* tot, TD* dy) {
+                                          const float* gamma, const float* tot, TD* dy,
+                                          float* dgamma, float* dbeta) {
+  if (blockIdx.x == 0)  // parameter gradients (the column totals are final here)
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      dbeta[c] += tot[c];
+      dgamma[c] += tot[C + c];
+    }
   const int64_t n8 = rows * C / 8;
   const float inv_n = 1.f / (float)rows;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
@@ -796,11 +788,8 @@ extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt
   if (rc) return rc;
   rc = lasr_reduce_cols(ws, (int)nparts, 2 * C, tot, nullptr, 2 * C, 0, st);
   if (rc) return rc;
-  bn_bwd_accum_kernel<<<(unsigned)cdiv(C, 256), 256, 0, st>>>(tot, C, dgamma, dbeta);
-  rc = lasr_check_launch("bn_swish_bwd/accum");
-  if (rc) return rc;
   const int64_t n = rows * C / 8;
-#define BA(TY, TH, TD) bn_swish_bwd_apply_kernel<TY, TH, TD><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy)
+#define BA(TY, TH, TD) bn_swish_bwd_apply_kernel<TY, TH, TD><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy, dgamma, dbeta)
   const bool yf = ydt == LASR_F32, hf = hdt == LASR_F32, df = dydt == LASR_F32;
   if (yf && hf && df) BA(float, float, float);
   else if (yf && hf) BA(float, float, bf16_t);
@@ -820,7 +809,7 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
   LASR_CHECK_ARG(K == DW_K, "lasr_glu_dwconv_bwd: only kernel size %d is built", DW_K);
   const int nchunk = (int)cdiv(T, DW_TT);
   const int nparts = B * nchunk;
-  LASR_CHECK_ARG(ws_floats >= (int64_t)(nparts + 1) * (DW_K + 1) * C, "lasr_glu_dwconv_bwd: workspace too small");
+  LASR_CHECK_ARG(ws_floats >= (int64_t)nparts * (DW_K + 1) * C, "lasr_glu_dwconv_bwd: workspace too small");
   LASR_CHECK_ARG(C % 2 == 0, "lasr_glu_dwconv_bwd: C must be even");
   dim3 g((unsigned)nparts, (unsigned)cdiv(C, 2 * DW_CP));
   hipStream_t st = (hipStream_t)stream;
@@ -831,9 +820,7 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
   else GB(bf16_t, bf16_t);
 #undef GB
   int rc = lasr_check_launch("glu_dwconv_bwd");
-  if (rc) return rc;
-  float* tot = ws + (int64_t)nparts * (DW_K + 1) * C;
-  rc = lasr_reduce_cols(ws, nparts, (int64_t)(DW_K + 1) * C, tot, nullptr, (DW_K + 1) * C, 0, st);
-  if (rc) return rc;
-  return lasr_scatter_kc(tot, DW_K, C, DW_K, dw, db, st);
+  if (rc || (!dw && !db)) return rc;  // no outputs: partials left in ws (deferred reduction)
+  LASR_CHECK_ARG(dw && db, "lasr_glu_dwconv_bwd: dw and db go together");
+  return lasr_reduce_cols(ws, nparts, (int64_t)(DW_K + 1) * C, dw, db, (int64_t)DW_K * C, 1, st);
 }

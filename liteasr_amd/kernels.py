@@ -444,7 +444,14 @@ def bn_swish_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy):
 
 
 def glu_dwconv_bwd(z1, dy, B, T, Cc, K, w, dz1, dw, db):
+    """dw [C, K] and db [C] accumulate; partials are [nparts][C*K + C] in their layout."""
     nparts = dwconv_nparts(B, T)
+    if _DEFER.depth:
+        ws = torch.empty(nparts * (K + 1) * Cc, dtype=torch.float32, device=z1.device)
+        N.call("lasr_glu_dwconv_bwd", ptr(z1), dt(z1), ptr(dy), dt(dy), B, T, Cc, K, ptr(w), ptr(dz1),
+               None, None, ptr(ws), ws.numel(), stream())
+        _defer(ws, nparts, (K + 1) * Cc, dw, db, split=K * Cc)
+        return
     ws = WS.get((nparts + 1) * (K + 1) * Cc, z1.device)
     N.call("lasr_glu_dwconv_bwd", ptr(z1), dt(z1), ptr(dy), dt(dy), B, T, Cc, K, ptr(w), ptr(dz1),
            ptr(dw), ptr(db), ptr(ws), ws.numel(), stream())
