@@ -1117,9 +1117,13 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     // very large outputs with long K (subsampling conv2: M 151k, N 256, K 2304): the
     // 128x256 tile halves the A re-reads (tile sweep: 237 vs 266 us)
     if (BM == 128 && BN == 128 && a->N >= 256 && a->K >= 1024 && cdiv(a->M, 128) * batch >= 1024) BN = 256;
-    // pre-activation copy + activation + dropout epilogue (the FFN fc1 forward, N 2048):
-    // 128x256 halves the per-output epilogue bookkeeping (cold-cache sweep 32 vs 38 us)
-    if (BM == 128 && BN == 128 && a->zout && a->N >= 1024) BN = 256;
+    // heavy epilogues over wide outputs (FFN fc1 forward: pre-activation copy + Swish +
+    // dropout; FFN dX fc2: activation-gradient aux + dropout; N 2048): 128x256 halves the
+    // per-output epilogue bookkeeping (cold-cache sweep: 32 vs 38 us, 40.2 vs 44.6 us)
+    if (BM == 128 && BN == 128 && (a->zout || a->aux) && a->N >= 1024) BN = 256;
+    // long-K residual outputs (FFN fc2 forward, K 2048, N 256, fp32 residual): 64x128
+    // (cold-cache sweep 26.0 vs 28.4 us for 64x64)
+    if (BM == 64 && BN == 64 && a->res && a->K >= 1024 && a->N >= 128) BN = 128;
   }
   if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;

@@ -84,6 +84,9 @@ CASES = [
      dict(bias=1, swish=1, drop=1)),
     ("fc1 plain", 7968, 2048, 256, "nt", torch.bfloat16, 1, {}),
     ("dX fc2 aux+drop (nn)", 7968, 2048, 256, "nn", torch.bfloat16, 1, dict(aux=1, drop=1)),
+    ("dX fc2 aux+drop (nt)", 7968, 2048, 256, "nt", torch.bfloat16, 1, dict(aux=1, drop=1)),
+    ("dX fc1 (nt K2048)", 7968, 256, 2048, "nt", torch.bfloat16, 1, {}),
+    ("dX dd (nt)", 7968, 256, 256, "nt", torch.bfloat16, 1, {}),
     ("dd bias (nt)", 7968, 256, 256, "nt", torch.bfloat16, 1, dict(bias=1)),
     ("dd res f32 (nt)", 7968, 256, 256, "nt", torch.float32, 1, dict(bias=1, res=1)),
     ("dX dd (nn)", 7968, 256, 256, "nn", torch.bfloat16, 1, {}),
