@@ -1121,9 +1121,6 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     // dropout; FFN dX fc2: activation-gradient aux + dropout; N 2048): 128x256 halves the
     // per-output epilogue bookkeeping (cold-cache sweep: 32 vs 38 us, 40.2 vs 44.6 us)
     if (BM == 128 && BN == 128 && (a->zout || a->aux) && a->N >= 1024) BN = 256;
-    // long-K residual outputs (FFN fc2 forward, K 2048, N 256, fp32 residual): 64x128
-    // (cold-cache sweep 26.0 vs 28.4 us for 64x64)
-    if (BM == 64 && BN == 64 && a->res && a->K >= 1024 && a->N >= 128) BN = 128;
   }
   if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
