@@ -463,16 +463,16 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
 }
 
 // ------------------------------- BatchNorm ---------------------------------------
-// 1024 threads = 32 channels x BNF_G partial-groups, combined exactly in double (fixed
+// 1024 threads = BNF_C channels x BNF_G partial-groups, combined exactly in double (fixed
 // order), then one thread per channel finalises.
-constexpr int BNF_G = 32;
+constexpr int BNF_C = 16, BNF_G = 1024 / BNF_C;
 __global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
     const float* stats, int nparts, int C, float eps, float momentum, const float* gamma,
     const float* beta, float* rmean, float* rvar, int64_t* nbt, float* mean, float* rstd,
     float* scale, float* shift, int update) {
-  __shared__ double sn[BNF_G][33], smu[BNF_G][33], sm2[BNF_G][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + tx;
+  __shared__ double sn[BNF_G][BNF_C + 1], smu[BNF_G][BNF_C + 1], sm2[BNF_G][BNF_C + 1];
+  const int tx = threadIdx.x % BNF_C, ty = threadIdx.x / BNF_C;
+  const int c = blockIdx.x * BNF_C + tx;
   if (blockIdx.x == 0 && threadIdx.x == 0 && update == 1 && nbt) nbt[0] += 1;
   if (update == 2) {  // eval mode: normalise with the running statistics
     if (ty == 0 && c < C) {
@@ -744,7 +744,7 @@ extern "C" int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float 
                                 float* running_mean, float* running_var, int64_t* num_batches,
                                 float* mean, float* rstd, float* scale, float* shift,
                                 int update_running, void* stream) {
-  bn_finalize_par_kernel<<<(unsigned)cdiv(C, 32), 32 * BNF_G, 0, (hipStream_t)stream>>>(
+  bn_finalize_par_kernel<<<(unsigned)cdiv(C, BNF_C), BNF_C * BNF_G, 0, (hipStream_t)stream>>>(
       stats_ws, nparts, C, eps, momentum, gamma, beta, running_mean, running_var, num_batches,
       mean, rstd, scale, shift, update_running);
   return lasr_check_launch("bn_finalize");
