@@ -321,6 +321,23 @@ int lasr_u2_prep(const int64_t* xlens, const int64_t* ys, const int64_t* ylens, 
                  int32_t* ylen32, void* stream);
 
 /* ------------------------------------------------------------------------
+ * SpecAugment (liteasr/utils/transform/spec_augment.py:14-125; applied per utterance in
+ * the reference's DataLoader workers, liteasr/dataset/asr_dataset.py:118).  Replaces the
+ * per-utterance SpecAugment.__call__ with one batched device call on the padded batch:
+ *   x, out [B, Tmax, F] fp32 (out must not alias x), xlens [B] int64 (device),
+ *   plan [B, plan_stride] int32 (device): center, warped (0 = no warp), nf, nt, then nf
+ *   freq and nt time [lo, hi) ranges in draw order (host-drawn with the reference's RNG
+ *   calls; liteasr_amd/utils/transform/spec_augment.py).
+ * Time warp = Pillow BICUBIC float resize, bit-exact; masks fill 0 (replace_with_zero) or
+ * the utterance's running mean.  Rows >= xlens[b] are copied unchanged.  ws: device
+ * scratch of lasr_spec_augment_ws_bytes(B, Tmax) bytes (unused with replace_with_zero).
+ * ---------------------------------------------------------------------- */
+int64_t lasr_spec_augment_ws_bytes(int B, int Tmax);
+int lasr_spec_augment(const float* x, float* out, const int64_t* xlens, const int32_t* plan,
+                      int plan_stride, int B, int Tmax, int F, int replace_with_zero, void* ws,
+                      int64_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * Optimizer: clip_grad_norm_ + NaN-skip + Noam/Adam over flat fp32 buffers
  * (liteasr/trainer.py:152-171, liteasr/optims/noam.py:33-46, optims/adam.py:27-34,
  *  torch.optim.Adam semantics).  State lives on the device:

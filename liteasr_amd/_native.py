@@ -106,8 +106,10 @@ SIGNATURES = {
     "lasr_adam_step": [_p, _p, _i, _p, _p, _p, _l, _p, _i, _p, _f, _i, _f, _f, _f, _f, _f, _f,
                        _f, _f, _p],
     "lasr_fill": [_p, _i, _l, _f, _p],
+    "lasr_spec_augment": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _l, _p],
+    "lasr_spec_augment_ws_bytes": [_i, _i],
 }
-_RESTYPES = {"lasr_last_error": C.c_char_p}
+_RESTYPES = {"lasr_last_error": C.c_char_p, "lasr_spec_augment_ws_bytes": C.c_int64}
 
 
 class NativeError(RuntimeError):

@@ -7,8 +7,11 @@ Audio records); ``collator`` pads xs with 0 and ys with -1 and returns int64 len
 
 MI355X-side difference: the collator decodes the whole minibatch with one native call
 (lasr_ark_read_padded) straight into the padded float32 batch instead of loading and
-padding utterance by utterance.  (The reference's ``memory_save`` pickle dump of batches
-is not carried over: it serialises Python objects to disk and is not on the step path.)
+padding utterance by utterance.  With a device-capable postprocess (SpecAugment) the
+collator only draws the augmentation plan and returns it as a fifth element; the trainer
+applies it to the batch on the GPU.  (The reference's ``memory_save`` pickle dump of
+batches is not carried over: it serialises Python objects to disk and is not on the step
+path.)
 """
 
 import logging
@@ -74,6 +77,12 @@ class AudioFileDataset(LiteasrDataset):
         xlens = torch.tensor([s.xlen for s in batch], dtype=torch.long)
         ylens = torch.tensor([s.ylen for s in batch], dtype=torch.long)
         post = self.postprocess if (self.train and self.postprocess is not None and len(self.postprocess)) else None
+        plan = None
+        if post is not None and post.device_capable:
+            # draw the augmentation here (same RNG order as the reference's per-utterance
+            # calls); the pixels are produced on the GPU by the trainer (apply_batch)
+            plan = post.plan_batch(xlens.tolist(), self.feat_dim)
+            post = None
         if post is None and all(s.start is None for s in batch):
             tmax = int(xlens.max()) if B else 0
             xs = torch.empty(B, tmax, self.feat_dim, dtype=torch.float32)
@@ -88,6 +97,8 @@ class AudioFileDataset(LiteasrDataset):
         for i, s in enumerate(batch):
             if s.ylen:
                 ys[i, : s.ylen] = torch.tensor(s.tokenids, dtype=torch.long)
+        if plan is not None:
+            return xs, xlens, ys, ylens, plan
         return xs, xlens, ys, ylens
 
     def __getitem__(self, index):

@@ -496,6 +496,23 @@ def u2_prep(xlens, ys, ylens, Tx, Tsub, sos, eos, chunk, out):
            ptr(out["enc_mask"]), ptr(out["pred_len"]), ptr(out["ylen"]), stream())
 
 
+def spec_augment(x, xlens, plan, replace_with_zero=False, out=None):
+    """Batched SpecAugment (csrc/specaug.hip) on a padded fp32 [B, T, F] device batch."""
+    B, T, F = x.shape
+    assert x.dtype == torch.float32 and x.is_contiguous()
+    assert xlens.dtype == torch.int64 and xlens.numel() == B and xlens.device == x.device
+    assert plan.dtype == torch.int32 and plan.dim() == 2 and plan.shape[0] == B and plan.is_contiguous()
+    assert plan.device == x.device
+    if out is None:
+        out = torch.empty_like(x)
+    assert out.shape == x.shape and out.dtype == torch.float32 and out.is_contiguous()
+    nbytes = N.load().lasr_spec_augment_ws_bytes(B, T)
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=x.device)
+    N.call("lasr_spec_augment", ptr(x), ptr(out), ptr(xlens), ptr(plan), plan.shape[1], B, T, F,
+           int(bool(replace_with_zero)), ptr(ws), nbytes, stream())
+    return out
+
+
 def sumsq_nparts(n):
     return N.load().lasr_sumsq_nparts(n)
 

@@ -49,6 +49,7 @@ class Trainer(object):
             tr_s, va_s = DistributedSampler(train_set), DistributedSampler(valid_set)
         else:
             tr_s = va_s = None
+        self._train_post = getattr(train_set, "postprocess", None)
         pin = torch.cuda.is_available()
         self.train_iter = EpochDataLoader(dataset=train_set, batch_size=1, shuffle=tr_s is None, sampler=tr_s,
                                           num_workers=cfg.distributed.num_workers, collate_fn=train_set.collator,
@@ -116,6 +117,10 @@ class Trainer(object):
             if self.stop():
                 break
             batch = to_device(batch, self.device)
+            if len(batch) == 5:  # device-side postprocess (SpecAugment plan from the collator)
+                xs, xlens, ys, ylens, plan = batch
+                xs = self._train_post.apply_batch(xs, xlens, plan)
+                batch = (xs, xlens, ys, ylens)
             if dist.is_initialized() and i % accum != 0:
                 ctx = self.model.no_sync
             else:

@@ -35,3 +35,14 @@ class PostProcess(object):
 
     def __len__(self):
         return len(self.workflow)
+
+    @property
+    def device_capable(self):
+        """True when the whole workflow runs as plan-on-host + one batched device call."""
+        return len(self.workflow) == 1 and getattr(self.workflow[0], "device_capable", False)
+
+    def plan_batch(self, lengths, feat_dim):
+        return self.workflow[0].plan_batch(lengths, feat_dim)
+
+    def apply_batch(self, xs, xlens, plan):
+        return self.workflow[0].apply_batch(xs, xlens, plan)

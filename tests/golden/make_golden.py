@@ -19,6 +19,10 @@ Fixtures
   u2_step.npz     tiny U2 (d 32, 2 enc / 1 dec, V 20, F 40): seed-42 init state_dict, a
                   batch, h_attn / h_ctc / loss / grads, params after clip(5) + Noam step,
                   BN running stats; plus a chunk-mask (stage 4) forward for config 4
+  spec_aug.npz    the reference SpecAugment (utils/transform/spec_augment.py) on seeded
+                  inputs: global random/numpy seeds per case, input regenerated from its own
+                  PCG64 seed, the augmented output, and one random.random() /
+                  numpy.random.rand() draw taken after the case (pins RNG consumption)
 """
 
 import os
@@ -276,6 +280,47 @@ def gen_loader():
     save("loader.npz", **arrs)
 
 
+SPEC_AUG_CASES = [
+    # name, cfg overrides, lengths (one call per utterance, in order), F
+    ("default_t600", {}, [600], 80),
+    ("default_t161", {}, [161], 80),
+    ("nowarp_t160", {}, [160], 80),
+    ("short_t50", {}, [50], 80),
+    ("tiny_t3", {}, [3], 80),
+    ("multi_zero", dict(freq_mask_times=2, time_mask_times=3, replace_with_zero=True), [400], 80),
+    ("multi_mean", dict(freq_mask_times=3, time_mask_times=2, time_warp=40), [333], 80),
+    ("copy_f40", dict(inplace=False, freq_mask=10, time_mask=30, time_warp=5), [97], 40),
+    ("batch4", {}, [300, 250, 200, 170], 80),
+]
+
+
+def gen_spec_aug():
+    import random
+
+    from liteasr.config import _SpecAugmentConfig
+    from liteasr.utils.transform.spec_augment import SpecAugment
+
+    arrs = {}
+    for ci, (name, over, lens, F) in enumerate(SPEC_AUG_CASES):
+        cfg = _SpecAugmentConfig(**over)
+        sa = SpecAugment(cfg)
+        random.seed(1000 + ci)
+        np.random.seed(2000 + ci)
+        for ui, t in enumerate(lens):
+            x = np.random.default_rng(3000 + 10 * ci + ui).standard_normal((t, F)).astype(np.float32)
+            x[:, :5] += 4.0  # non-zero mean so the mean fill is visible
+            arrs[f"{name}_u{ui}_out"] = sa(torch.from_numpy(x.copy())).numpy()
+        arrs[f"{name}_cfg"] = np.array([cfg.time_warp, cfg.freq_mask, cfg.freq_mask_times, cfg.time_mask,
+                                        cfg.time_mask_times, int(cfg.inplace), int(cfg.replace_with_zero)])
+        arrs[f"{name}_lens"] = np.array(lens)
+        arrs[f"{name}_F"] = np.array(F)
+        arrs[f"{name}_seeds"] = np.array([1000 + ci, 2000 + ci, 3000 + 10 * ci])
+        arrs[f"{name}_next_random"] = np.array(random.random())
+        arrs[f"{name}_next_numpy"] = np.array(np.random.rand())
+    arrs["cases"] = np.array([c[0] for c in SPEC_AUG_CASES])
+    save("spec_aug.npz", **arrs)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(4)
     gen_relshift()
@@ -283,3 +328,4 @@ if __name__ == "__main__":
     gen_ctc_kl()
     gen_u2_step()
     gen_loader()
+    gen_spec_aug()
