@@ -189,3 +189,39 @@ def test_trainer_step_semantics():
     tr.run()
     # batches 1,2 -> step (iter 1); 3,4 (contains NaN) -> skipped; 5,6 -> step (iter 2); stop
     assert tr.iter == 2 and tr.skipped == 1 and calls["step"] == 2 and calls["events"] == 2
+
+
+def test_collator_with_default_spec_aug(tmp_path, gold):
+    """PostProcessConfig with its default workflow ["spec_aug"] (config/__init__.py:54-56): the train
+    collator returns the un-augmented batch plus one SpecAugment plan row per utterance,
+    drawn in batch order; the valid split is not augmented."""
+    import random
+
+    from liteasr_amd.config import PostProcessConfig
+    from liteasr_amd.dataclass.vocab import Vocab
+    from liteasr_amd.dataset import AudioFileDataset
+    from liteasr_amd.utils.transform.spec_augment import SpecAugment
+
+    d = _datadir(str(tmp_path), "fm")
+    vocab = Vocab(os.path.join(d, "vocab.txt"))
+    from liteasr_amd.config import _SpecAugmentConfig
+
+    pp = PostProcessConfig()
+    assert pp.workflow == ["spec_aug"]
+    # the fixture's features are narrow (F < the default freq_mask 27, which would make the
+    # reference's randrange raise too): scale the mask sizes down
+    pp.spec_aug = _SpecAugmentConfig(time_warp=5, freq_mask=3, time_mask=6)
+    ds = AudioFileDataset("train", d, None, _dcfg(CFGS[0]), pp, vocab)
+    random.seed(3)
+    np.random.seed(4)
+    out = ds.collator([ds[0]])
+    assert len(out) == 5
+    xs, xl, _, _, plan = out
+    ref = torch.from_numpy(gold["fm_c0_b0_xs"])
+    assert torch.equal(xs.view(torch.int32), ref.view(torch.int32))
+    random.seed(3)
+    np.random.seed(4)
+    want = SpecAugment(pp.spec_aug).plan_batch(xl.tolist(), xs.shape[-1])
+    assert plan.dtype == torch.int32 and torch.equal(plan, want)
+    va = AudioFileDataset("valid", d, None, _dcfg(CFGS[0]), pp, vocab)
+    assert len(va.collator([va[0]])) == 4
