@@ -5,17 +5,24 @@ SRC   := $(wildcard liteasr_amd/csrc/*.hip)
 OBJ   := $(patsubst liteasr_amd/csrc/%.hip,build/obj/%.o,$(SRC))
 LIB   := liteasr_amd/lib/libliteasr_hip.so
 IOLIB := liteasr_amd/lib/libliteasr_io.so
+DECLIB := liteasr_amd/lib/libliteasr_decode.so
 CXX   ?= g++
 HDRS  := liteasr_amd/csrc/common.h include/liteasr_hip.h
 FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC
 
-all: $(LIB) $(IOLIB)
+all: $(LIB) $(IOLIB) $(DECLIB)
 
 # host-only native feature reader (no device code); -ffp-contract=off keeps the decode
 # arithmetic bit-identical to the reference's numpy float32 expressions
 $(IOLIB): liteasr_amd/csrc/io/ark_io.cpp include/liteasr_io.h
 	@mkdir -p liteasr_amd/lib
 	$(CXX) -O2 -std=c++17 -fPIC -shared -ffp-contract=off -pthread -o $@ $<
+
+# host-only CTC prefix beam search (inference); same fp-contract rule, so its double
+# arithmetic matches the reference's Python floats
+$(DECLIB): liteasr_amd/csrc/decode/prefix_beam.cpp include/liteasr_decode.h
+	@mkdir -p liteasr_amd/lib
+	$(CXX) -O2 -std=c++17 -fPIC -shared -ffp-contract=off -o $@ $<
 
 build/obj/%.o: liteasr_amd/csrc/%.hip $(HDRS)
 	@mkdir -p build/obj
@@ -26,6 +33,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 clean:
-	rm -rf build $(LIB) $(IOLIB)
+	rm -rf build $(LIB) $(IOLIB) $(DECLIB)
 
 .PHONY: all clean

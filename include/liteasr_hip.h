@@ -358,6 +358,17 @@ int lasr_adam_step(float* param, void* param_lp, int lp_dtype, const float* grad
                    void* stream);
 int lasr_fill(void* dst, int dt, int64_t n, float value, void* stream);
 
+/* ---- decoding (inference) -------------------------------------------
+ * Per row of logits [rows, V] (row stride ld, dtype F32/BF16): log_softmax, then the k
+ * largest log-probs in descending order (ties -> smaller index) into topk_val/topk_idx
+ * [rows, k], and optionally gathered[r] = log_softmax(row r)[gather_idx[r]] (-inf when
+ * the index is outside [0, V)).  Replaces the per-frame `ctc.log_softmax` + `torch.topk`
+ * of liteasr/models/u2.py:221-226 and the `log_softmax(h_attn)` gather of
+ * u2.py:300-313.  V <= 16384, 0 <= k <= V. */
+int lasr_logsoftmax_topk(const void* logits, int dtype, int64_t rows, int V, int64_t ld, int k,
+                         const int32_t* gather_idx, float* topk_val, int32_t* topk_idx,
+                         float* gathered, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -108,6 +108,7 @@ SIGNATURES = {
     "lasr_fill": [_p, _i, _l, _f, _p],
     "lasr_spec_augment": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _l, _p],
     "lasr_spec_augment_ws_bytes": [_i, _i],
+    "lasr_logsoftmax_topk": [_p, _i, _l, _i, _l, _i, _p, _p, _p, _p, _p],
 }
 _RESTYPES = {"lasr_last_error": C.c_char_p, "lasr_spec_augment_ws_bytes": C.c_int64}
 

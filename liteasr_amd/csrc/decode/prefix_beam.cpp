@@ -1,0 +1,131 @@
+// CTC prefix beam search on the host, over per-frame top-k candidates produced on the
+// device by lasr_logsoftmax_topk.  Follows liteasr/models/u2.py:218-263 step for step
+// (and log_add, u2.py:367-375), in double precision like the reference's Python floats:
+//  * next-hypothesis entries are created in the order the reference's defaultdict first
+//    touches them (blank: prefix; repeat: prefix then prefix+s; other: prefix+s), which
+//    fixes the order ties keep through the stable sort;
+//  * log_add: -inf if every argument is -inf, else a_max + log(0 + sum_i exp(a_i - a_max))
+//    summed left to right;
+//  * each frame keeps the `beam` best by log_add(pb, pnb), stable descending sort.
+// Built with -ffp-contract=off so exp/log/add are the plain libm/IEEE operations the
+// reference's math.exp / math.log / float + perform.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <vector>
+
+#include "../../../include/liteasr_decode.h"
+
+namespace {
+
+thread_local char g_err[256] = "";
+
+double log_add(const double* a, int n) {
+  bool all_ninf = true;
+  for (int i = 0; i < n; ++i) all_ninf = all_ninf && (a[i] == -INFINITY);
+  if (all_ninf) return -INFINITY;
+  double m = a[0];
+  for (int i = 1; i < n; ++i)
+    if (a[i] > m) m = a[i];
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += std::exp(a[i] - m);
+  return m + std::log(s);
+}
+
+struct Hyp {
+  std::vector<int32_t> prefix;
+  double pb, pnb;
+};
+
+struct NextHyps {
+  std::vector<Hyp> items;  // insertion order
+  std::map<std::vector<int32_t>, size_t> where;
+  Hyp& at(const std::vector<int32_t>& p) {
+    auto it = where.find(p);
+    if (it != where.end()) return items[it->second];
+    where.emplace(p, items.size());
+    items.push_back(Hyp{p, -INFINITY, -INFINITY});
+    return items.back();
+  }
+};
+
+}  // namespace
+
+extern "C" const char* lasr_decode_last_error(void) { return g_err; }
+
+extern "C" int lasr_ctc_prefix_beam_search(const float* topk_val, const int32_t* topk_idx, int T,
+                                           int k, int blank, int beam, int32_t* out_tok,
+                                           int64_t cap_tok, int32_t* out_len,
+                                           double* out_score) {
+  if (T < 0 || k <= 0 || beam <= 0 || (T > 0 && (topk_val == nullptr || topk_idx == nullptr)) ||
+      out_len == nullptr || out_score == nullptr || (cap_tok > 0 && out_tok == nullptr)) {
+    std::snprintf(g_err, sizeof g_err, "ctc_prefix_beam_search: bad arguments (T=%d k=%d beam=%d)",
+                  T, k, beam);
+    return -1;
+  }
+  std::vector<Hyp> cur{Hyp{{}, 0.0, -INFINITY}};
+  for (int t = 0; t < T; ++t) {
+    NextHyps nxt;
+    for (int j = 0; j < k; ++j) {
+      const int32_t s = topk_idx[(int64_t)t * k + j];
+      const double ps = (double)topk_val[(int64_t)t * k + j];
+      for (const Hyp& h : cur) {
+        const bool has_last = !h.prefix.empty();
+        const int32_t last = has_last ? h.prefix.back() : 0;
+        if (s == blank) {
+          Hyp& n = nxt.at(h.prefix);
+          const double a[3] = {n.pb, h.pb + ps, h.pnb + ps};
+          n.pb = log_add(a, 3);
+        } else if (has_last && s == last) {
+          {
+            Hyp& n = nxt.at(h.prefix);
+            const double a[2] = {n.pnb, h.pnb + ps};
+            n.pnb = log_add(a, 2);
+          }
+          std::vector<int32_t> np = h.prefix;
+          np.push_back(s);
+          Hyp& n = nxt.at(np);
+          const double a[2] = {n.pnb, h.pb + ps};
+          n.pnb = log_add(a, 2);
+        } else {
+          std::vector<int32_t> np = h.prefix;
+          np.push_back(s);
+          Hyp& n = nxt.at(np);
+          const double a[3] = {n.pnb, h.pb + ps, h.pnb + ps};
+          n.pnb = log_add(a, 3);
+        }
+      }
+    }
+    std::vector<std::pair<double, size_t>> order;
+    order.reserve(nxt.items.size());
+    for (size_t i = 0; i < nxt.items.size(); ++i) {
+      const double a[2] = {nxt.items[i].pb, nxt.items[i].pnb};
+      order.emplace_back(log_add(a, 2), i);
+    }
+    std::stable_sort(order.begin(), order.end(),
+                     [](const auto& x, const auto& y) { return x.first > y.first; });
+    std::vector<Hyp> kept;
+    for (size_t i = 0; i < order.size() && (int)i < beam; ++i)
+      kept.push_back(std::move(nxt.items[order[i].second]));
+    cur.swap(kept);
+  }
+  int64_t used = 0;
+  for (const Hyp& h : cur) used += (int64_t)h.prefix.size();
+  if (used > cap_tok) {
+    std::snprintf(g_err, sizeof g_err,
+                  "ctc_prefix_beam_search: %lld output tokens exceed capacity %lld",
+                  (long long)used, (long long)cap_tok);
+    return -2;
+  }
+  int64_t o = 0;
+  for (size_t i = 0; i < cur.size(); ++i) {
+    const Hyp& h = cur[i];
+    for (int32_t v : h.prefix) out_tok[o++] = v;
+    out_len[i] = (int32_t)h.prefix.size();
+    const double a[2] = {h.pb, h.pnb};
+    out_score[i] = log_add(a, 2);
+  }
+  return (int)cur.size();
+}

@@ -1,0 +1,158 @@
+"""Inference searches of U2 (liteasr/models/u2.py:160-317), SURVEY §8 f3.
+
+Device side: the encoder / decoder run through the same HIP kernels as training
+(nets/functional.py: encoder_out, ctc_logits, decoder_logits); per-frame log_softmax +
+top-k and the rescoring gathers are one HIP kernel (lasr_logsoftmax_topk).  Host side:
+the CTC prefix beam search is native C++ (libliteasr_decode.so, csrc/decode/), fed
+with the [T', beam] candidates; the attention beam's (beam x beam) bookkeeping is a few
+float32 numpy operations mirroring the reference's torch ops.  No CPU fallback: both
+libraries must be present.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .nets import functional as FN
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libliteasr_decode.so")
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(_LIB_PATH):
+            raise RuntimeError(f"{_LIB_PATH} missing: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(_LIB_PATH)
+        L.lasr_ctc_prefix_beam_search.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                  C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
+                                                  C.c_void_p]
+        L.lasr_ctc_prefix_beam_search.restype = C.c_int
+        L.lasr_decode_last_error.restype = C.c_char_p
+        _LIB = L
+    return _LIB
+
+
+def prefix_beam_search(topk_val: np.ndarray, topk_idx: np.ndarray, beam: int, blank: int = 0):
+    """Native CTC prefix beam search over per-frame candidates [T, k] (float32 log-probs,
+    int32 ids, descending).  Returns [(tokens list, score float)], best first."""
+    v = np.ascontiguousarray(topk_val, dtype=np.float32)
+    i = np.ascontiguousarray(topk_idx, dtype=np.int32)
+    T, k = v.shape
+    cap = max(1, beam * T)
+    tok = np.empty(cap, dtype=np.int32)
+    lens = np.empty(beam, dtype=np.int32)
+    score = np.empty(beam, dtype=np.float64)
+    n = _lib().lasr_ctc_prefix_beam_search(v.ctypes.data, i.ctypes.data, T, k, blank, beam,
+                                           tok.ctypes.data, cap, lens.ctypes.data, score.ctypes.data)
+    if n < 0:
+        raise RuntimeError("lasr_ctc_prefix_beam_search: " + _lib().lasr_decode_last_error().decode())
+    out, o = [], 0
+    for j in range(n):
+        out.append((tok[o:o + lens[j]].tolist(), float(score[j])))
+        o += int(lens[j])
+    return out
+
+
+def _mem_mask(B, T, dev):
+    return torch.zeros(B, T, dtype=torch.uint8, device=dev)
+
+
+def encode(model, x):
+    """`self.encoder(x)` for one utterance x [1, T, F] (no padding mask)."""
+    if x.device.type != "cuda":
+        raise RuntimeError("liteasr_amd decoding runs on the HIP device only")
+    B, Tx = x.shape[0], x.shape[1]
+    xlens = torch.full((B,), Tx, dtype=torch.int64, device=x.device)
+    ys = torch.full((B, 1), -1, dtype=torch.int64, device=x.device)
+    ylens = torch.zeros(B, dtype=torch.int64, device=x.device)
+    xe, prep, _ = model._run_encoder(x, xlens, ys, ylens)
+    return FN.encoder_out(xe, model, model.compute_dtype), prep.T
+
+
+def ctc_prefix_beam_search_nbest(model, x, beam=10):
+    """u2.py:218-263: (n-best [(tokens, score)], h [T', d], T')."""
+    h, T = encode(model, x)
+    logits = FN.ctc_logits(h, model)
+    vals, idx, _ = K.logsoftmax_topk(logits, min(beam, logits.shape[1]))
+    hyps = prefix_beam_search(vals.cpu().numpy(), idx.cpu().numpy(), beam, model.blank)
+    return hyps, h, T
+
+
+def rescore(model, hyps, h, T, ctc_weight=0.5):
+    """u2.py:268-317: decoder over the n-best (memory = h repeated, no memory mask),
+    score = sum of attention log-probs at the tokens + eos (fp32, as the reference's
+    0-d tensor sum) + ctc_weight * CTC score; first strict maximum wins."""
+    dev = h.device
+    n = len(hyps)
+    Lmax = max(1, max(len(t) for t, _ in hyps))
+    L1 = Lmax + 1
+    ys = torch.full((n, Lmax), -1, dtype=torch.int64)
+    for i, (t, _) in enumerate(hyps):
+        ys[i, :len(t)] = torch.tensor(t, dtype=torch.int64)
+    ylens = torch.tensor([len(t) for t, _ in hyps], dtype=torch.int64)
+    Tx = 4 * T + 3  # any Tx with ((Tx-1)//2-1)//2 == T; all frames valid
+    prep = model._prep_targets(ys.to(dev), ylens.to(dev), n, Tx)
+    mem = h.view(1, T, -1).expand(n, T, h.shape[1]).reshape(n * T, h.shape[1])
+    h_attn = FN.decoder_logits(model, mem, prep.ys_in, prep.dec_mask, _mem_mask(n, T, dev), n, L1, T)
+    gidx = torch.full((n, L1), -1, dtype=torch.int32)
+    for i, (t, _) in enumerate(hyps):
+        gidx[i, :len(t)] = torch.tensor(t, dtype=torch.int32)
+        gidx[i, len(t)] = model.eos
+    _, _, g = K.logsoftmax_topk(h_attn, 0, gather_idx=gidx.view(-1).to(dev))
+    g = g.view(n, L1).cpu().numpy()
+    f32 = np.float32
+    best, best_i = -float("inf"), 0
+    for i, (t, sc) in enumerate(hyps):
+        s = f32(0.0)
+        for j in range(len(t) + 1):  # tokens, then eos at position len(t)
+            s = f32(s + g[i, j])
+        s = f32(s + f32(sc * ctc_weight))
+        if s > best:
+            best, best_i = s, i
+    return best_i
+
+
+def attention_beam_search(model, x, beam=10):
+    """u2.py:163-216: left-to-right attention beam search (memory h repeated, no memory
+    mask), max T' steps, per-step log_softmax + topk(beam) on the device, the (beam x
+    beam) score bookkeeping in float32 on the host.  The reference's decoder cache only
+    skips recomputing earlier positions; here each step reruns the causal decoder over
+    the prefix, which yields the same last-position log-probs."""
+    h, T = encode(model, x)
+    dev = h.device
+    d = h.shape[1]
+    mem = h.view(1, T, d).expand(beam, T, d).reshape(beam * T, d)
+    sos, eos = model.sos, model.eos
+    init = np.array([0.0] + [-np.inf] * (beam - 1), dtype=np.float32)
+    hyps = np.full((beam, 1), sos, dtype=np.int64)
+    scores = init.reshape(beam, 1).copy()
+    end = np.zeros(beam, dtype=bool)
+    mmask = _mem_mask(beam, T, dev)
+    for i in range(1, T + 1):
+        if end.sum() == beam:
+            break
+        ys_in = torch.from_numpy(hyps.astype(np.int32)).to(dev)
+        tri = torch.triu(torch.ones(i, i, dtype=torch.uint8, device=dev), diagonal=1)
+        dmask = tri.unsqueeze(0).expand(beam, i, i).contiguous()
+        logits = FN.decoder_logits(model, mem, ys_in, dmask, mmask, beam, i, T)
+        last = logits[i - 1:]  # rows b*i + (i-1), stride i rows
+        vals, idx, _ = K.logsoftmax_topk(last, beam, rows=beam, ld=i * logits.stride(0))
+        st = vals.cpu().numpy()
+        it = idx.cpu().numpy().astype(np.int64)
+        st[end] = init
+        it[end] = eos
+        cand = (scores + st).reshape(-1).astype(np.float32)
+        order = np.argsort(-cand.astype(np.float64), kind="stable")[:beam]
+        scores = cand[order].reshape(beam, 1)
+        sel, off = order // beam, order % beam
+        hyps = np.concatenate([hyps[sel], it[sel, off][:, None]], axis=1)
+        end = hyps[:, -1] == eos
+    best = int(np.argmax(scores.reshape(-1)))
+    return hyps[best].tolist()

@@ -535,3 +535,29 @@ def set_dropout_counter(ctr):
 
 def counter_add(ctr, v=1):
     N.call("lasr_counter_add", ptr(ctr), int(v), stream())
+
+
+def logsoftmax_topk(logits, k, rows=None, ld=None, gather_idx=None):
+    """Per row of ``logits`` (2-D, unit column stride; ``rows``/``ld`` override the row
+    count/stride to walk a strided subset): log_softmax, then the k largest log-probs
+    (descending, ties to the smaller index) and/or log_softmax gathered at
+    ``gather_idx[r]`` (int32, -inf outside [0,V)).  Returns (vals f32 [rows,k],
+    idx i32 [rows,k], gathered f32 [rows] or None)."""
+    if logits.dim() != 2 or logits.stride(1) != 1:
+        raise ValueError("logsoftmax_topk: logits must be 2-D with unit column stride")
+    rows = logits.shape[0] if rows is None else int(rows)
+    ld = logits.stride(0) if ld is None else int(ld)
+    V = logits.shape[1]
+    dev = logits.device
+    if (rows - 1) * ld + V > logits.untyped_storage().nbytes() // logits.element_size() - logits.storage_offset():
+        raise ValueError("logsoftmax_topk: rows/ld walk past the logits storage")
+    vals = torch.empty(rows, k, dtype=torch.float32, device=dev)
+    idx = torch.empty(rows, k, dtype=torch.int32, device=dev)
+    gat = None
+    if gather_idx is not None:
+        if gather_idx.dtype != torch.int32 or gather_idx.numel() != rows or not gather_idx.is_contiguous():
+            raise ValueError("logsoftmax_topk: gather_idx must be contiguous int32 [rows]")
+        gat = torch.empty(rows, dtype=torch.float32, device=dev)
+    N.call("lasr_logsoftmax_topk", ptr(logits), dt(logits), rows, V, ld, k, ptr(gather_idx),
+           ptr(vals) if k > 0 else None, ptr(idx) if k > 0 else None, ptr(gat), stream())
+    return vals, idx, gat

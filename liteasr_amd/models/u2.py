@@ -25,6 +25,7 @@ from torch import Tensor
 from .. import kernels as K
 from ..config import II, MISSING, LiteasrDataclass
 from ..nets import functional as FN
+from .. import decoding as D
 from ..nets.modules import CTC, TransformerDecoder, TransformerEncoder, _Bound
 from ..utils.cfg import enum_value
 from ..utils.param_store import FlatParams
@@ -185,8 +186,9 @@ class U2(LiteasrModel):
         p = SimpleNamespace(B=B, Tx=Tx, T=Tsub, L=L, chunk_mask=chunk, **out)
         return p
 
-    # ----------------------------------------------------------------- forward
-    def forward(self, xs, xlens, ys, ylens):
+    def _run_encoder(self, xs, xlens, ys, ylens):
+        """Bookkeeping (_prep) + Conv2DLayer/PE + conformer layers: the encoder residual
+        stream x [B*T', d] fp32 (before after_norm), prep and the kernel env."""
         if xs.device.type != "cuda":
             raise RuntimeError("liteasr_amd.U2 runs on the HIP device only (no CPU path); "
                                "move the model and batch to cuda")
@@ -219,8 +221,49 @@ class U2(LiteasrModel):
         K.pe_fwd(None, T, T, d, enc.pe.table(T), 1.0, pos, env.p_pos, env.seed + 4)
         for layer in enc.enc_layers:
             x = FN.ConformerLayerFn.apply(x, pos, layer.final_norm.weight, layer, env)
+        return x, prep, env
+
+    # ----------------------------------------------------------------- forward
+    def forward(self, xs, xlens, ys, ylens):
+        x, prep, env = self._run_encoder(xs, xlens, ys, ylens)
+        B, T, L1 = prep.B, prep.T, prep.L + 1
         h_attn, h_ctc = FN.HeadsFn.apply(x, self.ctc.ctc_lo.weight, self, env)
         return h_attn.view(B, L1, -1), h_ctc.view(B, T, -1)
+
+    # --------------------------------------------------------------- inference
+    def _prep_targets(self, ys, ylens, B, Tx):
+        """_prep for a decoder-only pass: every one of the Tx frames valid."""
+        xs = torch.empty(B, Tx, 0, device=ys.device)  # shape / device only
+        xlens = torch.full((B,), Tx, dtype=torch.int64, device=ys.device)
+        return self._prep(xs, xlens, ys, ylens)
+
+    @torch.no_grad()
+    def inference(self, x):
+        """liteasr/models/u2.py:160-161."""
+        return self.attention_rescore(x)
+
+    @torch.no_grad()
+    def attention(self, x):
+        """liteasr/models/u2.py:163-216 (beam 10); returns the best hypothesis incl. sos."""
+        return D.attention_beam_search(self, x, beam=10)
+
+    @torch.no_grad()
+    def _ctc_prefix_beam_search(self, x):
+        """liteasr/models/u2.py:218-263: ([(tokens tuple, score)], h (1, T', d))."""
+        hyps, h, T = D.ctc_prefix_beam_search_nbest(self, x, beam=10)
+        return [(tuple(t), sc) for t, sc in hyps], h.view(1, T, -1)
+
+    @torch.no_grad()
+    def ctc_prefix_beam_search(self, x):
+        """liteasr/models/u2.py:265-267."""
+        hyps, _, _ = D.ctc_prefix_beam_search_nbest(self, x, beam=10)
+        return tuple(hyps[0][0])
+
+    @torch.no_grad()
+    def attention_rescore(self, x):
+        """liteasr/models/u2.py:269-317 (ctc weight 0.5)."""
+        hyps, h, T = D.ctc_prefix_beam_search_nbest(self, x, beam=10)
+        return tuple(hyps[D.rescore(self, hyps, h, T, ctc_weight=0.5)][0])
 
     @classmethod
     def build_model(cls, cfg: U2Config, task=None):

@@ -643,3 +643,43 @@ class HybridLossFn(torch.autograd.Function):
                   sv.nll, sv.beta, gc, sv.w / B, gdev=g, beta_ready=True)
         ctx.sv = None
         return ga.view(sv.shapes[0]), gc.view(sv.shapes[1]), None, None, None, None
+
+
+# ================================================================ inference ===
+def encoder_out(x, model, adt):
+    """Encoder after_norm (transformer_encoder.py:126) without the CTC dropout branch:
+    x [M, d] fp32 residual stream -> h [M, d] in the compute dtype."""
+    we = model.encoder.after_norm_weights()
+    h, _, _, _ = ln_forward(x.contiguous(), we.g, we.b, adt)
+    return h
+
+
+def ctc_logits(h, model):
+    """ctc_lo(h) (ctc.py:25-26, no dropout), [M, V] padded-row view."""
+    wc = model.ctc.weights()
+    out = K.padded_rows(h.shape[0], wc.W.shape[0], h.dtype, h.device)
+    K.linear(h, wc.W, out, bias=wc.b)
+    return out
+
+
+def decoder_logits(model, h, ys_in, dec_mask, mem_mask, B, L1, T):
+    """TransformerDecoder.forward (transformer_decoder.py:70-93) in eval mode for
+    decoding: ys_in int32 [B, L1], dec_mask u8 [B, L1, L1] (1 = masked), memory h
+    [B*T, d] (compute dtype), mem_mask u8 [B, T].  Returns h_attn [B*L1, V] (padded rows).
+    Same kernels and order as HeadsFn.forward, without dropout and saved state."""
+    wd = model.decoder.weights()
+    d, adt, dev = wd.d, h.dtype, h.device
+    R = B * L1
+    y = _e((R, d), F32, dev)
+    K.embed_pe_fwd(ys_in, L1, wd.E, wd.pe, math.sqrt(d), y, 0.0, 0)
+    for lw in wd.layers:
+        l1, _, _, _ = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
+        y1, _ = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, dec_mask, L1 * L1, L1, y, 0.0, 0, 0.0, 0)
+        l2, _, _, _ = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
+        y2, _ = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, mem_mask, T, 0, y1, 0.0, 0, 0.0, 0)
+        l3, _, _, _ = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)
+        y, _, _ = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, 0.0, 0, y2, 1.0, 0.0, 0)
+    yf, _, _, _ = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
+    out = K.padded_rows(R, wd.Wout.shape[0], adt, dev)
+    K.linear(yf, wd.Wout, out, bias=wd.bout)
+    return out

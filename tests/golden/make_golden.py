@@ -19,6 +19,11 @@ Fixtures
   u2_step.npz     tiny U2 (d 32, 2 enc / 1 dec, V 20, F 40): seed-42 init state_dict, a
                   batch, h_attn / h_ctc / loss / grads, params after clip(5) + Noam step,
                   BN running stats; plus a chunk-mask (stage 4) forward for config 4
+  decode.npz      tiny U2 (d 64, ff 256, 2 enc / 1 dec, V 30, F 40; seed-42 init, CTC / output projections scaled
+                  x6 so the posteriors are peaked) in eval mode on 3 single utterances:
+                  the reference's CTC log-probs, _ctc_prefix_beam_search n-best (token
+                  sequences + scores), ctc_prefix_beam_search / attention_rescore /
+                  attention (beam 10) results (u2.py:163-317)
   spec_aug.npz    the reference SpecAugment (utils/transform/spec_augment.py) on seeded
                   inputs: global random/numpy seeds per case, input regenerated from its own
                   PCG64 seed, the augmented output, and one random.random() /
@@ -197,6 +202,43 @@ def gen_u2_step():
          **{"init." + k: v for k, v in init.items()}, **grads, **after)
 
 
+def gen_decode():
+    torch.manual_seed(42)
+    model = U2(tiny_cfg(enc_dim=64, dec_dim=64, enc_ff_dim=256, dec_ff_dim=256, vocab_size=30))
+    with torch.no_grad():
+        model.ctc.ctc_lo.weight.mul_(6.0)
+        model.decoder.linear_out.weight.mul_(6.0)
+    model.eval()
+    # u2.py:283-288 hands _preprocess plain lists for xlens / ylens, which it cannot take
+    # (mask.py:24 AttributeError, u2.py:356 TypeError); wrap it so the lists become int64
+    # tensors -- the only change, the rest of attention_rescore runs as written.
+    _pp = model._preprocess
+    model._preprocess = lambda xs, xlens, ys, ylens: _pp(
+        xs, torch.as_tensor(xlens, dtype=torch.long), ys, torch.as_tensor(ylens, dtype=torch.long))
+    state = {k: v.clone() for k, v in model.state_dict().items() if not k.endswith(".pe.pe")}
+    g = torch.Generator().manual_seed(11)
+    arrs = {}
+    with torch.no_grad():
+        for u, T in enumerate((120, 97, 64)):
+            x = torch.randn(1, T, 40, generator=g)
+            hyps, h = model._ctc_prefix_beam_search(x)
+            logp = model.ctc.log_softmax(h).squeeze(0)
+            arrs[f"u{u}.x"] = x[0]
+            arrs[f"u{u}.ctc_logp"] = logp
+            arrs[f"u{u}.enc"] = h[0]
+            n = len(hyps)
+            lens = np.array([len(hh[0]) for hh in hyps], dtype=np.int64)
+            flat = np.array([t for hh in hyps for t in hh[0]], dtype=np.int64)
+            arrs[f"u{u}.nbest_len"] = lens
+            arrs[f"u{u}.nbest_tok"] = flat
+            arrs[f"u{u}.nbest_score"] = np.array([hh[1] for hh in hyps], dtype=np.float64)
+            arrs[f"u{u}.nbest_n"] = np.array(n)
+            arrs[f"u{u}.ctc_best"] = np.array(model.ctc_prefix_beam_search(x), dtype=np.int64)
+            arrs[f"u{u}.rescore_best"] = np.array(model.attention_rescore(x), dtype=np.int64)
+            arrs[f"u{u}.attn_best"] = np.array(model.attention(x), dtype=np.int64)
+    save("decode.npz", n_utt=np.array(3), **arrs, **{"init." + k: v for k, v in state.items()})
+
+
 def gen_loader():
     import shutil
     import tempfile
@@ -327,5 +369,6 @@ if __name__ == "__main__":
     gen_lengths()
     gen_ctc_kl()
     gen_u2_step()
+    gen_decode()
     gen_loader()
     gen_spec_aug()

@@ -79,3 +79,17 @@ def test_product_path_refuses_cpu():
     xs = torch.zeros(1, 40, 40)
     with pytest.raises(RuntimeError, match="HIP device only"):
         m(xs, torch.tensor([40]), torch.ones(1, 3, dtype=torch.long), torch.tensor([3]))
+
+
+def test_decode_header_symbols_exported():
+    """include/liteasr_decode.h <-> libliteasr_decode.so (host-only decoding library)."""
+    hdr = os.path.join(ROOT, "include", "liteasr_decode.h")
+    so = os.path.join(ROOT, "liteasr_amd", "lib", "libliteasr_decode.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", ROOT, so], check=True, capture_output=True)
+    src = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+    declared = set(re.findall(r"\b(lasr_[a-z0-9_]+)\s*\(", src))
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert declared == {"lasr_ctc_prefix_beam_search", "lasr_decode_last_error"}
+    assert declared <= exported
