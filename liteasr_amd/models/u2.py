@@ -230,6 +230,18 @@ class U2(LiteasrModel):
         h_attn, h_ctc = FN.HeadsFn.apply(x, self.ctc.ctc_lo.weight, self, env)
         return h_attn.view(B, L1, -1), h_ctc.view(B, T, -1)
 
+    def encode(self, xs, xlens):
+        """`self.encoder(xs, mask=padding_mask(xlens))` (transformer_encoder.py:107-127) as a
+        reusable, differentiable block: (h (B, T', d) fp32, key mask (B, T') bool, True =
+        padding).  Training-mode dropout / BN batch statistics follow `self.training`;
+        gradients reach the flat parameter store through the fused layer backward."""
+        B = xs.shape[0]
+        ys = torch.full((B, 1), -1, dtype=torch.int64, device=xs.device)
+        ylens = torch.zeros(B, dtype=torch.int64, device=xs.device)
+        x, prep, env = self._run_encoder(xs, xlens, ys, ylens)
+        h = FN.EncoderOutFn.apply(x, self.encoder.after_norm.weight, self, self.compute_dtype)
+        return h.view(B, prep.T, -1), prep.enc_mask.bool()
+
     # --------------------------------------------------------------- inference
     def _prep_targets(self, ys, ylens, B, Tx):
         """_prep for a decoder-only pass: every one of the Tx frames valid."""

@@ -645,6 +645,38 @@ class HybridLossFn(torch.autograd.Function):
         return ga.view(sv.shapes[0]), gc.view(sv.shapes[1]), None, None, None, None
 
 
+class EncoderOutFn(torch.autograd.Function):
+    """Encoder after_norm (transformer_encoder.py:126) as its own autograd node, for heads
+    other than U2's HeadsFn (encoder reuse, SURVEY §8 f4: Transducer / Paraformer heads
+    consume `self.encoder(xs, mask)`, transducer.py:128, paraformer.py:96).  Returns the
+    fp32 encoder output; backward writes the after_norm parameter gradients and hands
+    dx to the conformer layers' fused backward."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, model, adt):
+        x = x.contiguous()
+        we = model.encoder.after_norm_weights()
+        rows, d = x.shape
+        h = _e((rows, d), F32, x.device)
+        mean = _e(rows, F32, x.device)
+        rstd = _e(rows, F32, x.device)
+        K.layernorm_fwd(x, we.g, we.b, LN_EPS, h, mean, rstd)
+        ctx.sv = (x, mean, rstd)
+        ctx.model = model
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, mean, rstd = ctx.sv
+        enc = ctx.model.encoder
+        we, ge = enc.after_norm_weights(), enc.after_norm_grads()
+        dx = _e(x.shape, F32, x.device)
+        K.layernorm_bwd(x, dh.float().contiguous(), we.g, mean, rstd, dx, ge.g, ge.b)
+        enc.after_norm_ready()
+        ctx.sv = None
+        return dx, None, None, None
+
+
 # ================================================================ inference ===
 def encoder_out(x, model, adt):
     """Encoder after_norm (transformer_encoder.py:126) without the CTC dropout branch:

@@ -362,3 +362,35 @@ def test_graphed_step_ddp_two_ranks_gloo():
         p.join(timeout=60)
     for rank, ok, le, lg in res:
         assert ok, (rank, le, lg)
+
+
+@pytest.mark.gpu
+def test_encoder_reuse_forward_backward():
+    """U2.encode (SURVEY §8 f4 building block: the encoder as a differentiable module for
+    other heads): output, key mask and encoder parameter gradients of sum(h * R) against
+    the fp64 oracle encoder (transformer_encoder.py:107-127); non-encoder grads stay 0."""
+    cfg = TINY
+    params = O.init_params(cfg, seed=21)
+    buffers = O.init_buffers(cfg)
+    xs, xlens, _, _ = O.synthetic_batch(3, 140, 4, cfg["vocab_size"], seed=4)
+    p64 = {k: v.double().requires_grad_(True) for k, v in params.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in buffers.items()}
+    h_o, km_o = O.encoder(xs.double(), xlens, p64, cfg, b64, True)
+    R = torch.randn(h_o.shape, generator=torch.Generator().manual_seed(9), dtype=torch.float64)
+    (h_o * R).sum().backward()
+    go = {k: v.grad for k, v in p64.items() if k.startswith("encoder.")}
+    model = build(cfg, "fp32")
+    model.load_state_dict({**params, **buffers}, strict=False)
+    model = model.cuda().train()
+    h, km = model.encode(xs.cuda(), xlens.cuda())
+    (h * R.float().cuda()).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(km.cpu(), km_o)
+    assert rel(h.detach(), h_o.detach()) < 2e-4
+    g = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    errs, _ = grad_errs({k: g[k] for k in go}, go)
+    kink = {k for k in errs if k.startswith("encoder.embed.conv.")}  # see test_parity_fp32
+    worst = max((v, k) for k, v in errs.items() if k not in kink)
+    assert worst[0] < 2e-4, worst
+    assert max(errs[k] for k in kink) < 2e-2
+    assert all(float(g[k].abs().max()) == 0.0 for k in g if not k.startswith("encoder."))
