@@ -106,7 +106,13 @@ def rescore(model, hyps, h, T, ctc_weight=0.5):
         gidx[i, :len(t)] = torch.tensor(t, dtype=torch.int32)
         gidx[i, len(t)] = model.eos
     _, _, g = K.logsoftmax_topk(h_attn, 0, gather_idx=gidx.view(-1).to(dev))
-    g = g.view(n, L1).cpu().numpy()
+    return pick_best(hyps, g.view(n, L1).cpu().numpy(), ctc_weight)
+
+
+def pick_best(hyps, g, ctc_weight=0.5):
+    """Host half of rescoring (u2.py:300-315): g[i, j] = attention log-prob of hypothesis
+    i's j-th token (j = len: eos).  float32 running sum like the reference's 0-d tensor,
+    python-float CTC term cast to float32, first strict maximum wins."""
     f32 = np.float32
     best, best_i = -float("inf"), 0
     for i, (t, sc) in enumerate(hyps):

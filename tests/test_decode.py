@@ -87,6 +87,26 @@ def test_native_prefix_beam_ties_and_empty():
     assert D.prefix_beam_search(e, e.astype(np.int32), beam=3) == [([], 0.0)]
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_rescore_pick_matches_oracle(seed):
+    """Host half of attention rescoring: gathered log-probs -> best index, as the oracle's
+    restatement of u2.py:300-315 (incl. ties: first strict maximum wins)."""
+    from liteasr_amd import decoding as D
+
+    rng = np.random.default_rng(seed)
+    n, V, eos = 10, 12, 11
+    hyps = [(rng.integers(1, V - 1, rng.integers(0, 7)).tolist(), float(rng.normal() * 3)) for _ in range(n)]
+    if seed == 2:
+        hyps[3] = hyps[1]  # exact tie: the earlier one wins
+    L1 = max(len(t) for t, _ in hyps) + 1
+    attn = np.log(rng.dirichlet(np.ones(V), size=(n, L1))).astype(np.float32)
+    g = np.full((n, L1), -np.inf, np.float32)
+    for i, (t, _) in enumerate(hyps):
+        for j, w in enumerate(t + [eos]):
+            g[i, j] = attn[i, j, w]
+    assert D.pick_best(hyps, g) == R.rescore_pick(hyps, attn, eos)
+
+
 # ------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
