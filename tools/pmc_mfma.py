@@ -1,0 +1,52 @@
+"""MFMA utilisation from a rocprofv3 PMC pass (SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE).
+
+  rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d D -o run \
+      -- python3 bench.py --graph off --steps 3 --warmup 1 --no-cpu-baseline --no-roofline
+  python tools/pmc_mfma.py D/run_counter_collection.csv [--skip-steps-frac F]
+
+Per dispatch: elapsed shader cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs,
+MI355X_MICROARCH.md "DVFS give-back"); MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES /
+(elapsed x 1024 SIMDs) (busy counts SIMD cycles, 32 per v_mfma_f32_32x32x16_bf16, ibid.
+"s_memtime tick vs SQ PMC units").  Prints one JSON object: the whole run's
+cycle-weighted utilisation and the top kernels by elapsed cycles.
+"""
+
+import csv
+import json
+import sys
+from collections import defaultdict
+
+SIMDS = 256 * 4
+
+
+def main(path):
+    rows = defaultdict(lambda: defaultdict(float))  # dispatch id -> counter -> value
+    name = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d = r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id")
+            name[d] = r.get("Kernel_Name", "?")
+            rows[d][r["Counter_Name"]] += float(r["Counter_Value"])
+    per = defaultdict(lambda: [0, 0.0, 0.0])  # kernel -> launches, busy, elapsed
+    for d, c in rows.items():
+        if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
+            continue
+        k = name[d].split("(")[0][:90]
+        per[k][0] += 1
+        per[k][1] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
+        per[k][2] += c["GRBM_GUI_ACTIVE"] / 8.0
+    busy = sum(v[1] for v in per.values())
+    el = sum(v[2] for v in per.values())
+    top = sorted(per.items(), key=lambda kv: -kv[1][2])[:15]
+    out = {
+        "dispatches": sum(v[0] for v in per.values()),
+        "mfma_util_all_kernels": busy / (el * SIMDS) if el else None,
+        "elapsed_cycles_sum": el,
+        "top_kernels": [{"kernel": k, "launches": v[0], "elapsed_share": v[2] / el,
+                         "mfma_util": v[1] / (v[2] * SIMDS) if v[2] else None} for k, v in top],
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
