@@ -263,7 +263,7 @@ class U2(LiteasrModel):
     def _ctc_prefix_beam_search(self, x):
         """liteasr/models/u2.py:218-263: ([(tokens tuple, score)], h (1, T', d))."""
         hyps, h, T = D.ctc_prefix_beam_search_nbest(self, x, beam=10)
-        return [(tuple(t), sc) for t, sc in hyps], h.view(1, T, -1)
+        return [(tuple(t), sc) for t, sc in hyps], h.view(1, T, -1).clone()
 
     @torch.no_grad()
     def ctc_prefix_beam_search(self, x):

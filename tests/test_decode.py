@@ -168,3 +168,24 @@ def test_u2_decode_against_reference():
         assert list(model.attention_rescore(x)) == d[f"u{u}.rescore_best"].tolist()
         assert list(model.inference(x)) == d[f"u{u}.rescore_best"].tolist()
         assert list(model.attention(x)) == d[f"u{u}.attn_best"].tolist()
+
+
+@pytest.mark.gpu
+def test_graphed_encode_matches_eager():
+    """hipGraph-replayed batch-1 encoder == eager launches, bit for bit, across replays with
+    new contents and after a weight update (re-capture)."""
+    from liteasr_amd import decoding as D
+
+    model, d = _golden_model()
+    g = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for it in range(3):
+            x = torch.randn(1, 100, 40, generator=g).cuda()
+            he, Te = D.encode(model, x, graph=False)
+            he = he.clone()
+            hg, Tg = D.encode(model, x, graph=True)
+            torch.cuda.synchronize()
+            assert Te == Tg and torch.equal(he, hg), it
+            if it == 1:  # weight update -> new flat version -> re-capture
+                model.ctc.ctc_lo.weight.mul_(1.0)
+                model.encoder.after_norm.weight.add_(0.01)
