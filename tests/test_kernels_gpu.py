@@ -278,7 +278,8 @@ def _ctc_case(B, T, V, L, seed, dtype):
     return logits.to(dtype), tg, ilen, tlen
 
 
-@pytest.mark.parametrize("B,T,V,L", [(4, 50, 30, 12), (3, 249, 4233, 40), (2, 120, 200, 70)])
+@pytest.mark.parametrize("B,T,V,L", [(4, 50, 30, 12), (3, 249, 4233, 40), (2, 120, 200, 70),
+                                     (2, 999, 4233, 150)])  # SURVEY §8c F-c sizes, long config
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_ctc(B, T, V, L, dtype):
     kn = K()
@@ -312,9 +313,16 @@ def test_ctc(B, T, V, L, dtype):
     grad = torch.empty(B, T, V, device=DEV, dtype=torch.float32)
     kn.ctc_bwd(d_log, tg32, il, tl, lse, lpb, alpha, nll, beta, grad, 1.0)
     gg = grad.cpu().double()
-    # torch's own fp32 ctc_loss is 5.8e-4 (max-abs) off its fp64 result on the 249x4233
-    # case (the lattice sums ~600-nat log terms in fp32); allow 2e-3.
-    close(gg[fin], gref[fin], 2e-3, "ctc grad")
+    # The bar is the reference's own fp32 path (aten fp32 ctc_loss, what LiteASR runs):
+    # its max-abs gradient error vs fp64 is 5.8e-4 at 249x4233 and 1.1e-2 at the long
+    # 999x4233, L 150 case (the lattice sums thousands of nats in fp32).  Allow
+    # max(2e-3, 1.25 x that error), measured here on the same logits.
+    l32 = logits.float().requires_grad_()
+    n32 = F.ctc_loss(l32.log_softmax(-1).transpose(0, 1), tg.clamp(min=0), ilen, tlen, blank=0,
+                     reduction="none", zero_infinity=False)
+    g32 = torch.autograd.grad(n32[torch.isfinite(n32)].sum(), l32)[0].double()
+    err32 = (g32[fin] - gref[fin]).abs().max().item()
+    close(gg[fin], gref[fin], max(2e-3, 1.25 * err32), "ctc grad")
     # beta computed in the forward launch (alongside alpha): identical results
     alpha2, beta2, nll2 = torch.empty_like(alpha), torch.empty_like(beta), torch.empty_like(nll)
     kn.ctc_fwd(d_log, tg32, il, tl, lse, lpb, alpha2, nll2, beta=beta2)
