@@ -59,7 +59,7 @@ def build(cfgd, dtype, dropout, dev):
 
 
 def synthetic(cfgd, rank, dev):
-    from oracle.u2_oracle import synthetic_batch  # input generator only (SURVEY §8d recipe)
+    from liteasr_amd.utils.synthetic import synthetic_batch  # SURVEY §8d input recipe
 
     xs, xlens, ys, ylens = synthetic_batch(cfgd["B"], cfgd["T"], cfgd["L"], V, seed=1234 + rank)
     return [t.to(dev) for t in (xs, xlens, ys, ylens)]
@@ -200,9 +200,49 @@ def cpu_baseline(cfgd_name, budget_s=25.0):
                       f"{steps} timed step(s) = {el:.1f} s after 1 warm-up ({warm:.1f} s)"}
 
 
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _rank_entry(rank, world, port, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LASR_BENCH_SPAWNED="1")
+    sys.argv = [sys.argv[0]] + list(argv)
+    main()
+
+
+def spawn_ranks(n, argv=None, target=None):
+    """`bench.py --gpus N` without a launcher: one process per GPU, as the reference's
+    call_func -> mp.spawn (liteasr/distributed/utils.py:119-139).  The parent never touches
+    the GPU (spawned children start fresh interpreters); each rank runs main() with
+    RANK/LOCAL_RANK/WORLD_SIZE set, rendezvous on 127.0.0.1."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    argv = sys.argv[1:] if argv is None else argv
+    procs = [ctx.Process(target=target or _rank_entry, args=(r, n, port, argv)) for r in range(n)]
+    for p in procs:
+        p.start()
+    rc = 0
+    for p in procs:
+        p.join()
+        rc = rc or (p.exitcode or 0)
+    if rc:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher's WORLD_SIZE, N > 1 spawns them")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="small", choices=sorted(CONFIGS))
@@ -210,6 +250,11 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--graph", default="on", choices=["on", "off"],
                     help="replay the step from hipGraphs (liteasr_amd/graph_step.py) or launch eagerly")
+    ap.add_argument("--overlap", default="on", choices=["on", "off"],
+                    help="N>1 graphed step: all-reduce each gradient bucket between backward segments "
+                         "(on) or after the whole backward (off)")
+    ap.add_argument("--force-ddp", action="store_true",
+                    help="wrap in the DDP reducer even at N=1 (world-1 RCCL group; profiling the overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", type=int, default=0, metavar="N",
@@ -229,13 +274,24 @@ def main():
                           "algorithmic_flops_per_launch": flops}), flush=True)
         return
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    args.gpus = args.gpus or world
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    use_ddp = world > 1 or args.force_ddp
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    elif use_ddp:  # world-1 RCCL group: exercises the bucketed/overlapped path on one GPU
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     cfgd = CONFIGS[args.config]
 
     from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
@@ -244,7 +300,7 @@ def main():
     torch.manual_seed(42)
     model = build(cfgd, args.dtype, args.dropout, dev)
     net = model
-    if world > 1:
+    if use_ddp:
         from liteasr_amd.distributed.ddp import DistributedDataParallel
 
         net = DistributedDataParallel(model)
@@ -255,7 +311,7 @@ def main():
     if args.graph == "on":
         from liteasr_amd.graph_step import GraphedTrainStep
 
-        step = GraphedTrainStep(net, crit, opt, batch, clip=5.0, warmup=2)
+        step = GraphedTrainStep(net, crit, opt, batch, clip=5.0, warmup=2, overlap=args.overlap == "on")
     else:
         def step():
             loss = crit(net, *batch)
@@ -264,17 +320,19 @@ def main():
             opt.zero_grad()
             return loss
 
+    if args.graph == "on" and use_ddp:
+        step.enable_timing()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_ddp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_ddp:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -283,6 +341,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
     final_loss = loss.item()
+    launcher = "bench.py spawn" if os.environ.get("LASR_BENCH_SPAWNED") else (
+        "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "env")
     st = opt.device_state()
     utt = world * cfgd["B"] * args.steps / el
     if rank == 0:
@@ -298,7 +358,13 @@ def main():
                                 f"dec {cfgd['dec']}x, V {V}", "global_batch": world * cfgd["B"],
                        "per_gpu_batch": cfgd["B"], "seq_len": cfgd["T"], "label_len": cfgd["L"],
                        "ctc_weight": cfgd["w"], "dropout": args.dropout, "chunk_size": cfgd["chunk"],
-                       "parallelism": f"dp{world}", "launch": "hipgraph" if args.graph == "on" else "eager"},
+                       "parallelism": f"dp{world}", "launch": "hipgraph" if args.graph == "on" else "eager",
+                       "ranks_seen": world, "rank_launcher": launcher,
+                       "allreduce": None if not use_ddp else
+                       {"backend": dist.get_backend(), "buckets": len(net.reducer.buckets),
+                        "bucket_mb": 25, "overlap": args.overlap == "on" and args.graph == "on" or args.graph == "off",
+                        "segments": len(step.segs) if args.graph == "on" and step.segs else None,
+                        "timeline_last_step": step.overlap_report() if args.graph == "on" else None}},
             "step_tflops_per_gpu": round(cfgd["gflop"] * utt / world / 1e3, 2),
             "step_mfma_frac": round(cfgd["gflop"] * utt / world / 1e3 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(final_loss, 4), "optimizer_state": st,
@@ -308,7 +374,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.config)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_ddp:
         dist.destroy_process_group()
 
 

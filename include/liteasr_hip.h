@@ -275,12 +275,15 @@ int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float eps, float 
 /* mode: 0 batch stats, 1 batch stats + running-stat update (train), 2 running stats (eval) */
 int lasr_bn_swish_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
                       const float* shift, void* h, int hdt, void* stream);
-/* BN(train)+Swish backward: dgamma/dbeta accumulated, dy = BN'(dh * swish'(u)).
+/* BN+Swish backward: dgamma/dbeta accumulated, dy = BN'(dh * swish'(u)).
+ * batch_stats 1: train-mode BN (mean/rstd are the batch statistics, their gradient terms
+ * included); 0: eval-mode BN (mean/rstd = running statistics, constants).
  * ws >= (ceil(rows/64)+1)*2*C floats. */
 int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt, int64_t rows, int C,
                       const float* scale, const float* shift, const float* mean,
                       const float* rstd, const float* gamma, float* dgamma, float* dbeta,
-                      void* dy, int dydt, float* ws, int64_t ws_floats, void* stream);
+                      void* dy, int dydt, float* ws, int64_t ws_floats, int batch_stats,
+                      void* stream);
 int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int dydt, int B, int T, int C,
                         int K, const float* w, void* dz1, float* dw, float* db, float* ws,
                         int64_t ws_floats, void* stream);
@@ -350,7 +353,9 @@ int lasr_sumsq_partial(const float* g, int64_t n, float* ws, int64_t ws_floats, 
 /* state[5]: [0] taken steps, [1] lr of the last step, [2] grad norm, [3] skipped flag,
  * [4] clip coefficient.  ws/nparts: the lasr_sumsq_partial output (may cover several
  * gradient buffers concatenated). param_lp: optional low-precision working copy that is
- * refreshed in the same pass. */
+ * refreshed in the same pass.  Clip coefficient = min(max_norm / (norm + 1e-6), 1) for any
+ * max_norm, as torch.nn.utils.clip_grad_norm_ (0 zeroes the step's gradient; +inf = no
+ * clipping). */
 int lasr_adam_step(float* param, void* param_lp, int lp_dtype, const float* grad, float* m,
                    float* v, int64_t n, const float* ws, int nparts, float* state,
                    float max_norm, int lr_mode, float lr, float factor, float model_dim,

@@ -610,14 +610,16 @@ __global__ void bn_swish_bwd_apply_kernel(const TY* y, const TH* dh, int64_t row
                                           const float* scale, const float* shift,
                                           const float* mean, const float* rstd,
                                           const float* gamma, const float* tot, TD* dy,
-                                          float* dgamma, float* dbeta) {
+                                          float* dgamma, float* dbeta, int batch_stats) {
   if (blockIdx.x == 0)  // parameter gradients (the column totals are final here)
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       dbeta[c] += tot[c];
       dgamma[c] += tot[C + c];
     }
   const int64_t n8 = rows * C / 8;
-  const float inv_n = 1.f / (float)rows;
+  // eval mode (running statistics): mean / rstd are constants, so the batch-mean terms
+  // of the train-mode gradient vanish and dx = gamma * rstd * du
+  const float inv_n = batch_stats ? 1.f / (float)rows : 0.f;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
     const int c0 = (int)((e * 8) % C);
     float yv[8], gv[8], o[8];
@@ -769,7 +771,7 @@ extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt
                                  int C, const float* scale, const float* shift, const float* mean,
                                  const float* rstd, const float* gamma, float* dgamma,
                                  float* dbeta, void* dy, int dydt, float* ws, int64_t ws_floats,
-                                 void* stream) {
+                                 int batch_stats, void* stream) {
   const int64_t nparts = cdiv(rows, BN_ROWS);
   LASR_CHECK_ARG(ws_floats >= (nparts + 1) * 2 * C, "lasr_bn_swish_bwd: workspace too small");
   LASR_CHECK_ARG(nparts <= 65535, "lasr_bn_swish_bwd: too many rows");
@@ -789,7 +791,7 @@ extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt
   rc = lasr_reduce_cols(ws, (int)nparts, 2 * C, tot, nullptr, 2 * C, 0, st);
   if (rc) return rc;
   const int64_t n = rows * C / 8;
-#define BA(TY, TH, TD) bn_swish_bwd_apply_kernel<TY, TH, TD><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy, dgamma, dbeta)
+#define BA(TY, TH, TD) bn_swish_bwd_apply_kernel<TY, TH, TD><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy, dgamma, dbeta, batch_stats)
   const bool yf = ydt == LASR_F32, hf = hdt == LASR_F32, df = dydt == LASR_F32;
   if (yf && hf && df) BA(float, float, float);
   else if (yf && hf) BA(float, float, bf16_t);

@@ -32,8 +32,11 @@ __global__ __launch_bounds__(256) void opt_finalize_kernel(const float* ws, int 
   s = block_sum(s, red);
   if (threadIdx.x != 0) return;
   const float norm = sqrtf(s);
-  float coef = 1.f;
-  if (max_norm > 0.f) coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+  // torch.nn.utils.clip_grad_norm_: clip_coef = max_norm / (norm + 1e-6) clamped to <= 1
+  // for ANY max_norm (0 zeroes the gradients, as the reference does with the dataclass
+  // default clip_grad_norm = 0.0); "no clipping" is max_norm = +inf (coef 1; fminf
+  // drops the NaN of inf/inf)
+  const float coef = fminf(max_norm / (norm + 1e-6f), 1.f);
   const bool skip = isnan(norm);
   state[2] = norm;
   state[3] = skip ? 1.f : 0.f;

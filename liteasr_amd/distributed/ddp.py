@@ -58,6 +58,10 @@ class FlatReducer:
         for bi, b in enumerate(self.buckets):
             for u in b:
                 self.unit_bucket[u.name] = bi
+        # record mode (liteasr_amd.graph_step capture): buckets that become complete are
+        # appended here instead of being launched; the graphed step launches them eagerly
+        # between the replayed backward segments
+        self.record = None
         self._reset()
         for mod in model.modules():
             if isinstance(mod, _Bound):
@@ -102,15 +106,32 @@ class FlatReducer:
         name = mod if isinstance(mod, str) else mod._pfx
         if name not in self.unit_bucket:
             return
-        if not self.active:
+        if not self.active and self.record is None:
             self.active = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
         bi = self.unit_bucket[name]
         self.ready[bi] += 1
         # launch buckets strictly in order (every rank issues the same collective sequence)
         while self.next_bucket < len(self.buckets) and self.ready[self.next_bucket] == len(self.buckets[self.next_bucket]):
-            self._launch(self.next_bucket)
+            if self.record is not None:
+                self.record.append(self.next_bucket)
+            else:
+                self._launch(self.next_bucket)
             self.next_bucket += 1
+
+    def unit_names(self):
+        """Hook-unit names bucket by bucket, each bucket in backward-completion order."""
+        return [[u.name for u in b] for b in self.buckets]
+
+    def launch(self, bi):
+        """Start bucket ``bi``'s async all-reduce now (graphed step, between segments)."""
+        self._launch(bi)
+        self.next_bucket = max(self.next_bucket, bi + 1)
+
+    def wait(self):
+        """Wait for every launched bucket (the current stream waits on RCCL's stream) and
+        launch any bucket that never fired; called before the optimizer step."""
+        self._finalize()
 
     def _slice(self, b):
         lo = min(u.lo for u in b)
@@ -155,13 +176,17 @@ class DistributedDataParallel(nn.Module):
         st = module.store
         st.ensure_grad()
         dist.broadcast(st.flat, 0, group=process_group)
-        self._bn_buffers = [b for n, b in module.named_buffers() if not n.endswith(".pe") and not n.startswith("_")]
+        if hasattr(module, "bn_flat_buffers"):  # U2: BN statistics live in two flat buffers
+            self._bn_buffers = module.bn_flat_buffers()
+        else:
+            self._bn_buffers = [b for n, b in module.named_buffers() if not n.endswith(".pe") and not n.startswith("_")]
+        self._world = dist.get_world_size(process_group)
         self._sync_buffers()
         st._work_version = -1  # weights changed under the working copy
         self.reducer = FlatReducer(module, process_group, int(bucket_cap_mb * 1024 * 1024))
 
     def _sync_buffers(self):
-        if not self._bn_buffers:
+        if not self._bn_buffers or self._world == 1:  # rank 0 to itself: nothing to do
             return
         coalesced = getattr(dist, "_broadcast_coalesced", None)
         if coalesced is not None and self._bn_buffers[0].is_cuda:

@@ -435,12 +435,13 @@ def bn_swish_fwd(y, scale, shift, h):
            stream())
 
 
-def bn_swish_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy):
+def bn_swish_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy, batch_stats=True):
+    """batch_stats False: eval-mode BN (mean/rstd are the running statistics)."""
     rows, Cc = y.shape
     ws = WS.get(((rows + 63) // 64 + 1) * 2 * Cc, y.device)
     N.call("lasr_bn_swish_bwd", ptr(y), dt(y), ptr(dh), dt(dh), rows, Cc, ptr(scale), ptr(shift),
            ptr(mean), ptr(rstd), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dy), dt(dy), ptr(ws),
-           ws.numel(), stream())
+           ws.numel(), int(bool(batch_stats)), stream())
 
 
 def glu_dwconv_bwd(z1, dy, B, T, Cc, K, w, dz1, dw, db):

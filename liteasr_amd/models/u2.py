@@ -13,6 +13,7 @@ Extensions (default off = reference behaviour):
 
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass, field
 from enum import Enum
@@ -128,8 +129,10 @@ class U2(LiteasrModel):
             if isinstance(mod, _Bound):
                 mod._store = self.store
         self.register_buffer("_drop_ctr", torch.zeros(1, dtype=torch.int64), persistent=False)
+        self._flatten_bn()
         self.last_prep = None
         self._seed_base = 77
+        self._seg = None  # active graph-segmentation cuts (see `segmented`)
 
     def _apply(self, fn, recurse=True):
         """Device/dtype moves act on the flat buffers; parameters stay views."""
@@ -138,7 +141,32 @@ class U2(LiteasrModel):
             for k, b in mod._buffers.items():
                 if b is not None:
                     mod._buffers[k] = fn(b)
+        self._flatten_bn()
         return self
+
+    def _flatten_bn(self):
+        """BatchNorm running statistics as views of two flat buffers (fp32 mean/var, int64
+        num_batches_tracked), so the per-forward buffer broadcast of data parallelism
+        (DDP broadcast_buffers, liteasr/trainer.py:80-84) is two collectives on
+        contiguous memory instead of dozens of small copies + a coalesced broadcast."""
+        bns = [m for m in self.modules() if isinstance(m, torch.nn.BatchNorm1d)]
+        if not bns:
+            self._bn_flat = ()
+            return
+        f32 = torch.cat([t.detach().reshape(-1).float() for m in bns for t in (m.running_mean, m.running_var)])
+        i64 = torch.stack([m.num_batches_tracked.detach().reshape(()) for m in bns])
+        off = 0
+        for i, m in enumerate(bns):
+            C = m.running_mean.numel()
+            m._buffers["running_mean"] = f32[off:off + C]
+            m._buffers["running_var"] = f32[off + C:off + 2 * C]
+            m._buffers["num_batches_tracked"] = i64[i]
+            off += 2 * C
+        self._bn_flat = (f32, i64)
+
+    def bn_flat_buffers(self):
+        """The flat BN running-statistics buffers (see ``_flatten_bn``)."""
+        return list(self._bn_flat)
 
     def flat_parameters(self):
         return self.store
@@ -219,9 +247,39 @@ class U2(LiteasrModel):
         d = enc.h_dim
         pos = torch.empty(T, d, dtype=self.compute_dtype, device=xs.device)
         K.pe_fwd(None, T, T, d, enc.pe.table(T), 1.0, pos, env.p_pos, env.seed + 4)
-        for layer in enc.enc_layers:
+        for j, layer in enumerate(enc.enc_layers):
+            x = self._cut(x, j)
             x = FN.ConformerLayerFn.apply(x, pos, layer.final_norm.weight, layer, env)
+        x = self._cut(x, len(enc.enc_layers))
         return x, prep, env
+
+    # ---------------------------------------------------- backward segmentation
+    @contextlib.contextmanager
+    def segmented(self, cuts):
+        """Cut the autograd graph of the encoder residual stream before encoder layer j
+        for every j in ``cuts`` (j == enc_layers: between the last layer and the heads).
+        Inside the block each forward appends ``(j, x, x_leaf)`` to the yielded list,
+        where ``x_leaf = x.detach().requires_grad_()`` is what the rest of the forward
+        consumes, so the backward can run as separate pieces (``torch.autograd.grad`` from
+        the loss down to the top ``x_leaf``, then from each ``x`` down to the next leaf).
+        liteasr_amd.graph_step captures each piece as its own hipGraph so the data-parallel
+        gradient buckets can be all-reduced between the pieces, overlapping the rest of
+        the backward (the reference gets this overlap from DDP's autograd hooks,
+        liteasr/trainer.py:76-88).  Numerics are unchanged: the pieces run the same fused
+        backward nodes in the same order."""
+        self._seg = SimpleNamespace(cuts=frozenset(int(c) for c in cuts), pairs=[])
+        try:
+            yield self._seg.pairs
+        finally:
+            self._seg = None
+
+    def _cut(self, x, j):
+        seg = self._seg
+        if seg is None or j not in seg.cuts or not x.requires_grad:
+            return x
+        leaf = x.detach().requires_grad_(True)
+        seg.pairs.append((j, x, leaf))
+        return leaf
 
     # ----------------------------------------------------------------- forward
     def forward(self, xs, xlens, ys, ylens):

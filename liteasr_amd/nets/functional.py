@@ -308,7 +308,8 @@ def conv_forward(ln, w, env, x_in, p_res, s_res, training):
     K.bn_swish_fwd(y, scale, shift, h3)
     out = _e((M, d), F32, dev)
     K.linear(h3, w.Wpw2, out, bias=w.bpw2, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
-    return out, SimpleNamespace(z1=z1, y=y, mean=mean, rstd=rstd, scale=scale, shift=shift, h3=h3)
+    return out, SimpleNamespace(z1=z1, y=y, mean=mean, rstd=rstd, scale=scale, shift=shift, h3=h3,
+                                training=training)
 
 
 def conv_backward(gb, ln, sv, w, g, env):
@@ -319,7 +320,8 @@ def conv_backward(gb, ln, sv, w, g, env):
     dh3 = _e((M, d), adt, dev)
     K.gemm(gb, w.Wpw2, dh3)
     dy = _e((M, d), F32, dev)
-    K.bn_swish_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy)
+    K.bn_swish_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy,
+                   batch_stats=sv.training)
     dz1 = _e((M, 2 * d), adt, dev)
     K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
     K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0, rowsum=g.bpw1)

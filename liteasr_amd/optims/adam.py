@@ -40,7 +40,7 @@ class Adam(LiteasrOptimizer):
         self.store = find_store(params)
         self._groups = _Groups(params, cfg)
         self.fused = FlatAdamState(self.store)
-        self.max_norm = 0.0
+        self.max_norm = float("inf")  # step() alone does not clip
 
     @property
     def optimizer(self):
@@ -62,6 +62,7 @@ class Adam(LiteasrOptimizer):
         self.fused.step(float(max_norm), mode, lr, factor, dim, warm, b1, b2, g["eps"], g["weight_decay"])
 
     def step(self):
+        """torch.optim.Adam.step: no clipping (max_norm = +inf; a NaN norm still skips)."""
         self.clip_and_step(self.max_norm)
 
     def zero_grad(self):

@@ -1,52 +1,45 @@
-"""Minibatch policies over length-sorted utterances (liteasr/utils/batchify.py:12-159).
+"""Minibatch planning over length-sorted utterances (policies of liteasr/utils/batchify.py).
 
-SeqBatch: the batch size of a minibatch is fixed by its FIRST (longest) utterance:
-max(min_batch_size, int(batch_size / (1 + max(int(xlen / max_len_in), int(ylen / max_len_out))))).
-FrameBatch: a minibatch closes when (utterances + 1) * max length would exceed
-max_frame_in / max_frame_out / max_frame_inout."""
+Utterances arrive longest first.  A planner walks them once and decides, before adding
+each one, whether the open minibatch is closed first:
+
+* ``SeqBatch``  -- the minibatch's capacity is fixed when it is opened, from its first
+  (longest) utterance:  max(min_batch_size,
+  int(batch_size / (1 + max(int(xlen / max_len_in), int(ylen / max_len_out))))).
+* ``FrameBatch`` -- it closes when (size + 1) x max length would exceed any of the
+  enabled frame budgets max_frame_in / max_frame_out / max_frame_inout.
+
+Both keep the reference's edge behaviour: the "closes first?" test also runs on an empty
+minibatch, so an utterance that alone exceeds a frame budget emits an empty minibatch
+before it (it still gets a minibatch of its own).  ``policy.data[i]`` / ``policy[i]`` is
+the i-th minibatch as a list of utterance indices.
+"""
 
 from typing import List, Sequence
 
 
 class BatchifyPolicy(object):
     def __init__(self, dataset_cfg):
-        self._num = 0
-        self.data: List[List[int]] = []
-        self.minibatch: List[int] = []
         self.dataset_cfg = dataset_cfg
-        self.sample = None
+        self.data: List[List[int]] = []
 
-    @property
-    def empty(self) -> bool:
-        return len(self.minibatch) == 0
-
-    @property
-    def full(self) -> bool:
+    # subclasses: does the open minibatch (its indices, its samples) close before `nxt`?
+    def _closes_before(self, members, nxt) -> bool:
         raise NotImplementedError
-
-    def push(self, idx):
-        raise NotImplementedError
-
-    def refresh(self):
-        raise NotImplementedError
-
-    def pop(self):
-        self.data.append(self.minibatch)
-        self._num += len(self.minibatch)
-        self.minibatch = []
 
     def batchify(self, indices: Sequence[int], samples):
         assert len(indices) == len(samples), f"{len(samples)}"
-        self.refresh()
+        members, open_samples = [], []
         for idx in indices:
-            self.sample = samples[idx]
-            if self.full:
-                self.pop()
-                self.refresh()
-            self.push(idx)
-        if not self.empty:
-            self.pop()
-            self.refresh()
+            nxt = samples[idx]
+            if self._closes_before(open_samples, nxt):
+                self.data.append(members)
+                members, open_samples = [], []
+            members.append(idx)
+            open_samples.append(nxt)
+        if members:
+            self.data.append(members)
+        return self
 
     def __getitem__(self, index):
         return self.data[index]
@@ -56,46 +49,21 @@ class BatchifyPolicy(object):
 
 
 class SeqBatch(BatchifyPolicy):
-    @property
-    def full(self):
-        return len(self.minibatch) == self.dynamic_batch_size
-
-    def push(self, idx):
-        first = self.empty
-        self.minibatch.append(idx)
-        if first:
-            self.refresh()
-
-    def refresh(self):
+    def capacity(self, head) -> int:
         c = self.dataset_cfg
-        if self.empty:
-            self.factor, self.dynamic_batch_size, self.max_ilen, self.max_olen = 0, c.batch_size, 0, 0
-        else:
-            self.max_ilen, self.max_olen = self.sample.xlen, self.sample.ylen
-            self.factor = max(int(self.max_ilen / c.max_len_in), int(self.max_olen / c.max_len_out))
-            self.dynamic_batch_size = max(c.min_batch_size, int(c.batch_size / (1 + self.factor)))
+        factor = max(int(head.xlen / c.max_len_in), int(head.ylen / c.max_len_out))
+        return max(c.min_batch_size, int(c.batch_size / (1 + factor)))
+
+    def _closes_before(self, open_samples, nxt) -> bool:
+        cap = self.capacity(open_samples[0]) if open_samples else self.dataset_cfg.batch_size
+        return len(open_samples) == cap
 
 
 class FrameBatch(BatchifyPolicy):
-    @property
-    def full(self):
+    def _closes_before(self, open_samples, nxt) -> bool:
         c = self.dataset_cfg
-        mi = max(self.max_ilen, self.sample.xlen)
-        mo = max(self.max_olen, self.sample.ylen)
-        n = len(self.minibatch) + 1
-        if c.max_frame_in and mi * n > c.max_frame_in:
-            return True
-        if c.max_frame_out and mo * n > c.max_frame_out:
-            return True
-        return bool(c.max_frame_inout and (mi + mo) * n > c.max_frame_inout)
-
-    def push(self, idx):
-        self.minibatch.append(idx)
-        self.refresh()
-
-    def refresh(self):
-        if self.empty:
-            self.max_ilen = self.max_olen = 0
-        else:
-            self.max_ilen = max(self.max_ilen, self.sample.xlen)
-            self.max_olen = max(self.max_olen, self.sample.ylen)
+        n = len(open_samples) + 1
+        xmax = max([s.xlen for s in open_samples] + [nxt.xlen])
+        ymax = max([s.ylen for s in open_samples] + [nxt.ylen])
+        budgets = ((c.max_frame_in, xmax), (c.max_frame_out, ymax), (c.max_frame_inout, xmax + ymax))
+        return any(limit and length * n > limit for limit, length in budgets)

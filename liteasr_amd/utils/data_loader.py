@@ -1,29 +1,39 @@
-"""Endless epoch-counting loader (liteasr/utils/data_loader.py:6-29)."""
+"""Never-ending minibatch stream with an epoch counter (the reference's EpochDataLoader,
+liteasr/utils/data_loader.py:6-29, as the Trainer consumes it).
+
+The Trainer iterates ``for i, batch in enumerate(loader)`` forever and decides itself when
+to stop; each time the underlying torch DataLoader is exhausted, ``epoch`` advances and a
+new pass starts.  A DistributedSampler is re-seeded per pass through ``set_epoch`` so
+every rank reshuffles consistently.  Re-entering ``iter()`` resumes the current pass.
+"""
 
 from torch.utils.data.dataloader import DataLoader
 
+_EXHAUSTED = object()
+
 
 class EpochDataLoader(object):
-    def __init__(self, **kwargs):
-        self.data_loader = DataLoader(**kwargs)
+    def __init__(self, **loader_kwargs):
+        self.data_loader = DataLoader(**loader_kwargs)
         self.epoch = 0
-        self.data_iter = None
+        self._pass = None  # iterator over the current epoch
 
     def __len__(self):
         return len(self.data_loader)
 
-    def __iter__(self):
-        while True:
-            try:
-                if self.data_iter is None:
-                    self._init_data_iter(self.epoch)
-                yield next(self.data_iter)
-            except StopIteration:
-                self.epoch += 1
-                self._init_data_iter(self.epoch)
-                yield next(self.data_iter)
+    def _start_pass(self):
+        set_epoch = getattr(self.data_loader.sampler, "set_epoch", None)
+        if callable(set_epoch):
+            set_epoch(self.epoch)
+        self._pass = iter(self.data_loader)
 
-    def _init_data_iter(self, epoch):
-        if hasattr(self.data_loader.sampler, "set_epoch"):
-            self.data_loader.sampler.set_epoch(epoch)
-        self.data_iter = iter(self.data_loader)
+    def __iter__(self):
+        if self._pass is None:
+            self._start_pass()
+        while True:
+            item = next(self._pass, _EXHAUSTED)
+            if item is _EXHAUSTED:
+                self.epoch += 1
+                self._start_pass()
+                item = next(self._pass)  # an empty dataset ends the stream here
+            yield item

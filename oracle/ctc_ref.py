@@ -15,50 +15,59 @@ which is what the reference's autograd produces for log_softmax -> ctc_loss.
 import numpy as np
 
 
-def _lse(*xs):
-    m = max(xs)
-    if m == -np.inf:
-        return -np.inf
-    return m + np.log(sum(np.exp(x - m) for x in xs))
-
-
 def ctc_nll_and_grad(lp: np.ndarray, labels: np.ndarray, blank: int = 0):
     """lp: [T, V] log-probabilities (rows already log_softmax'ed); labels: [L] ints.
-    Returns (nll, grad [T, V] of nll w.r.t. the logits that produced lp)."""
+    Returns (nll, grad [T, V] of nll w.r.t. the logits that produced lp).
+
+    alpha_t(s) = lp_t(l'_s) + logsumexp(alpha_{t-1}(s), alpha_{t-1}(s-1),
+    [alpha_{t-1}(s-2) if l'_s != blank and l'_s != l'_{s-2}]), and beta mirrored; the
+    recursion is vectorised over the extended-label positions s (one numpy step per
+    frame), exact in float64."""
+    lp = np.asarray(lp, dtype=np.float64)
     T, V = lp.shape
     L = len(labels)
     ext = np.full(2 * L + 1, blank, dtype=np.int64)
     ext[1::2] = labels
     S = len(ext)
-    a = np.full((T, S), -np.inf)
-    b = np.full((T, S), -np.inf)
-    a[0, 0] = lp[0, ext[0]]
+    # skip transitions s-2 -> s allowed where the label differs from the one two back
+    skip = np.zeros(S, dtype=bool)
+    if S > 2:
+        skip[2:] = (ext[2:] != blank) & (ext[2:] != ext[:-2])
+    skip_b = np.zeros(S, dtype=bool)  # s+2 -> s in the backward pass
+    if S > 2:
+        skip_b[:-2] = (ext[:-2] != blank) & (ext[:-2] != ext[2:])
+    ninf = -np.inf
+    a = np.full((T, S), ninf)
+    b = np.full((T, S), ninf)
+    emit = lp[:, ext]  # [T, S]
+    a[0, 0] = emit[0, 0]
     if S > 1:
-        a[0, 1] = lp[0, ext[1]]
-    for t in range(1, T):
-        for s in range(S):
-            terms = [a[t - 1, s]]
-            if s >= 1:
-                terms.append(a[t - 1, s - 1])
-            if s >= 2 and ext[s] != blank and ext[s] != ext[s - 2]:
-                terms.append(a[t - 1, s - 2])
-            a[t, s] = _lse(*terms) + lp[t, ext[s]]
-    b[T - 1, S - 1] = lp[T - 1, ext[S - 1]]
-    if S > 1:
-        b[T - 1, S - 2] = lp[T - 1, ext[S - 2]]
-    for t in range(T - 2, -1, -1):
-        for s in range(S):
-            terms = [b[t + 1, s]]
-            if s + 1 < S:
-                terms.append(b[t + 1, s + 1])
-            if s + 2 < S and ext[s] != blank and ext[s] != ext[s + 2]:
-                terms.append(b[t + 1, s + 2])
-            b[t, s] = _lse(*terms) + lp[t, ext[s]]
-    ll = _lse(a[T - 1, S - 1], a[T - 1, S - 2]) if S > 1 else a[T - 1, 0]
+        a[0, 1] = emit[0, 1]
+    with np.errstate(invalid="ignore"):
+        for t in range(1, T):
+            prev = a[t - 1]
+            acc = prev.copy()
+            acc[1:] = np.logaddexp(acc[1:], prev[:-1])
+            sk = np.full(S, ninf)
+            sk[2:] = np.where(skip[2:], prev[:-2], ninf)
+            acc = np.logaddexp(acc, sk)
+            a[t] = acc + emit[t]
+        b[T - 1, S - 1] = emit[T - 1, S - 1]
+        if S > 1:
+            b[T - 1, S - 2] = emit[T - 1, S - 2]
+        for t in range(T - 2, -1, -1):
+            nxt = b[t + 1]
+            acc = nxt.copy()
+            acc[:-1] = np.logaddexp(acc[:-1], nxt[1:])
+            sk = np.full(S, ninf)
+            sk[:-2] = np.where(skip_b[:-2], nxt[2:], ninf)
+            acc = np.logaddexp(acc, sk)
+            b[t] = acc + emit[t]
+    ll = np.logaddexp(a[T - 1, S - 1], a[T - 1, S - 2]) if S > 1 else a[T - 1, 0]
     nll = -ll
-    grad = np.exp(lp).copy()
+    grad = np.exp(lp)
     if np.isfinite(nll):
-        for t in range(T):
-            for s in range(S):
-                grad[t, ext[s]] -= np.exp(a[t, s] + b[t, s] - lp[t, ext[s]] + nll)
+        occ = np.exp(a + b - emit + nll)  # [T, S] posterior occupancy of each lattice node
+        for s in range(S):
+            grad[:, ext[s]] -= occ[:, s]
     return nll, grad

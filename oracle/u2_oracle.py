@@ -249,14 +249,16 @@ def noam_lr(step: int, model_dim: int, factor: float = 1.0, warmup: int = 25000)
 
 
 def train_step(params: Params, buffers: dict, batch, cfg, ctc_weight=0.3, smoothing=0.1,
-               clip=5.0, opt_state=None, model_dim=None, chunk=0):
+               clip=5.0, opt_state=None, model_dim=None, chunk=0, training=True):
     """One reference training iteration (accum_grad=1): liteasr/trainer.py:147-171 with
     torch.optim.Adam(betas=(0.9, 0.98), eps=1e-9) under Noam (noam.py:33-39).
+    training=False runs the forward in eval mode (BN running statistics, no dropout but
+    the CTC head's always-on one) and still differentiates it.
     Returns (loss, grads, new_params, opt_state, grad_norm)."""
     xs, xlens, ys, ylens = batch
     names = [k for k in params if params[k].is_floating_point()]
     leaf = {k: params[k].detach().clone().requires_grad_() for k in names}
-    h_attn, h_ctc, _, tgt = u2_forward(xs, xlens, ys, ylens, leaf, cfg, buffers, True, chunk)
+    h_attn, h_ctc, _, tgt = u2_forward(xs, xlens, ys, ylens, leaf, cfg, buffers, training, chunk)
     loss, lc, la = hybrid_loss(h_attn, h_ctc, tgt, ys, xlens, ylens, ctc_weight, smoothing)
     loss.backward()
     grads = {k: (leaf[k].grad if leaf[k].grad is not None else torch.zeros_like(leaf[k])) for k in names}

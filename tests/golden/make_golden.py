@@ -24,6 +24,13 @@ Fixtures
                   the reference's CTC log-probs, _ctc_prefix_beam_search n-best (token
                   sequences + scores), ctc_prefix_beam_search / attention_rescore /
                   attention (beam 10) results (u2.py:163-317)
+  ctc_large.npz   SURVEY §8(c) F-c sizes: HybridCTCLoss(ctc_weight=1) on seeded logits at
+                  (T' 249, B 4, V 4233, L <= 40) and (T' 999, B 2, V 4233, L <= 150): loss,
+                  per-utterance loss, and the logits gradient on the blank + label columns
+                  (+16 random columns) for every frame; the logits are regenerated from
+                  their torch.Generator seed (a checksum is stored to detect drift)
+  host_policies.npz  SeqBatch / FrameBatch grouping of synthetic length lists (incl. the
+                  oversize-utterance edge), Trigger firing sequences, Vocab lookups
   spec_aug.npz    the reference SpecAugment (utils/transform/spec_augment.py) on seeded
                   inputs: global random/numpy seeds per case, input regenerated from its own
                   PCG64 seed, the augmented output, and one random.random() /
@@ -40,6 +47,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import refshim  # noqa: E402
+from inputs import CTC_LARGE_CASES, ctc_large_inputs  # noqa: E402  (shared with the tests)
 
 refshim.install()
 
@@ -134,6 +142,79 @@ def gen_ctc_kl():
     l3 = _crit(V, 0.0)(_FakeModel(h_attn, h_ctc0, V), None, xlens.clone().fill_(210), ys, ylens)
     l3.backward()
     save("kl.npz", ys=ys, ylens=ylens, h_attn=h_attn.detach(), loss=l3.detach(), grad=h_attn.grad)
+
+
+def gen_ctc_large():
+    arrs = {}
+    for name, Tp, B, V, L, seed in CTC_LARGE_CASES:
+        xlens, ys, ylens, h = ctc_large_inputs(Tp, B, V, L, seed)
+        hr = h.clone().requires_grad_()
+        loss = _crit(V, 1.0)(_FakeModel(torch.zeros(B, L + 1, V), hr, V), None, xlens, ys, ylens)
+        loss.backward()
+        per = []
+        for b in range(B):
+            lb = _crit(V, 1.0)(_FakeModel(torch.zeros(1, L + 1, V), h[b:b + 1].clone(), V), None,
+                               xlens[b:b + 1], ys[b:b + 1], ylens[b:b + 1])
+            per.append(float(lb))
+        g = torch.Generator().manual_seed(seed + 1000)
+        lab = sorted(set([0] + [int(v) for v in ys[ys >= 0].tolist()]))
+        extra = torch.randperm(V, generator=g)[:16].tolist()
+        cols = np.array(sorted(set(lab + extra)), dtype=np.int64)
+        arrs[f"{name}_dims"] = np.array([Tp, B, V, L, seed])
+        arrs[f"{name}_xlens"] = xlens
+        arrs[f"{name}_ys"] = ys
+        arrs[f"{name}_ylens"] = ylens
+        arrs[f"{name}_logit_sum"] = h.double().sum()
+        arrs[f"{name}_logit_head"] = h.reshape(-1)[:64]
+        arrs[f"{name}_loss"] = loss.detach()
+        arrs[f"{name}_loss_per_utt"] = np.array(per)
+        arrs[f"{name}_cols"] = cols
+        arrs[f"{name}_grad_cols"] = hr.grad[:, :, cols]
+    save("ctc_large.npz", **arrs)
+
+
+def gen_host_policies():
+    from liteasr.dataclass.vocab import Vocab
+    from liteasr.utils.batchify import FrameBatch, SeqBatch
+    from liteasr.utils.trigger import Trigger
+
+    rng = np.random.default_rng(5)
+    arrs = {}
+    xl = sorted(rng.integers(20, 900, size=40).tolist(), reverse=True)
+    xl[3] = 2000  # alone over the frame budgets below -> the oversize edge
+    xl = sorted(xl, reverse=True)
+    yl = rng.integers(1, 60, size=40).tolist()
+    samples = [types.SimpleNamespace(xlen=int(a), ylen=int(b)) for a, b in zip(xl, yl)]
+    arrs["xlen"], arrs["ylen"] = np.array(xl), np.array(yl)
+    cfgs = [("seq", dict(batch_size=8, min_batch_size=1, max_len_in=400, max_len_out=30)),
+            ("seq", dict(batch_size=5, min_batch_size=2, max_len_in=800, max_len_out=100)),
+            ("seq", dict(batch_size=3, min_batch_size=3, max_len_in=100, max_len_out=10)),
+            ("frame", dict(max_frame_in=1500, max_frame_out=None, max_frame_inout=None)),
+            ("frame", dict(max_frame_in=None, max_frame_out=120, max_frame_inout=None)),
+            ("frame", dict(max_frame_in=3000, max_frame_out=200, max_frame_inout=2600))]
+    for ci, (kind, c) in enumerate(cfgs):
+        pol = (SeqBatch if kind == "seq" else FrameBatch)(types.SimpleNamespace(**c))
+        pol.batchify(list(range(len(samples))), samples)
+        comp = [list(pol[b]) for b in range(len(pol))]
+        arrs[f"c{ci}_sizes"] = np.array([len(b) for b in comp])
+        arrs[f"c{ci}_idx"] = np.array(sum(comp, []))
+    # Trigger: which (counter, unit) pokes fire, for a few interval/unit pairs
+    pokes = [(e, i, u) for e in range(0, 4) for i in range(0, 12) for u in ("iteration", "epoch")]
+    for ti, (interval, unit) in enumerate([(1, "epoch"), (2, "epoch"), (3, "iteration"), (5, "iteration")]):
+        fired = []
+        trig = Trigger(interval, unit)
+        ev = trig(lambda: fired.append(1))
+        for k, (e, i, u) in enumerate(pokes):
+            n0 = len(fired)
+            ev(types.SimpleNamespace(epoch=e, iter=i), u)
+            if len(fired) > n0:
+                fired[-1] = k
+        arrs[f"trig{ti}_fired"] = np.array(fired, dtype=np.int64)
+    arrs["pokes"] = np.array([[e, i, 0 if u == "iteration" else 1] for e, i, u in pokes])
+    v = Vocab(os.path.join(HERE, "loader", "vocab.txt"))
+    arrs["vocab_conv"] = np.array(list(v.lookup(list(range(len(v))), convert=True)))
+    arrs["vocab_tokens"] = np.array(list(v.lookup(list(range(len(v))))))
+    save("host_policies.npz", **arrs)
 
 
 def tiny_cfg(**kw):
@@ -363,12 +444,12 @@ def gen_spec_aug():
     save("spec_aug.npz", **arrs)
 
 
+GENERATORS = dict(relshift=gen_relshift, lengths=gen_lengths, ctc_kl=gen_ctc_kl, u2_step=gen_u2_step,
+                  decode=gen_decode, loader=gen_loader, spec_aug=gen_spec_aug, ctc_large=gen_ctc_large,
+                  host_policies=gen_host_policies)
+
 if __name__ == "__main__":
+    # python tests/golden/make_golden.py [name ...]   (default: all)
     torch.set_num_threads(4)
-    gen_relshift()
-    gen_lengths()
-    gen_ctc_kl()
-    gen_u2_step()
-    gen_decode()
-    gen_loader()
-    gen_spec_aug()
+    for name in sys.argv[1:] or list(GENERATORS):
+        GENERATORS[name]()

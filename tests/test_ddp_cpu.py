@@ -79,6 +79,27 @@ def _worker(rank, world, port, q):
         with ddp.no_sync():
             _FakeBackward.apply(x, model, rank).sum().backward()
         res["grad_nosync"] = model.store.grad.clone()
+        # step 3: record mode (graphed step capture): completed buckets are listed in
+        # backward order instead of launched; launched afterwards they average as usual
+        red = ddp.reducer
+        model.store.grad.zero_()
+        red._reset()
+        red.record = []
+        _FakeBackward.apply(x, model, rank).sum().backward()
+        res["record"] = list(red.record)
+        res["grad_unreduced"] = model.store.grad.clone()
+        for bi in red.record:
+            red.launch(bi)
+        red.record = None
+        red.wait()
+        res["grad_record"] = model.store.grad.clone()
+        # graphed-step cut points: every bucket but the last ends at an encoder position
+        from liteasr_amd.graph_step import GraphedTrainStep
+
+        gs = GraphedTrainStep.__new__(GraphedTrainStep)
+        gs.model, gs.ddp = model, ddp
+        res["cuts"] = gs._cut_points()
+        res["bucket_units"] = red.unit_names()
         res["flat"] = flat0
         # forward-time buffer broadcast (BN running stats from rank 0)
         bn.fill_(float(rank + 20))
@@ -120,4 +141,39 @@ def test_flat_ddp_gloo_world2():
     # no_sync: rank-local values ((r+1) * i)
     assert torch.equal(b["grad_nosync"], 2 * a["grad_nosync"])
     assert a["bn_after_sync"] == b["bn_after_sync"] == 20.0
+    # record mode: every bucket recorded once, in order, nothing reduced until launched
+    assert a["record"] == list(range(a["nbuckets"]))
+    assert torch.equal(b["grad_unreduced"], 2 * a["grad_unreduced"])
+    assert torch.equal(a["grad_record"], a["grad_sync"]) and torch.equal(b["grad_record"], a["grad_sync"])
+    # cut points: one per bucket whose last unit completes before the embed's backward
+    n_layers = 3
+    ends = [u[-1] for u in a["bucket_units"]]
+    expect = set()
+    for e in ends:
+        if e in ("ctc", "decoder", "encoder.after_norm"):
+            expect.add(n_layers)
+        elif e.startswith("encoder.enc_layers."):
+            expect.add(int(e.rsplit(".", 1)[1]))
+    assert a["cuts"] == sorted(expect) and len(a["cuts"]) >= 2, (a["cuts"], ends)
     del st
+
+
+def _spawn_target(rank, world, port, argv):
+    """Stand-in for bench.py's per-rank main: the env bench.spawn_ranks sets, checked
+    through a real gloo rendezvous on 127.0.0.1."""
+    assert os.environ.get("RANK") is None  # the parent's env is clean; the child sets it
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    ok = dist.get_world_size() == world and t.item() == world * (world + 1) / 2 and argv == ["--x", "1"]
+    dist.destroy_process_group()
+    sys.exit(0 if ok else 3)
+
+
+def test_bench_spawns_one_process_per_rank():
+    """bench.py --gpus N (no launcher): N spawned ranks rendezvous as one world of N
+    (liteasr/distributed/utils.py:119-139 call_func -> mp.spawn)."""
+    import bench
+
+    assert bench.spawn_ranks(3, argv=["--x", "1"], target=_spawn_target) == 0

@@ -433,7 +433,8 @@ def test_attn_softmax(relpos):
 
 @pytest.mark.parametrize("B,H,T,masking,dk", [(2, 2, 37, "pad", 64), (3, 4, 130, "pad", 64), (2, 4, 249, "pad", 64),
                                                (2, 2, 100, "chunk", 64), (2, 1, 64, "none", 64), (1, 1, 1, "none", 64),
-                                               (2, 16, 249, "chunk", 32), (3, 3, 70, "pad", 32)])
+                                               (2, 16, 249, "chunk", 32), (3, 3, 70, "pad", 32),
+                                               (2, 4, 999, "pad", 64), (2, 16, 500, "chunk", 32)])
 def test_relattn_fused(B, H, T, masking, dk):
     """attn_fused.hip fwd + bwd vs the literal reference chain (attention.py:120-154) in fp64 on
     the same bf16-rounded operands; one utterance fully masked when masking == "pad"."""
@@ -737,3 +738,88 @@ def test_adam_noam_clip():
     kn.adam_step(p, None, gnan.to(DEV), m, v, ws, nparts, state, 5.0, 1, 0.0, 1.0, 256.0, 25000.0, 0.9, 0.98, 1e-9, 0.0)
     assert state[3].item() == 1.0 and state[0].item() == 3
     assert torch.equal(p, p_before)
+
+
+@pytest.mark.parametrize("max_norm", [0.0, 1.0, float("inf")])
+def test_clip_coef_matches_torch(max_norm):
+    """clip coefficient = min(max_norm / (norm + 1e-6), 1) for any max_norm, exactly as
+    torch.nn.utils.clip_grad_norm_ (the reference's default clip_grad_norm is 0.0,
+    liteasr/config/__init__.py:78, which zeroes the gradient); +inf is 'no clipping'."""
+    kn = K()
+    n = 4096
+    g = torch.randn(n, generator=torch.Generator().manual_seed(3))
+    ref = torch.zeros(n, requires_grad=True)
+    ref.grad = g.clone()
+    torch.nn.utils.clip_grad_norm_([ref], max_norm)
+    coef_ref = (ref.grad.double().norm() / g.double().norm()).item()
+    p = torch.zeros(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    state = torch.zeros(5, device=DEV)
+    nparts = kn.sumsq_nparts(n)
+    ws = torch.empty(nparts, device=DEV)
+    gd = g.to(DEV)
+    kn.sumsq_partial(gd, ws)
+    kn.adam_step(p, None, gd, m, v, ws, nparts, state, max_norm, 0, 1e-3, 1.0, 1.0, 1.0, 0.9, 0.999, 1e-8, 0.0)
+    coef = state[4].item()
+    assert abs(coef - coef_ref) <= 1e-6, (coef, coef_ref)
+    assert state[3].item() == 0.0 and state[0].item() == 1.0
+    # Adam's first moment is (1 - beta1) * coef * g
+    close(m, 0.1 * coef_ref * g.to(DEV), 1e-6, "m after clipped step")
+
+
+@pytest.mark.parametrize("name", ["t249", "t999"])
+def test_ctc_against_reference_golden_full_size(name):
+    """SURVEY §8(c) F-c: the fused log-softmax + CTC alpha/beta kernels at (T' 249, B 4,
+    V 4233, L 40) and (T' 999, B 2, V 4233, L 150) against the reference's HybridCTCLoss
+    (ctc_weight 1) outputs in tests/golden/ctc_large.npz (logits regenerated from their
+    seed).  Per-utterance loss within 1e-5 relative.  Gradient (blank + label + 16 random
+    columns, every frame), measured against the float64 restatement: ours within
+    max(2e-3, 1.5 x the reference's own fp32 error on the same logits) -- the golden is
+    aten's fp32 CTC, 1.4e-3 / 8.1e-3 of max off float64 here (the lattice accumulates
+    hundreds of fp32 log-prob additions) -- and ours vs the golden within the sum of both."""
+    import os
+    import sys
+
+    import numpy as np
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    sys.path.insert(0, root)
+    from inputs import ctc_large_inputs
+
+    from oracle import ctc_ref
+
+    kn = K()
+    d = np.load(os.path.join(root, "tests", "golden", "ctc_large.npz"))
+    Tp, B, V, L, seed = d[f"{name}_dims"].tolist()
+    xlens, ys, ylens, h = ctc_large_inputs(Tp, B, V, L, seed)
+    assert torch.equal(h.reshape(-1)[:64], torch.from_numpy(d[f"{name}_logit_head"]))
+    ilen = ((xlens - 1) // 2 - 1) // 2
+    cols = torch.from_numpy(d[f"{name}_cols"])
+    S = 2 * L + 1
+    dl = h.to(DEV)
+    tg32, il, tl = ys.to(DEV, torch.int32), ilen.to(DEV, torch.int32), ylens.to(DEV, torch.int32)
+    lse = torch.empty(B * Tp, device=DEV)
+    lpb = torch.empty(B * Tp * (L + 1), device=DEV)
+    alpha = torch.empty(B * Tp * S, device=DEV)
+    beta = torch.empty(B * Tp * S, device=DEV)
+    nll = torch.empty(B, device=DEV)
+    kn.ctc_fwd(dl, tg32, il, tl, lse, lpb, alpha, nll, beta=beta)
+    grad = torch.empty(B, Tp, V, device=DEV)
+    kn.ctc_bwd(dl, tg32, il, tl, lse, lpb, alpha, nll, beta, grad, 1.0 / B, beta_ready=True)
+    got = nll.cpu().double().numpy()
+    ref = d[f"{name}_loss_per_utt"]
+    assert np.allclose(got, ref, rtol=1e-5, atol=0), (got, ref)
+    gg = grad.cpu().double()[:, :, cols]
+    g64 = torch.zeros_like(gg)
+    for b in range(B):
+        lp = torch.log_softmax(h[b, : ilen[b]].double(), -1).numpy()
+        _, g = ctc_ref.ctc_nll_and_grad(lp, ys[b, : ylens[b]].numpy())
+        g64[b, : ilen[b]] = torch.from_numpy(g)[:, cols] / B
+    gold = torch.from_numpy(d[f"{name}_grad_cols"]).double()
+    m = g64.abs().max().item()
+    err_ref = (gold - g64).abs().max().item() / m  # the reference's own fp32 error
+    err_ours = (gg - g64).abs().max().item() / m
+    assert err_ours <= max(2e-3, 1.5 * err_ref), (err_ours, err_ref)
+    close(gg, gold, err_ref + err_ours + 1e-6, "ctc grad vs reference golden")

@@ -3,8 +3,13 @@ CPU oracle (oracle/u2_oracle.py, pinned to the reference by test_oracle_golden.p
 
 Tolerances (stated):
   fp32 build  loss rel 1e-5; logits / grads / updated params 2e-4 of each tensor's max-abs
-  bf16 build  loss rel 5e-3; logits 5e-2; grads cosine >= 0.995 and 2.5e-1 of max-abs
-              (a few-row dW such as the decoder FFN's sums ~27 bf16 products)
+  bf16 build  (oracle fed the same bf16-representable weights and features)
+              loss rel 5e-3; logits 2e-2; grads 5e-2 of each tensor's max-abs and cosine
+              >= 0.999, except the ReLU-gated weights (decoder FFN fc1, subsampling convs:
+              a pre-activation within bf16 rounding of 0 takes the other branch than in
+              fp64 and moves a whole output row of a dW summed over few rows -- the
+              decoder's is B*(L+1) ~ 26 rows): 0.35 of max-abs and cosine >= 0.998.
+              Measured worst (tools/bf16_errs.py): non-gated 3.9e-2, gated 0.29.
 Bookkeeping (targets, lengths, masks) is bit-exact (checked in test_kernels_gpu.py)."""
 
 import math
@@ -56,27 +61,31 @@ def cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
-def run_case(cfg_o, B, T, L, dtype, chunk=0, ctc_weight=0.3, seed=0):
+def run_case(cfg_o, B, T, L, dtype, chunk=0, ctc_weight=0.3, seed=0, training=True, round_bf16=False):
     from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
     from liteasr_amd.optims.noam import Noam, NoamConfig
 
     params = O.init_params(cfg_o, seed=seed + 11)
     buffers = O.init_buffers(cfg_o)
     batch = O.synthetic_batch(B, T, L, cfg_o["vocab_size"], seed=seed)
+    if round_bf16:  # both sides see the same bf16-representable weights and features
+        params = {k: (v.bfloat16().float() if v.is_floating_point() else v) for k, v in params.items()}
+        batch = (batch[0].bfloat16().float(),) + tuple(batch[1:])
     # oracle in fp64
     p64 = {k: v.double() for k, v in params.items()}
     b64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in buffers.items()}
     xs, xlens, ys, ylens = batch
     with torch.no_grad():
-        ha_o, hc_o, _, _ = O.u2_forward(xs.double(), xlens, ys, ylens, p64, cfg_o, {k: v.clone() for k, v in b64.items()}, True, chunk)
+        ha_o, hc_o, _, _ = O.u2_forward(xs.double(), xlens, ys, ylens, p64, cfg_o, {k: v.clone() for k, v in b64.items()},
+                                        training, chunk)
     loss_o, grads_o, new_o, _, norm_o = O.train_step(p64, b64, (xs.double(), xlens, ys, ylens), cfg_o,
                                                        ctc_weight=ctc_weight, smoothing=0.1, clip=5.0,
-                                                       model_dim=cfg_o["enc_dim"], chunk=chunk)
+                                                       model_dim=cfg_o["enc_dim"], chunk=chunk, training=training)
     # liteasr_amd on the GPU
     model = build(cfg_o, dtype, chunk)
     missing, unexpected = model.load_state_dict({**params, **buffers}, strict=False)
     assert not unexpected and all(k.endswith(".pe.pe") for k in missing), (missing, unexpected)
-    model = model.cuda().train()
+    model = model.cuda().train(training)
     crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=cfg_o["vocab_size"], smoothing=0.1, ctc_weight=ctc_weight))
     opt = Noam(model.parameters(), NoamConfig(model_dim=cfg_o["enc_dim"]))
     opt.zero_grad()
@@ -142,19 +151,28 @@ def test_parity_fp32(cfg, B, T, L):
             assert int(bufs[k]) == int(v), k
 
 
-@pytest.mark.parametrize("cfg,B,T,L", [(TINY, 3, 130, 8), (SMALL, 2, 210, 12)])
-def test_parity_bf16(cfg, B, T, L):
-    r = run_case(cfg, B, T, L, "bf16")
+def relu_gated(k):
+    return k.startswith("encoder.embed.conv.") or (k.startswith("decoder.") and ".feed_forward.fc1." in k)
+
+
+def _check_bf16(r):
     lg, lo = r["loss"]
     assert abs(lg - lo) <= 5e-3 * abs(lo), r["loss"]
-    assert rel(*r["h_attn"]) < 5e-2
-    assert rel(*r["h_ctc"]) < 5e-2
+    assert rel(*r["h_attn"]) < 2e-2
+    assert rel(*r["h_ctc"]) < 2e-2
     g, go = r["grads"]
     errs, floor = grad_errs(g, go)
     for k in go:
+        gated = relu_gated(k)
         if go[k].abs().max().item() > floor:
-            assert cos(g[k], go[k]) > 0.995, (k, cos(g[k], go[k]))
-        assert errs[k] < 2.5e-1, (k, errs[k])
+            c = cos(g[k], go[k])
+            assert c >= (0.998 if gated else 0.999), (k, c)
+        assert errs[k] < (0.35 if gated else 5e-2), (k, errs[k])
+
+
+@pytest.mark.parametrize("cfg,B,T,L", [(TINY, 3, 130, 8), (SMALL, 2, 210, 12)])
+def test_parity_bf16(cfg, B, T, L):
+    _check_bf16(run_case(cfg, B, T, L, "bf16", round_bf16=True))
 
 
 # d_k 32 with the streaming chunk mask (config 4's attention shape) through the fused kernels
@@ -163,16 +181,44 @@ LARGE_HEADS = O.default_cfg(enc_dim=128, enc_heads=4, enc_ff=256, enc_layers=2, 
 
 
 def test_parity_bf16_dk32_chunk_mask():
-    r = run_case(LARGE_HEADS, 2, 150, 6, "bf16", chunk=8)
+    _check_bf16(run_case(LARGE_HEADS, 2, 150, 6, "bf16", chunk=8, round_bf16=True))
+
+
+# config 4's layer shape at model level: d 512, 16 heads (d_k 32), ff 2048, V 4233, chunk 16
+LARGE = O.default_cfg(enc_dim=512, enc_heads=16, enc_ff=2048, enc_layers=2, dec_dim=512, dec_heads=16, dec_ff=2048,
+                      dec_layers=1, vocab_size=4233)
+# full depth (12 encoder / 6 decoder layers) at reduced width
+DEEP = O.default_cfg(enc_dim=128, enc_heads=4, enc_ff=256, enc_layers=12, dec_dim=128, dec_heads=4, dec_ff=256,
+                     dec_layers=6, vocab_size=64)
+
+
+def _check_fp32(r, tol):
     lg, lo = r["loss"]
-    assert abs(lg - lo) <= 5e-3 * abs(lo), r["loss"]
-    assert rel(*r["h_ctc"]) < 5e-2
+    assert abs(lg - lo) <= 1e-5 * abs(lo), r["loss"]
+    assert rel(*r["h_attn"]) < tol and rel(*r["h_ctc"]) < tol
     g, go = r["grads"]
-    errs, floor = grad_errs(g, go)
-    for k in go:
-        if go[k].abs().max().item() > floor:
-            assert cos(g[k], go[k]) > 0.995, (k, cos(g[k], go[k]))
-        assert errs[k] < 2.5e-1, (k, errs[k])
+    errs, _ = grad_errs(g, go)
+    kink = {k for k in errs if k.startswith("encoder.embed.conv.")}  # see test_parity_fp32
+    worst = max((v, k) for k, v in errs.items() if k not in kink)
+    assert worst[0] < tol, worst
+    assert max(errs[k] for k in kink) < 2e-2, {k: errs[k] for k in kink}
+
+
+def test_parity_large_width_chunk_fp32():
+    """d 512 / 16 heads / ff 2048 / V 4233 with the streaming chunk mask (stage 16), fp32
+    build vs the fp64 oracle.  5e-4: chunk-masked rows carry more cancellation (see
+    test_parity_chunk_mask_fp32)."""
+    _check_fp32(run_case(LARGE, 2, 200, 10, "fp32", chunk=16), 5e-4)
+
+
+def test_parity_large_width_chunk_bf16():
+    """Config 4's shape (d 512, 16 heads, chunk 16) in the bf16 build (fused d_k 32 attention)."""
+    _check_bf16(run_case(LARGE, 2, 200, 10, "bf16", chunk=16, round_bf16=True))
+
+
+def test_parity_full_depth_fp32():
+    """All 12 encoder / 6 decoder layers (reduced width), B 2, T 400, fp32 build vs fp64."""
+    _check_fp32(run_case(DEEP, 2, 400, 12, "fp32"), 2e-4)
 
 
 def test_parity_chunk_mask_fp32():
@@ -198,6 +244,24 @@ def test_parity_ctc_only_fp32():
             assert g[k].abs().max().item() == 0.0, k  # decoder gets exactly zero gradient
         else:
             assert errs[k] < 2e-4, (k, errs[k])
+
+
+def test_parity_eval_mode_grads_fp32():
+    """Eval mode with gradients (BatchNorm on its running statistics: the batch-mean terms
+    of the BN gradient vanish; dropout off except the CTC head's always-on one, 0 here)
+    against the fp64 oracle differentiated in eval mode; BN buffers stay untouched."""
+    r = run_case(TINY, 3, 130, 8, "fp32", training=False)
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 1e-5 * abs(lo), r["loss"]
+    g, go = r["grads"]
+    errs, _ = grad_errs(g, go)
+    kink = {k for k in errs if k.startswith("encoder.embed.conv.")}  # see test_parity_fp32
+    worst = max((v, k) for k, v in errs.items() if k not in kink)
+    assert worst[0] < 2e-4, worst
+    bufs, bo = r["bn"]
+    for k, v in bo.items():
+        if v.is_floating_point():
+            assert torch.equal(bufs[k].double().cpu(), v), k
 
 
 def test_eval_forward_uses_running_stats():
@@ -300,9 +364,11 @@ def test_graphed_step_matches_eager():
         o1.zero_grad()
         eager.append(l.item())
     m2, c2, o2 = _graph_setup(0.1)
-    gs = GraphedTrainStep(m2, c2, o2, batches[0], clip=5.0, warmup=1)  # warm-up = eager step 1
-    graphed = [gs(b).item() for b in batches[1:]]
-    assert graphed == eager[1:], (graphed, eager)
+    # construction runs a warm-up step and then restores parameters, optimizer state, BN
+    # buffers and the dropout counter: the replays start from the initial state
+    gs = GraphedTrainStep(m2, c2, o2, batches[0], clip=5.0, warmup=2)
+    graphed = [gs(b).item() for b in batches]
+    assert graphed == eager, (graphed, eager)
     assert torch.equal(m1.store.flat, m2.store.flat)
     assert o1.device_state() == o2.device_state()
 
@@ -318,9 +384,9 @@ def _ddp_graph_worker(rank, world, port, q):
         from liteasr_amd.graph_step import GraphedTrainStep
 
         out = {}
-        for mode in ("eager", "graph"):
+        for mode in ("eager", "graph_overlap", "graph_split"):
             m, c, o = _graph_setup(0.0)
-            net = DistributedDataParallel(m)
+            net = DistributedDataParallel(m, bucket_cap_mb=0.05)  # several buckets -> several segments
             bs = [[t.cuda() for t in O.synthetic_batch(2, 100, 5, 30, seed=50 + 7 * rank + i)] for i in range(3)]
             losses = []
             if mode == "eager":
@@ -331,37 +397,140 @@ def _ddp_graph_worker(rank, world, port, q):
                     o.zero_grad()
                     losses.append(l.item())
             else:
-                gs = GraphedTrainStep(net, c, o, bs[0], clip=5.0, warmup=1)
-                losses = [float("nan")] + [gs(b).item() for b in bs[1:]]
+                gs = GraphedTrainStep(net, c, o, bs[0], clip=5.0, warmup=1, overlap=mode == "graph_overlap")
+                if mode == "graph_overlap":
+                    assert len(gs.segs) == len(gs.cuts) + 1 >= 3, (gs.cuts, len(net.reducer.buckets))
+                losses = [gs(b).item() for b in bs]
             out[mode] = (losses, m.store.flat.double().cpu())
         le, fe = out["eager"]
-        lg, fg = out["graph"]
-        ok = max(abs(a - b) / abs(a) for a, b in zip(le[1:], lg[1:])) < 1e-5 and \
-            (fe - fg).abs().max().item() <= 1e-6 * fe.abs().max().item()
-        q.put((rank, ok, le, lg))
+        ok = True
+        for mode in ("graph_overlap", "graph_split"):
+            lg, fg = out[mode]
+            ok = ok and max(abs(a - b) / abs(a) for a, b in zip(le, lg)) < 1e-5 and \
+                (fe - fg).abs().max().item() <= 1e-6 * fe.abs().max().item()
+        q.put((rank, ok, le, [out[k][0] for k in ("graph_overlap", "graph_split")]))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, False, repr(e), None))
 
 
-def test_graphed_step_ddp_two_ranks_gloo():
-    """Split-graph DDP step (graph 1 fwd/bwd, eager bucketed all-reduce, graph 2 update) vs
-    the eager DDP step with hook-driven bucket all-reduce: 2 ranks sharing the one GPU,
-    gloo backend (RCCL cannot put two ranks on one device)."""
+def _two_ranks(worker):
     import multiprocessing as mp
     import random
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    ps = [ctx.Process(target=_ddp_graph_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in ps]
     for p in ps:
         p.join(timeout=60)
-    for rank, ok, le, lg in res:
+    return res
+
+
+def test_graphed_step_ddp_two_ranks_gloo():
+    """Graphed DDP steps vs the eager DDP step with hook-driven bucket all-reduce, 2 ranks
+    sharing the one GPU, gloo backend (RCCL cannot put two ranks on one device):
+    'graph_overlap' = backward segments as separate graphs with each bucket's all-reduce
+    launched between them (the bench path), 'graph_split' = one fwd/bwd graph, all
+    buckets, update graph."""
+    for rank, ok, le, lg in _two_ranks(_ddp_graph_worker):
         assert ok, (rank, le, lg)
+
+
+class _GradTap:
+    """Optimizer stand-in for GraphedTrainStep: 'step' copies the (all-reduced) flat
+    gradient out, zero_grad clears it -- both plain stream-ordered copies, capturable."""
+
+    def __init__(self, store):
+        self.store = store
+        self.out = torch.zeros_like(store.ensure_grad())
+
+    def clip_and_step(self, clip):
+        self.out.copy_(self.store.grad)
+
+    def zero_grad(self):
+        self.store.grad.zero_()
+
+
+DDP_CFG = O.default_cfg(enc_dim=64, enc_heads=4, enc_ff=256, enc_layers=3, dec_dim=64, dec_heads=4, dec_ff=256,
+                        dec_layers=2, vocab_size=40)
+
+
+def _ddp_equiv_worker(rank, world, port, q):
+    """the N-rank averaged gradient equals the single-process gradient on
+    the concatenated batch.  BN in eval mode (running statistics), so per-rank batch
+    statistics do not enter; dropout 0; fp32 build."""
+    try:
+        import torch.distributed as dist
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+        from liteasr_amd.distributed.ddp import DistributedDataParallel
+        from liteasr_amd.graph_step import GraphedTrainStep
+
+        cfg = DDP_CFG
+        params = O.init_params(cfg, seed=17)
+        buffers = O.init_buffers(cfg)
+        for k in buffers:  # non-trivial running statistics
+            if k.endswith("running_mean"):
+                buffers[k] = torch.randn(cfg["enc_dim"], generator=torch.Generator().manual_seed(1)) * 0.1
+            elif k.endswith("running_var"):
+                buffers[k] = torch.rand(cfg["enc_dim"], generator=torch.Generator().manual_seed(2)) + 0.5
+        Bfull = 4
+        full = [t.cuda() for t in O.synthetic_batch(Bfull, 180, 9, cfg["vocab_size"], seed=23)]
+        half = [t[rank * Bfull // world:(rank + 1) * Bfull // world].contiguous() for t in full]
+        crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=cfg["vocab_size"], smoothing=0.1, ctc_weight=0.3))
+
+        def fresh():
+            m = build(cfg, "fp32")
+            m.load_state_dict({**params, **buffers}, strict=False)
+            return m.cuda().eval()
+
+        # (1) single process, concatenated batch
+        m1 = fresh()
+        crit(m1, *full).backward()
+        g_single = m1.store.grad.double().cpu()
+        # (2) eager DDP, hook-driven bucket all-reduce (mean) overlapped with the backward
+        m2 = fresh()
+        net2 = DistributedDataParallel(m2, bucket_cap_mb=0.2)
+        crit(net2, *half).backward()
+        g_ddp = m2.store.grad.double().cpu()
+        # (3) the graphed, segmented DDP step (bench path): all-reduce between backward segments
+        m3 = fresh()
+        net3 = DistributedDataParallel(m3, bucket_cap_mb=0.2)
+        tap = _GradTap(m3.store)
+        gs = GraphedTrainStep(net3, crit, tap, half, warmup=1)
+        gs(half)
+        torch.cuda.synchronize()
+        g_graph = tap.out.double().cpu()
+        scale = g_single.abs().max().item()
+        err_ddp = (g_ddp - g_single).abs().max().item() / scale
+        # per-parameter, relative to each tensor's own max (floored at 1e-3 of the largest)
+        worst = 0.0
+        for n in m1.store.names:
+            o, k = m1.store.offsets[n], m1.store.shapes[n].numel()
+            a, b = g_ddp[o:o + k], g_single[o:o + k]
+            worst = max(worst, (a - b).abs().max().item() / max(b.abs().max().item(), 1e-3 * scale))
+        graph_eq = torch.equal(g_graph, g_ddp)
+        q.put((rank, err_ddp < 2e-4 and worst < 2e-4 and graph_eq, (err_ddp, worst, graph_eq, len(gs.segs)), None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, False, repr(e), traceback.format_exc()))
+
+
+def test_ddp_grads_equal_single_process_concatenated_batch():
+    """SURVEY §8(e) / trainer.py:142-171: world-2 averaged gradients (eager hook path and
+    the segmented graphed path) == one process on the concatenated batch, within 2e-4 of
+    each tensor's max; the graphed path bit-equal to the eager DDP path."""
+    for rank, ok, info, tb in _two_ranks(_ddp_equiv_worker):
+        assert ok, (rank, info, tb)
 
 
 @pytest.mark.gpu
