@@ -30,7 +30,8 @@ extern "C" {
 
 enum { LASR_F32 = 0, LASR_BF16 = 1, LASR_I32 = 2, LASR_I64 = 3, LASR_U8 = 4 };
 enum { LASR_OK = 0, LASR_ERR_INVALID = -1, LASR_ERR_LAUNCH = -2 };
-enum { LASR_ACT_NONE = 0, LASR_ACT_RELU = 1, LASR_ACT_SWISH = 2 };
+enum { LASR_ACT_NONE = 0, LASR_ACT_RELU = 1, LASR_ACT_SWISH = 2,
+       LASR_ACT_GATE = 3 /* aux_act only: multiply by the aux value itself */ };
 
 const char* lasr_last_error(void);
 int lasr_version(void);
@@ -72,8 +73,10 @@ typedef struct lasr_gemm_args {
   float beta;
   const float* bias;
   int act;
-  void* zout;  /* pre-activation copy (c_dtype, ld = ldc), optional */
-  const void* aux; int aux_dtype; int64_t ldaux; int aux_act;
+  void* zout;  /* optional (c_dtype, ld = ldc): zout_mode 0 the pre-activation copy, 1 the
+               * gate act'(pre-activation) * keep (keep = the epilogue's dropout keep flag,
+               * 0/1), which a later GEMM applies as aux with aux_act = LASR_ACT_GATE */
+  const void* aux; int aux_dtype; int64_t ldaux; int aux_act;  /* v *= aux_act'(aux) */
   float drop_p; uint64_t drop_seed;
   const void* res; int res_dtype; int64_t ldres; float res_scale;
   int split_k;  /* 1: none, > 1: forced, 0: auto (fills the chip; needs workspace), -1: auto,
@@ -83,8 +86,13 @@ typedef struct lasr_gemm_args {
    * M-contiguous i.e. lda_m == 1: the dW = dY^T X GEMMs, rowsum = dbias).  Replaces the
    * separate column sum of dY (aten sum over rows in Linear's backward). */
   float* rowsum;
+  int zout_mode;
 } lasr_gemm_args;
 int lasr_gemm(const lasr_gemm_args* args, void* stream);
+/* Dropout: one 32-bit counter-hash draw per element pair, 16-bit halves against
+ * thr = round(p * 65536); kept values scale by lasr_dropout_scale(p) = 65536 / (65536 - thr)
+ * (E[mask * scale] = 1 exactly).  Host helper, no device work. */
+float lasr_dropout_scale(float p);
 /* Tile and split-K lasr_gemm would use; flags (nullable): LASR_PLAN_GLDS (LDS-DMA
  * kernel), LASR_PLAN_ROWSUM_FUSED (rowsum computed in the GEMM; with split_k = -1 and a
  * split > 1 its [split][M] partials follow the [split][batch][M][N] C partials in the
@@ -98,6 +106,33 @@ int lasr_gemm_force_tile(int tile_m, int tile_n);
 /* Tuning hook: force the split-K factor of auto-split calls and the LDS ring depth (3..6)
  * of split-K LDS-DMA launches; (0, 0) restores the planner.  Benchmarks only. */
 int lasr_gemm_force_split(int split_k, int stages);
+
+/* ---- fused position-wise feed-forward chains (liteasr/nets/feed_forward.py:18-19 in the
+ * Conformer residual branches, conformer_layer.py:37-47,58-66) --------------------------
+ * fwd:    u = x W1^T + b1 ; z = act'(u) * keep1 (the gate) ; h = drop1(act(u)) ;
+ *         out = res + res_scale * drop2(h W2^T + b2)
+ *         x = LN output [M, D] bf16, z / h [M, F] bf16 (kept for the backward; F <= 2048),
+ *         out [M, D] fp32 (res nullable: out = res_scale * ...).
+ * bwd_dx: dz = (x W2) * z * scale1 ; dx = dz W1
+ *         x = gb, the gradient of the FFN output [M, D] bf16; z = the forward's gate [M, F]
+ *         bf16 in; dz [M, F] bf16 and dx [M, D] bf16 out.
+ * W1 [F, D], W2 [D, F] bf16 (working copies), b1 [F], b2 [D] fp32; D in {256, 512},
+ * F % 128 == 0, every pointer 16-B aligned, rows dense.  act: LASR_ACT_SWISH / _RELU.
+ * Dropout masks: same (seed, step counter, element index) function as lasr_gemm's
+ * epilogue (index m*F + f for drop1, m*D + n for drop2). */
+typedef struct lasr_ffn_args {
+  int M, D, F, act;
+  const void* x;
+  const void* W1; const float* b1;
+  const void* W2; const float* b2;
+  float p1; uint64_t seed1;
+  float p2; uint64_t seed2;
+  const float* res; float res_scale;
+  void* z; void* h; float* out;
+  void* dz; void* dx;
+} lasr_ffn_args;
+int lasr_ffn_fwd(const lasr_ffn_args* args, void* stream);
+int lasr_ffn_bwd_dx(const lasr_ffn_args* args, void* stream);
 
 /* Batched partial reductions (one launch for a backward node's deferred parameter
  * gradients): out[n] (+)= sum_p part[p*N + n], n < split -> out0[n], else out1[n-split].

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get(
 )
 
 F32, BF16, I32, I64, U8 = 0, 1, 2, 3, 4
-ACT_NONE, ACT_RELU, ACT_SWISH = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_SWISH, ACT_GATE = 0, 1, 2, 3
 
 _p = C.c_void_p
 _i = C.c_int
@@ -44,6 +44,23 @@ class GemmArgs(C.Structure):
         ("res", _p), ("res_dtype", _i), ("ldres", _l), ("res_scale", _f),
         ("split_k", _i), ("workspace", _p), ("workspace_bytes", _l),
         ("rowsum", _p),
+        ("zout_mode", _i),
+    ]
+
+
+class FfnArgs(C.Structure):
+    """Mirror of ``lasr_ffn_args``."""
+
+    _fields_ = [
+        ("M", _i), ("D", _i), ("F", _i), ("act", _i),
+        ("x", _p),
+        ("W1", _p), ("b1", _p),
+        ("W2", _p), ("b2", _p),
+        ("p1", _f), ("seed1", _u),
+        ("p2", _f), ("seed2", _u),
+        ("res", _p), ("res_scale", _f),
+        ("z", _p), ("h", _p), ("out", _p),
+        ("dz", _p), ("dx", _p),
     ]
 
 
@@ -68,6 +85,9 @@ SIGNATURES = {
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
                          _p, _p, _p, _i, _i, _p, _p, _l, _p],
     "lasr_reduce_multi": [C.POINTER(ReduceSeg), _i, _p],
+    "lasr_dropout_scale": [_f],
+    "lasr_ffn_fwd": [C.POINTER(FfnArgs), _p],
+    "lasr_ffn_bwd_dx": [C.POINTER(FfnArgs), _p],
     "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
     "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],
     "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,
@@ -110,7 +130,8 @@ SIGNATURES = {
     "lasr_spec_augment_ws_bytes": [_i, _i],
     "lasr_logsoftmax_topk": [_p, _i, _l, _i, _l, _i, _p, _p, _p, _p, _p],
 }
-_RESTYPES = {"lasr_last_error": C.c_char_p, "lasr_spec_augment_ws_bytes": C.c_int64}
+_RESTYPES = {"lasr_last_error": C.c_char_p, "lasr_spec_augment_ws_bytes": C.c_int64,
+             "lasr_dropout_scale": C.c_float}
 
 
 class NativeError(RuntimeError):

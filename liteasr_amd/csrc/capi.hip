@@ -37,3 +37,7 @@ extern "C" int lasr_counter_add(uint64_t* dev_counter, uint64_t v, void* stream)
   counter_add_kernel<<<1, 1, 0, (hipStream_t)stream>>>(dev_counter, v);
   return lasr_check_launch("counter_add");
 }
+
+// Multiplier of kept elements for drop probability p (common.h mkdrop): callers that apply a
+// stored keep mask (the GEMM gate, aux_act = LASR_ACT_GATE) scale by this.
+extern "C" float lasr_dropout_scale(float p) { return mkdrop(p, 0).scale; }

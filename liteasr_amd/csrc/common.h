@@ -141,10 +141,15 @@ LASR_DEV float block_max(float v, float* red) {
 }
 
 // ---- counter-based dropout RNG -----------------------------------------------
-// keep(seed, idx) is a pure function of (seed, logical element index), so the
-// backward pass regenerates the forward mask instead of storing it.
+// keep(seed, idx) is a pure function of (seed, device step counter, logical element
+// index), so the backward pass regenerates the forward mask instead of storing it.
+// One 32-bit draw serves a PAIR of elements (2k, 2k+1: its low / high 16 bits); element
+// idx is kept iff its 16-bit half >= thr = round(p * 65536), and kept values are scaled
+// by 65536 / (65536 - thr), so E[mask * scale] = 1 exactly (p is realised to 2^-16).
 struct DropCfg {
   float p;              // drop probability (0 = off)
+  uint32_t thr;         // 16-bit keep threshold
+  float scale;          // multiplier of kept elements
   uint64_t seed;        // per-site seed (host)
   const uint64_t* ctr;  // optional device step counter (read at run time, graph-safe)
 };
@@ -155,9 +160,16 @@ static inline DropCfg mkdrop(float p, uint64_t seed) {
   d.p = p;
   d.seed = seed;
   d.ctr = p > 0.f ? lasr_dropout_counter() : nullptr;
+  uint32_t thr = 0;
+  if (p > 0.f) {
+    const float t = p * 65536.f + 0.5f;
+    thr = t >= 65536.f ? 65536u : (uint32_t)t;
+  }
+  d.thr = thr;
+  d.scale = thr >= 65536u ? 0.f : 65536.f / (float)(65536u - thr);
   return d;
 }
-// 32-bit finaliser (lowbias32: 2 multiplies, 3 xor-shifts) for the per-element draws.
+// 32-bit finaliser (lowbias32: 2 multiplies, 3 xor-shifts).
 LASR_DEV uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -171,12 +183,59 @@ LASR_DEV uint32_t drop_key(const DropCfg& d) {
   const uint64_t s = d.seed + (d.ctr ? d.ctr[0] * 0xD1B54A32D192ED03ull : 0ull);
   return mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + 0x9E3779B9u));
 }
-// Multiplier of element idx (0 or 1/(1-p)): draw = mix32(idx * golden ^ key ^ hi-word
-// term); the site's mask is a pure function of (seed, step counter, idx).
+// The draw of element pair k (elements 2k and 2k+1).
+LASR_DEV uint32_t drop_bits(uint32_t key, uint64_t pair) {
+  const uint32_t hi = (uint32_t)(pair >> 32);
+  return mix32((uint32_t)pair ^ key ^ ((hi << 16) | (hi >> 16)));
+}
+// 1 (kept) or 0 for element idx.
+LASR_DEV float drop_keep_k(const DropCfg& d, uint32_t key, uint64_t idx) {
+  const uint32_t b = drop_bits(key, idx >> 1);
+  const uint32_t h = (idx & 1) ? (b >> 16) : (b & 0xFFFFu);
+  return h >= d.thr ? 1.f : 0.f;
+}
+// Multiplier of element idx (0 or scale).
 LASR_DEV float drop_mul_k(const DropCfg& d, uint32_t key, uint64_t idx) {
-  const uint32_t thr = (uint32_t)fminf(d.p * 4294967296.0f, 4294967295.0f);
-  const uint32_t x = ((uint32_t)idx * 0x9E3779B1u) ^ key ^ ((uint32_t)(idx >> 32) * 0x85EBCA77u);
-  return mix32(x) >= thr ? 1.f / (1.f - d.p) : 0.f;
+  return drop_keep_k(d, key, idx) * d.scale;
+}
+// Keep flags (1 / 0) of the N consecutive elements idx0 .. idx0+N-1, one draw per pair
+// when idx0 is even (the vector epilogues' case).
+template <int N>
+LASR_DEV void drop_keep_n(const DropCfg& d, uint32_t key, uint64_t idx0, float* k) {
+  if (idx0 & 1) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) k[q] = drop_keep_k(d, key, idx0 + q);
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < N; q += 2) {
+    const uint32_t b = drop_bits(key, (idx0 >> 1) + (q >> 1));
+    k[q] = (b & 0xFFFFu) >= d.thr ? 1.f : 0.f;
+    if (q + 1 < N) k[q + 1] = (b >> 16) >= d.thr ? 1.f : 0.f;
+  }
+}
+// The same keep flags as a bit mask (bit q = element idx0 + q), N <= 32.
+template <int N>
+LASR_DEV uint32_t drop_keep_mask(const DropCfg& d, uint32_t key, uint64_t idx0) {
+  uint32_t km = 0u;
+  if (idx0 & 1) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) km |= (drop_keep_k(d, key, idx0 + q) != 0.f ? 1u : 0u) << q;
+    return km;
+  }
+#pragma unroll
+  for (int q = 0; q < N; q += 2) {
+    const uint32_t b = drop_bits(key, (idx0 >> 1) + (q >> 1));
+    km |= ((b & 0xFFFFu) >= d.thr ? 1u : 0u) << q;
+    if (q + 1 < N) km |= ((b >> 16) >= d.thr ? 1u : 0u) << (q + 1);
+  }
+  return km;
+}
+template <int N>
+LASR_DEV void drop_mul_n(const DropCfg& d, uint32_t key, uint64_t idx0, float* m) {
+  drop_keep_n<N>(d, key, idx0, m);
+#pragma unroll
+  for (int q = 0; q < N; ++q) m[q] *= d.scale;
 }
 // Multiplier for element idx; 1 when dropout is off.
 LASR_DEV float drop_mul(const DropCfg& d, uint64_t idx) {

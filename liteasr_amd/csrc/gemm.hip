@@ -15,6 +15,7 @@
 // attention.py:35-37,58,69,145,149, subsampling.py:34,47, conformer_convolution.py:48,55,
 // ctc.py:29, transformer_decoder.py:91 (and their autograd backward GEMMs).
 #include "common.h"
+#include "tile.h"
 
 #include <type_traits>
 
@@ -24,8 +25,6 @@
 #define LASR_EXP 0
 #endif
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct GemmP {
   int M, N, K, batch, batch_div;
@@ -65,10 +64,72 @@ struct GemmP {
   float* rowsum;
   float* rs_ws;
   int v4;  // direct epilogue: 4-wide C/zout/aux/res/bias/ws access allowed (host-checked)
+  int zout_mode;  // 0: zout = pre-activation; 1: zout = act'(pre-activation) * keep (gate)
 };
 
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
   return dt == LASR_F32 ? ((const float*)p)[i] : bf2f(((const bf16_t*)p)[i]);
+}
+
+// Epilogue core on N consecutive columns after bias: zout (pre-activation or gate),
+// activation, aux factor, dropout (one draw per column pair), residual.  zst(vals) stores
+// the zout values; auxv / resv are the loaded aux / res values (nullable).  Every mode
+// switch is a wave-uniform branch around its own loop (a per-element select would make
+// the compiler evaluate every activation and its derivative for every element).
+template <int N, typename ZST>
+LASR_DEV void epi_core(const GemmP& p, uint64_t dbase, float (&v)[N], const float (&auxv)[N], bool has_aux,
+                       const float (&resv)[N], bool has_res, ZST zst) {
+  const bool drop = p.drop.p > 0.f;
+  const uint32_t km = drop ? drop_keep_mask<N>(p.drop, drop_key(p.drop), dbase) : 0u;
+  if (p.zout) {
+    if (p.zout_mode == 1) {
+      float g[N];
+      if (p.act == LASR_ACT_SWISH) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) g[q] = swish_grad(v[q]);
+      } else if (p.act == LASR_ACT_RELU) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) g[q] = v[q] > 0.f ? 1.f : 0.f;
+      } else {
+#pragma unroll
+        for (int q = 0; q < N; ++q) g[q] = 1.f;
+      }
+      if (drop) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) g[q] *= (km >> q) & 1u ? 1.f : 0.f;
+      }
+      zst(g);
+    } else {
+      zst(v);
+    }
+  }
+  if (p.act == LASR_ACT_SWISH) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = swishf(v[q]);
+  } else if (p.act == LASR_ACT_RELU) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = fmaxf(v[q], 0.f);
+  }
+  if (has_aux) {
+    if (p.aux_act == LASR_ACT_GATE) {
+#pragma unroll
+      for (int q = 0; q < N; ++q) v[q] *= auxv[q];
+    } else if (p.aux_act == LASR_ACT_RELU) {
+#pragma unroll
+      for (int q = 0; q < N; ++q) v[q] *= auxv[q] > 0.f ? 1.f : 0.f;
+    } else {
+#pragma unroll
+      for (int q = 0; q < N; ++q) v[q] *= swish_grad(auxv[q]);
+    }
+  }
+  if (drop) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] *= (km >> q) & 1u ? p.drop.scale : 0.f;  // x * 0 keeps NaN, as torch
+  }
+  if (has_res) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = resv[q] + p.res_scale * v[q];
+  }
 }
 
 // Full epilogue for one output element.
@@ -76,21 +137,17 @@ template <typename TC>
 LASR_DEV void epi_store(const GemmP& p, int z1, int z2, int z, int m, int n, float acc,
                         float alpha_eff) {
   if (m >= p.M || n >= p.N) return;
-  float v = acc * alpha_eff;
-  if (p.bias) v += p.bias[n];
+  float v[1] = {acc * alpha_eff};
+  if (p.bias) v[0] += p.bias[n];
   const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
-  if (p.zout) ((TC*)p.zout)[cidx] = from_f<TC>(v);
-  if (p.act == LASR_ACT_RELU) v = fmaxf(v, 0.f);
-  else if (p.act == LASR_ACT_SWISH) v = swishf(v);
-  if (p.aux) {
-    const float a = load_any(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n);
-    v *= (p.aux_act == LASR_ACT_RELU) ? (a > 0.f ? 1.f : 0.f) : swish_grad(a);
-  }
-  if (p.drop.p > 0.f) v *= drop_mul(p.drop, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n);
-  if (p.res) v = load_any(p.res, p.res_dtype, (int64_t)m * p.ldres + n) + p.res_scale * v;
+  float a[1], r[1];
+  if (p.aux) a[0] = load_any(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n);
+  if (p.res) r[0] = load_any(p.res, p.res_dtype, (int64_t)m * p.ldres + n);
+  epi_core<1>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, a, p.aux != nullptr, r, p.res != nullptr,
+              [&](const float (&zv)[1]) { ((TC*)p.zout)[cidx] = from_f<TC>(zv[0]); });
   TC* C = (TC*)p.C;
-  if (p.beta != 0.f) v += p.beta * to_f(C[cidx]);
-  C[cidx] = from_f<TC>(v);
+  if (p.beta != 0.f) v[0] += p.beta * to_f(C[cidx]);
+  C[cidx] = from_f<TC>(v[0]);
 }
 
 // 8 values of a (f32|bf16) matrix row starting at element idx; cnt < 8 -> tail.
@@ -127,31 +184,11 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
     for (int q = 0; q < 8; ++q) v[q] += q < cnt ? p.bias[n + q] : 0.f;
   }
   const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
-  if (p.zout) st_8((TC*)p.zout + cidx, v, p.c_vec, cnt);
-  if (p.act == LASR_ACT_RELU) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-  } else if (p.act == LASR_ACT_SWISH) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = swishf(v[q]);
-  }
-  if (p.aux) {
-    ld_any8(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, p.aux_vec, cnt, t);
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      v[q] *= (p.aux_act == LASR_ACT_RELU) ? (t[q] > 0.f ? 1.f : 0.f) : swish_grad(t[q]);
-  }
-  if (p.drop.p > 0.f) {
-    const uint64_t base = ((uint64_t)z * p.M + m) * (uint64_t)p.N + n;
-    const uint32_t key = drop_key(p.drop);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] *= drop_mul_k(p.drop, key, base + q);
-  }
-  if (p.res) {
-    ld_any8(p.res, p.res_dtype, (int64_t)m * p.ldres + n, p.res_vec, cnt, t);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = t[q] + p.res_scale * v[q];
-  }
+  float r[8];
+  if (p.aux) ld_any8(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, p.aux_vec, cnt, t);
+  if (p.res) ld_any8(p.res, p.res_dtype, (int64_t)m * p.ldres + n, p.res_vec, cnt, r);
+  epi_core<8>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
+              [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, p.c_vec, cnt); });
   TC* C = (TC*)p.C + cidx;
   if (p.beta != 0.f) {
     ld_any8(C, sizeof(TC) == 4 ? LASR_F32 : LASR_BF16, 0, p.c_vec, cnt, t);
@@ -165,34 +202,13 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
 // (sv, mode 1 only; N % 8 == 0 there), beta == 0; cnt < 8 only on a ragged last vector.
 template <typename TC>
 LASR_DEV void epi_fast8(const GemmP& p, int z1, int z2, int z, int m, int n, int cnt,
-                        const float* acc, float alpha_eff, const float* bv, const float* sv) {
+                        const float* acc, float alpha_eff, const float* bv, const float (&sv)[8]) {
   float v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff + bv[q];
   const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
-  if (p.zout) st_8((TC*)p.zout + cidx, v, true, cnt);
-  if (p.act == LASR_ACT_RELU) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-  } else if (p.act == LASR_ACT_SWISH) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = swishf(v[q]);
-  }
-  if (p.aux) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      v[q] *= (p.aux_act == LASR_ACT_RELU) ? (sv[q] > 0.f ? 1.f : 0.f) : swish_grad(sv[q]);
-  }
-  if (p.drop.p > 0.f) {
-    const uint64_t base = ((uint64_t)z * p.M + m) * (uint64_t)p.N + n;
-    const uint32_t key = drop_key(p.drop);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] *= drop_mul_k(p.drop, key, base + q);
-  }
-  if (p.res) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = sv[q] + p.res_scale * v[q];
-  }
+  epi_core<8>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, sv, p.aux != nullptr, sv, p.res != nullptr,
+              [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, true, cnt); });
   st_8((TC*)p.C + cidx, v, true, cnt);
 }
 
@@ -201,101 +217,8 @@ LASR_DEV float alpha_of(const GemmP& p) {
 }
 
 // ============================ bf16 MFMA kernel ===================================
-LASR_DEV int swz(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
-LASR_DEV int lds_off(int row, int chunk) { return row * 32 + ((chunk ^ swz(row)) << 3); }
-
-// 8 consecutive elements along the contiguous axis; zero outside [0,lim).
-LASR_DEV uint4 load8(const bf16_t* src, int start, int lim, bool vec) {
-  uint4 v = make_uint4(0, 0, 0, 0);
-  if (vec && start + 8 <= lim) {
-    v = *(const uint4*)src;
-  } else {
-    uint32_t e[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) e[j] = (start + j < lim) ? (uint32_t)src[j] : 0u;
-    v.x = e[0] | (e[1] << 16);
-    v.y = e[2] | (e[3] << 16);
-    v.z = e[4] | (e[5] << 16);
-    v.w = e[6] | (e[7] << 16);
-  }
-  return v;
-}
-
-// Tile loader for one operand: R_TILE rows (M or N) x 32 k, 16-B global loads.
-//  KC (operand K-contiguous in HBM): image [R_TILE][32 k], 64-B rows, chunk swizzle above;
-//     fragments read with ds_read_b128.
-//  !KC (operand M/N-contiguous, e.g. dW = dY^T X, dX = dY W): image [32 k][R_TILE] stored as
-//     it arrives (no transposing writes); 32-B column slots XOR-swizzled per k row by
-//     htr(k) so the 8 k-rows a 32-lane half touches in one ds_read_b64_tr_b16 land on 8
-//     distinct 32-B bank groups (conflict-free); fragments read with 2 transposed reads.
-template <int R_TILE>
-LASR_DEV int htr(int k) {
-  return R_TILE >= 128 ? ((k & 3) | ((k >> 1) & 4)) : (((k >> 1) & 1) | ((k >> 2) & 2));
-}
-template <int R_TILE>
-LASR_DEV int tr_off(int k, int col) {  // element offset of (k, col), col % 4 == 0
-  return k * R_TILE + ((((col >> 4) ^ htr<R_TILE>(k))) << 4) + (col & 15);
-}
-
-template <int R_TILE, bool KC>
-struct TileLoader {
-  static constexpr int UNITS = R_TILE * 4;  // 16-B units per 32-deep k tile
-  static constexpr int PER = (UNITS + 255) / 256;
-  uint4 r0[PER];
-
-  LASR_DEV void load(const bf16_t* base, int64_t ld_r, int64_t ld_k, int row0, int R, int k0,
-                     int kend, bool vec, int tid) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int u = tid + i * 256;
-      if (u < UNITS) {
-        if (KC) {
-          const int r = u >> 2, c = u & 3;
-          const int gr = row0 + r, gk = k0 + c * 8;
-          if (gr < R) r0[i] = load8(base + (int64_t)gr * ld_r + gk, gk, kend, vec);
-          else r0[i] = make_uint4(0, 0, 0, 0);
-        } else {
-          const int c = u % (R_TILE / 8), k = u / (R_TILE / 8);
-          const int gr = row0 + c * 8, gk = k0 + k;
-          if (gk < kend) r0[i] = load8(base + (int64_t)gk * ld_k + gr, gr, R, vec);
-          else r0[i] = make_uint4(0, 0, 0, 0);
-        }
-      }
-    }
-  }
-  LASR_DEV void store(bf16_t* lds, int tid) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int u = tid + i * 256;
-      if (u < UNITS) {
-        if (KC) {
-          const int r = u >> 2, c = u & 3;
-          *(uint4*)(lds + lds_off(r, c)) = r0[i];
-        } else {
-          const int c = u % (R_TILE / 8), k = u / (R_TILE / 8);
-          *(uint4*)(lds + tr_off<R_TILE>(k, c * 8)) = r0[i];
-        }
-      }
-    }
-  }
-};
-
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-// MFMA 16x16x32 operand fragment of rows rbase..rbase+15: lane l gets row rbase + (l&15),
-// k = 8(l>>4) .. 8(l>>4)+7.  EXEC must be full for the transposed reads (no divergence).
-template <int R_TILE, bool KC>
-LASR_DEV bf16x8 frag(const bf16_t* tile, int rbase, int lane) {
-  if (KC) return *(const bf16x8*)(tile + lds_off(rbase + (lane & 15), lane >> 4));
-  const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(tile + tr_off<R_TILE>(8 * g + q, rbase + pc)));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(tile + tr_off<R_TILE>(8 * g + 4 + q, rbase + pc)));
-  const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
+// ============================ bf16 MFMA kernel ===================================
+// (tile images, fragment reads, LDS-DMA issue and ring waits: tile.h)
 
 // Epilogue shared by the bf16 kernels: stage each half of the C tile (WM rows x BN cols,
 // fp32) through LDS, then every thread finishes 8 contiguous columns of a row with 16-B
@@ -518,31 +441,11 @@ LASR_DEV void epi_store4(const GemmP& p, int z1, int z2, int z, int m, int n, in
       for (int q = 0; q < 4; ++q) o[q] = q < cnt ? load_any(base, dtp, idx + q) : 0.f;
     }
   };
-  if (p.zout) st4((TC*)p.zout + cidx, v);
-  if (p.act == LASR_ACT_RELU) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-  } else if (p.act == LASR_ACT_SWISH) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = swishf(v[q]);
-  }
-  if (p.aux) {
-    ld4(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, t);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      v[q] *= (p.aux_act == LASR_ACT_RELU) ? (t[q] > 0.f ? 1.f : 0.f) : swish_grad(t[q]);
-  }
-  if (p.drop.p > 0.f) {
-    const uint64_t base = ((uint64_t)z * p.M + m) * (uint64_t)p.N + n;
-    const uint32_t key = drop_key(p.drop);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] *= drop_mul_k(p.drop, key, base + q);
-  }
-  if (p.res) {
-    ld4(p.res, p.res_dtype, (int64_t)m * p.ldres + n, t);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = t[q] + p.res_scale * v[q];
-  }
+  float r[4];
+  if (p.aux) ld4(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, t);
+  if (p.res) ld4(p.res, p.res_dtype, (int64_t)m * p.ldres + n, r);
+  epi_core<4>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
+              [&](const float (&zv)[4]) { st4((TC*)p.zout + cidx, zv); });
   TC* C = (TC*)p.C + cidx;
   if (p.beta != 0.f) {
     ld4(C, sizeof(TC) == 4 ? LASR_F32 : LASR_BF16, 0, t);
@@ -609,121 +512,6 @@ LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32
 // the tile about to be read.  A ragged last k tile goes through the register loader
 // (zero fill).  Rows past M/N read clamped (valid) addresses; they only feed discarded
 // outputs.  Blocks are remapped so consecutive tiles share an XCD (and its L2).
-template <int N>
-LASR_DEV void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt out of range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// Retire ring tile kt when `after` (<= S-2) later tiles of GL glds each are still in flight.
-template <int S, int GL>
-LASR_DEV void wait_ring(int after) {
-  if constexpr (S >= 6) if (after >= 4) { wait_vmcnt<4 * GL>(); return; }
-  if constexpr (S >= 5) if (after >= 3) { wait_vmcnt<3 * GL>(); return; }
-  if constexpr (S >= 4) if (after >= 2) { wait_vmcnt<2 * GL>(); return; }
-  if (after >= 1) wait_vmcnt<GL>();
-  else wait_vmcnt<0>();
-}
-LASR_DEV void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-typedef const __attribute__((address_space(1))) void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
-typedef int v2i __attribute__((ext_vector_type(2)));
-
-// Transposed LDS read in inline asm: hipcc would otherwise treat the builtin as possibly
-// aliasing the in-flight LDS-DMA and drain the ring (vmcnt(0)) before every k step.  asm
-// loads are invisible to hipcc's waitcnt bookkeeping, so the caller waits explicitly
-// (tie_lgkm) before the results are used.
-LASR_DEV v2i ds_tr_asm(const bf16_t* p) {
-  v2i r;
-  const uint32_t a = (uint32_t)(uintptr_t)(lptr_t)p;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-// s_waitcnt lgkmcnt(0) that the consumers of r[0..N) depend on (in/out operands).
-template <int N>
-LASR_DEV void tie_lgkm(v2i* r) {
-  if constexpr (N == 4)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]));
-  else if constexpr (N == 8)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]),
-                 "+v"(r[5]), "+v"(r[6]), "+v"(r[7]));
-  else if constexpr (N == 16)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]),
-                 "+v"(r[5]), "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]),
-                 "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15]));
-  else
-    static_assert(N < 0, "tie_lgkm: unsupported count");
-}
-// Raw halves of a transposed fragment (see frag<>): k = 8g+q and 8g+4+q rows.
-template <int R_TILE>
-LASR_DEV void frag_tr_raw(const bf16_t* tile, int rbase, int lane, v2i* r) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
-  r[0] = ds_tr_asm(tile + tr_off<R_TILE>(8 * g + q, rbase + pc));
-  r[1] = ds_tr_asm(tile + tr_off<R_TILE>(8 * g + 4 + q, rbase + pc));
-}
-typedef int v4i __attribute__((ext_vector_type(4)));
-LASR_DEV v4i ds_b128_asm(const bf16_t* p) {
-  v4i r;
-  const uint32_t a = (uint32_t)(uintptr_t)(lptr_t)p;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-// Row sums of an M-contiguous A tile image ([32 k][BM], tr_off layout): thread owns the 8
-// rows 8*(tid % (BM/8)).. and k rows tid / (BM/8) + j * (256 / (BM/8)).
-template <int BM>
-LASR_DEV void rowsum_tile(const bf16_t* tile, int tid, float* rs) {
-  constexpr int CH = BM / 8, KG = 256 / CH, KR = 32 / KG;
-  const int c = tid % CH, k0 = tid / CH;
-  v4i r[KR];
-#pragma unroll
-  for (int j = 0; j < KR; ++j) r[j] = ds_b128_asm(tile + tr_off<BM>(k0 + j * KG, 8 * c));
-  if constexpr (KR == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]));
-  else if constexpr (KR == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]));
-  else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]));
-#pragma unroll
-  for (int j = 0; j < KR; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t u = (uint32_t)r[j][q];
-      rs[2 * q] += __uint_as_float(u << 16);
-      rs[2 * q + 1] += __uint_as_float(u & 0xffff0000u);
-    }
-}
-
-LASR_DEV bf16x8 frag_from_raw(const v2i* r) {
-  const int __attribute__((ext_vector_type(4))) v = {r[0][0], r[0][1], r[1][0], r[1][1]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// Issue the glds of one operand tile (R_TILE rows x 32 k) into `dst`.
-template <int R_TILE, bool KC>
-LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0, bf16_t* dst,
-                        int tid) {
-  constexpr int PER = R_TILE * 4 / 256;  // 16-B positions per thread
-  const int wid = tid >> 6, lane = tid & 63;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int P = i * 256 + tid;  // linear 16-B position in the image
-    const bf16_t* src;
-    if (KC) {
-      const int r = P >> 2, c = (P & 3) ^ swz(r);
-      const int gr = min(row0 + r, R - 1);
-      src = base + (int64_t)gr * ld + k0 + c * 8;
-    } else {
-      constexpr int CPR = R_TILE / 8;
-      const int k = P / CPR, ps = P % CPR;
-      const int ls = ((((ps >> 1) ^ htr<R_TILE>(k))) << 1) | (ps & 1);
-      const int gc = min(row0 + ls * 8, ((R + 7) & ~7) - 8);  // host: row stride >= roundup8(R)
-      src = base + (int64_t)(k0 + k) * ld + gc;
-    }
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * 256 + wid * 64) * 8), 16, 0, 0);
-    (void)lane;
-  }
-}
 
 template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3>
 __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
@@ -1174,6 +962,9 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   LASR_CHECK_ARG(a->lda_m == 1 || a->lda_k == 1, "lasr_gemm: A needs a unit stride");
   LASR_CHECK_ARG(a->ldb_n == 1 || a->ldb_k == 1, "lasr_gemm: B needs a unit stride");
   LASR_CHECK_ARG(a->A && a->B && a->C, "lasr_gemm: null operand");
+  LASR_CHECK_ARG(a->zout_mode == 0 || a->zout_mode == 1, "lasr_gemm: zout_mode must be 0 or 1");
+  LASR_CHECK_ARG(a->act != LASR_ACT_GATE && (!a->aux || a->aux_act != LASR_ACT_NONE),
+                 "lasr_gemm: act GATE is only an aux_act; aux needs an aux_act");
   if (a->M == 0 || a->N == 0 || a->batch == 0) return LASR_OK;
   const int batch = a->batch > 0 ? a->batch : 1;
   const int bdiv = a->batch_div > 0 ? a->batch_div : 1;
@@ -1187,7 +978,7 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   p.B = a->B; p.ldb_n = a->ldb_n; p.ldb_k = a->ldb_k; p.sb1 = a->sb1; p.sb2 = a->sb2;
   p.C = a->C; p.ldc = a->ldc; p.sc1 = a->sc1; p.sc2 = a->sc2;
   p.alpha = a->alpha; p.alpha_dev = a->alpha_dev; p.beta = a->beta;
-  p.bias = a->bias; p.act = a->act; p.zout = a->zout;
+  p.bias = a->bias; p.act = a->act; p.zout = a->zout; p.zout_mode = a->zout_mode;
   p.aux = a->aux; p.aux_dtype = a->aux_dtype; p.ldaux = a->ldaux; p.aux_act = a->aux_act;
   p.drop = mkdrop(a->drop_p, a->drop_seed);
   p.res = a->res; p.res_dtype = a->res_dtype; p.ldres = a->ldres; p.res_scale = a->res_scale;

@@ -38,10 +38,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, i
   for (int i = 0; i < NPL; ++i) o[i] = (v[i] - mu) * rs * g[i] + b[i];
   stv<NPL>(y + row * D + c0, o);
   if (y2) {
-    const uint32_t key = d2.p > 0.f ? drop_key(d2) : 0u;
+    if (d2.p > 0.f) {
+      float dm[NPL];
+      drop_mul_n<NPL>(d2, drop_key(d2), (uint64_t)row * D + c0, dm);
 #pragma unroll
-    for (int i = 0; i < NPL; ++i)
-      o[i] *= d2.p > 0.f ? drop_mul_k(d2, key, (uint64_t)row * D + c0 + i) : 1.f;
+      for (int i = 0; i < NPL; ++i) o[i] *= dm[i];
+    }
     stv<NPL>(y2 + row * D + c0, o);
   }
 }
@@ -96,9 +98,10 @@ __global__ __launch_bounds__(1024) void ln_bwd_kernel(const TX* __restrict__ x,
       for (int i = 0; i < NPL; ++i) o[i] = rs * (g[i] - s1 - xv[i] * s2) + (dres ? r[i] : 0.f);
       stv<NPL>(dx + row * D + c0, o);
       if (gb) {
+        float dm[NPL];
+        if (bd.p > 0.f) drop_mul_n<NPL>(bd, key, (uint64_t)(row * D + c0), dm);
 #pragma unroll
-        for (int i = 0; i < NPL; ++i)
-          o[i] *= bscale * (bd.p > 0.f ? drop_mul_k(bd, key, (uint64_t)(row * D + c0 + i)) : 1.f);
+        for (int i = 0; i < NPL; ++i) o[i] *= bscale * (bd.p > 0.f ? dm[i] : 1.f);
         stv<NPL>(gb + row * D + c0, o);
       }
     }

@@ -71,13 +71,18 @@ def encode(model, x, graph=True):
     are captured once per input shape into a hipGraph and replayed; the returned h is that
     graph's static output, valid until the next encode of the same shape.  The cache is
     keyed on the flat parameter version, so a weight update re-captures (the working-copy
-    cast is host-conditional and must not be skipped by a stale graph)."""
+    cast is host-conditional and must not be skipped by a stale graph), and on the
+    train/eval mode.  (The fused Adam kernel rewrites flat and its working copy in place,
+    without a version bump: the graph reads them through the same pointers, so replays
+    after optimizer steps see the new weights.)"""
     if x.device.type != "cuda":
         raise RuntimeError("liteasr_amd decoding runs on the HIP device only")
     if not graph:
         return _encode_eager(model, x)
     st = model.store
-    key = (tuple(x.shape), x.dtype, st.flat._version, st.generation)
+    # model.training too: dropout and BatchNorm (batch vs running statistics) are baked
+    # into the captured launches, so a train()/eval() switch must re-capture
+    key = (tuple(x.shape), x.dtype, st.flat._version, st.generation, bool(model.training))
     cache = model.__dict__.setdefault("_encode_graphs", {})
     e = cache.get(key)
     if e is None:

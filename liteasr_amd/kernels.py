@@ -141,6 +141,7 @@ def gemm(
     split_k: int = 1,
     rowsum: Optional[torch.Tensor] = None,
     plan_only: bool = False,
+    zout_mode: int = 0,
 ):
     """c = epilogue(alpha * a @ b) for logical views a (..,M,K), b (..,K,N), c (..,M,N).
 
@@ -176,6 +177,7 @@ def gemm(
     args.bias = ptr(bias)
     args.act = act
     args.zout = ptr(zout)
+    args.zout_mode = zout_mode
     if aux is not None:
         args.aux, args.aux_dtype, args.ldaux, args.aux_act = ptr(aux), dt(aux), aux.stride(0), aux_act
     args.drop_p, args.drop_seed = drop_p, drop_seed
@@ -225,6 +227,55 @@ def gemm_plan(a, b, c, **kw):
 def linear(x, w, out, bias=None, **kw):
     """out[M,N] = x[M,K] @ w[N,K]^T (+bias, epilogue kw)."""
     return gemm(x, w.t(), out, bias=bias, **kw)
+
+
+def dropout_scale(p: float) -> float:
+    """Multiplier of kept elements at drop probability p (1 when p <= 0)."""
+    return float(N.load().lasr_dropout_scale(float(p))) if p > 0 else 1.0
+
+
+# --------------------------------------------------------- fused FFN chains ---
+def ffn_supported(x, W1):
+    """Shapes / dtypes the fused chains (ffn.hip) take: bf16, D in {256, 512}, F % 128 == 0."""
+    F, D = W1.shape
+    return x.dtype == torch.bfloat16 and D in (256, 512) and F % 128 == 0 and F <= 2048
+
+
+def _ffn_args(M, D, F, act, x, W1, W2, **kw):
+    for t in (x, W1, W2):
+        assert t.is_contiguous() and t.dtype == torch.bfloat16, "ffn operands: contiguous bf16"
+    a = N.FfnArgs()
+    a.M, a.D, a.F, a.act = M, D, F, act
+    a.x, a.W1, a.W2 = ptr(x), ptr(W1), ptr(W2)
+    a.b1, a.b2 = ptr(kw.get("b1")), ptr(kw.get("b2"))
+    a.p1, a.seed1 = float(kw.get("p1", 0.0)), int(kw.get("seed1", 0)) & 0xFFFFFFFFFFFFFFFF
+    a.p2, a.seed2 = float(kw.get("p2", 0.0)), int(kw.get("seed2", 0)) & 0xFFFFFFFFFFFFFFFF
+    a.res, a.res_scale = ptr(kw.get("res")), float(kw.get("res_scale", 1.0))
+    for k in ("z", "h", "out", "dz", "dx"):
+        setattr(a, k, ptr(kw.get(k)))
+    return a
+
+
+def ffn_fwd(ln, W1, b1, W2, b2, act, p1, seed1, res, res_scale, p2, seed2, z, h, out):
+    """z = ln W1^T + b1; h = drop1(act(z)); out = res + res_scale * drop2(h W2^T + b2)
+    in one launch (lasr_ffn_fwd); the [M, F] intermediate never round-trips HBM."""
+    M, D = ln.shape
+    F = W1.shape[0]
+    assert W1.shape == (F, D) and W2.shape == (D, F) and z.shape == h.shape == (M, F) and out.shape == (M, D)
+    assert out.dtype == torch.float32 and (res is None or (res.dtype == torch.float32 and res.is_contiguous()))
+    a = _ffn_args(M, D, F, act, ln, W1, W2, b1=b1, b2=b2, p1=p1, seed1=seed1, p2=p2, seed2=seed2,
+                  res=res, res_scale=res_scale, z=z, h=h, out=out)
+    N.call("lasr_ffn_fwd", C.byref(a), stream())
+
+
+def ffn_bwd_dx(gb, W1, W2, z, act, p1, seed1, dz, dx):
+    """dz = (gb W2) * act'(z) * drop1; dx = dz W1 in one launch (lasr_ffn_bwd_dx)."""
+    M, D = gb.shape
+    F = W1.shape[0]
+    assert W1.shape == (F, D) and W2.shape == (D, F) and z.shape == dz.shape == (M, F) and dx.shape == (M, D)
+    assert z.is_contiguous() and dz.is_contiguous() and dx.is_contiguous() and dx.dtype == torch.bfloat16
+    a = _ffn_args(M, D, F, act, gb, W1, W2, p1=p1, seed1=seed1, z=z, dz=dz, dx=dx)
+    N.call("lasr_ffn_bwd_dx", C.byref(a), stream())
 
 
 def colsum(x2d: torch.Tensor, out: torch.Tensor, accumulate=True):

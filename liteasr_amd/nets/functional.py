@@ -27,7 +27,7 @@ from types import SimpleNamespace
 import torch
 
 from .. import kernels as K
-from .._native import ACT_NONE, ACT_RELU, ACT_SWISH
+from .._native import ACT_GATE, ACT_NONE, ACT_RELU, ACT_SWISH
 
 F32 = torch.float32
 LN_EPS = 1e-12
@@ -57,26 +57,49 @@ def ln_forward(x, g, b, adt, y2=False, p2=0.0, seed2=0):
     return y, yd, mean, rstd
 
 
+# The single-launch FFN chains of ffn.hip: correct (tests/test_kernels_gpu.py::
+# test_ffn_fused_chains) but slower than the two GEMMs at the step's shapes,
+# so off unless LASR_FUSED_FFN=1.
+FUSED_FFN = os.environ.get("LASR_FUSED_FFN", "0") == "1"
+
+
+def _fused_ffn(x, W1):
+    return FUSED_FFN and K.ffn_supported(x, W1)
+
+
 def ffn_forward(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res):
+    """Returns (out, g, h): g = act'(fc1 pre-activation) * keep (the dropout keep flag) is
+    what the backward needs in place of the pre-activation (the fc1 epilogue writes it,
+    zout_mode 1), so the dX GEMM multiplies by g instead of re-deriving act' and the
+    dropout mask per element."""
     M = ln.shape[0]
     dev, adt = ln.device, ln.dtype
-    z = _e((M, W1.shape[0]), adt, dev)
+    g = _e((M, W1.shape[0]), adt, dev)
     h = _e((M, W1.shape[0]), adt, dev)
-    K.linear(ln, W1, h, bias=b1, act=act, zout=z, drop_p=p_ff, drop_seed=s_ff)
     out = _e((M, W2.shape[0]), F32, dev)
+    if _fused_ffn(ln, W1):  # one launch: the [M, F] intermediate stays on chip (ffn.hip)
+        K.ffn_fwd(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res, g, h, out)
+        return out, g, h
+    K.linear(ln, W1, h, bias=b1, act=act, zout=g, zout_mode=1, drop_p=p_ff, drop_seed=s_ff)
     K.linear(h, W2, out, bias=b2, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res)
-    return out, z, h
+    return out, g, h
 
 
-def ffn_backward(gb, ln, z, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
-    """gb: gradient of the FFN output (after the residual-branch dropout/scale)."""
+def ffn_backward(gb, ln, g, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
+    """gb: gradient of the FFN output (after the residual-branch dropout/scale); g: the
+    forward's gate act'(z) * keep."""
     M = gb.shape[0]
     dev, adt = gb.device, gb.dtype
     K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0, rowsum=gb2)
     dz = _e((M, W1.shape[0]), adt, dev)
-    K.gemm(gb, W2, dz, aux=z, aux_act=act, drop_p=p_ff, drop_seed=s_ff)
-    K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
     dln = _e((M, W1.shape[1]), adt, dev)
+    if _fused_ffn(gb, W1):  # dz and dln in one launch (ffn.hip)
+        K.ffn_bwd_dx(gb, W1, W2, g, act, p_ff, s_ff, dz, dln)
+        K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
+        return dln
+    # dz = (gb W2) * scale * g: the dropout scale as alpha, the gate as aux
+    K.gemm(gb, W2, dz, alpha=K.dropout_scale(p_ff), aux=g, aux_act=ACT_GATE)
+    K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
     K.gemm(dz, W1, dln)
     return dln
 

@@ -57,6 +57,11 @@ def test_host_entries_without_gpu(lib):
     assert isinstance(L.lasr_last_error(), (bytes, type(None)))
     assert L.lasr_sumsq_nparts(1 << 20) >= 1
     assert L.lasr_dwconv_nparts(4, 200) >= 1
+    # dropout: 16-bit threshold round(p * 65536), kept values scaled to keep E = 1 exactly
+    for p in (0.1, 0.25, 0.5):
+        thr = int(p * 65536 + 0.5)
+        assert abs(L.lasr_dropout_scale(p) - 65536 / (65536 - thr)) <= 1e-6
+    assert L.lasr_dropout_scale(0.0) == 1.0 and L.lasr_dropout_scale(1.0) == 0.0
 
 
 def test_extern_c_no_mangling(lib):

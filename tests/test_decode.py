@@ -189,3 +189,14 @@ def test_graphed_encode_matches_eager():
             if it == 1:  # weight update -> new flat version -> re-capture
                 model.ctc.ctc_lo.weight.mul_(1.0)
                 model.encoder.after_norm.weight.add_(0.01)
+    # a train()/eval() switch re-captures: BatchNorm uses batch statistics in train mode
+    x = torch.randn(2, 100, 40, generator=g).cuda()
+    with torch.no_grad():
+        for mode in (True, False, True):
+            model.train(mode)
+            he, _ = D.encode(model, x, graph=False)
+            he = he.clone()
+            hg, _ = D.encode(model, x, graph=True)
+            torch.cuda.synchronize()
+            assert torch.equal(he, hg), mode
+    model.eval()

@@ -1,0 +1,18 @@
+#!/bin/bash
+# all GPU tests, then bench (with trace when asked)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R; mkdir -p gpurun_out
+tag=${1:-x}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_$tag.log 2>&1; rc=$?
+echo "tests rc=$rc"; grep -E "passed|failed|^E |FAILED|Error" gpurun_out/t_$tag.log | tail -15
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline > gpurun_out/b1_$tag.json 2> gpurun_out/b1_$tag.err; rc=$?
+echo "bench rc=$rc"; cat gpurun_out/b1_$tag.json
+[ $rc -eq 0 ] || exit $rc
+if [ "$2" = "trace" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/tr_$tag -o run -- python3 $R/bench.py --no-cpu-baseline --no-roofline --steps 5 --warmup 3 > $R/gpurun_out/tr_$tag.log 2>&1; rc=$?
+  echo "trace rc=$rc"
+fi
+exit $rc
