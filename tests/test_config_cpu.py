@@ -4,17 +4,15 @@ semantics of the reference's config tree liteasr/config/), CPU only."""
 import logging
 import os
 import pickle
-import shutil
-import textwrap
 
 import pytest
 import yaml
 
+from cfgtree import user_tree
 from liteasr_amd.config.compose import (ConfigError, Node, compose, missing_keys, resolve,
                                         save_run_config)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LOADER = os.path.join(ROOT, "tests", "golden", "loader")
 GROUPS = ["task=asr_kaldi", "model=conformer_small", "criterion=hybrid_ctc_w03", "optimizer=noam_d256"]
 
 
@@ -80,52 +78,8 @@ def test_interpolation_rules():
         resolve({"a": "${b}", "b": "${a}"})
 
 
-def _user_tree(tmp_path):
-    """A config dir in the reference's own format (config.yaml + my_* group files that
-    extend the registered options and carry ??? for task-filled values)."""
-    d = tmp_path / "conf"
-    for g in ("model", "criterion", "optimizer", "task"):
-        (d / g).mkdir(parents=True)
-    (d / "config.yaml").write_text(textwrap.dedent("""\
-        defaults:
-          - liteasr_config
-          - task: my_task
-          - model: my_U2
-          - criterion: my_hybrid_ctc
-          - optimizer: my_noam
-          - _self_
-        common:
-          seed: 7
-          trigger:
-            - {name: report_loss, interval: 1, unit: iteration}
-        dataset: {batch_count: seq, batch_size: 4, min_batch_size: 1, max_len_in: 1000, max_len_out: 150}
-        postprocess: {workflow: []}
-        optimization: {max_epoch: 1, max_iter: 2, accum_grad: 1, clip_grad_norm: 5.0}
-        hydra:
-          run:
-            dir: runs/${task.name}_${model.name}
-          job_logging:
-            formatters: {mine: {format: '[%(levelname)s][%(name)s] - %(message)s'}}
-            handlers: {file: {formatter: mine}}
-        """))
-    (d / "model" / "my_U2.yaml").write_text(
-        "defaults:\n  - U2\nname: U2\ninput_dim: ???\nvocab_size: ???\nenc_dim: 64\nenc_ff_dim: 128\n"
-        "enc_layers: 2\ndec_dim: 64\ndec_ff_dim: 128\ndec_layers: 1\ndropout_rate: 0.0\n"
-        "enc_dropout_rate: ${model.dropout_rate}\n")
-    (d / "criterion" / "my_hybrid_ctc.yaml").write_text(
-        "defaults:\n  - hybrid_ctc\nname: hybrid_ctc\nvocab_size: ???\nsmoothing: 0.1\nctc_weight: 0.3\n")
-    (d / "optimizer" / "my_noam.yaml").write_text("defaults:\n  - noam\nname: noam\nmodel_dim: 64\n")
-    data = tmp_path / "data"
-    shutil.copytree(LOADER, data)
-    scp = (data / "feats_fm.scp").read_text().replace("@DIR@", str(data))
-    (data / "feats.scp").write_text(scp)
-    (d / "task" / "my_task.yaml").write_text(
-        f"defaults:\n  - asr\nname: asr\nvocab: {data / 'vocab.txt'}\ntrain: {data}\nvalid: {data}\n")
-    return d, data
-
-
 def test_user_config_tree_in_reference_format(tmp_path):
-    d, data = _user_tree(tmp_path)
+    d, data = user_tree(tmp_path)
     cfg = compose(str(d), "config", ["optimizer.warmup=10"])
     assert cfg.common.seed == 7 and cfg.optimization.max_iter == 2
     assert cfg.model.enc_dim == 64 and cfg.model.input_dim == "???" and cfg.model.enc_dropout_rate == 0.0
@@ -139,7 +93,7 @@ def test_user_config_tree_in_reference_format(tmp_path):
 def test_prepare_writes_run_dir_and_logs(tmp_path, monkeypatch):
     from liteasr_amd import train as T
 
-    d, data = _user_tree(tmp_path)
+    d, data = user_tree(tmp_path)
     monkeypatch.chdir(tmp_path)
     root = logging.getLogger()
     saved = root.handlers[:], root.level
