@@ -289,6 +289,32 @@ int lasr_im2col3x3s2(const void* y1, int dt, int B, int T1, int F1, int C, void*
                      void* stream);
 int lasr_col2im3x3s2(const void* dcol, int dt, int B, int T1, int F1, int C,
                      const void* y1, void* dy1, void* stream);
+/* conv2 as implicit GEMMs on the LDS-DMA MFMA kernel (no im2col / col2im buffers):
+ *  LASR_CONV2_FWD: out = y2 [M2, C] bf16 = relu(im2col(y1) W2p^T + bias)         (y1, w2p, bias)
+ *  LASR_CONV2_DW : out = dW [C, 9C] fp32 = dy2^T im2col(y1); rowsum (nullable) += column
+ *                  sums of dy2 (db2)                                        (dy2, y1, workspace)
+ *  LASR_CONV2_DX : out = dy1 [B,T1,F1,C] bf16 = col2im(dy2 W2p) * relu'(y1)      (dy2, w2p, y1)
+ * M2 = B*T2*F2 (T2 = (T1-3)/2+1, F2 = (F1-3)/2+1); W2p [C, 9C] bf16 with k = (kh*3+kw)*C + cin
+ * (the im2col column order above); dy2 [dy2_rows, C] bf16 with dy2_rows >=
+ * max(roundup32(M2), M2 + 1) and rows M2.. zero (the weight-gradient k padding and the taps
+ * that fall outside dy2).  C % 128 == 0, every pointer 16-B aligned.  DW splits K over
+ * workgroups when the workspace holds split*(9C*C + C) floats (summed in fixed order).
+ * Replaces nn.Conv2d(C, C, 3, 2)'s forward and backward at liteasr/nets/subsampling.py:42. */
+#define LASR_CONV2_FWD 0
+#define LASR_CONV2_DW 1
+#define LASR_CONV2_DX 2
+typedef struct lasr_conv2_args {
+  int mode;
+  int B, T1, F1, C;
+  const void* y1;
+  const void* w2p;
+  const float* bias;
+  const void* dy2; int64_t dy2_rows;
+  void* out;
+  float* rowsum;
+  void* workspace; int64_t workspace_bytes;
+} lasr_conv2_args;
+int lasr_conv2_gemm(const lasr_conv2_args* args, void* stream);
 /* Transpose the last two dims of [N][A][Bd] into [N][Bd][A] (fp32 -> dst dtype), or
  * (reverse=1) [N][Bd][A] -> [N][A][Bd] with optional accumulate into fp32. */
 int lasr_permute_last2(const void* src, int sdt, int64_t N, int64_t A, int64_t Bd, void* dst,

@@ -64,6 +64,22 @@ class FfnArgs(C.Structure):
     ]
 
 
+class Conv2Args(C.Structure):
+    """Mirror of ``lasr_conv2_args``."""
+
+    _fields_ = [
+        ("mode", _i),
+        ("B", _i), ("T1", _i), ("F1", _i), ("C", _i),
+        ("y1", _p), ("w2p", _p), ("bias", _p),
+        ("dy2", _p), ("dy2_rows", _l),
+        ("out", _p), ("rowsum", _p),
+        ("workspace", _p), ("workspace_bytes", _l),
+    ]
+
+
+CONV2_FWD, CONV2_DW, CONV2_DX = 0, 1, 2
+
+
 class ReduceSeg(C.Structure):
     """Mirror of ``lasr_reduce_seg``."""
 
@@ -106,6 +122,7 @@ SIGNATURES = {
     "lasr_reduce_batch": [_p, _i, _i, _i, _i, _p, _i, _p],
     "lasr_conv1_fwd": [_p, _i, _i, _i, _i, _p, _p, _p, _i, _p],
     "lasr_conv1_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _l, _p],
+    "lasr_conv2_gemm": [C.POINTER(Conv2Args), _p],
     "lasr_im2col3x3s2": [_p, _i, _i, _i, _i, _i, _p, _p],
     "lasr_col2im3x3s2": [_p, _i, _i, _i, _i, _i, _p, _p, _p],
     "lasr_permute_last2": [_p, _i, _l, _l, _l, _p, _i, _i, _i, _p],

@@ -17,6 +17,7 @@
 #include "common.h"
 #include "tile.h"
 
+#include <cstring>
 #include <type_traits>
 
 // Ablation hooks for GEMM experiments (tools/gemm_exp.sh); 0 in every product build.
@@ -25,6 +26,18 @@
 #define LASR_EXP 0
 #endif
 
+
+// Geometry of the subsampling conv2 (3x3, stride 2, C -> C, channels-last y1 [B,T1,F1,C]) for
+// the implicit-GEMM kernel instances (G_FWD / G_DW / G_DX below).
+struct ConvG {
+  int B, T1, F1, T2, F2, C;
+  int M2;               // B * T2 * F2 (rows of y2 / dy2)
+  int cls;              // G_DX: output parity class (t1 & 1) * 2 + (f1 & 1)
+  int q32, r32;         // G_DW: 32 = q32 * F2 + r32 (row-walk increments)
+  const bf16_t* zero;   // G_DX: >= 32 zero bf16 (taps that fall outside dy2)
+};
+typedef ConvG ConvGeom;
+enum { G_LIN = 0, G_FWD = 1, G_DW = 2, G_DX = 3 };
 
 struct GemmP {
   int M, N, K, batch, batch_div;
@@ -65,6 +78,7 @@ struct GemmP {
   float* rs_ws;
   int v4;  // direct epilogue: 4-wide C/zout/aux/res/bias/ws access allowed (host-checked)
   int zout_mode;  // 0: zout = pre-activation; 1: zout = act'(pre-activation) * keep (gate)
+  ConvGeom cv;    // implicit-GEMM instances of the subsampling conv2 only (G != 0)
 };
 
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
@@ -201,12 +215,11 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
 // Epilogue modes 0/1: bias already in registers (bv), the one aux/res source prefetched
 // (sv, mode 1 only; N % 8 == 0 there), beta == 0; cnt < 8 only on a ragged last vector.
 template <typename TC>
-LASR_DEV void epi_fast8(const GemmP& p, int z1, int z2, int z, int m, int n, int cnt,
-                        const float* acc, float alpha_eff, const float* bv, const float (&sv)[8]) {
+LASR_DEV void epi_fast8(const GemmP& p, int64_t cidx, int z, int m, int n, int cnt, const float* acc,
+                        float alpha_eff, const float* bv, const float (&sv)[8]) {
   float v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff + bv[q];
-  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
   epi_core<8>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, sv, p.aux != nullptr, sv, p.res != nullptr,
               [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, true, cnt); });
   st_8((TC*)p.C + cidx, v, true, cnt);
@@ -224,9 +237,24 @@ LASR_DEV float alpha_of(const GemmP& p) {
 // fp32) through LDS, then every thread finishes 8 contiguous columns of a row with 16-B
 // loads/stores (or writes its split-K partial).  The caller has passed a barrier after its
 // last LDS read of the main loop.
-template <int BM, int BN, typename TC, bool TRANS = false>
+// Element offset of output row m of a G_DX launch: class row (b, i, j) -> dy1 position
+// (b, 2i + pt, 2j + pf), channels-last.
+LASR_DEV int64_t dx_row(const ConvG& g, int m) {
+  const int pt = g.cls >> 1, pf = g.cls & 1;
+  const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
+  const int j = m % nJ, t = m / nJ, i = t % nI, b = t / nI;
+  return ((int64_t)(b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf) * g.C;
+}
+
+template <int BM, int BN, typename TC, bool TRANS = false, int G = G_LIN>
 LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem_epi, int m0,
                             int n0, int s, int z, int z1, int z2) {
+  // output-row offsets: linear (ldc, ld of the aux/res source), or the transposed-conv scatter
+  // of a G_DX launch (aux = y1 shares dy1's layout)
+  auto crow = [&](int m) -> int64_t {
+    if constexpr (G == G_DX) return dx_row(p.cv, m);
+    else return (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc;
+  };
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -242,7 +270,8 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
   static_assert(WM % RPI == 0, "epilogue tiling");
   const int ec8 = (tid % CPR) * 8, er0 = tid / CPR;
   const int en = n0 + ec8;
-  const bool fast = !split && p.epi_mode < 2;
+  // conv instances are host-checked onto the fast path (no split here, epi_mode < 2)
+  const bool fast = G != G_LIN || (!split && p.epi_mode < 2);
   float bv[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) bv[q] = 0.f;
@@ -267,13 +296,15 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
 #pragma unroll
         for (int it = 0; it < PF; ++it) {
           const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          ld8((const float*)src + (int64_t)m * src_ld + nc, sv[it]);
+          const int64_t ro = G == G_DX ? dx_row(p.cv, m) : (int64_t)m * src_ld;
+          ld8((const float*)src + ro + nc, sv[it]);
         }
       } else {
 #pragma unroll
         for (int it = 0; it < PF; ++it) {
           const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          ld8((const bf16_t*)src + (int64_t)m * src_ld + nc, sv[it]);
+          const int64_t ro = G == G_DX ? dx_row(p.cv, m) : (int64_t)m * src_ld;
+          ld8((const bf16_t*)src + ro + nc, sv[it]);
         }
       }
     };
@@ -308,7 +339,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
             float a8[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + ec8 + q];
-            epi_fast8<TC>(p, z1, z2, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
+            epi_fast8<TC>(p, crow(m) + en, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
           }
         }
       }
@@ -513,8 +544,106 @@ LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32
 // (zero fill).  Rows past M/N read clamped (valid) addresses; they only feed discarded
 // outputs.  Blocks are remapped so consecutive tiles share an XCD (and its L2).
 
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3>
+// Implicit-GEMM operand walkers of the subsampling conv2 instances (G != G_LIN).  Each
+// keeps per-thread element offsets of the 16-B LDS-DMA positions it issues (the positions
+// of glds_tile), so an issue is one add per position.
+//  G_FWD, A = im2col(y1) [M2, 9C], K-contiguous: row m = (b, t2, f2) starts at y1 position
+//    (b, 2 t2, 2 f2); column k = (kh*3 + kw)*C + cin adds ((kh F1 + kw) C + cin): separable.
+//  G_DX, A = dy2 rows of the taps that reach output class (pt, pf), K-contiguous: row m =
+//    (b, i, j), output (b, 2i+pt, 2j+pf); tap (dt, df) reads dy2 row (b, i-dt, j-df), or the
+//    zero row when that falls outside [0,T2) x [0,F2).
+//  G_DW, B = im2col(y1) [M2, 9C] with k = m2 rows (M/N-contiguous operand): every k row is a
+//    contiguous run of one tap; the row walk advances (b, t2, f2) by 32 rows per tile.
+template <int R_TILE>
+struct ConvRowsKC {  // G_FWD / G_DX A operand
+  static constexpr int PER = R_TILE * 4 / 256;
+  int off[PER];
+  int vm[PER];  // G_DX: bit dt*2+df set when tap (dt, df) is inside dy2
+  LASR_DEV void init_fwd(const ConvG& g, int row0, int R, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int P = i * 256 + tid, r = P >> 2, c = (P & 3) ^ swz(r);
+      const int m = min(row0 + r, R - 1);
+      const int f2 = m % g.F2, t = m / g.F2, t2 = t % g.T2, b = t / g.T2;
+      off[i] = ((b * g.T1 + 2 * t2) * g.F1 + 2 * f2) * g.C + c * 8;
+      vm[i] = 0;
+    }
+  }
+  LASR_DEV void init_dx(const ConvG& g, int row0, int R, int tid) {
+    const int pt = g.cls >> 1, pf = g.cls & 1;
+    const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int P = i * 256 + tid, r = P >> 2, c = (P & 3) ^ swz(r);
+      const int m = min(row0 + r, R - 1);
+      const int j = m % nJ, t = m / nJ, ii = t % nI, b = t / nI;
+      off[i] = ((b * g.T2 + ii) * g.F2 + j) * g.C + c * 8;
+      const int vt = (ii < g.T2 ? 1 : 0) | (ii >= 1 && ii - 1 < g.T2 ? 2 : 0);
+      const int vf = (j < g.F2 ? 1 : 0) | (j >= 1 && j - 1 < g.F2 ? 2 : 0);
+      vm[i] = ((vt & 1) && (vf & 1) ? 1 : 0) | ((vt & 1) && (vf & 2) ? 2 : 0) |
+              ((vt & 2) && (vf & 1) ? 4 : 0) | ((vt & 2) && (vf & 2) ? 8 : 0);
+    }
+  }
+  LASR_DEV void issue(const bf16_t* base, int64_t koff, bf16_t* dst, int tid) const {
+    const int wid = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)(base + off[i] + koff), (lptr_t)(dst + (i * 256 + wid * 64) * 8),
+                                       16, 0, 0);
+  }
+  LASR_DEV void issue_dx(const bf16_t* base, int64_t shift, int bit, const bf16_t* zero, bf16_t* dst,
+                         int tid) const {
+    const int wid = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c8 = ((i * 256 + tid) & 3) * 8;
+      const bf16_t* src = (vm[i] >> bit) & 1 ? base + off[i] + shift : zero + c8;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * 256 + wid * 64) * 8), 16, 0, 0);
+    }
+  }
+};
+
+template <int R_TILE>
+struct ConvRowsDW {  // G_DW B operand: tile [32 k][R_TILE n] of im2col(y1), k = m2
+  static constexpr int PER = R_TILE * 4 / 256, CPR = R_TILE / 8;
+  int noff[PER], f2[PER], t2[PER], b[PER];
+  LASR_DEV void init(const ConvG& g, int n0, int N, int kbeg, int tid) {
+    const int tap = n0 / g.C, kh = tap / 3, kw = tap - 3 * kh;
+    const int tbase = (kh * g.F1 + kw) * g.C - tap * g.C;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int P = i * 256 + tid, k = P / CPR, ps = P % CPR;
+      const int ls = ((((ps >> 1) ^ htr<R_TILE>(k))) << 1) | (ps & 1);
+      const int gc = min(n0 + ls * 8, ((N + 7) & ~7) - 8);
+      noff[i] = tbase + gc;
+      const int m = kbeg + k;
+      f2[i] = m % g.F2;
+      const int t = m / g.F2;
+      t2[i] = t % g.T2;
+      b[i] = t / g.T2;
+    }
+  }
+  // issue the tile whose k rows are the current walk positions, then advance 32 rows
+  LASR_DEV void issue(const ConvG& g, const bf16_t* base, bf16_t* dst, int tid) {
+    const int wid = tid >> 6;
+    const int last = ((g.B * g.T1 - g.T1 + 2 * (g.T2 - 1)) * g.F1 + 2 * (g.F2 - 1)) * g.C;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int rb = b[i] < g.B ? ((b[i] * g.T1 + 2 * t2[i]) * g.F1 + 2 * f2[i]) * g.C : last;
+      __builtin_amdgcn_global_load_lds((gptr_t)(base + rb + noff[i]), (lptr_t)(dst + (i * 256 + wid * 64) * 8),
+                                       16, 0, 0);
+      f2[i] += g.r32;
+      t2[i] += g.q32;
+      if (f2[i] >= g.F2) { f2[i] -= g.F2; t2[i] += 1; }
+      while (t2[i] >= g.T2) { t2[i] -= g.T2; b[i] += 1; }
+    }
+  }
+};
+
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN>
 __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
+  static_assert(G == G_LIN || (G == G_DW ? (!AKC && !BKC) : (AKC && (G == G_FWD) == BKC)),
+                "conv instance operand orientation");
   constexpr int BK = 32;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int TILE = (BM + BN) * BK;  // elements per ring stage
@@ -553,12 +682,35 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
   // full 32-deep tiles go through the glds ring; a ragged last tile is handled after the
   // loop (ordinary loads inside the loop would make hipcc drain the ring with vmcnt(0))
   const int nfull = (kend - kbeg) > 0 ? (kend - kbeg) / BK : 0;
+  [[maybe_unused]] ConvRowsKC<BM> ga;
+  [[maybe_unused]] ConvRowsDW<BN> gb;
+  if constexpr (G == G_FWD) ga.init_fwd(p.cv, m0, p.M, tid);
+  if constexpr (G == G_DX) ga.init_dx(p.cv, m0, p.M, tid);
+  if constexpr (G == G_DW) gb.init(p.cv, n0, p.N, kbeg, tid);
   auto issue = [&](int t) {
     bf16_t* dst = smem + (t % S) * TILE;
     const int k0 = kbeg + t * BK;
     if (LASR_EXP & 4) return;
-    glds_tile<BM, AKC>(A, lda, m0, p.M, k0, dst, tid);
-    glds_tile<BN, BKC>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
+    if constexpr (G == G_LIN) {
+      glds_tile<BM, AKC>(A, lda, m0, p.M, k0, dst, tid);
+      glds_tile<BN, BKC>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
+    } else if constexpr (G == G_FWD) {
+      const int C = p.cv.C, tap = k0 / C, kh = tap / 3, kw = tap - 3 * kh;
+      ga.issue(A, (int64_t)(kh * p.cv.F1 + kw) * C + (k0 - tap * C), dst, tid);
+      glds_tile<BN, true>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
+    } else if constexpr (G == G_DW) {
+      glds_tile<BM, false>(A, lda, m0, p.M, k0, dst, tid);
+      gb.issue(p.cv, B, dst + BM * BK, tid);
+    } else {
+      // class tap ti = k0 / C: (kh, kw) = (pt ? 1 : 2a, pf ? 1 : 2c), reading dy2 row (i-dt, j-df)
+      const int C = p.cv.C, ti = k0 / C, cin = k0 - ti * C;
+      const int pt = p.cv.cls >> 1, pf = p.cv.cls & 1, nkw = pf ? 1 : 2;
+      const int a = ti / nkw, c = ti - a * nkw;
+      const int dt = pt ? 0 : a, df = pf ? 0 : c;
+      const int kh = pt ? 1 : 2 * a, kw = pf ? 1 : 2 * c;
+      ga.issue_dx(A, cin - (int64_t)(dt * p.cv.F2 + df) * C, dt * 2 + df, p.cv.zero, dst, tid);
+      glds_tile<BN, false>(B + (kh * 3 + kw) * C, ldb, n0, p.N, cin, dst + BM * BK, tid);
+    }
   };
   auto compute = [&](const bf16_t* cur) {
     bf16x8 af[FM], bfr[FN];
@@ -615,7 +767,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
     if constexpr (!AKC)
       if (do_rs) rowsum_tile<BM>(smem + (kt % S) * TILE, tid, rs);
   }
-  if (nfull < nk) {  // ragged tail: register loader with zero fill
+  if (G == G_LIN && nfull < nk) {  // ragged tail: register loader with zero fill (conv: host-checked K % 32 == 0)
     __syncthreads();
     TileLoader<BM, AKC> la;
     TileLoader<BN, BKC> lb;
@@ -653,7 +805,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
   // split-K partials: fp32, 16-B per lane straight from the accumulators; final outputs:
   // staged through LDS (full 256-B rows per wave store)
   if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC>(p, acc, m0, n0, s, z, z1, z2);
-  else gemm_epilogue<BM, BN, TC, true>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
+  else gemm_epilogue<BM, BN, TC, true, G>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
 }
 
 // ============================ fp32 MFMA kernel ===================================
@@ -1058,4 +1210,121 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   // unfused: rowsum of A[M, K] (lda_m == 1) = column sums of the [K, M] matrix, ld lda_k
   return lasr_colsum(a->A, a->in_dtype, a->K, a->M, a->lda_k, a->rowsum, 1, (float*)a->workspace,
                      a->workspace_bytes / 4, stream);
+}
+
+// ========================= subsampling conv2, implicit GEMM ======================
+// (lasr_conv2_gemm, include/liteasr_hip.h) Same LDS-DMA kernel, gather instances G_FWD /
+// G_DW / G_DX: im2col(y1) is never materialised, and the data gradient is scattered straight
+// into dy1 per output parity class (no dcol, no col2im).  Replaces the reference's
+// nn.Conv2d(C, C, 3, 2) forward and backward (liteasr/nets/subsampling.py:31-47).
+static GemmP conv_params(const lasr_conv2_args* a) {
+  GemmP p;
+  memset(&p, 0, sizeof(p));
+  p.batch = 1;
+  p.batch_div = 1;
+  p.alpha = 1.f;
+  p.res_scale = 1.f;
+  p.split_k = 1;
+  p.drop = mkdrop(0.f, 0);
+  ConvG& g = p.cv;
+  g.B = a->B; g.T1 = a->T1; g.F1 = a->F1; g.C = a->C;
+  g.T2 = (a->T1 - 3) / 2 + 1;
+  g.F2 = (a->F1 - 3) / 2 + 1;
+  g.M2 = g.B * g.T2 * g.F2;
+  g.q32 = 32 / g.F2;
+  g.r32 = 32 % g.F2;
+  return p;
+}
+
+extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
+  LASR_CHECK_ARG(a != nullptr, "lasr_conv2_gemm: null args");
+  LASR_CHECK_ARG(a->mode == LASR_CONV2_FWD || a->mode == LASR_CONV2_DW || a->mode == LASR_CONV2_DX,
+                 "lasr_conv2_gemm: bad mode");
+  LASR_CHECK_ARG(a->B > 0 && a->T1 >= 3 && a->F1 >= 3 && a->C > 0 && a->C % 128 == 0,
+                 "lasr_conv2_gemm: needs B > 0, T1, F1 >= 3 and C % 128 == 0");
+  LASR_CHECK_ARG((int64_t)a->B * a->T1 * a->F1 * a->C < (1LL << 31) && 9LL * a->C * a->C < (1LL << 31),
+                 "lasr_conv2_gemm: tensors past 2^31 elements");
+  LASR_CHECK_ARG(a->y1 && a->out && aligned16(a->y1) && aligned16(a->out), "lasr_conv2_gemm: y1/out");
+  GemmP p = conv_params(a);
+  const ConvG& g = p.cv;
+  const int C = a->C;
+  const int64_t kpad = cdiv(g.M2, 32) * 32;
+  if (a->mode != LASR_CONV2_FWD)
+    LASR_CHECK_ARG(a->dy2 && aligned16(a->dy2) && a->dy2_rows >= kpad && a->dy2_rows >= g.M2 + 1,
+                   "lasr_conv2_gemm: dy2 needs >= max(roundup32(M2), M2 + 1) rows, the tail zero");
+  if (a->mode != LASR_CONV2_DW)
+    LASR_CHECK_ARG(a->w2p && aligned16(a->w2p), "lasr_conv2_gemm: w2p");
+  hipStream_t st = (hipStream_t)stream;
+  const int BN = C % 256 == 0 ? 256 : 128;
+  p.c_vec = 1;
+  if (a->mode == LASR_CONV2_FWD) {
+    LASR_CHECK_ARG(a->bias && aligned16(a->bias), "lasr_conv2_gemm: bias");
+    p.M = g.M2; p.N = C; p.K = 9 * C; p.kchunk = p.K;
+    p.A = a->y1; p.lda_m = 9 * C; p.lda_k = 1;
+    p.B = a->w2p; p.ldb_n = 9 * C; p.ldb_k = 1;
+    p.C = a->out; p.ldc = C;
+    p.bias = a->bias; p.bias_vec = 1; p.act = LASR_ACT_RELU;
+    p.epi_mode = 0;
+    dim3 grid((unsigned)(C / BN), (unsigned)cdiv(p.M, 128), 1);
+    LASR_CHECK_ARG(grid.y <= 65535, "lasr_conv2_gemm: grid too large");
+    if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, true, bf16_t, 3, 2, G_FWD><<<grid, 256, 0, st>>>(p);
+    else gemm_bf16_glds_kernel<128, 128, true, true, bf16_t, 3, 3, G_FWD><<<grid, 256, 0, st>>>(p);
+    return lasr_check_launch("lasr_conv2_gemm/fwd");
+  }
+  if (a->mode == LASR_CONV2_DW) {
+    p.M = C; p.N = 9 * C; p.K = (int)kpad;
+    p.A = a->dy2; p.lda_m = 1; p.lda_k = C;
+    p.B = a->y1; p.ldb_n = 1; p.ldb_k = 9 * C;
+    p.C = a->out; p.ldc = 9 * C;
+    p.epi_mode = 0; p.ws_vec = 1; p.v4 = 1;
+    const bool big = g_tile_m == 256 && C % 256 == 0;
+    const int TM = big ? 256 : 128, TN = big ? 256 : 128;
+    const int64_t tiles = (int64_t)(C / TM) * (9 * C / TN);
+    int split = 1;
+    const int kt = (int)(kpad / 32);
+    if (g_split > 0) split = g_split;
+    else while (tiles * split < 256 && kt / (split * 2) >= 16 && split * 2 <= 64) split *= 2;
+    const int64_t need = ((int64_t)split * C * 9 * C + (a->rowsum ? (int64_t)split * C : 0)) * 4;
+    if (split > 1 && (!a->workspace || a->workspace_bytes < need || !aligned16(a->workspace))) split = 1;
+    p.split_k = split;
+    p.kchunk = split > 1 ? (int)(cdiv(cdiv(kpad, split), 32) * 32) : (int)kpad;
+    p.ws = (float*)a->workspace;
+    p.rowsum = a->rowsum;
+    if (a->rowsum && split > 1) p.rs_ws = p.ws + (int64_t)split * C * 9 * C;
+    dim3 grid((unsigned)(9 * C / TN), (unsigned)(C / TM), (unsigned)split);
+    if (big) gemm_bf16_glds_kernel<256, 256, false, false, float, 3, 1, G_DW><<<grid, 256, 0, st>>>(p);
+    else if (g_stages >= 4) gemm_bf16_glds_kernel<128, 128, false, false, float, 4, 2, G_DW><<<grid, 256, 0, st>>>(p);
+    else gemm_bf16_glds_kernel<128, 128, false, false, float, 3, 3, G_DW><<<grid, 256, 0, st>>>(p);
+    int rc = lasr_check_launch("lasr_conv2_gemm/dw");
+    if (!rc && split > 1) {
+      const int64_t total = (int64_t)C * 9 * C;
+      const int nblk = (int)std::min<int64_t>(cdiv(total / 4, 256), 4096);
+      splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);
+      rc = lasr_check_launch("lasr_conv2_gemm/dw_reduce");
+    }
+    return rc;
+  }
+  // LASR_CONV2_DX: one launch per output parity class, heaviest (4 taps) first
+  p.N = C;
+  p.A = a->dy2; p.lda_m = C; p.lda_k = 1;
+  p.B = a->w2p; p.ldb_n = 1; p.ldb_k = 9 * C;
+  p.C = a->out; p.ldc = C;
+  p.aux = a->y1; p.aux_dtype = LASR_BF16; p.ldaux = C; p.aux_act = LASR_ACT_RELU; p.aux_vec = 1;
+  p.epi_mode = 1;
+  p.cv.zero = (const bf16_t*)a->dy2 + (int64_t)g.M2 * C;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int pt = cls >> 1, pf = cls & 1;
+    const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
+    p.cv.cls = cls;
+    p.M = g.B * nI * nJ;
+    p.K = (pt ? 1 : 2) * (pf ? 1 : 2) * C;
+    p.kchunk = p.K;
+    dim3 grid((unsigned)(C / BN), (unsigned)cdiv(p.M, 128), 1);
+    LASR_CHECK_ARG(grid.y <= 65535, "lasr_conv2_gemm: grid too large");
+    if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, false, bf16_t, 3, 2, G_DX><<<grid, 256, 0, st>>>(p);
+    else gemm_bf16_glds_kernel<128, 128, true, false, bf16_t, 3, 3, G_DX><<<grid, 256, 0, st>>>(p);
+    const int rc = lasr_check_launch("lasr_conv2_gemm/dx");
+    if (rc) return rc;
+  }
+  return LASR_OK;
 }

@@ -458,6 +458,49 @@ def col2im(dcol, y1, dy1):
     N.call("lasr_col2im3x3s2", ptr(dcol), dt(dcol), B, T1, F1, Cc, ptr(y1), ptr(dy1), stream())
 
 
+def conv2_dy2_rows(M2):
+    """Rows of the dy2 buffer lasr_conv2_gemm's backward modes need (rows M2.. zero)."""
+    return ((M2 + 1 + 31) // 32) * 32
+
+
+def _conv2(mode, y1, out, w2p=None, bias=None, dy2=None, rowsum=None):
+    B, T1, F1, Cc = y1.shape
+    assert y1.dtype == torch.bfloat16 and y1.is_contiguous() and out.is_contiguous()
+    a = N.Conv2Args()
+    a.mode, a.B, a.T1, a.F1, a.C = mode, B, T1, F1, Cc
+    a.y1, a.out = ptr(y1), ptr(out)
+    if w2p is not None:
+        assert w2p.dtype == torch.bfloat16 and w2p.is_contiguous() and tuple(w2p.shape) == (Cc, 9 * Cc)
+        a.w2p = ptr(w2p)
+    if bias is not None:
+        a.bias = ptr(bias)
+    if dy2 is not None:
+        assert dy2.dtype == torch.bfloat16 and dy2.is_contiguous() and dy2.shape[1] == Cc
+        a.dy2, a.dy2_rows = ptr(dy2), dy2.shape[0]
+    if rowsum is not None:
+        assert rowsum.dtype == torch.float32 and rowsum.is_contiguous() and rowsum.numel() == Cc
+        a.rowsum = ptr(rowsum)
+    if mode == N.CONV2_DW:
+        ws = WS.get(16 * (9 * Cc * Cc + Cc), y1.device)
+        a.workspace, a.workspace_bytes = ptr(ws), ws.numel() * 4
+    N.call("lasr_conv2_gemm", C.byref(a), stream())
+
+
+def conv2_fwd(y1, w2p, bias, y2):
+    """y2 [B*T2*F2, C] = relu(conv3x3s2(y1) + bias), y1 channels-last [B, T1, F1, C] bf16."""
+    _conv2(N.CONV2_FWD, y1, y2, w2p=w2p, bias=bias)
+
+
+def conv2_dw(dy2, y1, dw, rowsum=None):
+    """dw [C, 9C] fp32 = dy2^T im2col(y1) (dy2: conv2_dy2_rows(M2) rows, tail zero)."""
+    _conv2(N.CONV2_DW, y1, dw, dy2=dy2, rowsum=rowsum)
+
+
+def conv2_dx(dy2, w2p, y1, dy1):
+    """dy1 [B, T1, F1, C] bf16 = col2im(dy2 w2p) * relu'(y1)."""
+    _conv2(N.CONV2_DX, y1, dy1, w2p=w2p, dy2=dy2)
+
+
 def permute_last2(src, Nn, A, Bd, dst, reverse=False, accumulate=False):
     N.call("lasr_permute_last2", ptr(src), dt(src), Nn, A, Bd, ptr(dst), dt(dst), int(reverse),
            int(accumulate), stream())

@@ -353,6 +353,12 @@ def conv_backward(gb, ln, sv, w, g, env):
     return dln
 
 
+def _conv2_implicit(adt, C):
+    """conv2 on the implicit-GEMM instances (bf16 build, C % 128 == 0); LASR_CONV2_IM2COL=1
+    keeps the explicit im2col path (A/B measurements)."""
+    return adt == torch.bfloat16 and C % 128 == 0 and os.environ.get("LASR_CONV2_IM2COL", "0") != "1"
+
+
 # ============================================================ autograd nodes ====
 class EmbedFn(torch.autograd.Function):
     """Conv2DLayer (liteasr/nets/subsampling.py:42-48) + RelativePositionalEncoding's
@@ -371,16 +377,21 @@ class EmbedFn(torch.autograd.Function):
         xs = xs.contiguous()
         y1 = _e((B, T1, F1, C), adt, dev)
         K.conv1_fwd(xs, w.W1, w.b1, y1)
-        col = _e((B * T2 * F2, 9 * C), adt, dev)
-        K.im2col(y1, col)
         y2 = _e((B * T2 * F2, C), adt, dev)
-        K.linear(col, w.W2p, y2, bias=w.b2, act=ACT_RELU)
+        implicit = _conv2_implicit(adt, C)
+        if implicit:  # conv2 as implicit GEMM: im2col(y1) is never materialised
+            col = None
+            K.conv2_fwd(y1, w.W2p, w.b2, y2)
+        else:  # fp32 parity build: explicit im2col + GEMM
+            col = _e((B * T2 * F2, 9 * C), adt, dev)
+            K.im2col(y1, col)
+            K.linear(col, w.W2p, y2, bias=w.b2, act=ACT_RELU)
         xl = _e((B * T2, w.d), F32, dev)
         y2f = y2.view(B * T2, F2 * C)
         K.linear(y2f, w.Woutp, xl, bias=w.bout)
         x0 = _e((B * T2, w.d), F32, dev)
         K.pe_fwd(xl, B * T2, T2, w.d, None, math.sqrt(w.d), x0, env.p_pos, env.seed + 1)
-        ctx.sv = SimpleNamespace(xs=xs, y1=y1, col=col, y2=y2, dims=(B, T1, F1, T2, F2, C))
+        ctx.sv = SimpleNamespace(xs=xs, y1=y1, col=col, y2=y2, dims=(B, T1, F1, T2, F2, C), implicit=implicit)
         ctx.mod, ctx.env = mod, env
         return x0
 
@@ -398,16 +409,28 @@ class EmbedFn(torch.autograd.Function):
         dWo = _e((d, F2 * C), F32, dev)
         K.gemm(gb.t(), y2f, dWo, split_k=0, rowsum=g.bout)
         K.permute_last2(dWo, d, C, F2, g.out_w, reverse=True, accumulate=True)
-        dy2 = _e((M, F2 * C), adt, dev)
-        K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
-        dy2 = dy2.view(M * F2, C)
+        M2 = M * F2
         dW2 = _e((C, 9 * C), F32, dev)
-        K.gemm(dy2.t(), sv.col, dW2, split_k=0, rowsum=g.b2)
-        K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
-        dcol = _e((M * F2, 9 * C), adt, dev)
-        K.gemm(dy2, w.W2p, dcol)
         dy1 = torch.empty_like(sv.y1)
-        K.col2im(dcol, sv.y1, dy1)
+        if sv.implicit:
+            # dy2 with the zero tail rows the implicit backward GEMMs read (k padding, taps
+            # outside dy2); dW2 = dy2^T im2col(y1), dy1 = col2im(dy2 W2p) * relu'(y1)
+            dy2_full = _e((K.conv2_dy2_rows(M2), C), adt, dev)
+            dy2_full[M2:].zero_()
+            dy2 = dy2_full[:M2].view(M, F2 * C)
+            K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
+            K.conv2_dw(dy2_full, sv.y1, dW2, rowsum=g.b2)
+            K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
+            K.conv2_dx(dy2_full, w.W2p, sv.y1, dy1)
+        else:
+            dy2 = _e((M, F2 * C), adt, dev)
+            K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
+            dy2 = dy2.view(M2, C)
+            K.gemm(dy2.t(), sv.col, dW2, split_k=0, rowsum=g.b2)
+            K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
+            dcol = _e((M2, 9 * C), adt, dev)
+            K.gemm(dy2, w.W2p, dcol)
+            K.col2im(dcol, sv.y1, dy1)
         K.conv1_bwd(sv.xs, dy1, g.W1, g.b1)
         mod.on_grads_ready()
         return None, None, None, None

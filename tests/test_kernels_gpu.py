@@ -607,6 +607,69 @@ def test_subsampling_convs(dtype):
     close(acc, 1 + w2p.float().view(Cc, 9, Cc).permute(0, 2, 1), 1e-6, "permute rev")
 
 
+@pytest.mark.parametrize("B,T,Fd,Cc,ref64", [(2, 41, 80, 128, True), (2, 42, 81, 128, True), (3, 67, 40, 256, True),
+                                             (32, 1000, 80, 256, False)])
+def test_conv2_implicit_gemm(B, T, Fd, Cc, ref64):
+    """lasr_conv2_gemm (conv2 without im2col / col2im buffers) against the explicit im2col
+    path and, at small sizes, fp64 conv2d: forward bit-identical to im2col + GEMM (same k
+    order per output), weight / bias gradients within fp32 accumulation error, data gradient
+    within one bf16 rounding; odd and even T1/F1 (every output parity class, both edges), and
+    the full config-2 size (B 32, T 1000, 80-d)."""
+    from liteasr_amd import _native as Nn
+
+    kn = K()
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + T)
+    T1, F1 = (T - 3) // 2 + 1, (Fd - 3) // 2 + 1
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    M2 = B * T2 * F2
+    bf = torch.bfloat16
+    y1 = torch.relu(torch.randn(B, T1, F1, Cc, generator=g)).to(bf).to(DEV)
+    w2 = (torch.randn(Cc, Cc, 3, 3, generator=g) / (3 * Cc ** 0.5)).to(DEV)
+    b2 = (torch.randn(Cc, generator=g) * 0.1).to(DEV)
+    w2p = torch.empty(Cc, 9 * Cc, device=DEV, dtype=bf)
+    kn.permute_last2(w2.reshape(Cc, Cc, 9), Cc, Cc, 9, w2p)
+    # forward: implicit vs explicit
+    y2 = torch.empty(M2, Cc, device=DEV, dtype=bf)
+    kn.conv2_fwd(y1, w2p, b2, y2)
+    col = torch.empty(M2, 9 * Cc, device=DEV, dtype=bf)
+    kn.im2col(y1, col)
+    y2e = torch.empty_like(y2)
+    kn.linear(col, w2p, y2e, bias=b2, act=Nn.ACT_RELU)
+    assert torch.equal(y2.view(torch.int16), y2e.view(torch.int16)), "conv2 fwd != im2col + GEMM"
+    # backward operands: dy2 with its zero tail
+    rows = kn.conv2_dy2_rows(M2)
+    dy2f = torch.zeros(rows, Cc, device=DEV, dtype=bf)
+    dy2f[:M2] = (torch.randn(M2, Cc, generator=g) * (y2.float().cpu() > 0)).to(bf).to(DEV)
+    dy2 = dy2f[:M2]
+    dw = torch.empty(Cc, 9 * Cc, device=DEV)
+    db = torch.full((Cc,), 0.5, device=DEV)
+    kn.conv2_dw(dy2f, y1, dw, rowsum=db)
+    dy1 = torch.empty_like(y1)
+    kn.conv2_dx(dy2f, w2p, y1, dy1)
+    torch.cuda.synchronize()
+    dwe = torch.empty_like(dw)
+    kn.gemm(dy2.t(), col, dwe, split_k=0)
+    close(dw, dwe, 1e-5, "conv2 dW vs explicit")
+    close(db - 0.5, dy2.float().sum(0), 1e-5, "conv2 db")
+    if not ref64:
+        dcol = torch.empty_like(col)
+        kn.gemm(dy2, w2p, dcol)
+        dy1e = torch.empty_like(y1)
+        kn.col2im(dcol, y1, dy1e)
+        close(dy1, dy1e, 2e-2, "conv2 dX vs explicit")
+        return
+    y1r = y1.double().permute(0, 3, 1, 2).requires_grad_()
+    w2r = w2p.double().view(Cc, 3, 3, Cc).permute(0, 3, 1, 2).contiguous().requires_grad_()
+    pre = F.conv2d(y1r, w2r, b2.double(), stride=2)
+    close(y2.view(B, T2, F2, Cc), F.relu(pre).permute(0, 2, 3, 1), 1e-2, "conv2 fwd vs fp64")
+    gy1, gw = torch.autograd.grad(pre, (y1r, w2r), dy2.double().view(B, T2, F2, Cc).permute(0, 3, 1, 2))
+    close(dw.view(Cc, 3, 3, Cc), gw.permute(0, 2, 3, 1), 1e-5, "conv2 dW vs fp64")
+    ref = (gy1 * (y1r > 0)).permute(0, 2, 3, 1)
+    close(dy1, ref, 8e-3, "conv2 dX vs fp64")
+    # every position written (no stale values): masked positions exactly zero
+    assert torch.equal(dy1[y1 <= 0].float(), torch.zeros_like(dy1[y1 <= 0].float()))
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("Cc,T", [(64, 70), (200, 133)])
 def test_conformer_conv_module_pieces(dtype, Cc, T):
