@@ -315,6 +315,30 @@ typedef struct lasr_conv2_args {
   void* workspace; int64_t workspace_bytes;
 } lasr_conv2_args;
 int lasr_conv2_gemm(const lasr_conv2_args* args, void* stream);
+/* ---- Paraformer CIF predictor (liteasr/nets/paraformer/predictor.py:24-118) ----------
+ * fwd: alpha[b,t] = t < plen[b] ? sigmoid(z[b,t]) : 0; sum_alpha[b] = sum_t alpha;
+ *      beta = sum_alpha / ylen - 1e-4; integrate-and-fire over t (the reference's update
+ *      rules, incl. state += (beta - acc) * h on non-firing frames); fired states with a
+ *      non-zero |.|-sum go to out[b, 0..] in time order (rows past U dropped), the rest of
+ *      out[b] is zero.  Keeps alpha, acc (accumulated weight after t), fired (u8) and row
+ *      (output row of frame t, -1 for none) for the backward; mae[b] = |sum_alpha - ylen|
+ *      (nullable).  h [B,T,D] fp32, D in {64, 128, 256, 512, 1024}.
+ * bwd: from gout [B,U,D] and gsum [B] (the loss gradients of out and sum_alpha, both
+ *      nullable): dz [B,T] (the gradient of the predictor logits, zero past plen) and
+ *      dh [B,T,D] (written). */
+typedef struct lasr_cif_args {
+  int B, T, D, U;
+  const float* z; const int* plen; const int* ylen; const float* h;
+  float* alpha; float* acc; uint8_t* fired; int* row; float* sum_alpha; float* mae; float* out;
+  const float* gout; const float* gsum; float* dz; float* dh;
+} lasr_cif_args;
+int lasr_cif_fwd(const lasr_cif_args* args, void* stream);
+int lasr_cif_bwd(const lasr_cif_args* args, void* stream);
+/* Glancing sampler mix (liteasr/nets/paraformer/glancing_sampler.py:32), fp32 [rows, D],
+ * replace u8 [rows]: fwd out = replace ? a : b; bwd (a = the incoming gradient)
+ * out = replace ? a : 0 (embedding branch), out2 = replace ? 0 : a (CIF branch). */
+int lasr_glancing_mix(int64_t rows, int D, const uint8_t* replace, const float* a, const float* b,
+                      float* out, float* out2, int backward, void* stream);
 /* Transpose the last two dims of [N][A][Bd] into [N][Bd][A] (fp32 -> dst dtype), or
  * (reverse=1) [N][Bd][A] -> [N][A][Bd] with optional accumulate into fp32. */
 int lasr_permute_last2(const void* src, int sdt, int64_t N, int64_t A, int64_t Bd, void* dst,

@@ -80,6 +80,17 @@ class Conv2Args(C.Structure):
 CONV2_FWD, CONV2_DW, CONV2_DX = 0, 1, 2
 
 
+class CifArgs(C.Structure):
+    """Mirror of ``lasr_cif_args``."""
+
+    _fields_ = [
+        ("B", _i), ("T", _i), ("D", _i), ("U", _i),
+        ("z", _p), ("plen", _p), ("ylen", _p), ("h", _p),
+        ("alpha", _p), ("acc", _p), ("fired", _p), ("row", _p), ("sum_alpha", _p), ("mae", _p), ("out", _p),
+        ("gout", _p), ("gsum", _p), ("dz", _p), ("dh", _p),
+    ]
+
+
 class ReduceSeg(C.Structure):
     """Mirror of ``lasr_reduce_seg``."""
 
@@ -123,6 +134,9 @@ SIGNATURES = {
     "lasr_conv1_fwd": [_p, _i, _i, _i, _i, _p, _p, _p, _i, _p],
     "lasr_conv1_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _l, _p],
     "lasr_conv2_gemm": [C.POINTER(Conv2Args), _p],
+    "lasr_cif_fwd": [C.POINTER(CifArgs), _p],
+    "lasr_cif_bwd": [C.POINTER(CifArgs), _p],
+    "lasr_glancing_mix": [_l, _i, _p, _p, _p, _p, _p, _i, _p],
     "lasr_im2col3x3s2": [_p, _i, _i, _i, _i, _i, _p, _p],
     "lasr_col2im3x3s2": [_p, _i, _i, _i, _i, _i, _p, _p, _p],
     "lasr_permute_last2": [_p, _i, _l, _l, _l, _p, _i, _i, _i, _p],

@@ -1283,7 +1283,7 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     int split = 1;
     const int kt = (int)(kpad / 32);
     if (g_split > 0) split = g_split;
-    else while (tiles * split < 256 && kt / (split * 2) >= 16 && split * 2 <= 64) split *= 2;
+    else while (tiles * split < 512 && kt / (split * 2) >= 16 && split * 2 <= 64) split *= 2;
     const int64_t need = ((int64_t)split * C * 9 * C + (a->rowsum ? (int64_t)split * C : 0)) * 4;
     if (split > 1 && (!a->workspace || a->workspace_bytes < need || !aligned16(a->workspace))) split = 1;
     p.split_k = split;

@@ -334,7 +334,7 @@ extern "C" int lasr_colsum(const void* X, int dtype, int64_t M, int64_t N, int64
       else colsum_partial_kernel<bf16_t, false><<<g1, 256, 0, st>>>((const bf16_t*)X, M, N, ldx, rpc, workspace);
     }
   } else {
-    hipMemsetAsync(workspace, 0, N * sizeof(float), st);
+    if (hipMemsetAsync(workspace, 0, N * sizeof(float), st) != hipSuccess) return lasr_check_launch("colsum/memset");
   }
   int rc = lasr_check_launch("colsum");
   if (rc) return rc;

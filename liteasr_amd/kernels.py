@@ -656,3 +656,35 @@ def logsoftmax_topk(logits, k, rows=None, ld=None, gather_idx=None):
     N.call("lasr_logsoftmax_topk", ptr(logits), dt(logits), rows, V, ld, k, ptr(gather_idx),
            ptr(vals) if k > 0 else None, ptr(idx) if k > 0 else None, ptr(gat), stream())
     return vals, idx, gat
+
+
+# ------------------------------------------------------------ Paraformer CIF ---
+def cif_fwd(z, plen, ylen, h, B, T, U, st):
+    """Integrate-and-fire forward (lasr_cif_fwd); st: SimpleNamespace receiving alpha, acc,
+    fired, row, sum_alpha, mae and out ([B, U, D] fp32)."""
+    D = h.shape[-1]
+    a = N.CifArgs()
+    a.B, a.T, a.D, a.U = B, T, D, U
+    a.z, a.plen, a.ylen, a.h = ptr(z), ptr(plen), ptr(ylen), ptr(h)
+    a.alpha, a.acc, a.fired, a.row = ptr(st.alpha), ptr(st.acc), ptr(st.fired), ptr(st.row)
+    a.sum_alpha, a.mae, a.out = ptr(st.sum_alpha), ptr(st.mae), ptr(st.out)
+    N.call("lasr_cif_fwd", C.byref(a), stream())
+
+
+def cif_bwd(plen, ylen, h, B, T, U, st, gout, gsum, dz, dh):
+    D = h.shape[-1]
+    a = N.CifArgs()
+    a.B, a.T, a.D, a.U = B, T, D, U
+    a.plen, a.ylen, a.h = ptr(plen), ptr(ylen), ptr(h)
+    a.alpha, a.acc, a.fired, a.row, a.sum_alpha = ptr(st.alpha), ptr(st.acc), ptr(st.fired), ptr(st.row), \
+        ptr(st.sum_alpha)
+    a.gout, a.gsum, a.dz, a.dh = ptr(gout), ptr(gsum), ptr(dz), ptr(dh)
+    N.call("lasr_cif_bwd", C.byref(a), stream())
+
+
+def glancing_mix(replace, a, b, out, out2=None, backward=False):
+    """fwd: out = replace ? a : b; bwd (a = incoming gradient): out / out2 = the
+    embedding / CIF branch gradients.  fp32 [rows, D], replace u8 [rows]."""
+    rows, D = out.shape
+    N.call("lasr_glancing_mix", rows, D, ptr(replace), ptr(a), ptr(b), ptr(out), ptr(out2), int(backward),
+           stream())

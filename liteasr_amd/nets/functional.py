@@ -524,6 +524,74 @@ def _rows2d(g, rows):
     return g2 if g2.stride(1) == 1 else g2.contiguous()
 
 
+def decoder_layers_fwd(dec, wd, y, h, B, L1, T, masks, p, adt, seed_shift=0):
+    """Decoder layers + after_norm + linear_out (transformer_decoder.py:84-93,
+    transformer_layer.py:179-221; also ParallelDecoder, parallel_decoder.py:54-66) on the
+    fp32 input rows y [B*L1, d]; memory h [B*T, d] (compute dtype).  masks = (self mask,
+    its batch stride, its query stride (0: key padding), memory key mask); p = dropout
+    rates (residual, ffn, self-attn, src-attn).  Returns (h_attn [B*L1, V] padded rows,
+    saved state for decoder_layers_bwd)."""
+    smask, smsb, smsq, mmask = masks
+    pd, pff, pat, pca = p
+    R = B * L1
+    layers_sv = []
+    for i, lw in enumerate(wd.layers):
+        s = dec.dec_layers[i].seed + seed_shift
+        l1, _, m1, r1 = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
+        y1, sa = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, smask, smsb, smsq, y, pat, _seed(s, 1), pd,
+                             _seed(s, 2))
+        l2, _, m2, r2 = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
+        y2, ca = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, mmask, T, 0, y1, pca, _seed(s, 3), pd, _seed(s, 4))
+        l3, _, m3, r3 = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)
+        y3, z, hh = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, pff, _seed(s, 5), y2, 1.0, pd,
+                                _seed(s, 6))
+        layers_sv.append(SimpleNamespace(y=(y, y1, y2), ln=(l1, l2, l3), st=((m1, r1), (m2, r2), (m3, r3)), sa=sa,
+                                         ca=ca, z=z, hh=hh))
+        y = y3
+    yf, _, mf, rf = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
+    h_attn = K.padded_rows(R, wd.Wout.shape[0], adt, y.device)
+    K.linear(yf, wd.Wout, h_attn, bias=wd.bout)
+    return h_attn, SimpleNamespace(layers=layers_sv, yL=y, yf=yf, mf=mf, rf=rf, p=p, masks=masks,
+                                   seed_shift=seed_shift)
+
+
+def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
+    """Backward of decoder_layers_fwd: parameter gradients into gd, the memory gradient
+    accumulated into dh [B*T, d] fp32; returns the gradient of the input rows (fp32)."""
+    smask, smsb, smsq, mmask = sv.masks
+    pd, pff, pat, pca = sv.p
+    dev = g_attn.device
+    R, d = B * L1, wd.d
+    K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0, rowsum=gd.bout)
+    dyf = _e((R, d), adt, dev)
+    K.gemm(g_attn, wd.Wout, dyf)
+    dy = _e((R, d), F32, dev)
+    K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
+    gb = _e((R, d), adt, dev)
+    for i in range(len(wd.layers) - 1, -1, -1):
+        lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
+        s = dec.dec_layers[i].seed + sv.seed_shift
+        y0, y1, y2 = ls.y
+        l1, l2, l3 = ls.ln
+        (m1, r1), (m2, r2), (m3, r3) = ls.st
+        K.branch_grad(dy, gb, 1.0, pd, _seed(s, 6))
+        dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1, lg.ff.W2, lg.ff.b2,
+                           ACT_RELU, pff, _seed(s, 5))
+        dy2 = _e((R, d), F32, dev)
+        K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb, bscale=1.0, bp=pd,
+                        bseed=_seed(s, 4))
+        dln = mha_backward(gb, l2, h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, mmask, T, 0, pca, _seed(s, 3), dh)
+        dy1 = _e((R, d), F32, dev)
+        K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb, bscale=1.0, bp=pd,
+                        bseed=_seed(s, 2))
+        dln = mha_backward(gb, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, smask, smsb, smsq, pat,
+                           _seed(s, 1), None)
+        dy0 = _e((R, d), F32, dev)
+        K.layernorm_bwd(y0, dln, lw.ln1.g, m1, r1, dy0, lg.ln1.g, lg.ln1.b, dres=dy1)
+        dy = dy0
+    return dy
+
+
 class HeadsFn(torch.autograd.Function):
     """Encoder after_norm (transformer_encoder.py:126), CTC head with its always-on
     input dropout (ctc.py:28-30) and the full Transformer decoder
@@ -546,34 +614,14 @@ class HeadsFn(torch.autograd.Function):
         # ---- decoder
         wd = dec.weights()
         d = wd.d
-        pd = env.p_dec if tr else 0.0
-        pff = env.p_dec_ff if tr else 0.0
-        pat = env.p_dec_att if tr else 0.0
-        pca = env.p_dec_src_att if tr else 0.0
+        p = (env.p_dec if tr else 0.0, env.p_dec_ff if tr else 0.0, env.p_dec_att if tr else 0.0,
+             env.p_dec_src_att if tr else 0.0)
         y = _e((R, d), F32, dev)
         K.embed_pe_fwd(env.ys_in, L1, wd.E, wd.pe, math.sqrt(d), y, env.p_dec_pos if tr else 0.0,
                        env.seed + 3)
-        layers_sv = []
-        for i, lw in enumerate(wd.layers):
-            s = dec.dec_layers[i].seed
-            l1, _, m1, r1 = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
-            y1, sa = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, env.dec_mask, L1 * L1, L1, y,
-                                 pat, _seed(s, 1), pd, _seed(s, 2))
-            l2, _, m2, r2 = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
-            y2, ca = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, env.mask_k, T, 0, y1, pca,
-                                 _seed(s, 3), pd, _seed(s, 4))
-            l3, _, m3, r3 = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)
-            y3, z, hh = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, pff,
-                                    _seed(s, 5), y2, 1.0, pd, _seed(s, 6))
-            layers_sv.append(SimpleNamespace(y=(y, y1, y2), ln=(l1, l2, l3),
-                                             st=((m1, r1), (m2, r2), (m3, r3)), sa=sa, ca=ca, z=z,
-                                             hh=hh))
-            y = y3
-        yf, _, mf, rf = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
-        h_attn = K.padded_rows(R, V, adt, dev)
-        K.linear(yf, wd.Wout, h_attn, bias=wd.bout)
-        ctx.sv = SimpleNamespace(x=x, h=h, hd=hd, me=me, re=re, layers=layers_sv, yL=y, yf=yf,
-                                 mf=mf, rf=rf, p=(pd, pff, pat, pca))
+        masks = (env.dec_mask, L1 * L1, L1, env.mask_k)
+        h_attn, dsv = decoder_layers_fwd(dec, wd, y, h, B, L1, T, masks, p, adt)
+        ctx.sv = SimpleNamespace(x=x, h=h, hd=hd, me=me, re=re, dec=dsv)
         ctx.model, ctx.env = model, env
         return h_attn, h_ctc
 
@@ -584,7 +632,6 @@ class HeadsFn(torch.autograd.Function):
         dev, adt = sv.x.device, env.adt
         B, T, L1 = env.B, env.T, env.L1
         M, R = B * T, B * L1
-        pd, pff, pat, pca = sv.p
         d_enc = sv.x.shape[1]
         dh = _e((M, d_enc), F32, dev)  # accumulated gradient of h_enc
         # ---- CTC head
@@ -603,35 +650,7 @@ class HeadsFn(torch.autograd.Function):
         d = wd.d
         with K.deferred_reductions():  # decoder parameter-gradient reductions: one launch
             if g_attn is not None:
-                g_attn = _rows2d(g_attn, R)
-                K.gemm(g_attn.t(), sv.yf, gd.Wout, beta=1.0, split_k=0, rowsum=gd.bout)
-                dyf = _e((R, d), adt, dev)
-                K.gemm(g_attn, wd.Wout, dyf)
-                dy = _e((R, d), F32, dev)
-                K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
-                gb = _e((R, d), adt, dev)
-                for i in range(len(wd.layers) - 1, -1, -1):
-                    lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
-                    s = dec.dec_layers[i].seed
-                    y0, y1, y2 = ls.y
-                    l1, l2, l3 = ls.ln
-                    (m1, r1), (m2, r2), (m3, r3) = ls.st
-                    K.branch_grad(dy, gb, 1.0, pd, _seed(s, 6))
-                    dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1,
-                                       lg.ff.W2, lg.ff.b2, ACT_RELU, pff, _seed(s, 5))
-                    dy2 = _e((R, d), F32, dev)
-                    K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb,
-                                    bscale=1.0, bp=pd, bseed=_seed(s, 4))
-                    dln = mha_backward(gb, l2, sv.h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, env.mask_k, T,
-                                       0, pca, _seed(s, 3), dh)
-                    dy1 = _e((R, d), F32, dev)
-                    K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb,
-                                    bscale=1.0, bp=pd, bseed=_seed(s, 2))
-                    dln = mha_backward(gb, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, env.dec_mask,
-                                       L1 * L1, L1, pat, _seed(s, 1), None)
-                    dy0 = _e((R, d), F32, dev)
-                    K.layernorm_bwd(y0, dln, lw.ln1.g, m1, r1, dy0, lg.ln1.g, lg.ln1.b, dres=dy1)
-                    dy = dy0
+                dy = decoder_layers_bwd(_rows2d(g_attn, R), sv.dec, dec, wd, gd, sv.h, B, L1, T, dh, adt)
                 K.embed_bwd(env.ys_in, dy, math.sqrt(d), gd.E, env.p_dec_pos if env.training else 0.0,
                             env.seed + 3)
         dec.on_grads_ready()
@@ -642,6 +661,166 @@ class HeadsFn(torch.autograd.Function):
         enc.after_norm_ready()
         ctx.sv = None
         return dx, None, None, None
+
+
+class ParaformerHeadsFn(torch.autograd.Function):
+    """Everything of Paraformer.forward after the conformer layers (liteasr/models/
+    paraformer.py:97-113): encoder after_norm, the CIF predictor (predictor.py:24-118:
+    conv1d k3 + ReLU and linear + sigmoid as GEMMs, the integrate-and-fire scan in
+    csrc/cif.hip), target embedding + PE, the no-grad first decoder pass and its argmax,
+    the glancing sampler (host ``random.sample`` per utterance, the reference's RNG calls),
+    the mix and the second decoder pass.  Returns (hs_attn [B*L, V], sum_alpha [B])."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, model, env, ys, ylens_host, rng):
+        dev, adt = x.device, env.adt
+        enc, dec, pr = model.encoder, model.decoder, model.predictor
+        B, T = env.B, env.T
+        L = ys.shape[1]
+        M, R = B * T, B * L
+        tr = env.training
+        x = x.contiguous()
+        d = x.shape[1]
+        # ---- encoder after_norm: fp32 for the predictor, compute dtype for the decoder memory
+        we = enc.after_norm_weights()
+        h32, me, re = _e((M, d), F32, dev), _e(M, F32, dev), _e(M, F32, dev)
+        K.layernorm_fwd(x, we.g, we.b, LN_EPS, h32, me, re)
+        hm = h32.to(adt)
+        # ---- predictor: conv1d(k3, pad 1) as one GEMM over overlapping row windows of a
+        # zero-padded copy, then the scalar head
+        wp = pr.weights()
+        xpad = torch.zeros(B, T + 2, d, dtype=adt, device=dev)
+        xpad[:, 1:T + 1] = hm.view(B, T, d)
+        wc = _e((d, 3 * d), adt, dev)
+        K.permute_last2(wp.Wc.reshape(d, d, 3), d, d, 3, wc)  # [out][in][tap] -> [out][tap][in]
+        win = xpad.as_strided((B, T, 3 * d), ((T + 2) * d, d, 1))
+        cv = _e((B, T, d), adt, dev)
+        K.gemm(win, wc.t().unsqueeze(0).expand(B, 3 * d, d), cv, bias=wp.bc, act=ACT_RELU)
+        z = _e((M, 1), F32, dev)
+        K.gemm(cv.view(M, d), wp.Wl.t(), z, bias=wp.bl)
+        # ---- CIF
+        plen = env.pred_len
+        ylen = env.ylen
+        cs = SimpleNamespace(alpha=_e(M, F32, dev), acc=_e(M, F32, dev), fired=_e(M, torch.uint8, dev),
+                             row=_e(M, torch.int32, dev), sum_alpha=_e(B, F32, dev), mae=_e(B, F32, dev),
+                             out=_e((B, L, d), F32, dev))
+        K.cif_fwd(z, plen, ylen, h32, B, T, L, cs)
+        # ---- target embedding + PE (paraformer.py:103)
+        eos = model.eos
+        ys_in = ys.masked_fill(ys == model.ignore, eos).to(torch.int32).contiguous()
+        emb = _e((R, d), F32, dev)
+        p_pos = model.pos_dropout_rate if tr else 0.0
+        K.embed_pe_fwd(ys_in, L, model.embed_weight(), model.pe.table(L), math.sqrt(d), emb, p_pos, env.seed + 5)
+        # ---- first decoder pass, no grad (paraformer.py:106-109)
+        wd = dec.weights()
+        rates = dec.rates
+        p = (rates.drop if tr else 0.0, rates.ff if tr else 0.0, rates.self_att if tr else 0.0,
+             rates.src_att if tr else 0.0)
+        nomask = torch.zeros(B, L, dtype=torch.uint8, device=dev)
+        masks = (nomask, L, 0, env.mask_k)
+        cif_rows = cs.out.view(R, d)
+        hat, _ = decoder_layers_fwd(dec, wd, cif_rows, hm, B, L, T, masks, p, adt, seed_shift=8)
+        _, ids, _ = K.logsoftmax_topk(hat, 1)
+        # ---- glancing sampler on the host (glancing_sampler.py:16-30)
+        ys_hat = ids.view(B, L).long().cpu()
+        ys_in_h = ys_in.cpu().long()
+        pad = torch.arange(L)[None, :] >= ylens_host[:, None]
+        ys_hat = ys_hat.masked_fill(pad, eos)
+        num = torch.ceil(model.sample_ratio * (ys_hat != ys_in_h).sum(-1)).long()
+        rep = torch.zeros(B, L, dtype=torch.uint8)
+        for b in range(B):
+            rep[b, rng.sample(range(int(ylens_host[b])), int(num[b]))] = 1
+        rep = rep.to(dev)
+        mix = _e((R, d), F32, dev)
+        K.glancing_mix(rep, emb, cif_rows, mix)
+        # ---- second pass, with gradients
+        hs_attn, dsv = decoder_layers_fwd(dec, wd, mix, hm, B, L, T, masks, p, adt)
+        model.last_glance = SimpleNamespace(ys_hat=ys_hat, replace=rep.cpu().bool(), cif=cs)
+        ctx.sv = SimpleNamespace(x=x, me=me, re=re, h32=h32, hm=hm, xpad=xpad, cv=cv, cs=cs, rep=rep,
+                                 ys_in=ys_in, dec=dsv, dims=(B, T, L, d), p_pos=p_pos)
+        ctx.model, ctx.env = model, env
+        return hs_attn, cs.sum_alpha
+
+    @staticmethod
+    def backward(ctx, g_attn, g_sum):
+        sv, model, env = ctx.sv, ctx.model, ctx.env
+        enc, dec, pr = model.encoder, model.decoder, model.predictor
+        B, T, L, d = sv.dims
+        M, R = B * T, B * L
+        dev, adt = sv.x.device, env.adt
+        dh = torch.zeros(M, d, dtype=F32, device=dev)  # gradient of the after_norm output
+        wd, gd = dec.weights(), dec.grads()
+        with K.deferred_reductions():
+            if g_attn is not None:
+                dmix = decoder_layers_bwd(_rows2d(g_attn, R), sv.dec, dec, wd, gd, sv.hm, B, L, T, dh, adt)
+            else:
+                dmix = torch.zeros(R, d, dtype=F32, device=dev)
+        dec.on_grads_ready()
+        g_emb, g_cif = _e((R, d), F32, dev), _e((R, d), F32, dev)
+        K.glancing_mix(sv.rep, dmix, None, g_emb, g_cif, backward=True)
+        K.embed_bwd(sv.ys_in, g_emb, math.sqrt(d), model.embed_grad(), sv.p_pos, env.seed + 5)
+        # ---- CIF backward -> predictor logits / encoder output
+        dz = _e(M, F32, dev)
+        dh_cif = _e((B, T, d), F32, dev)
+        gs = g_sum.contiguous().float() if g_sum is not None else None
+        K.cif_bwd(env.pred_len, env.ylen, sv.h32, B, T, L, sv.cs, g_cif, gs, dz, dh_cif)
+        # ---- predictor head and conv1d backward
+        wp, gp = pr.weights(), pr.grads()
+        dza = dz.to(adt).view(M, 1)
+        K.gemm(dza.t(), sv.cv.view(M, d), gp.Wl, beta=1.0, rowsum=gp.bl)
+        dpre = _e((M, d), adt, dev)
+        K.gemm(dza, wp.Wl, dpre, aux=sv.cv.view(M, d), aux_act=ACT_RELU)
+        P = torch.zeros(B, T + 2, d, dtype=adt, device=dev)
+        P[:, 1:T + 1] = dpre.view(B, T, d)
+        Pk = P.view(-1, d)[1:-1]
+        kw = Pk.shape[0]
+        win = sv.xpad.view(-1)[: (kw - 1) * d + 3 * d].as_strided((kw, 3 * d), (d, 1))
+        dwc = _e((d, 3 * d), F32, dev)
+        K.gemm(Pk.t(), win, dwc, split_k=0, rowsum=gp.bc)
+        K.permute_last2(dwc, d, d, 3, gp.Wc.view(d, d, 3), reverse=True, accumulate=True)
+        wflip = wp.Wc.reshape(d, d, 3).flip(-1).permute(1, 2, 0).reshape(d, 3 * d).to(adt)
+        pwin = P.as_strided((B, T, 3 * d), ((T + 2) * d, d, 1))
+        dh_pred = _e((B, T, d), F32, dev)
+        K.gemm(pwin, wflip.t().unsqueeze(0).expand(B, 3 * d, d), dh_pred)
+        pr.on_grads_ready()
+        dh += dh_cif.view(M, d)
+        dh += dh_pred.view(M, d)
+        # ---- encoder after_norm
+        we, ge = enc.after_norm_weights(), enc.after_norm_grads()
+        dx = _e((M, d), F32, dev)
+        K.layernorm_bwd(sv.x, dh, we.g, sv.me, sv.re, dx, ge.g, ge.b)
+        enc.after_norm_ready()
+        ctx.sv = None
+        return dx, None, None, None, None, None, None
+
+
+class ParaformerLossFn(torch.autograd.Function):
+    """ParaformerLoss.__call__ (liteasr/criterions/paraformer_loss.py:39-56):
+    gamma * CE(hs_attn, ys; ignore -1, mean over targets) + mean |sum_alpha - ylens|."""
+
+    @staticmethod
+    def forward(ctx, hs_attn, sum_alpha, ys, ylens, count, gamma, cif):
+        dev = hs_attn.device
+        R, V = hs_attn.shape
+        B = sum_alpha.shape[0]
+        tgt = ys.reshape(-1).to(torch.int32).contiguous()
+        lse, rows = _e(R, F32, dev), _e(R, F32, dev)
+        K.lsm_kl_fwd(hs_attn, tgt, -1, 0.0, lse, rows)
+        loss = _e(1, F32, dev)
+        K.loss_combine(rows, gamma / max(count, 1), cif.mae, 1.0 / B, loss)
+        ctx.sv = SimpleNamespace(ha=hs_attn, tgt=tgt, lse=lse, scale=gamma / max(count, 1), B=B,
+                                 sign=torch.sign(sum_alpha.detach() - ylens.to(F32)))
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        sv = ctx.sv
+        g = g.contiguous().float()
+        ga = K.padded_rows(sv.ha.shape[0], sv.ha.shape[1], sv.ha.dtype, g.device)
+        K.lsm_kl_bwd(sv.ha, sv.tgt, -1, 0.0, sv.lse, ga, sv.scale, gdev=g)
+        gsum = sv.sign * (g / sv.B)
+        ctx.sv = None
+        return ga, gsum, None, None, None, None, None
 
 
 class HybridLossFn(torch.autograd.Function):

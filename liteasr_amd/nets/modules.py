@@ -443,3 +443,61 @@ class CTC(_Bound):
 
     def grads(self):
         return self._cached("g", lambda: SimpleNamespace(W=self._g("ctc_lo.weight"), b=self._g("ctc_lo.bias")))
+
+
+class ParallelDecoder(_Bound):
+    """liteasr/nets/paraformer/parallel_decoder.py:10-66: the Transformer decoder layers
+    without embedding / positional encoding (the input is the CIF output mixed with target
+    embeddings) and without a self-attention mask."""
+
+    def __init__(self, i_dim, h_dim, ff_dim, n_head, n_layer, dropout_rate, self_attn_dropout_rate,
+                 src_attn_dropout_rate, ff_dropout_rate):
+        super().__init__()
+        self.dec_layers = nn.ModuleList([
+            DecoderLayer(
+                size=h_dim,
+                self_attn=MultiHeadAttention(n_head=n_head, i_dim=h_dim, dropout_rate=self_attn_dropout_rate),
+                src_attn=MultiHeadAttention(n_head=n_head, i_dim=h_dim, dropout_rate=src_attn_dropout_rate),
+                feed_forward=PositionwiseFeedForward(i_dim=h_dim, h_units=ff_dim, dropout_rate=ff_dropout_rate),
+                dropout_rate=dropout_rate,
+            ) for _ in range(n_layer)
+        ])
+        self.after_norm = LayerNorm(h_dim)
+        self.linear_out = nn.Linear(h_dim, i_dim)
+        self.h_dim, self.n_head = h_dim, n_head
+        self.rates = SimpleNamespace(drop=dropout_rate, self_att=self_attn_dropout_rate, src_att=src_attn_dropout_rate,
+                                     ff=ff_dropout_rate)
+
+    def weights(self):
+        return self._cached("w", lambda: SimpleNamespace(
+            d=self.h_dim, H=self.n_head, layers=[l._w_all(False) for l in self.dec_layers],
+            ln_f=SimpleNamespace(g=self._p("after_norm.weight"), b=self._p("after_norm.bias")),
+            Wout=self._w("linear_out.weight"), bout=self._p("linear_out.bias")))
+
+    def grads(self):
+        return self._cached("g", lambda: SimpleNamespace(
+            layers=[l._w_all(True) for l in self.dec_layers],
+            ln_f=SimpleNamespace(g=self._g("after_norm.weight"), b=self._g("after_norm.bias")),
+            Wout=self._g("linear_out.weight"), bout=self._g("linear_out.bias")))
+
+
+class Predictor(_Bound):
+    """liteasr/nets/paraformer/predictor.py:12-22: Conv1d(d, d, 3, padding 1) -> ReLU ->
+    Linear(d, 1) -> Sigmoid, then the CIF scan (csrc/cif.hip)."""
+
+    def __init__(self, size):
+        super().__init__()
+        self.conv = nn.Conv1d(in_channels=size, out_channels=size, kernel_size=3, padding=1)
+        self.relu = nn.ReLU()
+        self.lin = nn.Linear(size, 1)
+        self.sigmoid = nn.Sigmoid()
+        self.size = size
+
+    def weights(self):
+        return SimpleNamespace(Wc=self._p("conv.weight"), bc=self._p("conv.bias"), Wl=self._w("lin.weight"),
+                               bl=self._p("lin.bias"))
+
+    def grads(self):
+        return self._cached("g", lambda: SimpleNamespace(Wc=self._g("conv.weight"), bc=self._g("conv.bias"),
+                                                         Wl=self._g("lin.weight"), bl=self._g("lin.bias")))
+

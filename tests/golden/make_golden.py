@@ -444,9 +444,90 @@ def gen_spec_aug():
     save("spec_aug.npz", **arrs)
 
 
+def gen_paraformer():
+    """Tiny Paraformer (d 64, 2 enc / 1 dec, V 20, F 40) through the reference's model and
+    ParaformerLoss: seed-42 init state_dict, a batch, python-random seed for the glancing
+    sampler, every intermediate the oracle restates (encoder output, alpha, h_cif,
+    sum_alpha, first-pass argmax, replace map), hs_attn, loss and every gradient."""
+    import random
+
+    from liteasr.criterions.paraformer_loss import ParaformerLoss
+    from liteasr.models.paraformer import Paraformer
+
+    cfg = types.SimpleNamespace(dropout_rate=0.0, use_rel=True, input_dim=40, enc_dim=64, enc_ff_dim=128,
+                                enc_attn_heads=4, enc_dropout_rate=0.0, enc_pos_dropout_rate=0.0,
+                                enc_attn_dropout_rate=0.0, enc_ff_dropout_rate=0.0, enc_layers=2,
+                                activation="swish", sample_ratio=0.75, vocab_size=20, dec_dim=64, dec_ff_dim=128,
+                                dec_attn_heads=4, dec_dropout_rate=0.0, dec_self_attn_dropout_rate=0.0,
+                                dec_src_attn_dropout_rate=0.0, dec_ff_dropout_rate=0.0, dec_layers=1,
+                                pos_dropout_rate=0.0)
+    arrs = {}
+    for case, (seed, xl, yl) in enumerate([(3, [120, 113, 97], [6, 4, 2]), (4, [160, 160, 131, 90], [9, 7, 9, 3])]):
+        torch.manual_seed(42)
+        model = Paraformer(cfg)
+        model.train()
+        init = {k: v.clone() for k, v in model.state_dict().items() if not k.endswith(".pe.pe") and k != "pe.pe"}
+        g = torch.Generator().manual_seed(seed)
+        xlens = torch.tensor(xl)
+        B, Tx, L, V = len(xl), max(xl), max(yl), 20
+        xs = torch.randn(B, Tx, 40, generator=g).masked_fill(padding_mask(xlens).unsqueeze(-1), 0.0)
+        ylens = torch.tensor(yl)
+        ys = torch.randint(1, V - 1, (B, L), generator=g).masked_fill(padding_mask(ylens), -1)
+        rec = {}
+        pred_fwd = model.predictor.forward
+
+        def pred_hook(xs_, xlens_=None, ylens_=None):
+            rec["h_enc"] = xs_.detach().clone()
+            out = pred_fwd(xs_, xlens_, ylens_)
+            rec["h_cif"] = out[0].detach().clone()
+            return out
+
+        model.predictor.forward = pred_hook
+        samp_fwd = model.sampler.forward
+
+        def samp_hook(hs, embed_ys, ys_, ys_hat, ylens_):
+            rec["ys_hat"] = ys_hat.clone()
+            st = random.getstate()
+            out = samp_fwd(hs, embed_ys, ys_, ys_hat, ylens_)
+            random.setstate(st)  # replay the same draws to record the replace map
+            rep = torch.zeros_like(ys_, dtype=torch.bool)
+            dist = (ys_hat != ys_).sum(-1)
+            num = torch.ceil(model.sampler.sample_ratio * dist).long()
+            for b in range(ys_.size(0)):
+                rep[b][random.sample(range(ylens_[b]), num[b])] = True
+            rec["replace"] = rep
+            return out
+
+        model.sampler.forward = samp_hook
+        crit = ParaformerLoss(types.SimpleNamespace(vocab_size=V, gamma=1.0))
+
+        class _Rec:
+            def __call__(self, *a):
+                rec["out"] = model(*a)
+                return rec["out"]
+
+            def get_target(self, y, yl):
+                return model.get_target(y, yl)
+
+        random.seed(100 + case)
+        loss = crit(_Rec(), xs, xlens, ys, ylens)
+        hs_attn, sum_alpha = rec["out"]
+        loss.backward()
+        pre = f"c{case}."
+        arrs.update({pre + "xs": xs, pre + "xlens": xlens, pre + "ys": ys, pre + "ylens": ylens,
+                     pre + "random_seed": np.array(100 + case), pre + "hs_attn": hs_attn.detach(),
+                     pre + "sum_alpha": sum_alpha.detach(), pre + "loss": loss.detach(),
+                     pre + "h_enc": rec["h_enc"], pre + "h_cif": rec["h_cif"], pre + "ys_hat": rec["ys_hat"],
+                     pre + "replace": rec["replace"]})
+        arrs.update({pre + "grad." + n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+        if case == 0:
+            arrs.update({"init." + k: v for k, v in init.items()})
+    save("paraformer.npz", **arrs)
+
+
 GENERATORS = dict(relshift=gen_relshift, lengths=gen_lengths, ctc_kl=gen_ctc_kl, u2_step=gen_u2_step,
                   decode=gen_decode, loader=gen_loader, spec_aug=gen_spec_aug, ctc_large=gen_ctc_large,
-                  host_policies=gen_host_policies)
+                  host_policies=gen_host_policies, paraformer=gen_paraformer)
 
 if __name__ == "__main__":
     # python tests/golden/make_golden.py [name ...]   (default: all)

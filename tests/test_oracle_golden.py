@@ -258,3 +258,38 @@ def test_host_policies_match_reference():
     v = Vocab(os.path.join(ROOT, "tests", "golden", "loader", "vocab.txt"))
     assert list(v.lookup(list(range(len(v))), convert=True)) == d["vocab_conv"].tolist()
     assert list(v.lookup(list(range(len(v))))) == d["vocab_tokens"].tolist()
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_paraformer_oracle_matches_reference(case):
+    """oracle/paraformer_ref.py (CIF predictor, glancing sampler, parallel decoder,
+    ParaformerLoss) vs the reference Paraformer run (tests/golden/paraformer.npz): every
+    intermediate, the loss and every gradient, same Python ``random`` seed."""
+    import random
+
+    from oracle import paraformer_ref as PR
+
+    z = np.load(os.path.join(G, "paraformer.npz"))
+    pre = f"c{case}."
+    g = lambda k: torch.from_numpy(z[pre + k])  # noqa: E731
+    cfg = PR.default_cfg(enc_dim=64, enc_heads=4, enc_ff=128, enc_layers=2, dec_dim=64, dec_heads=4, dec_ff=128,
+                         dec_layers=1, vocab_size=20, input_dim=40)
+    init = {k[5:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("init.")}
+    isbn = lambda k: "running" in k or "num_batches" in k  # noqa: E731
+    bn = {k: v.clone() for k, v in init.items() if isbn(k)}
+    p = {k: v.clone().requires_grad_() for k, v in init.items() if not isbn(k)}
+    random.seed(int(z[pre + "random_seed"]))
+    hs, sa, ex = PR.paraformer_forward(g("xs"), g("xlens"), g("ys"), g("ylens"), p, cfg, bn, True)
+    loss, _, _ = PR.paraformer_loss(hs, sa, g("ys"), g("ylens"))
+    loss.backward()
+    rel = lambda a, b: ((a.detach().double() - b.double()).abs().max() / (b.double().abs().max() + 1e-30)).item()  # noqa: E731
+    assert torch.equal(ex["ys_hat"], g("ys_hat")) and torch.equal(ex["replace"], g("replace"))
+    assert rel(ex["h_enc"], g("h_enc")) < 1e-5 and rel(ex["hs_cif"], g("h_cif")) < 1e-5
+    assert rel(sa, g("sum_alpha")) < 1e-6 and rel(hs, g("hs_attn")) < 1e-5
+    assert abs(loss.item() - float(z[pre + "loss"])) < 1e-5 * abs(float(z[pre + "loss"]))
+    gold = {k[len(pre) + 5:]: torch.from_numpy(z[k]) for k in z.files if k.startswith(pre + "grad.")}
+    assert set(gold) == set(p)
+    floor = 1e-3 * max(v.abs().max().item() for v in gold.values())
+    for k, v in gold.items():
+        err = (p[k].grad.double() - v.double()).abs().max().item() / max(v.abs().max().item(), floor)
+        assert err < 1e-4, (k, err)
