@@ -100,10 +100,62 @@ def roofline_case(cfgd, dev):
     flops = 2.0 * M * N * Kd
     bytes_ = 2.0 * (Kd * M + Kd * N) + 4.0 * M * N
     S, minb = _DW_INSTANCE[(tm, tn)]
-    meta = {"kernel": f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}>",
+    meta = {"kernel": f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}, 0>",
             "shape": f"M={M} N={N} K={Kd} split_k={split}",
             "grid": [-(-N // tn), -(-M // tm), split]}
     return launch, flops, bytes_, meta
+
+
+def hottest_case(cfgd, dev):
+    """The single hottest GEMM instance by ms/step (rocprof, profiles/r02): the FFN fc1
+    forward, h = dropout(swish(LN @ W1^T + b1)) plus the gate g = swish'(u) * keep stored
+    for the backward (gemm_bf16_glds_kernel<128,256,true,true,bf16,3,2,0>, 24 per step).
+    Algorithmic bytes: LN and W1 read once, h and g written once (bf16)."""
+    import torch
+
+    from liteasr_amd import kernels as K
+    from liteasr_amd._native import ACT_SWISH
+
+    T1 = (cfgd["T"] - 3) // 2 + 1
+    M = cfgd["B"] * ((T1 - 3) // 2 + 1)
+    F, D = cfgd["ff"], cfgd["d"]
+    ln = torch.randn(M, D, device=dev).bfloat16()
+    w1 = (torch.randn(F, D, device=dev) * 0.05).bfloat16()
+    b1 = torch.zeros(F, device=dev)
+    h = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    g = torch.empty_like(h)
+
+    def launch():
+        K.linear(ln, w1, h, bias=b1, act=ACT_SWISH, zout=g, zout_mode=1, drop_p=0.1, drop_seed=11)
+
+    flops = 2.0 * M * F * D
+    bytes_ = 2.0 * (M * D + F * D) + 2 * 2.0 * M * F + 4.0 * F
+    meta = {"kernel": "gemm_bf16_glds_kernel<128, 256, true, true, unsigned short, 3, 2, 0>",
+            "shape": f"M={M} N={F} K={D} bias+swish+gate+dropout", "grid": [F // 256, -(-M // 128), 1]}
+    return launch, flops, bytes_, meta
+
+
+def _time_case(launch, iters):
+    import torch
+
+    for _ in range(5):
+        launch()
+    st = torch.cuda.current_stream()  # lasr_* launches go to kernels.stream() == this stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        launch()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def _roof(flops, bytes_, sec):
+    t_flop = flops / (PEAK_BF16_TFLOPS * 1e12)
+    t_byte = bytes_ / (PEAK_HBM_GBS * 1e9)
+    if t_byte >= t_flop:
+        return "hbm", bytes_ / sec / 1e9, PEAK_HBM_GBS, "GB/s"
+    return "mfma", flops / sec / 1e12, PEAK_BF16_TFLOPS, "TFLOP/s"
 
 
 def dominant_kernel_roofline(cfgd, dev, iters=50):
@@ -115,22 +167,8 @@ def dominant_kernel_roofline(cfgd, dev, iters=50):
     from liteasr_amd import kernels as K
 
     launch, flops, bytes_, meta = roofline_case(cfgd, dev)
-    for _ in range(5):
-        launch()
-    st = torch.cuda.current_stream()  # lasr_* launches go to kernels.stream() == this stream
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(iters):
-        launch()
-    e1.record(st)
-    e1.synchronize()
-    sec = e0.elapsed_time(e1) / iters * 1e-3
-    t_flop = flops / (PEAK_BF16_TFLOPS * 1e12)
-    t_byte = bytes_ / (PEAK_HBM_GBS * 1e9)
-    if t_byte >= t_flop:
-        bound, ach, peak, unit = "hbm", bytes_ / sec / 1e9, PEAK_HBM_GBS, "GB/s"
-    else:
-        bound, ach, peak, unit = "mfma", flops / sec / 1e12, PEAK_BF16_TFLOPS, "TFLOP/s"
+    sec = _time_case(launch, iters)
+    bound, ach, peak, unit = _roof(flops, bytes_, sec)
     traffic = pmc_traffic(meta)
     out = {"kernel": meta["kernel"], "shape": meta["shape"], "bound": bound, "achieved": round(ach, 2),
            "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
@@ -140,6 +178,15 @@ def dominant_kernel_roofline(cfgd, dev, iters=50):
            "achieved_tflops": round(flops / sec / 1e12, 2)}
     if traffic:
         out["traffic_source"] = traffic["source"]
+    launch, flops, bytes_, meta = hottest_case(cfgd, dev)
+    sec = _time_case(launch, iters)
+    bound, ach, peak, unit = _roof(flops, bytes_, sec)
+    traffic = pmc_traffic(meta)
+    out["hottest_instance"] = {
+        "kernel": meta["kernel"], "shape": meta["shape"], "bound": bound, "achieved": round(ach, 2), "peak": peak,
+        "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic["bytes_per_launch"] if traffic else None,
+        "algorithmic_bytes_per_launch": bytes_, "algorithmic_flops_per_launch": flops,
+        "avg_launch_us": round(sec * 1e6, 2), "achieved_tflops": round(flops / sec / 1e12, 2)}
     return out
 
 
@@ -152,7 +199,7 @@ def pmc_traffic(meta):
     import json
 
     for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*",
-                                              "roofline_pmc.json")), reverse=True):
+                                              "roofline_pmc*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
@@ -179,7 +226,7 @@ def cpu_baseline(cfgd_name, budget_s=25.0):
                         dec_pos_dropout=0.1, dec_ff_dropout=0.1)
     params = O.init_params(cfg, seed=1)
     bufs = O.init_buffers(cfg)
-    Bs = 2 if cfgd["T"] > 2000 else 4
+    Bs = 2 if cfgd["T"] > 2000 else 8  # B=8 when B=32 is too slow for the budget
     batch = O.synthetic_batch(Bs, cfgd["T"], cfgd["L"], V, seed=5)
     st = None
     t0 = time.perf_counter()
@@ -193,7 +240,7 @@ def cpu_baseline(cfgd_name, budget_s=25.0):
         steps += 1
         el = time.perf_counter() - t0
         # ~10-25 s of timed CPU work (at least 3 steps), bounded so the bench stays short
-        if el + el / steps > budget_s or (steps >= 3 and el >= 10.0):
+        if el + el / steps > budget_s or (steps >= 3 and el >= 12.0):
             break
     return {"value": round(Bs * steps / el, 3), "unit": "utterances/sec", "cores": n, "kind": "port",
             "sample": f"oracle (torch CPU fp32) {cfgd_name} U2, B={Bs} T={cfgd['T']} L={cfgd['L']}, dropout 0.1, "
@@ -259,6 +306,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", type=int, default=0, metavar="N",
                     help="only launch the roofline kernel N times (for rocprofv3 --pmc passes)")
+    ap.add_argument("--roofline-case", default="dw", choices=["dw", "hot"],
+                    help="--roofline-only: the dominant-family kernel (dw) or the hottest instance (hot)")
     args = ap.parse_args()
 
     import torch
@@ -266,7 +315,8 @@ def main():
 
     if args.roofline_only:
         torch.cuda.set_device(0)
-        launch, flops, bytes_, meta = roofline_case(CONFIGS[args.config], torch.device("cuda", 0))
+        case = roofline_case if args.roofline_case == "dw" else hottest_case
+        launch, flops, bytes_, meta = case(CONFIGS[args.config], torch.device("cuda", 0))
         for _ in range(args.roofline_only):
             launch()
         torch.cuda.synchronize()

@@ -107,6 +107,19 @@ int lasr_gemm_force_tile(int tile_m, int tile_n);
  * of split-K LDS-DMA launches; (0, 0) restores the planner.  Benchmarks only. */
 int lasr_gemm_force_split(int split_k, int stages);
 
+/* FFN data gradient through the activation with the gate recomputed (liteasr/nets/
+ * feed_forward.py:18-19 backward): dz = (gb @ W2) * act'(ln @ W1^T + b1) * keep * scale,
+ * keep / scale = the fc1 forward's dropout draws (lasr_gemm epilogue, element m*F + f, same
+ * (p1, seed1, step counter)).  The forward then stores only h = drop(act(u)).  ln, gb [M, D],
+ * W1 [F, D], W2 [D, F], dz [M, F] bf16; b1 [F] fp32; D % 32 == 0, F % 128 == 0, 16-B aligned. */
+typedef struct lasr_ffn_dz_args {
+  int M, D, F, act;
+  const void* ln; const void* W1; const float* b1;
+  const void* gb; const void* W2;
+  float p1; uint64_t seed1;
+  void* dz;
+} lasr_ffn_dz_args;
+int lasr_ffn_dz(const lasr_ffn_dz_args* args, void* stream);
 /* ---- fused position-wise feed-forward chains (liteasr/nets/feed_forward.py:18-19 in the
  * Conformer residual branches, conformer_layer.py:37-47,58-66) --------------------------
  * fwd:    u = x W1^T + b1 ; z = act'(u) * keep1 (the gate) ; h = drop1(act(u)) ;

@@ -80,6 +80,18 @@ class Conv2Args(C.Structure):
 CONV2_FWD, CONV2_DW, CONV2_DX = 0, 1, 2
 
 
+class FfnDzArgs(C.Structure):
+    """Mirror of ``lasr_ffn_dz_args``."""
+
+    _fields_ = [
+        ("M", _i), ("D", _i), ("F", _i), ("act", _i),
+        ("ln", _p), ("W1", _p), ("b1", _p),
+        ("gb", _p), ("W2", _p),
+        ("p1", _f), ("seed1", _u),
+        ("dz", _p),
+    ]
+
+
 class CifArgs(C.Structure):
     """Mirror of ``lasr_cif_args``."""
 
@@ -134,6 +146,7 @@ SIGNATURES = {
     "lasr_conv1_fwd": [_p, _i, _i, _i, _i, _p, _p, _p, _i, _p],
     "lasr_conv1_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _l, _p],
     "lasr_conv2_gemm": [C.POINTER(Conv2Args), _p],
+    "lasr_ffn_dz": [C.POINTER(FfnDzArgs), _p],
     "lasr_cif_fwd": [C.POINTER(CifArgs), _p],
     "lasr_cif_bwd": [C.POINTER(CifArgs), _p],
     "lasr_glancing_mix": [_l, _i, _p, _p, _p, _p, _p, _i, _p],

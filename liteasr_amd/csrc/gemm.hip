@@ -14,931 +14,10 @@
 // Replaces aten addmm/mm/bmm at liteasr/nets/feed_forward.py:18-19,
 // attention.py:35-37,58,69,145,149, subsampling.py:34,47, conformer_convolution.py:48,55,
 // ctc.py:29, transformer_decoder.py:91 (and their autograd backward GEMMs).
-#include "common.h"
-#include "tile.h"
-
-#include <cstring>
-#include <type_traits>
-
-// Ablation hooks for GEMM experiments (tools/gemm_exp.sh); 0 in every product build.
-// bit 1: skip the MFMAs, bit 2: skip the epilogue stores, bit 4: skip the glds loads.
-#ifndef LASR_EXP
-#define LASR_EXP 0
-#endif
-
-
-// Geometry of the subsampling conv2 (3x3, stride 2, C -> C, channels-last y1 [B,T1,F1,C]) for
-// the implicit-GEMM kernel instances (G_FWD / G_DW / G_DX below).
-struct ConvG {
-  int B, T1, F1, T2, F2, C;
-  int M2;               // B * T2 * F2 (rows of y2 / dy2)
-  int cls;              // G_DX: output parity class (t1 & 1) * 2 + (f1 & 1)
-  int q32, r32;         // G_DW: 32 = q32 * F2 + r32 (row-walk increments)
-  const bf16_t* zero;   // G_DX: >= 32 zero bf16 (taps that fall outside dy2)
-};
-typedef ConvG ConvGeom;
-enum { G_LIN = 0, G_FWD = 1, G_DW = 2, G_DX = 3 };
-
-struct GemmP {
-  int M, N, K, batch, batch_div;
-  const void* A;
-  int64_t lda_m, lda_k, sa1, sa2;
-  const void* B;
-  int64_t ldb_n, ldb_k, sb1, sb2;
-  void* C;
-  int64_t ldc, sc1, sc2;
-  float alpha;
-  const float* alpha_dev;
-  float beta;
-  const float* bias;
-  int act;
-  void* zout;
-  const void* aux;
-  int aux_dtype;
-  int64_t ldaux;
-  int aux_act;
-  DropCfg drop;
-  const void* res;
-  int res_dtype;
-  int64_t ldres;
-  float res_scale;
-  int split_k;
-  int kchunk;
-  float* ws;
-  int a_vec, b_vec;
-  int c_vec, aux_vec, res_vec, ws_vec;  // 8-wide epilogue access allowed
-  // Epilogue mode of the bf16 kernel: 0 = no per-element loads, 1 = exactly one of
-  // aux/res, 16-B aligned and prefetched before the staging barrier, 2 = generic.
-  int epi_mode;
-  int bias_vec;
-  // rowsum[m] += sum_k A[m,k] (bias gradient of a dW = dY^T X GEMM): computed by the
-  // n-tile-0 blocks of the LDS-DMA kernel (A M-contiguous); split-K slices write
-  // partials to rs_ws[s*M + m], summed in fixed order by splitk_reduce_kernel.
-  float* rowsum;
-  float* rs_ws;
-  int v4;  // direct epilogue: 4-wide C/zout/aux/res/bias/ws access allowed (host-checked)
-  int zout_mode;  // 0: zout = pre-activation; 1: zout = act'(pre-activation) * keep (gate)
-  ConvGeom cv;    // implicit-GEMM instances of the subsampling conv2 only (G != 0)
-};
-
-LASR_DEV float load_any(const void* p, int dt, int64_t i) {
-  return dt == LASR_F32 ? ((const float*)p)[i] : bf2f(((const bf16_t*)p)[i]);
-}
-
-// Epilogue core on N consecutive columns after bias: zout (pre-activation or gate),
-// activation, aux factor, dropout (one draw per column pair), residual.  zst(vals) stores
-// the zout values; auxv / resv are the loaded aux / res values (nullable).  Every mode
-// switch is a wave-uniform branch around its own loop (a per-element select would make
-// the compiler evaluate every activation and its derivative for every element).
-template <int N, typename ZST>
-LASR_DEV void epi_core(const GemmP& p, uint64_t dbase, float (&v)[N], const float (&auxv)[N], bool has_aux,
-                       const float (&resv)[N], bool has_res, ZST zst) {
-  const bool drop = p.drop.p > 0.f;
-  const uint32_t km = drop ? drop_keep_mask<N>(p.drop, drop_key(p.drop), dbase) : 0u;
-  if (p.zout) {
-    if (p.zout_mode == 1) {
-      float g[N];
-      if (p.act == LASR_ACT_SWISH) {
-#pragma unroll
-        for (int q = 0; q < N; ++q) g[q] = swish_grad(v[q]);
-      } else if (p.act == LASR_ACT_RELU) {
-#pragma unroll
-        for (int q = 0; q < N; ++q) g[q] = v[q] > 0.f ? 1.f : 0.f;
-      } else {
-#pragma unroll
-        for (int q = 0; q < N; ++q) g[q] = 1.f;
-      }
-      if (drop) {
-#pragma unroll
-        for (int q = 0; q < N; ++q) g[q] *= (km >> q) & 1u ? 1.f : 0.f;
-      }
-      zst(g);
-    } else {
-      zst(v);
-    }
-  }
-  if (p.act == LASR_ACT_SWISH) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] = swishf(v[q]);
-  } else if (p.act == LASR_ACT_RELU) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] = fmaxf(v[q], 0.f);
-  }
-  if (has_aux) {
-    if (p.aux_act == LASR_ACT_GATE) {
-#pragma unroll
-      for (int q = 0; q < N; ++q) v[q] *= auxv[q];
-    } else if (p.aux_act == LASR_ACT_RELU) {
-#pragma unroll
-      for (int q = 0; q < N; ++q) v[q] *= auxv[q] > 0.f ? 1.f : 0.f;
-    } else {
-#pragma unroll
-      for (int q = 0; q < N; ++q) v[q] *= swish_grad(auxv[q]);
-    }
-  }
-  if (drop) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] *= (km >> q) & 1u ? p.drop.scale : 0.f;  // x * 0 keeps NaN, as torch
-  }
-  if (has_res) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] = resv[q] + p.res_scale * v[q];
-  }
-}
-
-// Full epilogue for one output element.
-template <typename TC>
-LASR_DEV void epi_store(const GemmP& p, int z1, int z2, int z, int m, int n, float acc,
-                        float alpha_eff) {
-  if (m >= p.M || n >= p.N) return;
-  float v[1] = {acc * alpha_eff};
-  if (p.bias) v[0] += p.bias[n];
-  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
-  float a[1], r[1];
-  if (p.aux) a[0] = load_any(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n);
-  if (p.res) r[0] = load_any(p.res, p.res_dtype, (int64_t)m * p.ldres + n);
-  epi_core<1>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, a, p.aux != nullptr, r, p.res != nullptr,
-              [&](const float (&zv)[1]) { ((TC*)p.zout)[cidx] = from_f<TC>(zv[0]); });
-  TC* C = (TC*)p.C;
-  if (p.beta != 0.f) v[0] += p.beta * to_f(C[cidx]);
-  C[cidx] = from_f<TC>(v[0]);
-}
-
-// 8 values of a (f32|bf16) matrix row starting at element idx; cnt < 8 -> tail.
-LASR_DEV void ld_any8(const void* base, int dt, int64_t idx, bool vec, int cnt, float* o) {
-  if (vec && cnt == 8) {
-    if (dt == LASR_F32) ld8((const float*)base + idx, o);
-    else ld8((const bf16_t*)base + idx, o);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = q < cnt ? load_any(base, dt, idx + q) : 0.f;
-  }
-}
-template <typename T>
-LASR_DEV void st_8(T* dst, const float* v, bool vec, int cnt) {
-  if ((LASR_EXP & 2) && v[0] != 1234.5f) return;
-  if (vec && cnt == 8) st8(dst, v);
-  else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (q < cnt) dst[q] = from_f<T>(v[q]);
-  }
-}
-
-// Epilogue for 8 consecutive columns n..n+7 of row m (same order as epi_store).
-template <typename TC>
-LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, const float* acc,
-                         float alpha_eff) {
-  const int cnt = min(8, p.N - n);
-  float v[8], t[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff;
-  if (p.bias) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] += q < cnt ? p.bias[n + q] : 0.f;
-  }
-  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
-  float r[8];
-  if (p.aux) ld_any8(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, p.aux_vec, cnt, t);
-  if (p.res) ld_any8(p.res, p.res_dtype, (int64_t)m * p.ldres + n, p.res_vec, cnt, r);
-  epi_core<8>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
-              [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, p.c_vec, cnt); });
-  TC* C = (TC*)p.C + cidx;
-  if (p.beta != 0.f) {
-    ld_any8(C, sizeof(TC) == 4 ? LASR_F32 : LASR_BF16, 0, p.c_vec, cnt, t);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] += p.beta * t[q];
-  }
-  st_8(C, v, p.c_vec, cnt);
-}
-
-// Epilogue modes 0/1: bias already in registers (bv), the one aux/res source prefetched
-// (sv, mode 1 only; N % 8 == 0 there), beta == 0; cnt < 8 only on a ragged last vector.
-template <typename TC>
-LASR_DEV void epi_fast8(const GemmP& p, int64_t cidx, int z, int m, int n, int cnt, const float* acc,
-                        float alpha_eff, const float* bv, const float (&sv)[8]) {
-  float v[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff + bv[q];
-  epi_core<8>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, sv, p.aux != nullptr, sv, p.res != nullptr,
-              [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, true, cnt); });
-  st_8((TC*)p.C + cidx, v, true, cnt);
-}
-
-LASR_DEV float alpha_of(const GemmP& p) {
-  return p.alpha_dev ? p.alpha * p.alpha_dev[0] : p.alpha;
-}
-
-// ============================ bf16 MFMA kernel ===================================
-// ============================ bf16 MFMA kernel ===================================
-// (tile images, fragment reads, LDS-DMA issue and ring waits: tile.h)
-
-// Epilogue shared by the bf16 kernels: stage each half of the C tile (WM rows x BN cols,
-// fp32) through LDS, then every thread finishes 8 contiguous columns of a row with 16-B
-// loads/stores (or writes its split-K partial).  The caller has passed a barrier after its
-// last LDS read of the main loop.
-// Element offset of output row m of a G_DX launch: class row (b, i, j) -> dy1 position
-// (b, 2i + pt, 2j + pf), channels-last.
-LASR_DEV int64_t dx_row(const ConvG& g, int m) {
-  const int pt = g.cls >> 1, pf = g.cls & 1;
-  const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
-  const int j = m % nJ, t = m / nJ, i = t % nI, b = t / nI;
-  return ((int64_t)(b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf) * g.C;
-}
-
-template <int BM, int BN, typename TC, bool TRANS = false, int G = G_LIN>
-LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem_epi, int m0,
-                            int n0, int s, int z, int z1, int z2) {
-  // output-row offsets: linear (ldc, ld of the aux/res source), or the transposed-conv scatter
-  // of a G_DX launch (aux = y1 shares dy1's layout)
-  auto crow = [&](int m) -> int64_t {
-    if constexpr (G == G_DX) return dx_row(p.cv, m);
-    else return (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc;
-  };
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  constexpr int LDC = BN + 4;  // +4 floats: the 4 row-groups of a write land on distinct banks
-  float* cs = reinterpret_cast<float*>(smem_epi);
-  const int rq = (lane >> 4) * 4, cl = lane & 15;
-  const float al = alpha_of(p);
-  const bool split = p.split_k > 1;
-  float* wsp = split ? p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N : nullptr;
-  // A thread's 8-column slot is the same in every epilogue iteration (256 % (BN/8) == 0):
-  // its bias is loaded once; the aux/res rows of a half are prefetched before the barrier.
-  constexpr int CPR = BN / 8, RPI = 256 / CPR, ITERS = WM / RPI;
-  static_assert(WM % RPI == 0, "epilogue tiling");
-  const int ec8 = (tid % CPR) * 8, er0 = tid / CPR;
-  const int en = n0 + ec8;
-  // conv instances are host-checked onto the fast path (no split here, epi_mode < 2)
-  const bool fast = G != G_LIN || (!split && p.epi_mode < 2);
-  float bv[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) bv[q] = 0.f;
-  if (fast && p.bias && en < p.N) {
-    if (p.bias_vec && en + 8 <= p.N) ld8(p.bias + en, bv);
-    else
-#pragma unroll
-      for (int q = 0; q < 8; ++q) bv[q] = en + q < p.N ? p.bias[en + q] : 0.f;
-  }
-  const void* src = p.aux ? p.aux : p.res;
-  const int src_dt = p.aux ? p.aux_dtype : p.res_dtype;
-  const int64_t src_ld = p.aux ? p.ldaux : p.ldres;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    // prefetch PF row-iterations of the aux/res source at a time (register budget)
-    constexpr int PF = ITERS < 2 ? ITERS : 2;
-    float sv[PF][8];
-    auto prefetch = [&](int b) {
-      if (!(fast && p.epi_mode == 1)) return;
-      const int mlast = p.M - 1, nc = min(en, p.N - 8);
-      if (src_dt == LASR_F32) {
-#pragma unroll
-        for (int it = 0; it < PF; ++it) {
-          const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          const int64_t ro = G == G_DX ? dx_row(p.cv, m) : (int64_t)m * src_ld;
-          ld8((const float*)src + ro + nc, sv[it]);
-        }
-      } else {
-#pragma unroll
-        for (int it = 0; it < PF; ++it) {
-          const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          const int64_t ro = G == G_DX ? dx_row(p.cv, m) : (int64_t)m * src_ld;
-          ld8((const bf16_t*)src + ro + nc, sv[it]);
-        }
-      }
-    };
-    prefetch(0);
-    if (wr == h) {
-      if constexpr (TRANS) {
-        // C^T fragments: lane owns row cl, columns rq..rq+3 -> one 16-B LDS write each
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            *(f32x4*)(cs + (i * 16 + cl) * LDC + wc * WN + j * 16 + rq) = acc[i][j];
-      } else {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) cs[(i * 16 + rq + e) * LDC + wc * WN + j * 16 + cl] = acc[i][j][e];
-      }
-    }
-    __syncthreads();
-    if (fast) {
-#pragma unroll
-      for (int b = 0; b < ITERS; b += PF) {
-        if (b > 0) prefetch(b);
-#pragma unroll
-        for (int it = 0; it < PF; ++it) {
-          const int r = er0 + (b + it) * RPI;
-          const int m = m0 + h * WM + r;
-          if (m < p.M && en < p.N) {
-            float a8[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + ec8 + q];
-            epi_fast8<TC>(p, crow(m) + en, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
-          }
-        }
-      }
-      __syncthreads();
-      continue;
-    }
-    constexpr int NV = WM * BN / 8;
-    for (int v = tid; v < NV; v += 256) {
-      const int r = v / (BN / 8), c8 = (v % (BN / 8)) * 8;
-      const int m = m0 + h * WM + r, n = n0 + c8;
-      if (m < p.M && n < p.N) {
-        float a8[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + c8 + q];
-        if (split) {
-          float* dst = wsp + (int64_t)m * p.N + n;
-          if (p.ws_vec && n + 8 <= p.N) st8(dst, a8);
-          else
-            for (int q = 0; q < 8 && n + q < p.N; ++q) dst[q] = a8[q];
-        } else {
-          epi_store8<TC>(p, z1, z2, z, m, n, a8, al);
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
-template <int BM, int BN, bool AKC, bool BKC, typename TC>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
-  constexpr int BK = 32;
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  constexpr int MAIN_BYTES = 2 * (BM + BN) * BK * 2;
-  constexpr int EPI_BYTES = WM * (BN + 4) * 4;
-  __shared__ __attribute__((aligned(16))) char smem_epi[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
-  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_epi);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-
-  const int zz = blockIdx.z;
-  const int s = zz % p.split_k, z = zz / p.split_k;
-  const int z1 = z / p.batch_div, z2 = z % p.batch_div;
-  const bf16_t* A = (const bf16_t*)p.A + z1 * p.sa1 + z2 * p.sa2;
-  const bf16_t* B = (const bf16_t*)p.B + z1 * p.sb1 + z2 * p.sb2;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = s * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  TileLoader<BM, AKC> la;
-  TileLoader<BN, BKC> lb;
-  const int64_t a_ldr = AKC ? p.lda_m : 0, a_ldk = AKC ? 0 : p.lda_k;
-  const int64_t b_ldr = BKC ? p.ldb_n : 0, b_ldk = BKC ? 0 : p.ldb_k;
-
-  if (nk > 0) {
-    la.load(A, a_ldr, a_ldk, m0, p.M, kbeg, kend, p.a_vec, tid);
-    lb.load(B, b_ldr, b_ldk, n0, p.N, kbeg, kend, p.b_vec, tid);
-    la.store(smem, tid);
-    lb.store(smem + BM * BK, tid);
-  }
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    bf16_t* cur = smem + (kt & 1) * (BM + BN) * BK;
-    bf16_t* nxt = smem + ((kt + 1) & 1) * (BM + BN) * BK;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      const int k0 = kbeg + (kt + 1) * BK;
-      la.load(A, a_ldr, a_ldk, m0, p.M, k0, kend, p.a_vec, tid);
-      lb.load(B, b_ldr, b_ldk, n0, p.N, k0, kend, p.b_vec, tid);
-    }
-    bf16x8 af[FM], bfr[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = frag<BM, AKC>(cur, wr * WM + i * 16, lane);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bfr[j] = frag<BN, BKC>(cur + BM * BK, wc * WN + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (more) {
-      la.store(nxt, tid);
-      lb.store(nxt + BM * BK, tid);
-    }
-    __syncthreads();
-  }
-
-  gemm_epilogue<BM, BN, TC>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
-}
-
-// Epilogue of 4 consecutive columns n..n+3 of row m (same order as epi_store8); cnt < 4 or
-// !vec -> element-wise tail.
-template <typename TC, bool VEC>
-LASR_DEV void epi_store4(const GemmP& p, int z1, int z2, int z, int m, int n, int cnt, const float* acc,
-                         float al) {
-  float v[4], t[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = acc[q] * al;
-  if (p.bias) {
-    if (VEC) {
-      ldv<4>(p.bias + n, t);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) t[q] = q < cnt ? p.bias[n + q] : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] += t[q];
-  }
-  const int64_t cidx = (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc + n;
-  auto st4 = [&](TC* dst, const float* x) {
-    if (VEC) stv<4>(dst, x);
-    else
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (q < cnt) dst[q] = from_f<TC>(x[q]);
-  };
-  auto ld4 = [&](const void* base, int dtp, int64_t idx, float* o) {
-    if (VEC) {
-      if (dtp == LASR_F32) ldv<4>((const float*)base + idx, o);
-      else ldv<4>((const bf16_t*)base + idx, o);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = q < cnt ? load_any(base, dtp, idx + q) : 0.f;
-    }
-  };
-  float r[4];
-  if (p.aux) ld4(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, t);
-  if (p.res) ld4(p.res, p.res_dtype, (int64_t)m * p.ldres + n, r);
-  epi_core<4>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
-              [&](const float (&zv)[4]) { st4((TC*)p.zout + cidx, zv); });
-  TC* C = (TC*)p.C + cidx;
-  if (p.beta != 0.f) {
-    ld4(C, sizeof(TC) == 4 ? LASR_F32 : LASR_BF16, 0, t);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] += p.beta * t[q];
-  }
-  if ((LASR_EXP & 2) && v[0] != 1234.5f) return;
-  st4(C, v);
-}
-
-// Epilogue straight from the accumulators, no LDS and no barrier.  The main loop issues
-// the MFMAs with the operands swapped (D = B-frag x A-frag), so acc[i][j] is a fragment of
-// C^T: lane l owns row m = mb + (l & 15) and the 4 consecutive columns nb + 4 (l >> 4) + e
-// -> one 8-B (bf16) / 16-B (fp32) access per 4 outputs (a wave instruction covers 16 rows
-// x 32 / 64 contiguous bytes; the L2 merges the row segments before write-back).
-template <int BM, int BN, typename TC>
-LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], int m0, int n0, int s,
-                                   int z, int z1, int z2) {
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const float al = alpha_of(p);
-  const int mr = m0 + wr * WM + (lane & 15), nc = n0 + wc * WN + 4 * (lane >> 4);
-  if (p.split_k > 1) {
-    float* wsp = p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = mr + i * 16;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = nc + j * 16;
-        if (n >= p.N) continue;
-        float* dst = wsp + (int64_t)m * p.N + n;
-        const float a[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (p.v4 && n + 4 <= p.N) stv<4>(dst, a);
-        else
-          for (int q = 0; q < 4 && n + q < p.N; ++q) dst[q] = a[q];
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = mr + i * 16;
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = nc + j * 16;
-      if (n >= p.N) continue;
-      const float a[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.v4 && n + 4 <= p.N) epi_store4<TC, true>(p, z1, z2, z, m, n, 4, a, al);
-      else epi_store4<TC, false>(p, z1, z2, z, m, n, min(4, p.N - n), a, al);
-    }
-  }
-}
-
-// ---------------- bf16 kernel, LDS-DMA pipeline (16-B aligned operands) ----------------
-// Same tiles, LDS images, fragment reads and epilogue as gemm_bf16_kernel, but every full
-// 32-deep k tile is copied HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging) into an
-// S-stage ring, S-1 tiles in flight.  The image is lane-linear per wave instruction, so the
-// swizzles of lds_off / tr_off are applied to the SOURCE address (the XOR maps are
-// involutions).  One raw barrier per k tile, preceded by a counted vmcnt that retires only
-// the tile about to be read.  A ragged last k tile goes through the register loader
-// (zero fill).  Rows past M/N read clamped (valid) addresses; they only feed discarded
-// outputs.  Blocks are remapped so consecutive tiles share an XCD (and its L2).
-
-// Implicit-GEMM operand walkers of the subsampling conv2 instances (G != G_LIN).  Each
-// keeps per-thread element offsets of the 16-B LDS-DMA positions it issues (the positions
-// of glds_tile), so an issue is one add per position.
-//  G_FWD, A = im2col(y1) [M2, 9C], K-contiguous: row m = (b, t2, f2) starts at y1 position
-//    (b, 2 t2, 2 f2); column k = (kh*3 + kw)*C + cin adds ((kh F1 + kw) C + cin): separable.
-//  G_DX, A = dy2 rows of the taps that reach output class (pt, pf), K-contiguous: row m =
-//    (b, i, j), output (b, 2i+pt, 2j+pf); tap (dt, df) reads dy2 row (b, i-dt, j-df), or the
-//    zero row when that falls outside [0,T2) x [0,F2).
-//  G_DW, B = im2col(y1) [M2, 9C] with k = m2 rows (M/N-contiguous operand): every k row is a
-//    contiguous run of one tap; the row walk advances (b, t2, f2) by 32 rows per tile.
-template <int R_TILE>
-struct ConvRowsKC {  // G_FWD / G_DX A operand
-  static constexpr int PER = R_TILE * 4 / 256;
-  int off[PER];
-  int vm[PER];  // G_DX: bit dt*2+df set when tap (dt, df) is inside dy2
-  LASR_DEV void init_fwd(const ConvG& g, int row0, int R, int tid) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int P = i * 256 + tid, r = P >> 2, c = (P & 3) ^ swz(r);
-      const int m = min(row0 + r, R - 1);
-      const int f2 = m % g.F2, t = m / g.F2, t2 = t % g.T2, b = t / g.T2;
-      off[i] = ((b * g.T1 + 2 * t2) * g.F1 + 2 * f2) * g.C + c * 8;
-      vm[i] = 0;
-    }
-  }
-  LASR_DEV void init_dx(const ConvG& g, int row0, int R, int tid) {
-    const int pt = g.cls >> 1, pf = g.cls & 1;
-    const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int P = i * 256 + tid, r = P >> 2, c = (P & 3) ^ swz(r);
-      const int m = min(row0 + r, R - 1);
-      const int j = m % nJ, t = m / nJ, ii = t % nI, b = t / nI;
-      off[i] = ((b * g.T2 + ii) * g.F2 + j) * g.C + c * 8;
-      const int vt = (ii < g.T2 ? 1 : 0) | (ii >= 1 && ii - 1 < g.T2 ? 2 : 0);
-      const int vf = (j < g.F2 ? 1 : 0) | (j >= 1 && j - 1 < g.F2 ? 2 : 0);
-      vm[i] = ((vt & 1) && (vf & 1) ? 1 : 0) | ((vt & 1) && (vf & 2) ? 2 : 0) |
-              ((vt & 2) && (vf & 1) ? 4 : 0) | ((vt & 2) && (vf & 2) ? 8 : 0);
-    }
-  }
-  LASR_DEV void issue(const bf16_t* base, int64_t koff, bf16_t* dst, int tid) const {
-    const int wid = tid >> 6;
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-      __builtin_amdgcn_global_load_lds((gptr_t)(base + off[i] + koff), (lptr_t)(dst + (i * 256 + wid * 64) * 8),
-                                       16, 0, 0);
-  }
-  LASR_DEV void issue_dx(const bf16_t* base, int64_t shift, int bit, const bf16_t* zero, bf16_t* dst,
-                         int tid) const {
-    const int wid = tid >> 6;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c8 = ((i * 256 + tid) & 3) * 8;
-      const bf16_t* src = (vm[i] >> bit) & 1 ? base + off[i] + shift : zero + c8;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * 256 + wid * 64) * 8), 16, 0, 0);
-    }
-  }
-};
-
-template <int R_TILE>
-struct ConvRowsDW {  // G_DW B operand: tile [32 k][R_TILE n] of im2col(y1), k = m2
-  static constexpr int PER = R_TILE * 4 / 256, CPR = R_TILE / 8;
-  int noff[PER], f2[PER], t2[PER], b[PER];
-  LASR_DEV void init(const ConvG& g, int n0, int N, int kbeg, int tid) {
-    const int tap = n0 / g.C, kh = tap / 3, kw = tap - 3 * kh;
-    const int tbase = (kh * g.F1 + kw) * g.C - tap * g.C;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int P = i * 256 + tid, k = P / CPR, ps = P % CPR;
-      const int ls = ((((ps >> 1) ^ htr<R_TILE>(k))) << 1) | (ps & 1);
-      const int gc = min(n0 + ls * 8, ((N + 7) & ~7) - 8);
-      noff[i] = tbase + gc;
-      const int m = kbeg + k;
-      f2[i] = m % g.F2;
-      const int t = m / g.F2;
-      t2[i] = t % g.T2;
-      b[i] = t / g.T2;
-    }
-  }
-  // issue the tile whose k rows are the current walk positions, then advance 32 rows
-  LASR_DEV void issue(const ConvG& g, const bf16_t* base, bf16_t* dst, int tid) {
-    const int wid = tid >> 6;
-    const int last = ((g.B * g.T1 - g.T1 + 2 * (g.T2 - 1)) * g.F1 + 2 * (g.F2 - 1)) * g.C;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int rb = b[i] < g.B ? ((b[i] * g.T1 + 2 * t2[i]) * g.F1 + 2 * f2[i]) * g.C : last;
-      __builtin_amdgcn_global_load_lds((gptr_t)(base + rb + noff[i]), (lptr_t)(dst + (i * 256 + wid * 64) * 8),
-                                       16, 0, 0);
-      f2[i] += g.r32;
-      t2[i] += g.q32;
-      if (f2[i] >= g.F2) { f2[i] -= g.F2; t2[i] += 1; }
-      while (t2[i] >= g.T2) { t2[i] -= g.T2; b[i] += 1; }
-    }
-  }
-};
-
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN>
-__global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
-  static_assert(G == G_LIN || (G == G_DW ? (!AKC && !BKC) : (AKC && (G == G_FWD) == BKC)),
-                "conv instance operand orientation");
-  constexpr int BK = 32;
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  constexpr int TILE = (BM + BN) * BK;  // elements per ring stage
-  constexpr int MAIN_BYTES = S * TILE * 2;  // >= the rowsum combine slab (256/(BM/8) x BM floats)
-  constexpr int EPI_BYTES = WM * (BN + 4) * 4;
-  constexpr int GL = (BM + BN) * 4 / 256;  // glds per thread per k tile
-  __shared__ __attribute__((aligned(16))) char smem_epi[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
-  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_epi);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-
-  // XCD-aware (bijective) remap of the 2-D tile index
-  const int nx = gridDim.x, nwg = gridDim.x * gridDim.y;
-  const int orig = blockIdx.y * nx + blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tx = wg % nx, ty = wg / nx;
-
-  const int zz = blockIdx.z;
-  const int s = zz % p.split_k, z = zz / p.split_k;
-  const int z1 = z / p.batch_div, z2 = z % p.batch_div;
-  const bf16_t* A = (const bf16_t*)p.A + z1 * p.sa1 + z2 * p.sa2;
-  const bf16_t* B = (const bf16_t*)p.B + z1 * p.sb1 + z2 * p.sb2;
-  const int m0 = ty * BM, n0 = tx * BN;
-  const int kbeg = s * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  const int64_t lda = AKC ? p.lda_m : p.lda_k, ldb = BKC ? p.ldb_n : p.ldb_k;
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // full 32-deep tiles go through the glds ring; a ragged last tile is handled after the
-  // loop (ordinary loads inside the loop would make hipcc drain the ring with vmcnt(0))
-  const int nfull = (kend - kbeg) > 0 ? (kend - kbeg) / BK : 0;
-  [[maybe_unused]] ConvRowsKC<BM> ga;
-  [[maybe_unused]] ConvRowsDW<BN> gb;
-  if constexpr (G == G_FWD) ga.init_fwd(p.cv, m0, p.M, tid);
-  if constexpr (G == G_DX) ga.init_dx(p.cv, m0, p.M, tid);
-  if constexpr (G == G_DW) gb.init(p.cv, n0, p.N, kbeg, tid);
-  auto issue = [&](int t) {
-    bf16_t* dst = smem + (t % S) * TILE;
-    const int k0 = kbeg + t * BK;
-    if (LASR_EXP & 4) return;
-    if constexpr (G == G_LIN) {
-      glds_tile<BM, AKC>(A, lda, m0, p.M, k0, dst, tid);
-      glds_tile<BN, BKC>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
-    } else if constexpr (G == G_FWD) {
-      const int C = p.cv.C, tap = k0 / C, kh = tap / 3, kw = tap - 3 * kh;
-      ga.issue(A, (int64_t)(kh * p.cv.F1 + kw) * C + (k0 - tap * C), dst, tid);
-      glds_tile<BN, true>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
-    } else if constexpr (G == G_DW) {
-      glds_tile<BM, false>(A, lda, m0, p.M, k0, dst, tid);
-      gb.issue(p.cv, B, dst + BM * BK, tid);
-    } else {
-      // class tap ti = k0 / C: (kh, kw) = (pt ? 1 : 2a, pf ? 1 : 2c), reading dy2 row (i-dt, j-df)
-      const int C = p.cv.C, ti = k0 / C, cin = k0 - ti * C;
-      const int pt = p.cv.cls >> 1, pf = p.cv.cls & 1, nkw = pf ? 1 : 2;
-      const int a = ti / nkw, c = ti - a * nkw;
-      const int dt = pt ? 0 : a, df = pf ? 0 : c;
-      const int kh = pt ? 1 : 2 * a, kw = pf ? 1 : 2 * c;
-      ga.issue_dx(A, cin - (int64_t)(dt * p.cv.F2 + df) * C, dt * 2 + df, p.cv.zero, dst, tid);
-      glds_tile<BN, false>(B + (kh * 3 + kw) * C, ldb, n0, p.N, cin, dst + BM * BK, tid);
-    }
-  };
-  auto compute = [&](const bf16_t* cur) {
-    bf16x8 af[FM], bfr[FN];
-    v2i ra[2 * FM], rb[2 * FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      if constexpr (AKC) af[i] = frag<BM, true>(cur, wr * WM + i * 16, lane);
-      else frag_tr_raw<BM>(cur, wr * WM + i * 16, lane, ra + 2 * i);
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      if constexpr (BKC) bfr[j] = frag<BN, true>(cur + BM * BK, wc * WN + j * 16, lane);
-      else frag_tr_raw<BN>(cur + BM * BK, wc * WN + j * 16, lane, rb + 2 * j);
-    }
-    if constexpr (!AKC) {
-      tie_lgkm<2 * FM>(ra);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = frag_from_raw(ra + 2 * i);
-    }
-    if constexpr (!BKC) {
-      tie_lgkm<2 * FN>(rb);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = frag_from_raw(rb + 2 * j);
-    }
-    if (LASR_EXP & 1) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) acc[i][0][0] += (float)af[i][0] + (float)bfr[0][i & 1];
-      return;
-    }
-    // swapped operands: acc[i][j] accumulates the C^T fragment (gemm_epilogue_direct)
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-  };
-
-  // fused bias gradient (rowsum of A) on the n-tile-0 blocks; uniform per block
-  const bool do_rs = !AKC && p.rowsum != nullptr && tx == 0;
-  float rs[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) rs[q] = 0.f;
-
-#pragma unroll
-  for (int t = 0; t < S - 1; ++t)
-    if (t < nfull) issue(t);
-
-  for (int kt = 0; kt < nfull; ++kt) {
-    const int after = min(S - 2, nfull - 1 - kt);  // tiles issued after kt (still in flight)
-    wait_ring<S, GL>(after);
-    lds_barrier();
-    if (kt + S - 1 < nfull) issue(kt + S - 1);
-    compute(smem + (kt % S) * TILE);
-    if constexpr (!AKC)
-      if (do_rs) rowsum_tile<BM>(smem + (kt % S) * TILE, tid, rs);
-  }
-  if (G == G_LIN && nfull < nk) {  // ragged tail: register loader with zero fill (conv: host-checked K % 32 == 0)
-    __syncthreads();
-    TileLoader<BM, AKC> la;
-    TileLoader<BN, BKC> lb;
-    const int k0 = kbeg + nfull * BK;
-    la.load(A, AKC ? p.lda_m : 0, AKC ? 0 : p.lda_k, m0, p.M, k0, kend, true, tid);
-    lb.load(B, BKC ? p.ldb_n : 0, BKC ? 0 : p.ldb_k, n0, p.N, k0, kend, true, tid);
-    la.store(smem, tid);
-    lb.store(smem + BM * BK, tid);
-    __syncthreads();
-    compute(smem);
-    if constexpr (!AKC)
-      if (do_rs) rowsum_tile<BM>(smem, tid, rs);
-  }
-  __syncthreads();
-  if constexpr (!AKC) {
-    if (do_rs) {  // combine the k groups in fixed order, then one slot per row
-      constexpr int CH = BM / 8, KG = 256 / CH;
-      float* red = reinterpret_cast<float*>(smem_epi);
-      const int c = tid % CH, kg = tid / CH;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) red[kg * BM + 8 * c + q] = rs[q];
-      __syncthreads();
-      if (tid < BM) {
-        float t = 0.f;
-        for (int g = 0; g < KG; ++g) t += red[g * BM + tid];
-        const int m = m0 + tid;
-        if (m < p.M) {
-          if (p.split_k > 1) p.rs_ws[(int64_t)s * p.M + m] = t;
-          else p.rowsum[m] += t;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // split-K partials: fp32, 16-B per lane straight from the accumulators; final outputs:
-  // staged through LDS (full 256-B rows per wave store)
-  if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC>(p, acc, m0, n0, s, z, z1, z2);
-  else gemm_epilogue<BM, BN, TC, true, G>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
-}
-
-// ============================ fp32 MFMA kernel ===================================
-template <bool AKC, bool BKC, typename TC>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
-  constexpr int BM = 64, BN = 64, BK = 16, LD = BK + 1;
-  __shared__ float As[BM * LD], Bs[BN * LD];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int zz = blockIdx.z;
-  const int s = zz % p.split_k, z = zz / p.split_k;
-  const int z1 = z / p.batch_div, z2 = z % p.batch_div;
-  const float* A = (const float*)p.A + z1 * p.sa1 + z2 * p.sa2;
-  const float* B = (const float*)p.B + z1 * p.sb1 + z2 * p.sb2;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = s * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
-
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + q * 256;
-      int r, k;
-      if (AKC) { r = e >> 4; k = e & 15; } else { r = e & 63; k = e >> 6; }
-      const int gm = m0 + r, gk = k0 + k;
-      As[r * LD + k] = (gm < p.M && gk < kend) ? A[(int64_t)gm * p.lda_m + (int64_t)gk * p.lda_k] : 0.f;
-      if (BKC) { r = e >> 4; k = e & 15; } else { r = e & 63; k = e >> 6; }
-      const int gn = n0 + r, gk2 = k0 + k;
-      Bs[r * LD + k] = (gn < p.N && gk2 < kend) ? B[(int64_t)gn * p.ldb_n + (int64_t)gk2 * p.ldb_k] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      float af[2], bfv[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = As[(wr * 32 + i * 16 + (lane & 15)) * LD + kk + (lane >> 4)];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfv[j] = Bs[(wc * 32 + j * 16 + (lane & 15)) * LD + kk + (lane >> 4)];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  const int rq = (lane >> 4) * 4, cl = lane & 15;
-  if (p.split_k > 1) {
-    float* ws = p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + wr * 32 + i * 16 + rq + e, n = n0 + wc * 32 + j * 16 + cl;
-          if (m < p.M && n < p.N) ws[(int64_t)m * p.N + n] = acc[i][j][e];
-        }
-    return;
-  }
-  const float al = alpha_of(p);
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wr * 32 + i * 16 + rq + e, n = n0 + wc * 32 + j * 16 + cl;
-        epi_store<TC>(p, z1, z2, z, m, n, acc[i][j][e], al);
-      }
-}
-
-// Split-K reduction: sums the split partials in fixed order, then the epilogue.
-template <typename TC>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
-  const int64_t MN = (int64_t)p.M * p.N;
-  const int64_t total = MN * p.batch;
-  const float al = alpha_of(p);
-  if (p.v4) {
-    // 4 consecutive columns per thread (N % 4 == 0): 16-B partial loads, 4 slices in
-    // flight, summed in slice order
-    const int64_t sstride = (int64_t)p.batch * MN;
-    for (int64_t i4 = blockIdx.x * 256 + threadIdx.x; i4 < total / 4; i4 += (int64_t)gridDim.x * 256) {
-      const int64_t i = i4 * 4;
-      const int z = (int)(i / MN);
-      const int64_t r = i - (int64_t)z * MN;
-      const float* src = p.ws + (int64_t)z * MN + r;
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      int sl = 0;
-      for (; sl + 4 <= p.split_k; sl += 4) {
-        f32x4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *(const f32x4*)(src + (int64_t)(sl + u) * sstride);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[e] += v[u][e];
-      }
-      for (; sl < p.split_k; ++sl) {
-        const f32x4 v = *(const f32x4*)(src + (int64_t)sl * sstride);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] += v[e];
-      }
-      const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
-      epi_store4<TC, true>(p, z / p.batch_div, z % p.batch_div, z, m, n, 4, acc, al);
-    }
-  } else {
-    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-      const int z = (int)(i / MN);
-      const int64_t r = i - (int64_t)z * MN;
-      float acc = 0.f;
-      for (int s = 0; s < p.split_k; ++s) acc += p.ws[((int64_t)s * p.batch + z) * MN + r];
-      const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
-      epi_store<TC>(p, z / p.batch_div, z % p.batch_div, z, m, n, acc, al);
-    }
-  }
-  if (p.rs_ws) {  // bias-gradient partials (batch == 1)
-    for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < p.M; m += (int64_t)gridDim.x * 256) {
-      float acc = 0.f;
-      for (int s = 0; s < p.split_k; ++s) acc += p.rs_ws[(int64_t)s * p.M + m];
-      p.rowsum[m] += acc;
-    }
-  }
-}
+#include "gemm_kernel.h"
 
 // ================================ host launcher ==================================
-static int g_stages = 0;  // lasr_gemm_force_split (tuning hook)
+int g_stages = 0;  // lasr_gemm_force_split (tuning hook)
 
 template <bool AKC, bool BKC, typename TC>
 static void launch_bf16(const GemmP& p, int BM, int BN, bool glds, dim3 grid, hipStream_t st) {
@@ -986,7 +65,6 @@ static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int
   }
 }
 
-static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 static bool getenv_flag(const char* name) {
   static int cached = -1;  // read once (A/B switch for benchmarking the register-staged path)
   if (cached < 0) {
@@ -998,7 +76,7 @@ static bool getenv_flag(const char* name) {
 
 // Tuning hook (tools/gemm_graph_bench.py): force the LDS-DMA tile of every later call;
 // 0 = the planner's choice.  Process-wide, not for product use.
-static int g_tile_m = 0, g_tile_n = 0, g_split = 0;
+int g_tile_m = 0, g_tile_n = 0, g_split = 0;
 extern "C" int lasr_gemm_force_tile(int tile_m, int tile_n) {
   const bool ok = (tile_m == 0 && tile_n == 0) ||
                   ((tile_m == 64 || tile_m == 128 || tile_m == 256) &&
@@ -1060,7 +138,8 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     // heavy epilogues over wide outputs (FFN fc1 forward: pre-activation copy + Swish +
     // dropout; FFN dX fc2: activation-gradient aux + dropout; N 2048): 128x256 halves the
     // per-output epilogue bookkeeping (cold-cache sweep: 32 vs 38 us, 40.2 vs 44.6 us)
-    if (BM == 128 && BN == 128 && (a->zout || a->aux) && a->N >= 1024) BN = 256;
+    // (also the gate-free fc1 forward: bias + Swish + dropout without zout)
+    if (BM == 128 && BN == 128 && (a->zout || a->aux || (a->act && a->drop_p > 0.f)) && a->N >= 1024) BN = 256;
   }
   if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
@@ -1083,7 +162,6 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
 // LDS-DMA eligibility: bf16, 16-B aligned rows/columns; for a non-K-contiguous operand the
 // row stride covers the extent rounded up to 8 (a 16-B chunk never leaves its row; the
 // padding columns only feed discarded outputs).
-static bool aligned16(const void* ptr);
 static bool getenv_flag(const char* name);
 static bool gemm_uses_glds(const lasr_gemm_args* a) {
   if (a->in_dtype != LASR_BF16) return false;
@@ -1212,119 +290,3 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
                      a->workspace_bytes / 4, stream);
 }
 
-// ========================= subsampling conv2, implicit GEMM ======================
-// (lasr_conv2_gemm, include/liteasr_hip.h) Same LDS-DMA kernel, gather instances G_FWD /
-// G_DW / G_DX: im2col(y1) is never materialised, and the data gradient is scattered straight
-// into dy1 per output parity class (no dcol, no col2im).  Replaces the reference's
-// nn.Conv2d(C, C, 3, 2) forward and backward (liteasr/nets/subsampling.py:31-47).
-static GemmP conv_params(const lasr_conv2_args* a) {
-  GemmP p;
-  memset(&p, 0, sizeof(p));
-  p.batch = 1;
-  p.batch_div = 1;
-  p.alpha = 1.f;
-  p.res_scale = 1.f;
-  p.split_k = 1;
-  p.drop = mkdrop(0.f, 0);
-  ConvG& g = p.cv;
-  g.B = a->B; g.T1 = a->T1; g.F1 = a->F1; g.C = a->C;
-  g.T2 = (a->T1 - 3) / 2 + 1;
-  g.F2 = (a->F1 - 3) / 2 + 1;
-  g.M2 = g.B * g.T2 * g.F2;
-  g.q32 = 32 / g.F2;
-  g.r32 = 32 % g.F2;
-  return p;
-}
-
-extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
-  LASR_CHECK_ARG(a != nullptr, "lasr_conv2_gemm: null args");
-  LASR_CHECK_ARG(a->mode == LASR_CONV2_FWD || a->mode == LASR_CONV2_DW || a->mode == LASR_CONV2_DX,
-                 "lasr_conv2_gemm: bad mode");
-  LASR_CHECK_ARG(a->B > 0 && a->T1 >= 3 && a->F1 >= 3 && a->C > 0 && a->C % 128 == 0,
-                 "lasr_conv2_gemm: needs B > 0, T1, F1 >= 3 and C % 128 == 0");
-  LASR_CHECK_ARG((int64_t)a->B * a->T1 * a->F1 * a->C < (1LL << 31) && 9LL * a->C * a->C < (1LL << 31),
-                 "lasr_conv2_gemm: tensors past 2^31 elements");
-  LASR_CHECK_ARG(a->y1 && a->out && aligned16(a->y1) && aligned16(a->out), "lasr_conv2_gemm: y1/out");
-  GemmP p = conv_params(a);
-  const ConvG& g = p.cv;
-  const int C = a->C;
-  const int64_t kpad = cdiv(g.M2, 32) * 32;
-  if (a->mode != LASR_CONV2_FWD)
-    LASR_CHECK_ARG(a->dy2 && aligned16(a->dy2) && a->dy2_rows >= kpad && a->dy2_rows >= g.M2 + 1,
-                   "lasr_conv2_gemm: dy2 needs >= max(roundup32(M2), M2 + 1) rows, the tail zero");
-  if (a->mode != LASR_CONV2_DW)
-    LASR_CHECK_ARG(a->w2p && aligned16(a->w2p), "lasr_conv2_gemm: w2p");
-  hipStream_t st = (hipStream_t)stream;
-  const int BN = C % 256 == 0 ? 256 : 128;
-  p.c_vec = 1;
-  if (a->mode == LASR_CONV2_FWD) {
-    LASR_CHECK_ARG(a->bias && aligned16(a->bias), "lasr_conv2_gemm: bias");
-    p.M = g.M2; p.N = C; p.K = 9 * C; p.kchunk = p.K;
-    p.A = a->y1; p.lda_m = 9 * C; p.lda_k = 1;
-    p.B = a->w2p; p.ldb_n = 9 * C; p.ldb_k = 1;
-    p.C = a->out; p.ldc = C;
-    p.bias = a->bias; p.bias_vec = 1; p.act = LASR_ACT_RELU;
-    p.epi_mode = 0;
-    dim3 grid((unsigned)(C / BN), (unsigned)cdiv(p.M, 128), 1);
-    LASR_CHECK_ARG(grid.y <= 65535, "lasr_conv2_gemm: grid too large");
-    if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, true, bf16_t, 3, 2, G_FWD><<<grid, 256, 0, st>>>(p);
-    else gemm_bf16_glds_kernel<128, 128, true, true, bf16_t, 3, 3, G_FWD><<<grid, 256, 0, st>>>(p);
-    return lasr_check_launch("lasr_conv2_gemm/fwd");
-  }
-  if (a->mode == LASR_CONV2_DW) {
-    p.M = C; p.N = 9 * C; p.K = (int)kpad;
-    p.A = a->dy2; p.lda_m = 1; p.lda_k = C;
-    p.B = a->y1; p.ldb_n = 1; p.ldb_k = 9 * C;
-    p.C = a->out; p.ldc = 9 * C;
-    p.epi_mode = 0; p.ws_vec = 1; p.v4 = 1;
-    const bool big = g_tile_m == 256 && C % 256 == 0;
-    const int TM = big ? 256 : 128, TN = big ? 256 : 128;
-    const int64_t tiles = (int64_t)(C / TM) * (9 * C / TN);
-    int split = 1;
-    const int kt = (int)(kpad / 32);
-    if (g_split > 0) split = g_split;
-    else while (tiles * split < 512 && kt / (split * 2) >= 16 && split * 2 <= 64) split *= 2;
-    const int64_t need = ((int64_t)split * C * 9 * C + (a->rowsum ? (int64_t)split * C : 0)) * 4;
-    if (split > 1 && (!a->workspace || a->workspace_bytes < need || !aligned16(a->workspace))) split = 1;
-    p.split_k = split;
-    p.kchunk = split > 1 ? (int)(cdiv(cdiv(kpad, split), 32) * 32) : (int)kpad;
-    p.ws = (float*)a->workspace;
-    p.rowsum = a->rowsum;
-    if (a->rowsum && split > 1) p.rs_ws = p.ws + (int64_t)split * C * 9 * C;
-    dim3 grid((unsigned)(9 * C / TN), (unsigned)(C / TM), (unsigned)split);
-    if (big) gemm_bf16_glds_kernel<256, 256, false, false, float, 3, 1, G_DW><<<grid, 256, 0, st>>>(p);
-    else if (g_stages >= 4) gemm_bf16_glds_kernel<128, 128, false, false, float, 4, 2, G_DW><<<grid, 256, 0, st>>>(p);
-    else gemm_bf16_glds_kernel<128, 128, false, false, float, 3, 3, G_DW><<<grid, 256, 0, st>>>(p);
-    int rc = lasr_check_launch("lasr_conv2_gemm/dw");
-    if (!rc && split > 1) {
-      const int64_t total = (int64_t)C * 9 * C;
-      const int nblk = (int)std::min<int64_t>(cdiv(total / 4, 256), 4096);
-      splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);
-      rc = lasr_check_launch("lasr_conv2_gemm/dw_reduce");
-    }
-    return rc;
-  }
-  // LASR_CONV2_DX: one launch per output parity class, heaviest (4 taps) first
-  p.N = C;
-  p.A = a->dy2; p.lda_m = C; p.lda_k = 1;
-  p.B = a->w2p; p.ldb_n = 1; p.ldb_k = 9 * C;
-  p.C = a->out; p.ldc = C;
-  p.aux = a->y1; p.aux_dtype = LASR_BF16; p.ldaux = C; p.aux_act = LASR_ACT_RELU; p.aux_vec = 1;
-  p.epi_mode = 1;
-  p.cv.zero = (const bf16_t*)a->dy2 + (int64_t)g.M2 * C;
-  for (int cls = 0; cls < 4; ++cls) {
-    const int pt = cls >> 1, pf = cls & 1;
-    const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
-    p.cv.cls = cls;
-    p.M = g.B * nI * nJ;
-    p.K = (pt ? 1 : 2) * (pf ? 1 : 2) * C;
-    p.kchunk = p.K;
-    dim3 grid((unsigned)(C / BN), (unsigned)cdiv(p.M, 128), 1);
-    LASR_CHECK_ARG(grid.y <= 65535, "lasr_conv2_gemm: grid too large");
-    if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, false, bf16_t, 3, 2, G_DX><<<grid, 256, 0, st>>>(p);
-    else gemm_bf16_glds_kernel<128, 128, true, false, bf16_t, 3, 3, G_DX><<<grid, 256, 0, st>>>(p);
-    const int rc = lasr_check_launch("lasr_conv2_gemm/dx");
-    if (rc) return rc;
-  }
-  return LASR_OK;
-}

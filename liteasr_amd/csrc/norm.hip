@@ -11,9 +11,11 @@ constexpr int LN_ROWS_PER_BLOCK = 32;  // backward: rows per block (one partial 
 // Lane l owns the NPL contiguous columns [l*NPL, (l+1)*NPL) of a row (vector loads).
 template <int NPL, typename TX, typename TY, typename TY2>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, int64_t rows,
-                                                     const float* gamma, const float* beta,
-                                                     float eps, TY* y, float* mean, float* rstd,
-                                                     TY2* y2, DropCfg d2) {
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     TY* __restrict__ y, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, TY2* __restrict__ y2,
+                                                     DropCfg d2) {
   constexpr int D = NPL * 64;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
@@ -57,12 +59,16 @@ struct LnbCfg {
 };
 
 template <int NPL, typename TX, typename TD, typename TR, typename TDX, typename TGB>
+// (every pointer __restrict__: lets the compiler issue a wave's second-row loads ahead of
+// its first-row stores)
 __global__ __launch_bounds__(1024) void ln_bwd_kernel(const TX* __restrict__ x,
                                                       const TD* __restrict__ dy, int64_t rows,
-                                                      const float* gamma, const float* mean,
-                                                      const float* rstd, const TR* dres, TDX* dx,
-                                                      float* part, TGB* gb, float bscale,
-                                                      DropCfg bd) {
+                                                      const float* __restrict__ gamma,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd,
+                                                      const TR* __restrict__ dres, TDX* __restrict__ dx,
+                                                      float* __restrict__ part, TGB* __restrict__ gb,
+                                                      float bscale, DropCfg bd) {
   constexpr int D = NPL * 64, WAVES = LnbCfg<NPL>::WAVES, RPW = LnbCfg<NPL>::RPW;
   __shared__ float sp[WAVES][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -688,3 +688,18 @@ def glancing_mix(replace, a, b, out, out2=None, backward=False):
     rows, D = out.shape
     N.call("lasr_glancing_mix", rows, D, ptr(replace), ptr(a), ptr(b), ptr(out), ptr(out2), int(backward),
            stream())
+
+
+def ffn_dz(ln, W1, b1, gb, W2, act, p1, seed1, dz):
+    """dz = (gb @ W2) * act'(ln @ W1^T + b1) * keep * scale (lasr_ffn_dz; the fc1 forward's
+    dropout draws for (p1, seed1))."""
+    M, D = ln.shape
+    F_ = W1.shape[0]
+    for t in (ln, W1, gb, W2, dz):
+        assert t.dtype == torch.bfloat16 and t.is_contiguous()
+    assert tuple(W2.shape) == (D, F_) and tuple(gb.shape) == (M, D) and tuple(dz.shape) == (M, F_)
+    a = N.FfnDzArgs()
+    a.M, a.D, a.F, a.act = M, D, F_, act
+    a.ln, a.W1, a.b1, a.gb, a.W2 = ptr(ln), ptr(W1), ptr(b1), ptr(gb), ptr(W2)
+    a.p1, a.seed1, a.dz = p1, int(seed1) & 0xFFFFFFFFFFFFFFFF, ptr(dz)
+    N.call("lasr_ffn_dz", C.byref(a), stream())

@@ -67,38 +67,69 @@ def _fused_ffn(x, W1):
     return FUSED_FFN and K.ffn_supported(x, W1)
 
 
+# FFN data gradient with the gate recomputed (lasr_ffn_dz): the forward stores only h and the
+# backward recomputes u = ln W1^T per tile instead of writing and re-reading an [M, F] gate.
+# Correct (tests/test_kernels_gpu.py::test_ffn_dz_recomputed_gate) but slower at the step's
+# shapes (60 us vs 33.5 us for the stored-gate dX GEMM), so opt-in with
+# LASR_FFN_GATE_RECOMPUTE=1.
+GATE_STORE = os.environ.get("LASR_FFN_GATE_RECOMPUTE", "0") != "1"
+
+
+class _GateRecompute:
+    """ffn_forward's stand-in for the stored gate: the backward recomputes it from ln, W1, b1."""
+
+    __slots__ = ("b1",)
+
+    def __init__(self, b1):
+        self.b1 = b1
+
+
+def _recompute_gate(ln, W1):
+    M, D = ln.shape
+    F_ = W1.shape[0]
+    return (not GATE_STORE and ln.dtype == torch.bfloat16 and D % 32 == 0 and F_ % 128 == 0
+            and ln.is_contiguous() and W1.is_contiguous())
+
+
 def ffn_forward(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res):
-    """Returns (out, g, h): g = act'(fc1 pre-activation) * keep (the dropout keep flag) is
-    what the backward needs in place of the pre-activation (the fc1 epilogue writes it,
-    zout_mode 1), so the dX GEMM multiplies by g instead of re-deriving act' and the
-    dropout mask per element."""
+    """Returns (out, g, h).  g is what the backward needs for act' and the dropout keep:
+    either the stored gate act'(u) * keep (fc1 epilogue, zout_mode 1; fp32 build) or a
+    _GateRecompute marker (bf16 build: lasr_ffn_dz recomputes u in the backward)."""
     M = ln.shape[0]
     dev, adt = ln.device, ln.dtype
-    g = _e((M, W1.shape[0]), adt, dev)
     h = _e((M, W1.shape[0]), adt, dev)
     out = _e((M, W2.shape[0]), F32, dev)
     if _fused_ffn(ln, W1):  # one launch: the [M, F] intermediate stays on chip (ffn.hip)
+        g = _e((M, W1.shape[0]), adt, dev)
         K.ffn_fwd(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res, g, h, out)
         return out, g, h
-    K.linear(ln, W1, h, bias=b1, act=act, zout=g, zout_mode=1, drop_p=p_ff, drop_seed=s_ff)
+    if _recompute_gate(ln, W1):
+        g = _GateRecompute(b1)
+        K.linear(ln, W1, h, bias=b1, act=act, drop_p=p_ff, drop_seed=s_ff)
+    else:
+        g = _e((M, W1.shape[0]), adt, dev)
+        K.linear(ln, W1, h, bias=b1, act=act, zout=g, zout_mode=1, drop_p=p_ff, drop_seed=s_ff)
     K.linear(h, W2, out, bias=b2, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res)
     return out, g, h
 
 
 def ffn_backward(gb, ln, g, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
     """gb: gradient of the FFN output (after the residual-branch dropout/scale); g: the
-    forward's gate act'(z) * keep."""
+    forward's gate act'(z) * keep, or the marker to recompute it."""
     M = gb.shape[0]
     dev, adt = gb.device, gb.dtype
     K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0, rowsum=gb2)
     dz = _e((M, W1.shape[0]), adt, dev)
     dln = _e((M, W1.shape[1]), adt, dev)
-    if _fused_ffn(gb, W1):  # dz and dln in one launch (ffn.hip)
+    if isinstance(g, _GateRecompute):
+        K.ffn_dz(ln, W1, g.b1, gb, W2, act, p_ff, s_ff, dz)
+    elif _fused_ffn(gb, W1):  # dz and dln in one launch (ffn.hip)
         K.ffn_bwd_dx(gb, W1, W2, g, act, p_ff, s_ff, dz, dln)
         K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
         return dln
-    # dz = (gb W2) * scale * g: the dropout scale as alpha, the gate as aux
-    K.gemm(gb, W2, dz, alpha=K.dropout_scale(p_ff), aux=g, aux_act=ACT_GATE)
+    else:
+        # dz = (gb W2) * scale * g: the dropout scale as alpha, the gate as aux
+        K.gemm(gb, W2, dz, alpha=K.dropout_scale(p_ff), aux=g, aux_act=ACT_GATE)
     K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
     K.gemm(dz, W1, dln)
     return dln

@@ -964,3 +964,44 @@ def test_ffn_fused_chains(M, D, F, act, p):
         dz64 = (gb.double() @ W2.double()) * z.cpu().double()  # the saved bf16 gate, as used
         close(dz, dz64, 2e-2, "ffn dz vs float64")
         close(dx, dz.cpu().double() @ W1.double(), 2e-2, "ffn dx vs float64 (of the bf16 dz)")
+
+
+@pytest.mark.parametrize("M,D,F,act,p", [(7968, 256, 2048, "swish", 0.1), (300, 256, 512, "relu", 0.0),
+                                         (130, 512, 2048, "swish", 0.3), (64, 64, 256, "relu", 0.1)])
+def test_ffn_dz_recomputed_gate(M, D, F, act, p):
+    """lasr_ffn_dz (fc1 product recomputed per tile) == the stored-gate path (fc1 epilogue
+    writes act'(u)*keep, the fc2 dX GEMM multiplies by it) up to the gate's bf16 rounding, and
+    matches a float64 reference built from the forward's own dropout mask (the kept h)."""
+    from liteasr_amd import _native as Nn
+
+    kn = K()
+    g = torch.Generator(device="cpu").manual_seed(M + D)
+    bf = torch.bfloat16
+    ln = torch.randn(M, D, generator=g).to(bf).to(DEV)
+    w1 = (torch.randn(F, D, generator=g) / D ** 0.5).to(bf).to(DEV)
+    b1 = (torch.randn(F, generator=g) * 0.1).to(DEV)
+    w2 = (torch.randn(D, F, generator=g) / F ** 0.5).to(bf).to(DEV)
+    gb = torch.randn(M, D, generator=g).to(bf).to(DEV)
+    a = Nn.ACT_SWISH if act == "swish" else Nn.ACT_RELU
+    seed = 1234
+    h = torch.empty(M, F, device=DEV, dtype=bf)
+    gate = torch.empty_like(h)
+    kn.linear(ln, w1, h, bias=b1, act=a, zout=gate, zout_mode=1, drop_p=p, drop_seed=seed)
+    dz_old = torch.empty(M, F, device=DEV, dtype=bf)
+    kn.gemm(gb, w2, dz_old, alpha=kn.dropout_scale(p), aux=gate, aux_act=Nn.ACT_GATE)
+    dz = torch.empty_like(dz_old)
+    kn.ffn_dz(ln, w1, b1, gb, w2, a, p, seed, dz)
+    torch.cuda.synchronize()
+    close(dz, dz_old, 1e-2, "ffn_dz vs stored gate")
+    # float64 reference: u, act', the forward's keep (h != 0 where act(u) != 0)
+    u = ln.double() @ w1.double().t() + b1.double()
+    if act == "swish":
+        s = torch.sigmoid(u)
+        d = s * (1 + u * (1 - s))
+        hv = u * s
+    else:
+        d = (u > 0).double()
+        hv = torch.relu(u)
+    keep = ((h.double() != 0) | (hv.abs() < 1e-30)).double() if p > 0 else torch.ones_like(u)
+    ref = (gb.double() @ w2.double()) * d * keep * (kn.dropout_scale(p) if p > 0 else 1.0)
+    close(dz, ref, 8e-3, "ffn_dz vs fp64")

@@ -13,10 +13,10 @@ from tools.gemm_graph_bench import graph_time, make  # noqa: E402
 
 SHAPES = [("ffn W1 2048x256", 2048, 256, 7968), ("ffn W2 256x2048", 256, 2048, 7968),
           ("Wo 256x256", 256, 256, 7968), ("pw1 512x256", 512, 256, 7968), ("qkv 768x256", 768, 256, 7968)]
-TILES = [(0, 0), (64, 64), (64, 128), (128, 64), (128, 128), (128, 256), (256, 128)]
+TILES = [(0, 0), (64, 64), (64, 128), (128, 64), (128, 128)]
 
 
-SPLITS = (0, 8, 16, 32)
+SPLITS = (0, 4, 8, 16)
 STAGES = (0,)
 
 
