@@ -12,11 +12,17 @@ import sqlite3
 import sys
 
 
+def _is_comm(name):
+    """RCCL kernels: the ring/tree collectives and, in a world-1 group, oneRankReduce."""
+    n = name.lower()
+    return "nccl" in n or "rccl" in n or "onerankreduce" in n
+
+
 def main():
     db = sys.argv[1]
     c = sqlite3.connect(db)
     rows = list(c.execute("select name, start, end from kernels order by start"))
-    is_ar = [("nccl" in n.lower() or "rccl" in n.lower()) for n, _, _ in rows]
+    is_ar = [_is_comm(n) for n, _, _ in rows]
     # a step ends with the optimizer kernel; take the last adam launch as the step end
     ends = [i for i, (n, _, _) in enumerate(rows) if "adam_kernel" in n]
     if len(ends) < 2:
@@ -28,10 +34,10 @@ def main():
     for k, (n, s, e) in enumerate(step):
         if is_ar[lo + k]:
             after = step[k + 1:]
-            busy_after = sum(x[2] - x[1] for x in after if not ("nccl" in x[0].lower() or "rccl" in x[0].lower()))
+            busy_after = sum(x[2] - x[1] for x in after if not _is_comm(x[0]))
             out["allreduce"].append({"at_us": round((s - t0) / 1e3, 1), "dur_us": round((e - s) / 1e3, 1),
                                      "kernels_after": len(after), "gpu_us_after": round(busy_after / 1e3, 1),
-                                     "name": n.split("(")[0][:60]})
+                                     "name": n.split("(")[1 if n.startswith("void (") else 0][:60]})
     print(json.dumps(out, indent=1))
 
 
