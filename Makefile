@@ -7,7 +7,7 @@ LIB   := liteasr_amd/lib/libliteasr_hip.so
 IOLIB := liteasr_amd/lib/libliteasr_io.so
 DECLIB := liteasr_amd/lib/libliteasr_decode.so
 CXX   ?= g++
-HDRS  := liteasr_amd/csrc/common.h liteasr_amd/csrc/tile.h liteasr_amd/csrc/gemm_kernel.h include/liteasr_hip.h
+HDRS  := liteasr_amd/csrc/common.h liteasr_amd/csrc/tile.h liteasr_amd/csrc/gemm_kernel.h liteasr_amd/csrc/gemm_launch.h include/liteasr_hip.h
 FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC
 
 all: $(LIB) $(IOLIB) $(DECLIB)

@@ -69,6 +69,9 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 # template instance lasr_gemm launches for a split-K weight-gradient tile (gemm.hip
 # launch_bf16): ring depth and launch bound per tile
 _DW_INSTANCE = {(128, 128): (3, 3), (64, 128): (4, 3), (128, 64): (4, 3), (64, 64): (4, 3)}
+# ... with 64-deep ring stages (LASR_PLAN_KSUB2): ring depth, launch bound, sub-tiles
+_DW_INSTANCE_KS2 = {(128, 128): (2, 2), (64, 128): (3, 2), (128, 64): (3, 2), (64, 64): (3, 3)}
+PLAN_KSUB2 = 4
 
 
 def roofline_case(cfgd, dev):
@@ -92,15 +95,20 @@ def roofline_case(cfgd, dev):
     dz = torch.randn(rows, M, device=dev).bfloat16()
     ln = torch.randn(rows, N, device=dev).bfloat16()
     dw = torch.zeros(M, N, device=dev)
-    tm, tn, split = K.gemm_plan(dz.t(), ln, dw, beta=1.0, split_k=-1)
+    tm, tn, split, flags = K.gemm_plan(dz.t(), ln, dw, flags=True, beta=1.0, split_k=-1)
 
     def launch():
         K.gemm(dz.t(), ln, dw, beta=1.0, split_k=-1)
 
     flops = 2.0 * M * N * Kd
     bytes_ = 2.0 * (Kd * M + Kd * N) + 4.0 * M * N
-    S, minb = _DW_INSTANCE[(tm, tn)]
-    meta = {"kernel": f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}, 0>",
+    if flags & PLAN_KSUB2:
+        S, minb = _DW_INSTANCE_KS2[(tm, tn)]
+        inst = f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}, 0, 2>"
+    else:
+        S, minb = _DW_INSTANCE[(tm, tn)]
+        inst = f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}, 0>"
+    meta = {"kernel": inst,
             "shape": f"M={M} N={N} K={Kd} split_k={split}",
             "grid": [-(-N // tn), -(-M // tm), split]}
     return launch, flops, bytes_, meta
@@ -130,7 +138,7 @@ def hottest_case(cfgd, dev):
 
     flops = 2.0 * M * F * D
     bytes_ = 2.0 * (M * D + F * D) + 2 * 2.0 * M * F + 4.0 * F
-    meta = {"kernel": "gemm_bf16_glds_kernel<128, 256, true, true, unsigned short, 3, 2, 0>",
+    meta = {"kernel": "gemm_bf16_glds_kernel<128, 256, true, true, unsigned short, 3, 2, 0, 1>",
             "shape": f"M={M} N={F} K={D} bias+swish+gate+dropout", "grid": [F // 256, -(-M // 128), 1]}
     return launch, flops, bytes_, meta
 

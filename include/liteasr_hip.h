@@ -99,6 +99,7 @@ float lasr_dropout_scale(float p);
  * workspace, else it is written to rowsum directly). */
 #define LASR_PLAN_GLDS 1
 #define LASR_PLAN_ROWSUM_FUSED 2
+#define LASR_PLAN_KSUB2 4 /* 64-deep LDS ring stages (two 32-deep sub-tiles per wait) */
 int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k, int* flags);
 /* Tuning hook: force the bf16 LDS-DMA tile (64/128/256 x 64/128/256) of every later
  * lasr_gemm call in the process; (0, 0) restores the planner.  Benchmarks only. */
@@ -106,6 +107,10 @@ int lasr_gemm_force_tile(int tile_m, int tile_n);
 /* Tuning hook: force the split-K factor of auto-split calls and the LDS ring depth (3..6)
  * of split-K LDS-DMA launches; (0, 0) restores the planner.  Benchmarks only. */
 int lasr_gemm_force_split(int split_k, int stages);
+/* Tuning hook: force the k depth of the bf16 LDS-DMA ring stages of every later lasr_gemm
+ * call (1 = 32-deep stages, 2 = 64-deep: two 32-deep sub-tiles per counted wait + barrier);
+ * 0 restores the planner.  Benchmarks only. */
+int lasr_gemm_force_ksub(int ksub);
 
 /* FFN data gradient through the activation with the gate recomputed (liteasr/nets/
  * feed_forward.py:18-19 backward): dz = (gb @ W2) * act'(ln @ W1^T + b1) * keep * scale,

@@ -497,12 +497,17 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
 // dK, dV of one key block: loops over the query blocks; per block the Qu / dO images (A of
 // the scores, B of dK / dV), query stats and the position window are staged (next block
 // prefetched), the K / V fragments of the block stay in registers.
+// LDS: the G windows (score_tile) and the P / dS images live in one union region (a
+// barrier separates the last G read from the first P / dS write), so a workgroup takes
+// <= 80 KB and two fit on a CU: the 512-workgroup grid of the small config runs in one round
+// (d_k 64 with a query-dependent mask needs > 256 VGPRs: one wave per SIMD there).
 template <int DK, bool RM>
-__global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
+__global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_kernel(RelAttnP a) {
   constexpr int KS = DK / 32;
-  __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
-  __shared__ __attribute__((aligned(16))) bf16_t pimg[64 * 64];  // P  [i][j]
-  __shared__ __attribute__((aligned(16))) bf16_t simg[64 * 64];  // dS [i][j]
+  constexpr int GBYTES = 4 * 16 * GLD * 4, PBYTES = 2 * 64 * 64 * 2;
+  __shared__ __attribute__((aligned(16))) char ush[GBYTES > PBYTES ? GBYTES : PBYTES];
+  bf16_t* pimg = reinterpret_cast<bf16_t*>(ush);  // P  [i][j]
+  bf16_t* simg = pimg + 64 * 64;                  // dS [i][j]
   __shared__ __attribute__((aligned(16))) bf16_t oimg[64 * 64];  // dO [i][c]
   __shared__ __attribute__((aligned(16))) bf16_t qimg[64 * 64];  // Qu [i][c]
   __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
@@ -516,7 +521,7 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
   const bf16_t* ph = a.pos + h * DK;
   const bf16_t* quh = a.qu + base * a.ldq + h * DK;
   const bf16_t* doh = a.dctx + base * a.ldc + h * DK;
-  float* gw = gsh[w];
+  float* gw = reinterpret_cast<float*>(ush) + w * 16 * GLD;
   KeyMask km;
   keymask_fetch(a, b, j0, lane, km);
   const uint32_t mbits = keymask_bits(km);
@@ -570,6 +575,7 @@ __global__ __launch_bounds__(256, 1) void relattn_bwd_kv_kernel(RelAttnP a) {
     }
     score_tile<DK, RM>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mbits, msh, gw, s, lane);
     dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
+    __syncthreads();  // every wave's G window consumed: the P / dS images overwrite them
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll

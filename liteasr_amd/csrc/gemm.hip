@@ -19,44 +19,26 @@
 // ================================ host launcher ==================================
 int g_stages = 0;  // lasr_gemm_force_split (tuning hook)
 
+// bf16 launch table: gemm_launch.h, instantiated per operand layout in gemm_l{0..3}.hip
 template <bool AKC, bool BKC, typename TC>
-static void launch_bf16(const GemmP& p, int BM, int BN, bool glds, dim3 grid, hipStream_t st) {
-  if constexpr (!AKC && !BKC && std::is_same<TC, float>::value) {
-    // split-K weight-gradient GEMMs: one block per CU, so a deeper ring hides the latency
-    const int S = g_stages;
-    if (glds && p.split_k > 1 && S >= 4) {
-#define DWL(bm, bn, s, mb) gemm_bf16_glds_kernel<bm, bn, false, false, float, s, mb><<<grid, 256, 0, st>>>(p)
-      if (BM == 128 && BN == 128) { if (S == 4) DWL(128, 128, 4, 2); else if (S == 5) DWL(128, 128, 5, 1); else DWL(128, 128, 6, 1); return; }
-      if (BM == 64 && BN == 128) { if (S == 4) DWL(64, 128, 4, 3); else if (S == 5) DWL(64, 128, 5, 2); else DWL(64, 128, 6, 2); return; }
-      if (BM == 128 && BN == 64) { if (S == 4) DWL(128, 64, 4, 3); else if (S == 5) DWL(128, 64, 5, 2); else DWL(128, 64, 6, 2); return; }
-      if (BM == 64 && BN == 64) { if (S == 4) DWL(64, 64, 4, 4); else if (S == 5) DWL(64, 64, 5, 3); else DWL(64, 64, 6, 3); return; }
-#undef DWL
-    }
-  }
-  if (glds) {
-    if (BM == 256 && BN == 256) gemm_bf16_glds_kernel<256, 256, AKC, BKC, TC, 3, 1><<<grid, 256, 0, st>>>(p);
-    else if (BM == 256) gemm_bf16_glds_kernel<256, 128, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
-    else if (BN == 256) gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
-    else if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
-    else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
-    else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
-    else gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
-    return;
-  }
-  if (BM == 128 && BN == 128) gemm_bf16_kernel<128, 128, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
-  else if (BM == 128) gemm_bf16_kernel<128, 64, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
-  else if (BN == 128) gemm_bf16_kernel<64, 128, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
-  else gemm_bf16_kernel<64, 64, AKC, BKC, TC><<<grid, 256, 0, st>>>(p);
-}
+void launch_bf16(const GemmP& p, int BM, int BN, int ks, bool glds, dim3 grid, hipStream_t st);
+#define LASR_EXTERN_LAUNCH(ak, bk)                                                                    \
+  extern template void launch_bf16<ak, bk, float>(const GemmP&, int, int, int, bool, dim3, hipStream_t); \
+  extern template void launch_bf16<ak, bk, bf16_t>(const GemmP&, int, int, int, bool, dim3, hipStream_t);
+LASR_EXTERN_LAUNCH(true, true)
+LASR_EXTERN_LAUNCH(true, false)
+LASR_EXTERN_LAUNCH(false, true)
+LASR_EXTERN_LAUNCH(false, false)
+#undef LASR_EXTERN_LAUNCH
 
 template <typename TC>
-static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int BN, bool glds,
+static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int BN, int ks, bool glds,
                      dim3 grid, hipStream_t st) {
   if (bf16in) {
-    if (akc && bkc) launch_bf16<true, true, TC>(p, BM, BN, glds, grid, st);
-    else if (akc) launch_bf16<true, false, TC>(p, BM, BN, glds, grid, st);
-    else if (bkc) launch_bf16<false, true, TC>(p, BM, BN, glds, grid, st);
-    else launch_bf16<false, false, TC>(p, BM, BN, glds, grid, st);
+    if (akc && bkc) launch_bf16<true, true, TC>(p, BM, BN, ks, glds, grid, st);
+    else if (akc) launch_bf16<true, false, TC>(p, BM, BN, ks, glds, grid, st);
+    else if (bkc) launch_bf16<false, true, TC>(p, BM, BN, ks, glds, grid, st);
+    else launch_bf16<false, false, TC>(p, BM, BN, ks, glds, grid, st);
   } else {
     if (akc && bkc) gemm_f32_kernel<true, true, TC><<<grid, 256, 0, st>>>(p);
     else if (akc) gemm_f32_kernel<true, false, TC><<<grid, 256, 0, st>>>(p);
@@ -76,7 +58,7 @@ static bool getenv_flag(const char* name) {
 
 // Tuning hook (tools/gemm_graph_bench.py): force the LDS-DMA tile of every later call;
 // 0 = the planner's choice.  Process-wide, not for product use.
-int g_tile_m = 0, g_tile_n = 0, g_split = 0;
+int g_tile_m = 0, g_tile_n = 0, g_split = 0, g_ksub = 0;
 extern "C" int lasr_gemm_force_tile(int tile_m, int tile_n) {
   const bool ok = (tile_m == 0 && tile_n == 0) ||
                   ((tile_m == 64 || tile_m == 128 || tile_m == 256) &&
@@ -98,8 +80,14 @@ extern "C" int lasr_gemm_force_split(int split_k, int stages) {
   return LASR_OK;
 }
 
+extern "C" int lasr_gemm_force_ksub(int ksub) {
+  LASR_CHECK_ARG(ksub >= 0 && ksub <= 2, "lasr_gemm_force_ksub: ksub must be 0, 1 or 2");
+  g_ksub = ksub;
+  return LASR_OK;
+}
+
 // Tile and split-K choice for one call (shared by lasr_gemm and lasr_gemm_plan).
-static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) {
+static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, int* kso = nullptr) {
   const int batch = a->batch > 0 ? a->batch : 1;
   const bool bf = a->in_dtype == LASR_BF16;
   int BM = 64, BN = 64;
@@ -140,6 +128,8 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
     // per-output epilogue bookkeeping (cold-cache sweep: 32 vs 38 us, 40.2 vs 44.6 us)
     // (also the gate-free fc1 forward: bias + Swish + dropout without zout)
     if (BM == 128 && BN == 128 && (a->zout || a->aux || (a->act && a->drop_p > 0.f)) && a->N >= 1024) BN = 256;
+    // (FFN fc2 forward, M 7968 N 256 K 2048: 64 x 128 wins the cold-operand sweep, 24.2 vs
+    // 27.6 us, but loses inside the step, 33.5 vs 24 us per launch: kept at 64 x 64)
   }
   if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
@@ -154,6 +144,15 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito) 
   if (split > 1 && (!plain || !a->workspace ||
                     a->workspace_bytes < ((int64_t)split * batch * a->M * a->N + rs_floats) * 4))
     split = 1;
+  // ring depth of the LDS-DMA kernel: 64-deep stages (two 32-deep sub-tiles per counted
+  // wait + barrier) for 64 x 64 tiles and long k loops; 32-deep for the wide 128 x 256 tiles
+  // (their 64-deep ring fits only 2 stages) and short-K big tiles (tools/ksub_sweep.py)
+  if (kso) {
+    const int64_t kc = split > 1 ? cdiv(a->K, split) : a->K;
+    const bool small = BM * BN <= 64 * 128;
+    *kso = (bf && BM < 256 && BN < 256 && ((BM == 64 && BN == 64) || kc >= 1024 || (kc >= 512 && small))) ? 2 : 1;
+    if (g_ksub) *kso = g_ksub;
+  }
   *BMo = BM;
   *BNo = BN;
   *splito = split;
@@ -176,10 +175,12 @@ static bool gemm_uses_glds(const lasr_gemm_args* a) {
 
 extern "C" int lasr_gemm_plan(const lasr_gemm_args* a, int* tile_m, int* tile_n, int* split_k, int* flags) {
   LASR_CHECK_ARG(a && tile_m && tile_n && split_k, "lasr_gemm_plan: null argument");
-  gemm_plan(a, tile_m, tile_n, split_k);
+  int ks = 1;
+  gemm_plan(a, tile_m, tile_n, split_k, &ks);
   if (flags) {
     const bool glds = gemm_uses_glds(a);
-    *flags = (glds ? LASR_PLAN_GLDS : 0) | (a->rowsum && glds && a->lda_k != 1 ? LASR_PLAN_ROWSUM_FUSED : 0);
+    *flags = (glds ? LASR_PLAN_GLDS : 0) | (a->rowsum && glds && a->lda_k != 1 ? LASR_PLAN_ROWSUM_FUSED : 0) |
+             (glds && ks == 2 && *tile_m < 256 ? LASR_PLAN_KSUB2 : 0);
   }
   return LASR_OK;
 }
@@ -248,8 +249,8 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
     p.epi_mode = !base_ok ? 2 : nsrc == 0 ? 0 : src_ok ? 1 : 2;
   }
 
-  int BM, BN, split;
-  gemm_plan(a, &BM, &BN, &split);
+  int BM, BN, split, ks;
+  gemm_plan(a, &BM, &BN, &split, &ks);
   p.split_k = split;
   const int kstep = bf ? 32 : 16;
   p.kchunk = split > 1 ? (int)(cdiv(cdiv(a->K, split), kstep) * kstep) : a->K;
@@ -274,8 +275,8 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
     p.rowsum = a->rowsum;
     if (split > 1) p.rs_ws = p.ws + (int64_t)split * batch * a->M * a->N;
   }
-  if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, glds, grid, st);
-  else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, glds, grid, st);
+  if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, ks, glds, grid, st);
+  else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, ks, glds, grid, st);
   int rc = lasr_check_launch("lasr_gemm");
   if (!rc && split > 1 && a->split_k >= 0) {
     const int64_t total = (int64_t)a->M * a->N * batch;

@@ -683,14 +683,18 @@ LASR_DEV void ffn_gate(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], f32x4 (&g
   }
 }
 
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN>
+// KS: 32-deep k sub-tiles per ring stage (G_LIN only).  KS = 2 makes the stage 64 deep: one
+// counted wait + barrier per 64 k and twice the DMA bytes per issue (the guide's "fix BK first").
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN, int KS = 1>
 __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
   static_assert(G == G_LIN || (G == G_DW ? (!AKC && !BKC) : (AKC && (G == G_FWD) == BKC)),
                 "gather / FFN instance operand orientation");
+  static_assert(KS == 1 || (KS == 2 && G == G_LIN), "k sub-tiles: generic instances only");
   constexpr int BK = 32;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  constexpr int TILE = (BM + BN) * BK;  // elements per ring stage
-  constexpr int MAIN_BYTES = S * TILE * 2;  // >= the rowsum combine slab (256/(BM/8) x BM floats)
+  constexpr int TILE = (BM + BN) * BK;  // elements per 32-deep sub-tile
+  constexpr int STAGE = KS * TILE;      // elements per ring stage
+  constexpr int MAIN_BYTES = S * STAGE * 2;  // >= the rowsum combine slab (256/(BM/8) x BM floats)
   constexpr int EPI_BYTES = WM * (BN + 4) * 4;
   constexpr int GL = (BM + BN) * 4 / 256;  // glds per thread per k tile
   __shared__ __attribute__((aligned(16))) char smem_epi[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
@@ -733,12 +737,15 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
   if constexpr (G == G_DX) ga.init_dx(p.cv, m0, p.M, tid);
   if constexpr (G == G_DW) gb.init(p.cv, n0, p.N, kbeg, tid);
   auto issue = [&](int t) {
-    bf16_t* dst = smem + (t % S) * TILE;
-    const int k0 = kbeg + t * BK;
+    bf16_t* dst = smem + (t % S) * STAGE;
+    const int k0 = kbeg + t * (KS * BK);
     if (LASR_EXP & 4) return;
     if constexpr (G == G_LIN) {
-      glds_tile<BM, AKC>(A, lda, m0, p.M, k0, dst, tid);
-      glds_tile<BN, BKC>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
+#pragma unroll
+      for (int u = 0; u < KS; ++u) {
+        glds_tile<BM, AKC>(A, lda, m0, p.M, k0 + u * BK, dst + u * TILE, tid);
+        glds_tile<BN, BKC>(B, ldb, n0, p.N, k0 + u * BK, dst + u * TILE + BM * BK, tid);
+      }
     } else if constexpr (G == G_FFN) {
       if (t < nk1) {
         glds_tile<BM, true>((const bf16_t*)p.A1, p.lda1, m0, p.M, t * BK, dst, tid);
@@ -820,24 +827,41 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) rs[q] = 0.f;
 
+  const int nst = nfull / KS;  // full ring stages; KS > 1 leaves nfull % KS sub-tiles
 #pragma unroll
   for (int t = 0; t < S - 1; ++t)
-    if (t < nfull) issue(t);
+    if (t < nst) issue(t);
 
   [[maybe_unused]] f32x4 gate[G == G_FFN ? FM : 1][G == G_FFN ? FN : 1];
-  for (int kt = 0; kt < nfull; ++kt) {
-    const int after = min(S - 2, nfull - 1 - kt);  // tiles issued after kt (still in flight)
-    wait_ring<S, GL>(after);
+  for (int kt = 0; kt < nst; ++kt) {
+    const int after = min(S - 2, nst - 1 - kt);  // stages issued after kt (still in flight)
+    wait_ring<S, GL * KS>(after);
     lds_barrier();
-    if (kt + S - 1 < nfull) issue(kt + S - 1);
+    if (kt + S - 1 < nst) issue(kt + S - 1);
     if constexpr (G == G_FFN) {
-      compute(smem + (kt % S) * TILE, kt < nk1);
+      compute(smem + (kt % S) * STAGE, kt < nk1);
       if (kt == nk1 - 1) ffn_gate<BM, BN>(p, acc, gate, m0, n0, wr, wc, lane);
     } else {
-      compute(smem + (kt % S) * TILE);
+#pragma unroll
+      for (int u = 0; u < KS; ++u) compute(smem + (kt % S) * STAGE + u * TILE);
     }
     if constexpr (!AKC)
-      if (do_rs) rowsum_tile<BM>(smem + (kt % S) * TILE, tid, rs);
+      if (do_rs)
+#pragma unroll
+        for (int u = 0; u < KS; ++u) rowsum_tile<BM>(smem + (kt % S) * STAGE + u * TILE, tid, rs);
+  }
+  if constexpr (KS > 1) {
+    // leftover full sub-tile(s): the loop's last wait was vmcnt(0), so no DMA is in flight
+    for (int j = nst * KS; j < nfull; ++j) {
+      __syncthreads();
+      glds_tile<BM, AKC>(A, lda, m0, p.M, kbeg + j * BK, smem, tid);
+      glds_tile<BN, BKC>(B, ldb, n0, p.N, kbeg + j * BK, smem + BM * BK, tid);
+      wait_vmcnt<0>();
+      lds_barrier();
+      compute(smem);
+      if constexpr (!AKC)
+        if (do_rs) rowsum_tile<BM>(smem, tid, rs);
+    }
   }
   if constexpr (G == G_FFN) {
 #pragma unroll

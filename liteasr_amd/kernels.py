@@ -195,8 +195,10 @@ def gemm(
         ws = WS.get(need, c.device)
         args.workspace, args.workspace_bytes = ptr(ws), ws.numel() * 4
     if plan_only:
-        tm, tn, sp = C.c_int(), C.c_int(), C.c_int()
-        N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp), None)
+        tm, tn, sp, fl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp), C.byref(fl))
+        if plan_only == "flags":
+            return tm.value, tn.value, sp.value, fl.value
         return tm.value, tn.value, sp.value
     if (_DEFER.depth and split_k == 0 and beta in (0.0, 1.0) and alpha == 1.0 and alpha_dev is None
             and bias is None and act == N.ACT_NONE and zout is None and aux is None and res is None
@@ -219,9 +221,10 @@ def gemm(
     return c
 
 
-def gemm_plan(a, b, c, **kw):
-    """(tile_m, tile_n, split_k) lasr_gemm would use for this call (nothing is launched)."""
-    return gemm(a, b, c, plan_only=True, **kw)
+def gemm_plan(a, b, c, flags=False, **kw):
+    """(tile_m, tile_n, split_k) lasr_gemm would use for this call (nothing is launched);
+    flags=True appends the LASR_PLAN_* bits (LDS-DMA path, fused rowsum, 64-deep stages)."""
+    return gemm(a, b, c, plan_only="flags" if flags else True, **kw)
 
 
 def linear(x, w, out, bias=None, **kw):
