@@ -112,6 +112,15 @@ int lasr_gemm_force_split(int split_k, int stages);
  * 0 restores the planner.  Benchmarks only. */
 int lasr_gemm_force_ksub(int ksub);
 
+/* Grouped split-K weight gradients (liteasr/trainer.py:142 loss.backward: the per-module
+ * weight gradients of one Conformer layer / the decoder): n <= 8 independent partials-only
+ * problems dW_i = A_i^T B_i (args[i] as for lasr_gemm with split_k = -1: A M-contiguous,
+ * B N-contiguous, bf16, no epilogue, workspace for [split][M][N] partials + [split][M]
+ * rowsum partials when rowsum is set) that plan the same tile with 64-deep stages, in one
+ * launch; the partials are bit-identical to separate lasr_gemm calls.  The caller reduces
+ * them (lasr_reduce_multi). */
+int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* stream);
+
 /* FFN data gradient through the activation with the gate recomputed (liteasr/nets/
  * feed_forward.py:18-19 backward): dz = (gb @ W2) * act'(ln @ W1^T + b1) * keep * scale,
  * keep / scale = the fc1 forward's dropout draws (lasr_gemm epilogue, element m*F + f, same

@@ -121,6 +121,7 @@ SIGNATURES = {
     "lasr_gemm_force_tile": [C.c_int, C.c_int],
     "lasr_gemm_force_split": [C.c_int, C.c_int],
     "lasr_gemm_force_ksub": [C.c_int],
+    "lasr_gemm_dw_group": [C.POINTER(GemmArgs), _i, _p],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
                          _p, _p, _p, _i, _i, _p, _p, _l, _p],

@@ -291,3 +291,51 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
                      a->workspace_bytes / 4, stream);
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Grouped split-K weight gradients (partials only): the deferred dW GEMMs of one backward
+// node in one launch.  Every problem must be what lasr_gemm would run as a partials-only
+// (split_k = -1) LDS-DMA launch with 64-deep stages, A M-contiguous and B N-contiguous
+// (dW = dY^T X), and all must share the planned tile; the partials (+ fused rowsum partials)
+// land exactly where lasr_gemm would put them, bit for bit.
+int launch_dw_group(const DwGroupP& g, int BM, int BN, int blocks, hipStream_t st);
+
+extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* stream) {
+  LASR_CHECK_ARG(args && n >= 1 && n <= LASR_DW_GROUP_MAX, "lasr_gemm_dw_group: 1..%d problems", LASR_DW_GROUP_MAX);
+  DwGroupP g = {};
+  g.n = n;
+  int BM0 = 0, BN0 = 0, blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const lasr_gemm_args* a = args + i;
+    LASR_CHECK_ARG(a->in_dtype == LASR_BF16 && a->c_dtype == LASR_F32, "lasr_gemm_dw_group: bf16 in, fp32 partials");
+    LASR_CHECK_ARG(a->lda_m == 1 && a->lda_k != 1 && a->ldb_n == 1 && a->ldb_k != 1,
+                   "lasr_gemm_dw_group: A M-contiguous and B N-contiguous (dW = dY^T X)");
+    LASR_CHECK_ARG(a->split_k == -1 && a->workspace && (a->batch <= 1) && a->M > 0 && a->N > 0 && a->K > 0,
+                   "lasr_gemm_dw_group: partials-only problems with a workspace");
+    LASR_CHECK_ARG(!a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f && !a->bias,
+                   "lasr_gemm_dw_group: no epilogue");
+    LASR_CHECK_ARG(gemm_uses_glds(a), "lasr_gemm_dw_group: operands not LDS-DMA eligible");
+    int BM, BN, split, ks;
+    gemm_plan(a, &BM, &BN, &split, &ks);
+    LASR_CHECK_ARG(split > 1 && ks == 2, "lasr_gemm_dw_group: plan is not a split-K 64-deep launch");
+    LASR_CHECK_ARG(i == 0 || (BM == BM0 && BN == BN0), "lasr_gemm_dw_group: problems plan different tiles");
+    BM0 = BM;
+    BN0 = BN;
+    g.M[i] = a->M; g.N[i] = a->N; g.K[i] = a->K;
+    g.split[i] = split;
+    g.kchunk[i] = (int)(cdiv(cdiv(a->K, split), 32) * 32);
+    g.v4[i] = a->N % 4 == 0 && aligned16(a->workspace);
+    g.A[i] = a->A; g.lda[i] = a->lda_k;
+    g.B[i] = a->B; g.ldb[i] = a->ldb_k;
+    g.ws[i] = (float*)a->workspace;
+    g.rs_ws[i] = a->rowsum ? (float*)a->workspace + (int64_t)split * a->M * a->N : nullptr;
+    g.start[i] = blocks;
+    const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)split;
+    LASR_CHECK_ARG(blocks + nb + 8 < (1ll << 31), "lasr_gemm_dw_group: too many blocks");
+    blocks += (int)cdiv(nb, 8) * 8;
+  }
+  g.start[n] = blocks;
+  LASR_CHECK_ARG(launch_dw_group(g, BM0, BN0, blocks, (hipStream_t)stream) == 0,
+                 "lasr_gemm_dw_group: no grouped instance for tile %dx%d", BM0, BN0);
+  return lasr_check_launch("lasr_gemm_dw_group");
+}

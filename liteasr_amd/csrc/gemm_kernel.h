@@ -685,8 +685,17 @@ LASR_DEV void ffn_gate(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], f32x4 (&g
 
 // KS: 32-deep k sub-tiles per ring stage (G_LIN only).  KS = 2 makes the stage 64 deep: one
 // counted wait + barrier per 64 k and twice the DMA bytes per issue (the guide's "fix BK first").
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN, int KS = 1>
-__global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
+// XCD-aware (bijective) remap of tile `orig` among `nwg` tiles: tiles that share an XCD (the
+// hardware deals blocks round-robin over the 8 XCDs) get consecutive tile indices.
+LASR_DEV int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+}
+
+// One output tile (tx, ty) of K slice / batch index zz: the body shared by the launch-grid
+// kernel (gemm_bf16_glds_kernel) and the grouped weight-gradient kernel (gemm_dw_group_kernel).
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int G, int KS>
+LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const int zz) {
   static_assert(G == G_LIN || (G == G_DW ? (!AKC && !BKC) : (AKC && (G == G_FWD) == BKC)),
                 "gather / FFN instance operand orientation");
   static_assert(KS == 1 || (KS == 2 && G == G_LIN), "k sub-tiles: generic instances only");
@@ -702,14 +711,6 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
 
-  // XCD-aware (bijective) remap of the 2-D tile index
-  const int nx = gridDim.x, nwg = gridDim.x * gridDim.y;
-  const int orig = blockIdx.y * nx + blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tx = wg % nx, ty = wg / nx;
-
-  const int zz = blockIdx.z;
   const int s = zz % p.split_k, z = zz / p.split_k;
   const int z1 = z / p.batch_div, z2 = z % p.batch_div;
   const bf16_t* A = (const bf16_t*)p.A + z1 * p.sa1 + z2 * p.sa2;
@@ -908,6 +909,54 @@ __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
   // staged through LDS (full 256-B rows per wave store)
   if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC>(p, acc, m0, n0, s, z, z1, z2);
   else gemm_epilogue<BM, BN, TC, true, G>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
+}
+
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN, int KS = 1>
+__global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
+  const int nx = gridDim.x;
+  const int wg = xcd_remap(blockIdx.y * nx + blockIdx.x, gridDim.x * gridDim.y);
+  gemm_glds_tile<BM, BN, AKC, BKC, TC, S, G, KS>(p, wg % nx, wg / nx, blockIdx.z);
+}
+
+// Grouped split-K weight-gradient GEMMs (partials only): up to LASR_DW_GROUP_MAX independent
+// problems dW_i = A_i^T B_i (A [K, M] and B [K, N] row-major, i.e. both M/N-contiguous), each
+// with its own split, in ONE launch.  Problem i owns the blocks [start[i], start[i+1]) (starts
+// multiples of 8, so the XCD remap inside a problem stays exact), K-slice-major like the
+// launch grid of the single-problem kernel; the tile code and the partial layout
+// ([split][M][N] + [split][M] rowsum partials) are those of gemm_bf16_glds_kernel, so the
+// partials are bit-identical to separate launches.
+#define LASR_DW_GROUP_MAX 8
+struct DwGroupP {
+  int n;
+  int start[LASR_DW_GROUP_MAX + 1];
+  int M[LASR_DW_GROUP_MAX], N[LASR_DW_GROUP_MAX], K[LASR_DW_GROUP_MAX];
+  int split[LASR_DW_GROUP_MAX], kchunk[LASR_DW_GROUP_MAX], v4[LASR_DW_GROUP_MAX];
+  const void* A[LASR_DW_GROUP_MAX];
+  const void* B[LASR_DW_GROUP_MAX];
+  int64_t lda[LASR_DW_GROUP_MAX], ldb[LASR_DW_GROUP_MAX];
+  float* ws[LASR_DW_GROUP_MAX];
+  float* rs_ws[LASR_DW_GROUP_MAX];  // null: no fused bias rowsum
+};
+
+template <int BM, int BN, int S, int MINB>
+__global__ __launch_bounds__(256, MINB) void gemm_dw_group_kernel(DwGroupP g) {
+  const int blk = blockIdx.x;
+  int i = 0;
+  for (int j = 1; j < g.n; ++j)
+    if (blk >= g.start[j]) i = j;
+  const int ntx = (g.N[i] + BN - 1) / BN, nty = (g.M[i] + BM - 1) / BM, ntile = ntx * nty;
+  const int local = blk - g.start[i];
+  if (local >= ntile * g.split[i]) return;  // alignment padding
+  GemmP p = {};
+  p.M = g.M[i]; p.N = g.N[i]; p.K = g.K[i]; p.batch = 1; p.batch_div = 1;
+  p.A = g.A[i]; p.lda_m = 1; p.lda_k = g.lda[i];
+  p.B = g.B[i]; p.ldb_n = 1; p.ldb_k = g.ldb[i];
+  p.split_k = g.split[i]; p.kchunk = g.kchunk[i]; p.ws = g.ws[i]; p.v4 = g.v4[i];
+  p.rowsum = g.rs_ws[i];  // only tested for null when split_k > 1: the partials go to rs_ws
+  p.rs_ws = g.rs_ws[i];
+  p.alpha = 1.f;
+  const int wg = xcd_remap(local % ntile, ntile);
+  gemm_glds_tile<BM, BN, false, false, float, S, G_LIN, 2>(p, wg % ntx, wg / ntx, local / ntile);
 }
 
 // ============================ fp32 MFMA kernel ===================================

@@ -9,6 +9,7 @@ no CPU path (the CPU restatement lives in ``oracle/`` and is test-only).
 from __future__ import annotations
 
 import contextlib
+import os
 import ctypes as C
 import math
 from typing import Optional
@@ -70,6 +71,7 @@ class _Deferred:
     def __init__(self):
         self.depth = 0
         self.segs = []
+        self.gemms = []  # queued partials-only dW GEMMs: (tile key, args, operand refs)
 
 
 _DEFER = _Deferred()
@@ -94,7 +96,30 @@ def _defer(part, P, Ncols, out0, out1=None, split=None, accumulate=True):
                         int(accumulate)))
 
 
+# Grouped weight gradients: dW GEMMs marked group=True inside a deferred_reductions block are
+# queued and launched at its end, one lasr_gemm_dw_group launch per planned tile (<= 8
+# problems each), before the reductions.  LASR_DW_GROUP=0 launches them one by one instead.
+DW_GROUP = os.environ.get("LASR_DW_GROUP", "1") != "0"
+_GROUP_TILES = {(64, 64), (64, 128), (128, 64)}
+_GROUP_MAX = 8
+
+
+def _flush_gemm_group():
+    q, _DEFER.gemms = _DEFER.gemms, []
+    byt = {}
+    for key, args, refs in q:
+        byt.setdefault(key, []).append(args)
+    for key, lst in byt.items():
+        for i in range(0, len(lst), _GROUP_MAX):
+            chunk = lst[i:i + _GROUP_MAX]
+            arr = (N.GemmArgs * len(chunk))(*chunk)
+            N.call("lasr_gemm_dw_group", arr, len(chunk), stream())
+    # the operand references in q die here, after the launches were enqueued
+
+
 def flush_reductions():
+    if _DEFER.gemms:
+        _flush_gemm_group()
     segs, _DEFER.segs = _DEFER.segs, []
     if not segs:
         return
@@ -142,11 +167,16 @@ def gemm(
     rowsum: Optional[torch.Tensor] = None,
     plan_only: bool = False,
     zout_mode: int = 0,
+    group: bool = False,
 ):
     """c = epilogue(alpha * a @ b) for logical views a (..,M,K), b (..,K,N), c (..,M,N).
 
     Views may be arbitrarily strided as long as each operand has one unit stride
-    (the kernel handles K-contiguous and M/N-contiguous operands)."""
+    (the kernel handles K-contiguous and M/N-contiguous operands).
+
+    group=True (a split-K weight gradient inside deferred_reductions): the launch itself may
+    be deferred to the end of the block and grouped with the block's other dW GEMMs, so
+    the caller must not modify a or b before the block exits."""
     M, K = a.shape[-2], a.shape[-1]
     K2, Nn = b.shape[-2], b.shape[-1]
     assert K == K2 and c.shape[-2] == M and c.shape[-1] == Nn, (a.shape, b.shape, c.shape)
@@ -212,7 +242,11 @@ def gemm(
             part = torch.empty(sp * M * Nn + nrs, dtype=torch.float32, device=c.device)
             args.split_k = -1
             args.workspace, args.workspace_bytes = ptr(part), part.numel() * 4
-            N.call("lasr_gemm", C.byref(args), stream())
+            if (group and DW_GROUP and (tm.value, tn.value) in _GROUP_TILES and (fl.value & 5) == 5
+                    and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16):
+                _DEFER.gemms.append(((tm.value, tn.value), N.GemmArgs.from_buffer_copy(args), (a, b)))
+            else:
+                N.call("lasr_gemm", C.byref(args), stream())
             _defer(part, sp, M * Nn, c, accumulate=beta == 1.0)
             if rowsum is not None and fl.value & 2:  # LASR_PLAN_ROWSUM_FUSED: partials follow C's
                 _defer(part[sp * M * Nn:], sp, M, rowsum)

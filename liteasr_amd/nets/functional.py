@@ -118,19 +118,19 @@ def ffn_backward(gb, ln, g, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
     forward's gate act'(z) * keep, or the marker to recompute it."""
     M = gb.shape[0]
     dev, adt = gb.device, gb.dtype
-    K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0, rowsum=gb2)
+    K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0, rowsum=gb2, group=True)
     dz = _e((M, W1.shape[0]), adt, dev)
     dln = _e((M, W1.shape[1]), adt, dev)
     if isinstance(g, _GateRecompute):
         K.ffn_dz(ln, W1, g.b1, gb, W2, act, p_ff, s_ff, dz)
     elif _fused_ffn(gb, W1):  # dz and dln in one launch (ffn.hip)
         K.ffn_bwd_dx(gb, W1, W2, g, act, p_ff, s_ff, dz, dln)
-        K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
+        K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1, group=True)
         return dln
     else:
         # dz = (gb W2) * scale * g: the dropout scale as alpha, the gate as aux
         K.gemm(gb, W2, dz, alpha=K.dropout_scale(p_ff), aux=g, aux_act=ACT_GATE)
-    K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1)
+    K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1, group=True)
     K.gemm(dz, W1, dln)
     return dln
 
@@ -206,7 +206,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     M = B * T
     scale = dk ** -0.5
     ldS = ld_scores(T)
-    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo)
+    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo, group=True)
     dctx = _e((M, d), adt, dev)
     K.gemm(gb, w.Wo, dctx)
     dqkv = _e((M, 3 * d), adt, dev)
@@ -227,7 +227,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
                dp.view(T, H, dk).permute(1, 0, 2), alpha=scale, split_k=0)
         K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
         K.gemm(dp.t(), pos, g.Wpos, beta=1.0)
-        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv)
+        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
         dln = _e((M, d), adt, dev)
         K.gemm(dqkv, w.Wqkv, dln)
         return dln
@@ -255,7 +255,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     K.reduce_batch(dpb, B, H, T, dk, dp)
     K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
     K.gemm(dp.t(), pos, g.Wpos, beta=1.0)
-    K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv)
+    K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
     dln = _e((M, d), adt, dev)
     K.gemm(dqkv, w.Wqkv, dln)
     return dln
@@ -305,7 +305,7 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
     R = B * Tq
     scale = dk ** -0.5
     ldS = ld_scores(Tk)
-    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo)
+    K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo, group=True)
     dctx = _e((R, d), adt, dev)
     K.gemm(gb, w.Wo, dctx)
     dctx4 = _heads(dctx, B, Tq, H, dk)
@@ -334,12 +334,12 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
     K.gemm(dS[..., :Tk].transpose(-1, -2), q4, dk4, alpha=scale)
     dln = _e((R, d), adt, dev)
     if mem is None:
-        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv)
+        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
         K.gemm(dqkv, w.Wqkv, dln)
     else:
-        K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq)
+        K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq, group=True)
         K.gemm(dq, w.Wq, dln)
-        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv)
+        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
         K.gemm(dkv, w.Wkv, dmem, beta=1.0)
     return dln
 
@@ -370,7 +370,7 @@ def conv_backward(gb, ln, sv, w, g, env):
     B, T = env.B, env.T
     M, d = ln.shape
     dev, adt = ln.device, ln.dtype
-    K.gemm(gb.t(), sv.h3, g.Wpw2, beta=1.0, split_k=0, rowsum=g.bpw2)
+    K.gemm(gb.t(), sv.h3, g.Wpw2, beta=1.0, split_k=0, rowsum=g.bpw2, group=True)
     dh3 = _e((M, d), adt, dev)
     K.gemm(gb, w.Wpw2, dh3)
     dy = _e((M, d), F32, dev)
@@ -378,7 +378,7 @@ def conv_backward(gb, ln, sv, w, g, env):
                    batch_stats=sv.training)
     dz1 = _e((M, 2 * d), adt, dev)
     K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
-    K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0, rowsum=g.bpw1)
+    K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0, rowsum=g.bpw1, group=True)
     dln = _e((M, d), adt, dev)
     K.gemm(dz1, w.Wpw1, dln)
     return dln
@@ -529,14 +529,17 @@ class ConformerLayerFn(torch.autograd.Function):
             dln = ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2,
                                g.ff.b2, ACT_SWISH, pff, _seed(s, 6))
             dx3 = _e((M, d), F32, dev)
+            gb = _e((M, d), adt, dev)  # fresh: grouped dW GEMMs read it at the end of the node
             K.layernorm_bwd(x3, dln, w.ln_d.g, md, rd, dx3, g.ln_d.g, g.ln_d.b, dres=dx4, gb=gb,
                             bscale=1.0, bp=pd, bseed=_seed(s, 5))
             dln = conv_backward(gb, ln_c, sv.svc, w.conv, g.conv, env)
             dx2 = _e((M, d), F32, dev)
+            gb = _e((M, d), adt, dev)  # fresh: grouped dW GEMMs read it at the end of the node
             K.layernorm_bwd(x2, dln, w.ln_c.g, mc, rc, dx2, g.ln_c.g, g.ln_c.b, dres=dx3, gb=gb,
                             bscale=1.0, bp=pd, bseed=_seed(s, 4))
             dln = relmha_backward(gb, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3))
             dx1 = _e((M, d), F32, dev)
+            gb = _e((M, d), adt, dev)  # fresh: grouped dW GEMMs read it at the end of the node
             K.layernorm_bwd(x1, dln, w.ln_b.g, mb, rb, dx1, g.ln_b.g, g.ln_b.b, dres=dx2, gb=gb,
                             bscale=0.5, bp=pd, bseed=_seed(s, 2))
             dln = ffn_backward(gb, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1,
@@ -598,21 +601,24 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
     K.gemm(g_attn, wd.Wout, dyf)
     dy = _e((R, d), F32, dev)
     K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
-    gb = _e((R, d), adt, dev)
     for i in range(len(wd.layers) - 1, -1, -1):
         lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
         s = dec.dec_layers[i].seed + sv.seed_shift
         y0, y1, y2 = ls.y
         l1, l2, l3 = ls.ln
         (m1, r1), (m2, r2), (m3, r3) = ls.st
+        # fresh gb per branch: the grouped dW GEMMs read it at the end of the node
+        gb = _e((R, d), adt, dev)
         K.branch_grad(dy, gb, 1.0, pd, _seed(s, 6))
         dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1, lg.ff.W2, lg.ff.b2,
                            ACT_RELU, pff, _seed(s, 5))
         dy2 = _e((R, d), F32, dev)
+        gb = _e((R, d), adt, dev)
         K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb, bscale=1.0, bp=pd,
                         bseed=_seed(s, 4))
         dln = mha_backward(gb, l2, h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, mmask, T, 0, pca, _seed(s, 3), dh)
         dy1 = _e((R, d), F32, dev)
+        gb = _e((R, d), adt, dev)
         K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb, bscale=1.0, bp=pd,
                         bseed=_seed(s, 2))
         dln = mha_backward(gb, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, smask, smsb, smsq, pat,

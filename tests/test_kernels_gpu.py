@@ -266,6 +266,42 @@ def test_gemm_ksub2_bit_identical(ta, tb, M, N, Kd, tile):
     close(outs[1][1], ref, 1e-2, "zout")
 
 
+@pytest.mark.parametrize("R", [3001, 7968])
+def test_gemm_dw_group_bit_identical(R):
+    """Grouped split-K weight gradients (lasr_gemm_dw_group: the dW GEMMs of a backward node
+    queued with group=True and launched together at the end of deferred_reductions) give
+    the same bits as one lasr_gemm launch per problem, with and without the fused bias
+    rowsum, accumulating (beta 1) and overwriting (beta 0)."""
+    kn = K()
+    g = torch.Generator().manual_seed(R)
+    probs = [(2048, 256, True, 1.0), (256, 2048, True, 1.0), (256, 256, True, 1.0), (768, 256, True, 0.0),
+             (512, 256, False, 1.0), (2048, 256, True, 1.0), (256, 256, False, 1.0)]
+    ins = [(torch.randn(R, M, generator=g).to(DEV, torch.bfloat16), torch.randn(R, N, generator=g).to(DEV, torch.bfloat16),
+            torch.randn(M, N, generator=g).to(DEV), torch.randn(M, generator=g).to(DEV) if rs else None, beta)
+           for M, N, rs, beta in probs]
+    outs = {}
+    for grouped in (False, True):
+        res = []
+        with kn.deferred_reductions():
+            for dy, x, dw0, db0, beta in ins:
+                dw = dw0.clone()
+                db = db0.clone() if db0 is not None else None
+                kn.gemm(dy.t(), x, dw, beta=beta, split_k=0, rowsum=db, group=grouped)
+                res.append((dw, db))
+            assert (len(kn._DEFER.gemms) > 0) == (grouped and kn.DW_GROUP)
+        torch.cuda.synchronize()
+        outs[grouped] = res
+    for (a, ab), (b, bb) in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
+        if ab is not None:
+            assert torch.equal(ab, bb)
+    for (dy, x, dw0, db0, beta), (dw, db) in zip(ins, outs[True]):
+        ref = beta * dw0.double() + dy.double().t() @ x.double()
+        close(dw, ref, 1e-2, "grouped dW")
+        if db0 is not None:
+            close(db, db0.double() + dy.double().sum(0), 1e-5, "grouped db")
+
+
 def test_gemm_dropout_matches_branch_grad():
     kn = K()
     M, N, Kd = 128, 256, 64
