@@ -25,6 +25,8 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .. import kernels as K
+
 from ..nets.modules import _Bound
 
 BUCKET_BYTES = 25 * 1024 * 1024
@@ -139,6 +141,7 @@ class FlatReducer:
         return self.store.grad[lo:hi]
 
     def _launch(self, bi):
+        K.join_side()  # node-end gradient work forked to the side stream (kernels.py)
         g = self._slice(self.buckets[bi])
         if g.is_cuda and dist.get_backend(self.pg) == "nccl":
             w = dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)

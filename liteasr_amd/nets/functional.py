@@ -463,6 +463,7 @@ class EmbedFn(torch.autograd.Function):
             K.gemm(dy2, w.W2p, dcol)
             K.col2im(dcol, sv.y1, dy1)
         K.conv1_bwd(sv.xs, dy1, g.W1, g.b1)
+        K.join_side()  # end of the backward: every gradient complete on the current stream
         mod.on_grads_ready()
         return None, None, None, None
 
