@@ -80,7 +80,8 @@ typedef struct lasr_gemm_args {
   float drop_p; uint64_t drop_seed;
   const void* res; int res_dtype; int64_t ldres; float res_scale;
   int split_k;  /* 1: none, > 1: forced, 0: auto (fills the chip; needs workspace), -1: auto,
-                 fp32 partials only (no reduction; the caller sums the [split] slabs) */
+                 fp32 partials only (no reduction; the caller sums the [split] slabs),
+                 <= -2: -split_k slices, fp32 partials only */
   void* workspace; int64_t workspace_bytes;
   /* optional fused bias gradient: rowsum[m] += sum_k A[m,k] (fp32, batch == 1, A
    * M-contiguous i.e. lda_m == 1: the dW = dY^T X GEMMs, rowsum = dbias).  Replaces the

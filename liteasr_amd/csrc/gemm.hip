@@ -140,6 +140,7 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
     BN = g_tile_n;
   }
   if (autosplit && g_split) split = g_split;
+  if (a->split_k <= -2 && plain && a->workspace) split = -a->split_k;  // explicit partials-only
   const int64_t rs_floats = a->rowsum ? (int64_t)split * a->M : 0;
   if (split > 1 && (!plain || !a->workspace ||
                     a->workspace_bytes < ((int64_t)split * batch * a->M * a->N + rs_floats) * 4))
@@ -310,7 +311,7 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     LASR_CHECK_ARG(a->in_dtype == LASR_BF16 && a->c_dtype == LASR_F32, "lasr_gemm_dw_group: bf16 in, fp32 partials");
     LASR_CHECK_ARG(a->lda_m == 1 && a->lda_k != 1 && a->ldb_n == 1 && a->ldb_k != 1,
                    "lasr_gemm_dw_group: A M-contiguous and B N-contiguous (dW = dY^T X)");
-    LASR_CHECK_ARG(a->split_k == -1 && a->workspace && (a->batch <= 1) && a->M > 0 && a->N > 0 && a->K > 0,
+    LASR_CHECK_ARG(a->split_k < 0 && a->workspace && (a->batch <= 1) && a->M > 0 && a->N > 0 && a->K > 0,
                    "lasr_gemm_dw_group: partials-only problems with a workspace");
     LASR_CHECK_ARG(!a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f && !a->bias,
                    "lasr_gemm_dw_group: no epilogue");
@@ -318,6 +319,9 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     int BM, BN, split, ks;
     gemm_plan(a, &BM, &BN, &split, &ks);
     LASR_CHECK_ARG(split > 1 && ks == 2, "lasr_gemm_dw_group: plan is not a split-K 64-deep launch");
+    // a 128 x 64 plan runs as 64 x 128 tiles: same tile count for these shapes, and a tile's
+    // shape does not change any output's summation order (k order within the slice)
+    if (BM == 128 && BN == 64 && a->N >= 128) { BM = 64; BN = 128; }
     LASR_CHECK_ARG(i == 0 || (BM == BM0 && BN == BN0), "lasr_gemm_dw_group: problems plan different tiles");
     BM0 = BM;
     BN0 = BN;

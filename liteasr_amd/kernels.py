@@ -100,7 +100,10 @@ def _defer(part, P, Ncols, out0, out1=None, split=None, accumulate=True):
 # queued and launched at its end, one lasr_gemm_dw_group launch per planned tile (<= 8
 # problems each), before the reductions.  LASR_DW_GROUP=0 launches them one by one instead.
 DW_GROUP = os.environ.get("LASR_DW_GROUP", "1") != "0"
-_GROUP_TILES = {(64, 64), (64, 128), (128, 64)}
+_GROUP_TILES = {(64, 64): (64, 64), (64, 128): (64, 128), (128, 64): (64, 128)}  # plan -> group tile
+# grouped problems fill the chip together: each takes 1/DW_GROUP_SPLIT_DIV of the K slices
+# the planner gives a lone launch (fewer fp32 partial slabs to write and reduce)
+DW_GROUP_SPLIT_DIV = int(os.environ.get("LASR_DW_GROUP_SPLIT_DIV", "2"))
 _GROUP_MAX = 8
 
 
@@ -286,15 +289,22 @@ def gemm(
         tm, tn, sp, fl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp), C.byref(fl))
         sp = sp.value
+        grouped = (group and DW_GROUP and sp > 1 and (tm.value, tn.value) in _GROUP_TILES
+                   and (fl.value & 5) == 5 and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16)
+        if grouped and DW_GROUP_SPLIT_DIV > 1:
+            sp = max(2, sp // DW_GROUP_SPLIT_DIV)
+            args.split_k = -sp
+            N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(C.c_int()), C.byref(fl))
+            grouped = (tm.value, tn.value) in _GROUP_TILES and (fl.value & 5) == 5
         if sp > 1:
             # partials-only launch (split_k = -1) into a buffer that lives until the flush
             nrs = sp * M if rowsum is not None else 0
             part = torch.empty(sp * M * Nn + nrs, dtype=torch.float32, device=c.device)
-            args.split_k = -1
+            args.split_k = -sp if grouped else -1
             args.workspace, args.workspace_bytes = ptr(part), part.numel() * 4
-            if (group and DW_GROUP and (tm.value, tn.value) in _GROUP_TILES and (fl.value & 5) == 5
-                    and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16):
-                _DEFER.gemms.append(((tm.value, tn.value), N.GemmArgs.from_buffer_copy(args), (a, b)))
+            if grouped:
+                key = _GROUP_TILES[(tm.value, tn.value)]
+                _DEFER.gemms.append((key, N.GemmArgs.from_buffer_copy(args), (a, b)))
             else:
                 N.call("lasr_gemm", C.byref(args), stream())
             _defer(part, sp, M * Nn, c, accumulate=beta == 1.0)

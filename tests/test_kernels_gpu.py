@@ -267,11 +267,12 @@ def test_gemm_ksub2_bit_identical(ta, tb, M, N, Kd, tile):
 
 
 @pytest.mark.parametrize("R", [3001, 7968])
-def test_gemm_dw_group_bit_identical(R):
+def test_gemm_dw_group_bit_identical(R, monkeypatch):
     """Grouped split-K weight gradients (lasr_gemm_dw_group: the dW GEMMs of a backward node
     queued with group=True and launched together at the end of deferred_reductions) give
-    the same bits as one lasr_gemm launch per problem, with and without the fused bias
-    rowsum, accumulating (beta 1) and overwriting (beta 0)."""
+    the same dW bits as one lasr_gemm launch per problem at the same K slicing, with and
+    without the fused bias rowsum, accumulating (beta 1) and overwriting (beta 0); with the
+    default fewer slices they match float64 at the bf16 bar."""
     kn = K()
     g = torch.Generator().manual_seed(R)
     probs = [(2048, 256, True, 1.0), (256, 2048, True, 1.0), (256, 256, True, 1.0), (768, 256, True, 0.0),
@@ -280,7 +281,10 @@ def test_gemm_dw_group_bit_identical(R):
             torch.randn(M, N, generator=g).to(DEV), torch.randn(M, generator=g).to(DEV) if rs else None, beta)
            for M, N, rs, beta in probs]
     outs = {}
-    for grouped in (False, True):
+    monkeypatch.setattr(kn, "DW_GROUP_SPLIT_DIV", 1)  # same K slices as the lone launches: same bits
+    for grouped in (False, True, "fewer-slices"):
+        if grouped == "fewer-slices":
+            monkeypatch.setattr(kn, "DW_GROUP_SPLIT_DIV", 2)
         res = []
         with kn.deferred_reductions():
             for dy, x, dw0, db0, beta in ins:
@@ -288,14 +292,16 @@ def test_gemm_dw_group_bit_identical(R):
                 db = db0.clone() if db0 is not None else None
                 kn.gemm(dy.t(), x, dw, beta=beta, split_k=0, rowsum=db, group=grouped)
                 res.append((dw, db))
-            assert (len(kn._DEFER.gemms) > 0) == (grouped and kn.DW_GROUP)
+            assert (len(kn._DEFER.gemms) > 0) == (bool(grouped) and kn.DW_GROUP)
         torch.cuda.synchronize()
         outs[grouped] = res
     for (a, ab), (b, bb) in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
         if ab is not None:
-            assert torch.equal(ab, bb)
-    for (dy, x, dw0, db0, beta), (dw, db) in zip(ins, outs[True]):
+            # a 128 x 64 plan runs on the 64 x 128 group tile: its rowsum partials group the k
+            # rows per thread differently (rowsum_tile<BM>), so they agree to fp32 rounding
+            assert torch.allclose(ab, bb, rtol=1e-6, atol=1e-4)
+    for (dy, x, dw0, db0, beta), (dw, db) in zip(ins, outs["fewer-slices"]):
         ref = beta * dw0.double() + dy.double().t() @ x.double()
         close(dw, ref, 1e-2, "grouped dW")
         if db0 is not None:

@@ -16,7 +16,7 @@ import torch
 
 from liteasr_amd import _native as N
 from liteasr_amd import kernels as K
-from liteasr_amd._native import ACT_SWISH
+from liteasr_amd._native import ACT_GATE, ACT_SWISH
 
 TILES = [(0, 0), (64, 64), (128, 64), (64, 128), (128, 128), (256, 128), (128, 256), (256, 256)]
 REPS = 20
@@ -68,6 +68,11 @@ def make(M, N_, Kd, layout, out, batch=1, **kw):
         extra["zout"] = torch.empty(M, N_, device=dev, dtype=out)
     if kw.get("aux"):
         extra["aux"], extra["aux_act"] = torch.randn(M, N_, device=dev).bfloat16(), ACT_SWISH
+    if kw.get("gate"):  # FFN dX through the stored gate (functional.ffn_backward)
+        extra["aux"], extra["aux_act"], extra["alpha"] = torch.rand(M, N_, device=dev).bfloat16(), ACT_GATE, 1.11
+    if kw.get("gatez"):  # FFN fc1 forward storing the gate (functional.ffn_forward)
+        extra["act"], extra["zout_mode"] = ACT_SWISH, 1
+        extra["zout"] = torch.empty(M, N_, device=dev, dtype=out)
     if kw.get("res"):
         extra["res"] = torch.randn(M, N_, device=dev)
     if kw.get("drop"):
@@ -83,6 +88,8 @@ CASES = [
     ("fc1 fwd bias+swish+z+drop", 7968, 2048, 256, "nt", torch.bfloat16, 1,
      dict(bias=1, swish=1, drop=1)),
     ("fc1 plain", 7968, 2048, 256, "nt", torch.bfloat16, 1, {}),
+    ("fc1 fwd gate (prod)", 7968, 2048, 256, "nt", torch.bfloat16, 1, dict(bias=1, gatez=1, drop=1)),
+    ("dX fc2 gate (prod)", 7968, 2048, 256, "nn", torch.bfloat16, 1, dict(gate=1)),
     ("dX fc2 aux+drop (nn)", 7968, 2048, 256, "nn", torch.bfloat16, 1, dict(aux=1, drop=1)),
     ("dX fc2 aux+drop (nt)", 7968, 2048, 256, "nt", torch.bfloat16, 1, dict(aux=1, drop=1)),
     ("dX fc1 (nt K2048)", 7968, 256, 2048, "nt", torch.bfloat16, 1, {}),
