@@ -66,51 +66,56 @@ def synthetic(cfgd, rank, dev):
 
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
-# template instance lasr_gemm launches for a split-K weight-gradient tile (gemm.hip
-# launch_bf16): ring depth and launch bound per tile
-_DW_INSTANCE = {(128, 128): (3, 3), (64, 128): (4, 3), (128, 64): (4, 3), (64, 64): (4, 3)}
-# ... with 64-deep ring stages (LASR_PLAN_KSUB2): ring depth, launch bound, sub-tiles
-_DW_INSTANCE_KS2 = {(128, 128): (2, 2), (64, 128): (3, 2), (128, 64): (3, 2), (64, 64): (3, 3)}
-PLAN_KSUB2 = 4
 
 
 def roofline_case(cfgd, dev):
-    """The dominant kernel family of the step (rocprof, profiles/r01): the weight-gradient
-    GEMMs (both operands M/N-contiguous, LDS transposed reads, split-K fp32 partials; ~25 %
-    of the step).  Representative launch: the FFN fc1 dW, dW1[ff, d] = dZ^T[ff, rows] @
-    LN[rows, d] with rows = B*T' -- the largest and most frequent shape (4 of the 11 dW
-    launches of a Conformer layer).  Run in the library's partials-only mode (split_k=-1)
-    so the timed launches are that kernel alone; the fixed-order split-K reduction is a
-    separate kernel (splitk_reduce_kernel).
-    Algorithmic bytes: each bf16 operand read once + the fp32 result written once.  The
-    split-K partial slabs are NOT counted: they are traffic this design adds, so they
-    show up as PMC traffic above the algorithmic bytes."""
+    """The dominant kernel family of the step (rocprof): the weight-gradient GEMMs (both
+    operands M/N-contiguous, LDS transposed reads, split-K fp32 partials).  In the step they
+    run grouped per backward node (lasr_gemm_dw_group, kernels.deferred_reductions); the
+    representative launch is the FFN group of one Conformer layer exactly as the step issues
+    it: dW1 = dZ^T LN (ff x d) and dW2 = G^T H (d x ff) of both macaron FFNs, rows = B*T',
+    planned by the product (tile, 64-deep stages, K slices) and launched alone (the fixed-
+    order reduction of the partials is a separate kernel, lasr_reduce_multi).
+    Algorithmic bytes: each problem's bf16 operands read once + its fp32 result written
+    once.  The split-K partial slabs are NOT counted: they are traffic this design adds, so
+    they show up as PMC traffic above the algorithmic bytes."""
     import torch
 
+    from liteasr_amd import _native as Nn
     from liteasr_amd import kernels as K
 
     T1 = (cfgd["T"] - 3) // 2 + 1
     rows = cfgd["B"] * ((T1 - 3) // 2 + 1)
-    M, N, Kd = cfgd["ff"], cfgd["d"], rows
-    dz = torch.randn(rows, M, device=dev).bfloat16()
-    ln = torch.randn(rows, N, device=dev).bfloat16()
-    dw = torch.zeros(M, N, device=dev)
-    tm, tn, split, flags = K.gemm_plan(dz.t(), ln, dw, flags=True, beta=1.0, split_k=-1)
+    F, D = cfgd["ff"], cfgd["d"]
+    probs = []
+    for _ in range(2):  # ffm (macaron) and ff
+        dz = torch.randn(rows, F, device=dev).bfloat16()
+        ln = torch.randn(rows, D, device=dev).bfloat16()
+        gb = torch.randn(rows, D, device=dev).bfloat16()
+        h = torch.randn(rows, F, device=dev).bfloat16()
+        probs.append((gb, h, torch.zeros(D, F, device=dev), torch.zeros(D, device=dev)))  # W2
+        probs.append((dz, ln, torch.zeros(F, D, device=dev), torch.zeros(F, device=dev)))  # W1
+    with K.deferred_reductions():
+        for a, b, c, r in probs:
+            K.gemm(a.t(), b, c, beta=1.0, split_k=0, rowsum=r, group=True)
+        q = list(K._DEFER.gemms)
+        K._DEFER.gemms.clear()
+        K._DEFER.segs.clear()
+    assert q and all(k == q[0][0] for k, _, _ in q), "FFN weight gradients did not group"
+    arr = (Nn.GemmArgs * len(q))(*[x[1] for x in q])
+    keep = [x[2] for x in q] + [probs]  # the partial buffers are referenced by the args
 
     def launch():
-        K.gemm(dz.t(), ln, dw, beta=1.0, split_k=-1)
+        Nn.call("lasr_gemm_dw_group", arr, len(q), K.stream())
 
-    flops = 2.0 * M * N * Kd
-    bytes_ = 2.0 * (Kd * M + Kd * N) + 4.0 * M * N
-    if flags & PLAN_KSUB2:
-        S, minb = _DW_INSTANCE_KS2[(tm, tn)]
-        inst = f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}, 0, 2>"
-    else:
-        S, minb = _DW_INSTANCE[(tm, tn)]
-        inst = f"gemm_bf16_glds_kernel<{tm}, {tn}, false, false, float, {S}, {minb}, 0>"
-    meta = {"kernel": inst,
-            "shape": f"M={M} N={N} K={Kd} split_k={split}",
-            "grid": [-(-N // tn), -(-M // tm), split]}
+    launch.keep = keep
+    flops = sum(2.0 * a.shape[0] * a.shape[1] * b.shape[1] for a, b, _, _ in probs)
+    bytes_ = sum(2.0 * (a.numel() + b.numel()) + 4.0 * c.numel() for a, b, c, _ in probs)
+    tm, tn = q[0][0]
+    S, minb = {(64, 64): (3, 3), (64, 128): (3, 2)}[(tm, tn)]
+    splits = sorted({-x[1].split_k for x in q})
+    meta = {"kernel": f"gemm_dw_group_kernel<{tm}, {tn}, {S}, {minb}>",
+            "shape": f"{len(q)} problems: 2x (M={F} N={D}) + 2x (M={D} N={F}), K={rows}, split_k={splits}"}
     return launch, flops, bytes_, meta
 
 

@@ -103,7 +103,7 @@ DW_GROUP = os.environ.get("LASR_DW_GROUP", "1") != "0"
 _GROUP_TILES = {(64, 64): (64, 64), (64, 128): (64, 128), (128, 64): (64, 128)}  # plan -> group tile
 # grouped problems fill the chip together: each takes 1/DW_GROUP_SPLIT_DIV of the K slices
 # the planner gives a lone launch (fewer fp32 partial slabs to write and reduce)
-DW_GROUP_SPLIT_DIV = int(os.environ.get("LASR_DW_GROUP_SPLIT_DIV", "2"))
+DW_GROUP_SPLIT_DIV = int(os.environ.get("LASR_DW_GROUP_SPLIT_DIV", "4"))
 _GROUP_MAX = 8
 
 
@@ -289,10 +289,11 @@ def gemm(
         tm, tn, sp, fl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp), C.byref(fl))
         sp = sp.value
-        grouped = (group and DW_GROUP and sp > 1 and (tm.value, tn.value) in _GROUP_TILES
+        grouped = (group and DW_GROUP and (tm.value, tn.value) in _GROUP_TILES
                    and (fl.value & 5) == 5 and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16)
-        if grouped and DW_GROUP_SPLIT_DIV > 1:
-            sp = max(2, sp // DW_GROUP_SPLIT_DIV)
+        if grouped and (DW_GROUP_SPLIT_DIV > 1 or sp < 2):
+            # short K too (the positional-projection weight, K = T'): two slices join the group
+            sp = max(2, sp // max(1, DW_GROUP_SPLIT_DIV))
             args.split_k = -sp
             N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(C.c_int()), C.byref(fl))
             grouped = (tm.value, tn.value) in _GROUP_TILES and (fl.value & 5) == 5

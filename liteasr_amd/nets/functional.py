@@ -226,7 +226,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
         K.gemm(dBDh.view(H, B * T, ldS)[..., :T].transpose(-1, -2), sv.qv.view(M, H, dk).permute(1, 0, 2),
                dp.view(T, H, dk).permute(1, 0, 2), alpha=scale, split_k=0)
         K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
-        K.gemm(dp.t(), pos, g.Wpos, beta=1.0)
+        K.gemm(dp.t(), pos, g.Wpos, beta=1.0, split_k=0, group=True)
         K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
         dln = _e((M, d), adt, dev)
         K.gemm(dqkv, w.Wqkv, dln)
@@ -254,7 +254,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     dp = _e((T, d), adt, dev)
     K.reduce_batch(dpb, B, H, T, dk, dp)
     K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
-    K.gemm(dp.t(), pos, g.Wpos, beta=1.0)
+    K.gemm(dp.t(), pos, g.Wpos, beta=1.0, split_k=0, group=True)
     K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
     dln = _e((M, d), adt, dev)
     K.gemm(dqkv, w.Wqkv, dln)

@@ -289,11 +289,16 @@ def test_eval_forward_uses_running_stats():
 
 def test_deferred_reductions_bit_exact(monkeypatch):
     """kernels.deferred_reductions (one lasr_reduce_multi launch per backward node) gives
-    the same gradients, bit for bit, as the immediate per-call reductions."""
+    the same gradients, bit for bit, as the immediate per-call reductions.  Grouping of the
+    deferred dW GEMMs is off here: it slices K differently (bit-exactness of the grouped
+    launch itself at equal slicing: test_gemm_dw_group_bit_identical; the grouped step vs
+    the oracle: the parity tests)."""
     import contextlib
 
     from liteasr_amd import kernels as Kn
     from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+
+    monkeypatch.setattr(Kn, "DW_GROUP", False)
 
     params = O.init_params(SMALL, seed=5)
     xs, xlens, ys, ylens = [t.cuda() for t in O.synthetic_batch(2, 300, 9, SMALL["vocab_size"], seed=4)]
