@@ -911,11 +911,22 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   else gemm_epilogue<BM, BN, TC, true, G>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
 }
 
+// Tile order of a weight-gradient GEMM (both operands [K, M] / [K, N] with K = rows): the
+// tiles that share the LARGER operand's column strip get consecutive indices, so after the
+// XCD remap they sit on one XCD and that strip is fetched from HBM once (the smaller operand
+// is the one re-fetched per XCD).  M >= N: N-tiles fastest; N > M: M-tiles fastest.
+LASR_DEV void dw_tile_order(int wg, int nx, int ny, bool n_major, int& tx, int& ty) {
+  if (n_major) { tx = wg / ny; ty = wg % ny; }
+  else { tx = wg % nx; ty = wg / nx; }
+}
+
 template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN, int KS = 1>
 __global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
-  const int nx = gridDim.x;
-  const int wg = xcd_remap(blockIdx.y * nx + blockIdx.x, gridDim.x * gridDim.y);
-  gemm_glds_tile<BM, BN, AKC, BKC, TC, S, G, KS>(p, wg % nx, wg / nx, blockIdx.z);
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int wg = xcd_remap(blockIdx.y * nx + blockIdx.x, nx * ny);
+  int tx, ty;
+  dw_tile_order(wg, nx, ny, !AKC && !BKC && G == G_LIN && p.N > p.M, tx, ty);
+  gemm_glds_tile<BM, BN, AKC, BKC, TC, S, G, KS>(p, tx, ty, blockIdx.z);
 }
 
 // Grouped split-K weight-gradient GEMMs (partials only): up to LASR_DW_GROUP_MAX independent
@@ -956,7 +967,9 @@ __global__ __launch_bounds__(256, MINB) void gemm_dw_group_kernel(DwGroupP g) {
   p.rs_ws = g.rs_ws[i];
   p.alpha = 1.f;
   const int wg = xcd_remap(local % ntile, ntile);
-  gemm_glds_tile<BM, BN, false, false, float, S, G_LIN, 2>(p, wg % ntx, wg / ntx, local / ntile);
+  int tx, ty;
+  dw_tile_order(wg, ntx, nty, p.N > p.M, tx, ty);
+  gemm_glds_tile<BM, BN, false, false, float, S, G_LIN, 2>(p, tx, ty, local / ntile);
 }
 
 // ============================ fp32 MFMA kernel ===================================
