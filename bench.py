@@ -112,7 +112,7 @@ def roofline_case(cfgd, dev):
     flops = sum(2.0 * a.shape[0] * a.shape[1] * b.shape[1] for a, b, _, _ in probs)
     bytes_ = sum(2.0 * (a.numel() + b.numel()) + 4.0 * c.numel() for a, b, c, _ in probs)
     tm, tn = q[0][0]
-    S, minb = {(64, 64): (3, 3), (64, 128): (3, 2)}[(tm, tn)]
+    S, minb = {(64, 64): (3, 3), (128, 128): (2, 2)}[(tm, tn)]
     splits = sorted({-x[1].split_k for x in q})
     meta = {"kernel": f"gemm_dw_group_kernel<{tm}, {tn}, {S}, {minb}>",
             "shape": f"{len(q)} problems: 2x (M={F} N={D}) + 2x (M={D} N={F}), K={rows}, split_k={splits}"}

@@ -6,6 +6,7 @@ int launch_dw_group(const DwGroupP& g, int BM, int BN, int blocks, hipStream_t s
   if (BM == 64 && BN == 64) gemm_dw_group_kernel<64, 64, 3, 3><<<blocks, 256, 0, st>>>(g);
   else if (BM == 64 && BN == 128) gemm_dw_group_kernel<64, 128, 3, 2><<<blocks, 256, 0, st>>>(g);
   else if (BM == 128 && BN == 64) gemm_dw_group_kernel<128, 64, 3, 2><<<blocks, 256, 0, st>>>(g);
+  else if (BM == 128 && BN == 128) gemm_dw_group_kernel<128, 128, 2, 2><<<blocks, 256, 0, st>>>(g);
   else return -1;
   return 0;
 }

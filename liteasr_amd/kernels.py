@@ -100,10 +100,19 @@ def _defer(part, P, Ncols, out0, out1=None, split=None, accumulate=True):
 # queued and launched at its end, one lasr_gemm_dw_group launch per planned tile (<= 8
 # problems each), before the reductions.  LASR_DW_GROUP=0 launches them one by one instead.
 DW_GROUP = os.environ.get("LASR_DW_GROUP", "1") != "0"
-_GROUP_TILES = {(64, 64): (64, 64), (64, 128): (64, 128), (128, 64): (64, 128)}  # plan -> group tile
-# grouped problems fill the chip together: each takes 1/DW_GROUP_SPLIT_DIV of the K slices
-# the planner gives a lone launch (fewer fp32 partial slabs to write and reduce)
-DW_GROUP_SPLIT_DIV = int(os.environ.get("LASR_DW_GROUP_SPLIT_DIV", "4"))
+# plan tile -> group (lasr_gemm_dw_group runs the 64 x 128 / 128 x 64 plans, the FFN-sized
+# weights, on 128 x 128 tiles)
+_GROUP_TILES = {(64, 64): (64, 64), (64, 128): (128, 128), (128, 64): (128, 128)}
+# grouped problems fill the chip together: each takes 1/div of the K slices the planner gives
+# a lone launch (fewer fp32 partial slabs to write and reduce); 128 x 128 groups keep half
+# (tools: LASR_DW_GROUP_SPLIT_DIV overrides both)
+_DIV_ENV = os.environ.get("LASR_DW_GROUP_SPLIT_DIV")
+DW_GROUP_SPLIT_DIV = {(64, 64): 4, (128, 128): 2} if _DIV_ENV is None else int(_DIV_ENV)
+
+
+def _group_div(key):
+    d = DW_GROUP_SPLIT_DIV
+    return d.get(key, 1) if isinstance(d, dict) else d
 _GROUP_MAX = 8
 
 
@@ -291,9 +300,10 @@ def gemm(
         sp = sp.value
         grouped = (group and DW_GROUP and (tm.value, tn.value) in _GROUP_TILES
                    and (fl.value & 5) == 5 and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16)
-        if grouped and (DW_GROUP_SPLIT_DIV > 1 or sp < 2):
+        div = _group_div(_GROUP_TILES[(tm.value, tn.value)]) if grouped else 1
+        if grouped and (div > 1 or sp < 2):
             # short K too (the positional-projection weight, K = T'): two slices join the group
-            sp = max(2, sp // max(1, DW_GROUP_SPLIT_DIV))
+            sp = max(2, sp // max(1, div))
             args.split_k = -sp
             N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(C.c_int()), C.byref(fl))
             grouped = (tm.value, tn.value) in _GROUP_TILES and (fl.value & 5) == 5

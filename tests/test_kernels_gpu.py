@@ -281,10 +281,11 @@ def test_gemm_dw_group_bit_identical(R, monkeypatch):
             torch.randn(M, N, generator=g).to(DEV), torch.randn(M, generator=g).to(DEV) if rs else None, beta)
            for M, N, rs, beta in probs]
     outs = {}
+    default_div = kn.DW_GROUP_SPLIT_DIV
     monkeypatch.setattr(kn, "DW_GROUP_SPLIT_DIV", 1)  # same K slices as the lone launches: same bits
     for grouped in (False, True, "fewer-slices"):
         if grouped == "fewer-slices":
-            monkeypatch.setattr(kn, "DW_GROUP_SPLIT_DIV", 2)
+            monkeypatch.setattr(kn, "DW_GROUP_SPLIT_DIV", default_div)
         res = []
         with kn.deferred_reductions():
             for dy, x, dw0, db0, beta in ins:
@@ -298,7 +299,7 @@ def test_gemm_dw_group_bit_identical(R, monkeypatch):
     for (a, ab), (b, bb) in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
         if ab is not None:
-            # a 128 x 64 plan runs on the 64 x 128 group tile: its rowsum partials group the k
+            # FFN-sized plans run on 128 x 128 group tiles: their rowsum partials group the k
             # rows per thread differently (rowsum_tile<BM>), so they agree to fp32 rounding
             assert torch.allclose(ab, bb, rtol=1e-6, atol=1e-4)
     for (dy, x, dw0, db0, beta), (dw, db) in zip(ins, outs["fewer-slices"]):
