@@ -298,6 +298,19 @@ int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, const void* k,
                      const float* stats, const void* ctx, const void* dctx, int64_t ldc,
                      float* Dbuf, void* dqu, void* dbd, int ldS, int dbd_head_major, void* dk_out,
                      void* dv_out, int64_t lddkv, void* stream);
+/* Plain scaled dot-product attention on the fused kernels (no positional term), Tq queries
+ * and Tk keys per utterance (liteasr/nets/attention.py:41-71, the decoder's self and source
+ * attention): q [B*Tq, ldq], k / v [B*Tk, ldkv], mask[b*mask_sb + i*mask_sq + j] != 0 ->
+ * masked (-1e38 before the softmax), stats / ctx as lasr_relattn_fwd.  No attention dropout. */
+int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B, int H,
+                  int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                  float* stats, void* ctx, int64_t ldc, void* stream);
+/* Backward of lasr_attn_fwd (recompute): dq [B*Tq, ldq], dk / dv [B*Tk, lddkv]; Dbuf
+ * [B*H*Tq] scratch. */
+int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B, int H,
+                  int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                  const float* stats, const void* ctx, const void* dctx, int64_t ldc, float* Dbuf, void* dq,
+                  void* dk_out, void* dv_out, int64_t lddkv, void* stream);
 /* dst[t, h*dk + c] = sum_b src[b,h,t,c]  (pos-projection grad reduced over batch). */
 int lasr_reduce_batch(const float* src, int B, int H, int T, int dk, void* dst, int dt,
                       void* stream);

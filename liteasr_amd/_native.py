@@ -123,6 +123,9 @@ SIGNATURES = {
     "lasr_gemm_force_ksub": [C.c_int],
     "lasr_gemm_dw_group": [C.POINTER(GemmArgs), _i, _p],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
+    "lasr_attn_fwd": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
+    "lasr_attn_bwd": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l, _p, _p, _p, _p,
+                      _l, _p],
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
                          _p, _p, _p, _i, _i, _p, _p, _l, _p],
     "lasr_reduce_multi": [C.POINTER(ReduceSeg), _i, _p],

@@ -44,6 +44,8 @@ struct RelAttnP {
   const uint8_t* mask;                  // mask[b*msb + i*msq + j] != 0 -> masked
   int64_t msb, msq;
   int B, H, T;
+  int Tk;                               // key rows per utterance (T: self-attention; a
+                                        // different count only with an all-zero pos table)
   float scale;
   float* stats;                         // [B*H*T][2]: row max, 1/row sum
   bf16_t* ctx;                          // [B*T, ldc]
@@ -157,7 +159,7 @@ LASR_DEV void keymask_fetch(const RelAttnP& a, int b, int j0, int lane, KeyMask&
   km.r0 = km.r1 = km.r2 = km.r3 = 0u;
   if (a.mask && a.msq == 0) {
     const uint8_t* mr = a.mask + (int64_t)b * a.msb;
-    const int j = j0 + (lane & 15), jm = a.T - 1;
+    const int j = j0 + (lane & 15), jm = a.Tk - 1;
     km.r0 = mr[min(j, jm)];
     km.r1 = mr[min(j + 16, jm)];
     km.r2 = mr[min(j + 32, jm)];
@@ -176,8 +178,8 @@ struct MaskBlk {
   uint32_t w0, w1, w2, w3;
 };
 LASR_DEV MaskBlk mask_fetch(const RelAttnP& a, int b, int i0, int j0, int tid) {
-  const int r = tid >> 2, c16 = (tid & 3) * 16, jm = a.T - 1;
-  const uint8_t* mr = a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + r, jm) * a.msq;
+  const int r = tid >> 2, c16 = (tid & 3) * 16, im = a.T - 1, jm = a.Tk - 1;
+  const uint8_t* mr = a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + r, im) * a.msq;
   uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int e = 0; e < 16; ++e) w[e >> 2] |= (mr[min(j0 + c16 + e, jm)] ? 1u : 0u) << (8 * (e & 3));
@@ -190,7 +192,7 @@ LASR_DEV void mask_store(uint8_t* msh, const MaskBlk& m, int tid) {
 // Scaled, masked scores of wave w's 16 query rows (iw = i0 + 16w ..) x the 64 keys j0 ..
 // from the staged K image and relative-position window.
 // s[c][q]: row iw + 4*(lane/16) + q, key j0 + 16c + lane%16.  -inf past T, -1e38 masked.
-template <int DK, bool RM>
+template <int DK, bool RM, bool RP = true>
 LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* peimg, const bf16x8 (&qu)[DK / 32],
                          const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int b, int w, int iw, int j0,
                          uint32_t mbits, const uint8_t* mtile, float* gw, f32x4 (&s)[4], int lane) {
@@ -202,6 +204,21 @@ LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* pe
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) acc = mfma(qu[ks], frag_row(kimg, 16 * c, 32 * ks, lane), acc);
     s[c] = acc;
+  }
+  if constexpr (!RP) {  // plain attention: no positional term
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 4 * g + q, j = j0 + 16 * c + col;
+        float v = s[c][q] * a.scale;
+        bool masked = (mbits >> c) & 1u;
+        if constexpr (RM) masked = mtile[(16 * w + r) * MLD + 16 * c + col] != 0;
+        if (j >= a.Tk) v = -INFINITY;
+        else if (masked) v = -1e38f;
+        s[c][q] = v;
+      }
+    return;
   }
   const int mb = j0 - iw - 15 + T - 1;  // first m of the wave's 80-wide window
 #pragma unroll
@@ -232,7 +249,7 @@ LASR_DEV void score_tile(const RelAttnP& a, const bf16_t* kimg, const bf16_t* pe
       float v = (s[c][q] + gw[r * GLD + 16 * c + col - r + 15]) * a.scale;
       bool masked = (mbits >> c) & 1u;
       if constexpr (RM) masked = mtile[(16 * w + r) * MLD + 16 * c + col] != 0;
-      if (j >= T) v = -INFINITY;
+      if (j >= a.Tk) v = -INFINITY;
       else if (masked) v = -1e38f;
       s[c][q] = v;
     }
@@ -272,7 +289,7 @@ LASR_DEV void load_qfrags(const RelAttnP& a, int b, int h, int iw, int lane, bf1
 // Forward, one pass with the online softmax: per key block, stage K / V / the position
 // window (the next block's global loads in flight while this one computes), S on MFMA,
 // running max / sum, O = O * exp(m_old - m_new) + P V.
-template <int DK, bool RM>
+template <int DK, bool RM, bool RP>
 __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
@@ -283,18 +300,19 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T;
-  const int i0 = blockIdx.x * 64, iw = i0 + 16 * w;
-  const int64_t base = (int64_t)b * T;
-  const bf16_t* kh = a.k + base * a.ldkv + h * DK;
-  const bf16_t* vh = a.v + base * a.ldkv + h * DK;
+  const int i0 = blockIdx.x * 64, iw = i0 + 16 * w, Tk = a.Tk;
+  const int64_t base = (int64_t)b * T, kbase = (int64_t)b * Tk;
+  const bf16_t* kh = a.k + kbase * a.ldkv + h * DK;
+  const bf16_t* vh = a.v + kbase * a.ldkv + h * DK;
   const bf16_t* ph = a.pos + h * DK;
   float* gw = gsh[w];
   bf16_t* pw = psh[w];
 
   bf16x8 qu[KS], qv[KS], qv1[KS];
   load_qfrags<DK>(a, b, h, iw, lane, qu, qv, qv1);
-    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, T, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, T, tid);
-  PeWin rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
+    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, Tk, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, Tk, tid);
+  PeWin rp{};
+  if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
   KeyMask km;
   keymask_fetch(a, b, 0, lane, km);
   MaskBlk mk{};
@@ -306,22 +324,22 @@ __global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
   for (int q = 0; q < 4; ++q) { mrun[q] = -INFINITY; lrun[q] = 0.f; }
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) o[t] = zero4();
-  for (int j0 = 0; j0 < T; j0 += 64) {
+  for (int j0 = 0; j0 < Tk; j0 += 64) {
     __syncthreads();  // previous block's images consumed
     blk_store<DK>(ksh, rk, tid);
     blk_store<DK>(vsh, rv, tid);
-    pe_store<DK>(pesh, rp, tid);
+    if constexpr (RP) pe_store<DK>(pesh, rp, tid);
     const uint32_t mb_cur = keymask_bits(km);
     if constexpr (RM) mask_store(msh, mk, tid);
     __syncthreads();
     // prefetch the next key block (unconditional: clamped rows keep the last one in
     // bounds, and no branch merge forces a wait on the loads)
-    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, T, tid);
-    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, T, tid);
-    rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
+    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, Tk, tid);
+    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, Tk, tid);
+    if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
     keymask_fetch(a, b, j0 + 64, lane, km);
     if constexpr (RM) mk = mask_fetch(a, b, i0, j0 + 64, tid);
-    score_tile<DK, RM>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
+    score_tile<DK, RM, RP>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float bm = rmax16(fmaxf(fmaxf(s[0][q], s[1][q]), fmaxf(s[2][q], s[3][q])));
@@ -389,7 +407,7 @@ LASR_DEV void dscore_tile(const RelAttnP& a, const bf16_t* vimg, const bf16x8 (&
   }
 }
 
-template <int DK, bool RM>
+template <int DK, bool RM, bool RP>
 __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   constexpr int KS = DK / 32;
   __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
@@ -400,16 +418,17 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T;
-  const int i0 = blockIdx.x * 64, iw = i0 + 16 * w;
-  const int64_t base = (int64_t)b * T, zrow = ((int64_t)b * a.H + h) * T;
-  const bf16_t* kh = a.k + base * a.ldkv + h * DK;
-  const bf16_t* vh = a.v + base * a.ldkv + h * DK;
+  const int i0 = blockIdx.x * 64, iw = i0 + 16 * w, Tk = a.Tk;
+  const int64_t base = (int64_t)b * T, kbase = (int64_t)b * Tk, zrow = ((int64_t)b * a.H + h) * T;
+  const bf16_t* kh = a.k + kbase * a.ldkv + h * DK;
+  const bf16_t* vh = a.v + kbase * a.ldkv + h * DK;
   const bf16_t* ph = a.pos + h * DK;
   float* gw = gsh[w];
   bf16_t* pw = psh[w];
 
-    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, T, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, T, tid);
-  PeWin rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
+    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, Tk, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, Tk, tid);
+  PeWin rp{};
+  if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
   KeyMask km;
   keymask_fetch(a, b, 0, lane, km);
   MaskBlk mk{};
@@ -445,20 +464,20 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
   for (int t = 0; t < DK / 16; ++t) dq[t] = zero4();
   bf16_t* dbd = a.dbd + (a.dbd_hb ? ((int64_t)h * a.B + b) * T : zrow) * a.ldS;
   f32x4 s[4], p[4], ds[4];
-  for (int j0 = 0; j0 < T; j0 += 64) {
+  for (int j0 = 0; j0 < Tk; j0 += 64) {
     __syncthreads();
     blk_store<DK>(ksh, rk, tid);
     blk_store<DK>(vsh, rv, tid);
-    pe_store<DK>(pesh, rp, tid);
+    if constexpr (RP) pe_store<DK>(pesh, rp, tid);
     const uint32_t mb_cur = keymask_bits(km);
     if constexpr (RM) mask_store(msh, mk, tid);
     __syncthreads();
-    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, T, tid);  // next block (unconditional, clamped)
-    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, T, tid);
-    rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
+    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, Tk, tid);  // next block (unconditional, clamped)
+    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, Tk, tid);
+    if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
     keymask_fetch(a, b, j0 + 64, lane, km);
     if constexpr (RM) mk = mask_fetch(a, b, i0, j0 + 64, tid);
-    score_tile<DK, RM>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
+    score_tile<DK, RM, RP>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
     dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -468,7 +487,7 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
         const bf16_t v = f2bf(ds[c][q]);
         pw[r * PLD + 16 * c + col] = v;
         // inverse rel_shift: the bd entry this score read (none for j == i+1)
-        if (i < T && j < T && j != i + 1) {
+        if (RP && i < T && j < T && j != i + 1) {
           const int64_t off = j <= i ? (int64_t)i * a.ldS + (T - 1 - i + j) : (int64_t)(i + 1) * a.ldS + (j - i - 2);
           dbd[off] = v;
         }
@@ -490,7 +509,7 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
     for (int t = 0; t < DK / 16; ++t) dst[16 * t] = f2bf(dq[t][q] * a.scale);
   }
   // bd row 0, columns 0..T-2 are read by no score (rel_shift pads them): zero gradient
-  if (blockIdx.x == 0)
+  if (RP && blockIdx.x == 0)
     for (int c = tid; c < T - 1; c += 256) dbd[c] = f2bf(0.f);
 }
 
@@ -501,7 +520,7 @@ __global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
 // barrier separates the last G read from the first P / dS write), so a workgroup takes
 // <= 80 KB and two fit on a CU: the 512-workgroup grid of the small config runs in one round
 // (d_k 64 with a query-dependent mask needs > 256 VGPRs: one wave per SIMD there).
-template <int DK, bool RM>
+template <int DK, bool RM, bool RP>
 __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_kernel(RelAttnP a) {
   constexpr int KS = DK / 32;
   constexpr int GBYTES = 4 * 16 * GLD * 4, PBYTES = 2 * 64 * 64 * 2;
@@ -516,8 +535,8 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
   __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T;
-  const int j0 = blockIdx.x * 64;
-  const int64_t base = (int64_t)b * T, zrow = ((int64_t)b * a.H + h) * T;
+  const int j0 = blockIdx.x * 64, Tk = a.Tk;
+  const int64_t base = (int64_t)b * T, kbase = (int64_t)b * Tk, zrow = ((int64_t)b * a.H + h) * T;
   const bf16_t* ph = a.pos + h * DK;
   const bf16_t* quh = a.qu + base * a.ldq + h * DK;
   const bf16_t* doh = a.dctx + base * a.ldc + h * DK;
@@ -525,10 +544,11 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
   KeyMask km;
   keymask_fetch(a, b, j0, lane, km);
   const uint32_t mbits = keymask_bits(km);
-  blk_store<DK>(ksh, blk_fetch<DK>(a.k + base * a.ldkv + h * DK, a.ldkv, j0, T, tid), tid);
-  blk_store<DK>(vsh, blk_fetch<DK>(a.v + base * a.ldkv + h * DK, a.ldkv, j0, T, tid), tid);
+  blk_store<DK>(ksh, blk_fetch<DK>(a.k + kbase * a.ldkv + h * DK, a.ldkv, j0, Tk, tid), tid);
+  blk_store<DK>(vsh, blk_fetch<DK>(a.v + kbase * a.ldkv + h * DK, a.ldkv, j0, Tk, tid), tid);
   Blk rq = blk_fetch<DK>(quh, a.ldq, 0, T, tid), ro = blk_fetch<DK>(doh, a.ldc, 0, T, tid);
-  PeWin rp = pe_fetch<DK>(ph, a.ldp, T, j0 + T - 64, tid);
+  PeWin rp{};
+  if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, j0 + T - 64, tid);
   MaskBlk mk{};
   if constexpr (RM) mk = mask_fetch(a, b, 0, j0, tid);
 
@@ -541,7 +561,7 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
     __syncthreads();  // images of the previous query block consumed
     blk_store<DK>(qimg, rq, tid);
     blk_store<DK>(oimg, ro, tid);
-    pe_store<DK>(pesh, rp, tid);
+    if constexpr (RP) pe_store<DK>(pesh, rp, tid);
     if constexpr (RM) mask_store(msh, mk, tid);
     // per-row operands of this wave's 16 queries (global; qv / qv1 are not staged)
     bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
@@ -566,14 +586,14 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
     __syncthreads();
     rq = blk_fetch<DK>(quh, a.ldq, i0 + 64, T, tid);  // next block (unconditional, clamped)
     ro = blk_fetch<DK>(doh, a.ldc, i0 + 64, T, tid);
-    rp = pe_fetch<DK>(ph, a.ldp, T, j0 - (i0 + 64) + T - 64, tid);
+    if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, j0 - (i0 + 64) + T - 64, tid);
     if constexpr (RM) mk = mask_fetch(a, b, i0 + 64, j0, tid);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       qu[ks] = frag_row(qimg, 16 * w, 32 * ks, lane);
       dof[ks] = frag_row(oimg, 16 * w, 32 * ks, lane);
     }
-    score_tile<DK, RM>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mbits, msh, gw, s, lane);
+    score_tile<DK, RM, RP>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mbits, msh, gw, s, lane);
     dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
     __syncthreads();  // every wave's G window consumed: the P / dS images overwrite them
 #pragma unroll
@@ -600,9 +620,9 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = j0 + 16 * w + 4 * g + q;
-    if (j >= T) continue;
-    bf16_t* pk = a.dk + (base + j) * a.lddkv + h * DK + col;
-    bf16_t* pv = a.dv + (base + j) * a.lddkv + h * DK + col;
+    if (j >= Tk) continue;
+    bf16_t* pk = a.dk + (kbase + j) * a.lddkv + h * DK + col;
+    bf16_t* pv = a.dv + (kbase + j) * a.lddkv + h * DK + col;
 #pragma unroll
     for (int t = 0; t < DK / 16; ++t) {
       pk[16 * t] = f2bf(dk[t][q] * a.scale);
@@ -612,6 +632,32 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
 }
 
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <bool RP>
+void launch_fwd(const RelAttnP& a, int dk, bool rm, hipStream_t st) {
+  const dim3 grid((unsigned)cdiv(a.T, 64), (unsigned)a.H, (unsigned)a.B);
+  if (dk == 64 && rm) relattn_fwd_kernel<64, true, RP><<<grid, 256, 0, st>>>(a);
+  else if (dk == 64) relattn_fwd_kernel<64, false, RP><<<grid, 256, 0, st>>>(a);
+  else if (rm) relattn_fwd_kernel<32, true, RP><<<grid, 256, 0, st>>>(a);
+  else relattn_fwd_kernel<32, false, RP><<<grid, 256, 0, st>>>(a);
+}
+
+template <bool RP>
+int launch_bwd(const RelAttnP& a, int dk, bool rm, hipStream_t st) {
+  const dim3 gq((unsigned)cdiv(a.T, 64), (unsigned)a.H, (unsigned)a.B);
+  if (dk == 64 && rm) relattn_bwd_q_kernel<64, true, RP><<<gq, 256, 0, st>>>(a);
+  else if (dk == 64) relattn_bwd_q_kernel<64, false, RP><<<gq, 256, 0, st>>>(a);
+  else if (rm) relattn_bwd_q_kernel<32, true, RP><<<gq, 256, 0, st>>>(a);
+  else relattn_bwd_q_kernel<32, false, RP><<<gq, 256, 0, st>>>(a);
+  int rc = lasr_check_launch("relattn_bwd_q");
+  if (rc) return rc;
+  const dim3 gk((unsigned)cdiv(a.Tk, 64), (unsigned)a.H, (unsigned)a.B);
+  if (dk == 64 && rm) relattn_bwd_kv_kernel<64, true, RP><<<gk, 256, 0, st>>>(a);
+  else if (dk == 64) relattn_bwd_kv_kernel<64, false, RP><<<gk, 256, 0, st>>>(a);
+  else if (rm) relattn_bwd_kv_kernel<32, true, RP><<<gk, 256, 0, st>>>(a);
+  else relattn_bwd_kv_kernel<32, false, RP><<<gk, 256, 0, st>>>(a);
+  return lasr_check_launch("relattn_bwd_kv");
+}
 
 }  // namespace
 
@@ -631,14 +677,9 @@ extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, con
   a.pos = (const bf16_t*)pos;
   a.ldq = ldq; a.ldkv = ldkv; a.ldp = ldp;
   a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
-  a.B = B; a.H = H; a.T = T; a.scale = scale;
+  a.B = B; a.H = H; a.T = T; a.Tk = T; a.scale = scale;
   a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
-  dim3 grid((unsigned)cdiv(T, 64), (unsigned)H, (unsigned)B);
-  const bool rm = a.mask && a.msq != 0;
-  if (dk == 64 && rm) relattn_fwd_kernel<64, true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-  else if (dk == 64) relattn_fwd_kernel<64, false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-  else if (rm) relattn_fwd_kernel<32, true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-  else relattn_fwd_kernel<32, false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+  launch_fwd<true>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
   return lasr_check_launch("relattn_fwd");
 }
 
@@ -662,23 +703,53 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   a.pos = (const bf16_t*)pos;
   a.ldq = ldq; a.ldkv = ldkv; a.ldp = ldp;
   a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
-  a.B = B; a.H = H; a.T = T; a.scale = scale;
+  a.B = B; a.H = H; a.T = T; a.Tk = T; a.scale = scale;
   a.stats = (float*)stats; a.ldc = ldc;
   a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
   a.dqu = (bf16_t*)dqu; a.dbd = (bf16_t*)dbd; a.ldS = ldS; a.dbd_hb = dbd_head_major;
   a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
-  hipStream_t st = (hipStream_t)stream;
-  dim3 grid((unsigned)cdiv(T, 64), (unsigned)H, (unsigned)B);
-  const bool rm = a.mask && a.msq != 0;
-  if (dk == 64 && rm) relattn_bwd_q_kernel<64, true><<<grid, 256, 0, st>>>(a);
-  else if (dk == 64) relattn_bwd_q_kernel<64, false><<<grid, 256, 0, st>>>(a);
-  else if (rm) relattn_bwd_q_kernel<32, true><<<grid, 256, 0, st>>>(a);
-  else relattn_bwd_q_kernel<32, false><<<grid, 256, 0, st>>>(a);
-  int rc = lasr_check_launch("relattn_bwd_q");
-  if (rc) return rc;
-  if (dk == 64 && rm) relattn_bwd_kv_kernel<64, true><<<grid, 256, 0, st>>>(a);
-  else if (dk == 64) relattn_bwd_kv_kernel<64, false><<<grid, 256, 0, st>>>(a);
-  else if (rm) relattn_bwd_kv_kernel<32, true><<<grid, 256, 0, st>>>(a);
-  else relattn_bwd_kv_kernel<32, false><<<grid, 256, 0, st>>>(a);
-  return lasr_check_launch("relattn_bwd_kv");
+  return launch_bwd<true>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
+}
+
+// Plain scaled dot-product attention (no positional term) on the same kernels, with Tk keys
+// per utterance: the decoder's self attention (Tk = Tq, causal + padding mask) and source
+// attention over the encoder output (Tk = T', key padding).
+extern "C" int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                             int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc, void* stream) {
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_fwd: d_k=%d (32 or 64)", dk);
+  LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_fwd: bad B/H/T");
+  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc >= H * dk, "lasr_attn_fwd: row strides must be multiples of 8");
+  LASR_CHECK_ARG(al16(q) && al16(k) && al16(v), "lasr_attn_fwd: 16-B alignment");
+  if (B == 0 || Tq == 0) return LASR_OK;
+  RelAttnP a = {};
+  a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.ldq = ldq; a.ldkv = ldkv;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
+  a.B = B; a.H = H; a.T = Tq; a.Tk = Tk; a.scale = scale;
+  a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
+  launch_fwd<false>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
+  return lasr_check_launch("attn_fwd");
+}
+
+extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                             int64_t mask_sq, float scale, const float* stats, const void* ctx, const void* dctx,
+                             int64_t ldc, float* Dbuf, void* dq, void* dk_out, void* dv_out, int64_t lddkv,
+                             void* stream) {
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_bwd: d_k=%d (32 or 64)", dk);
+  LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_bwd: bad B/H/T");
+  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk && lddkv % 8 == 0,
+                 "lasr_attn_bwd: row strides must be multiples of 8");
+  LASR_CHECK_ARG(al16(q) && al16(k) && al16(v) && al16(dctx) && al16(ctx), "lasr_attn_bwd: 16-B alignment");
+  if (B == 0 || Tq == 0) return LASR_OK;
+  RelAttnP a = {};
+  a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.ldq = ldq; a.ldkv = ldkv;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
+  a.B = B; a.H = H; a.T = Tq; a.Tk = Tk; a.scale = scale;
+  a.stats = (float*)stats; a.ldc = ldc;
+  a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
+  a.dqu = (bf16_t*)dq; a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
+  return launch_bwd<false>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
 }

@@ -535,6 +535,22 @@ def relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, d
            stream())
 
 
+def attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx):
+    """Plain attention on the fused kernels (lasr_attn_fwd): q [B*Tq, H*d_k], k / v
+    [B*Tk, H*d_k] row-major views (k and v share a row stride), stats [B*H*Tq*2] fp32."""
+    assert v.stride(0) == k.stride(0)
+    N.call("lasr_attn_fwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, q.shape[1] // H,
+           ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ctx.stride(0), stream())
+
+
+def attn_bwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dq, dk, dv):
+    assert dq.stride(0) == q.stride(0) and v.stride(0) == k.stride(0) and dv.stride(0) == dk.stride(0)
+    assert dctx.stride(0) == ctx.stride(0)
+    N.call("lasr_attn_bwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, q.shape[1] // H,
+           ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx), ctx.stride(0), ptr(Dbuf), ptr(dq),
+           ptr(dk), ptr(dv), dk.stride(0), stream())
+
+
 def reduce_batch(src, B, H, T, dk, dst):
     N.call("lasr_reduce_batch", ptr(src), B, H, T, dk, ptr(dst), dt(dst), stream())
 

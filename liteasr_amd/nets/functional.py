@@ -262,26 +262,16 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
 
 
 # ============================================================ plain MHA =========
-# Decoder self-attention on the fused kernels (attn_fused.hip): plain scaled dot-product
-# attention is the relative-position kernel with a zero positional table (qu = qv = q, the
-# bd term and its gradient vanish exactly), so scores / softmax / P.V (3 launches forward,
-# 5 backward) become 1 + 2 launches.  LASR_FUSED_DEC_SELF=0 keeps the materialised path.
-FUSED_DEC_SELF = os.environ.get("LASR_FUSED_DEC_SELF", "1") != "0"
-_ZPOS = {}
+# Decoder attention on the fused kernels (attn_fused.hip, lasr_attn_fwd/bwd: the relative-
+# position kernels without the positional term, Tq queries x Tk keys): scores / softmax /
+# P.V (3 launches forward, 5 backward) become 1 + 2 launches, for the self attention (causal +
+# padding mask) and the source attention over the encoder output (key padding).
+# LASR_FUSED_DEC_ATTN=0 keeps the materialised path.
+FUSED_DEC_ATTN = os.environ.get("LASR_FUSED_DEC_ATTN", "1") != "0"
 
 
-def _zero_pos(T, d, dev, adt):
-    """A cached all-zero positional table with >= T rows and >= d columns."""
-    key = (str(dev), adt)
-    z = _ZPOS.get(key)
-    if z is None or z.shape[0] < T or z.shape[1] < d:
-        z = torch.zeros(max(T, 1024), max(d, 512), dtype=adt, device=dev)
-        _ZPOS[key] = z
-    return z[:T, :d]
-
-
-def _fused_dec_self(mem, adt, dk, p_att):
-    return FUSED_DEC_SELF and mem is None and fused_relattn(adt, dk, p_att)
+def _fused_dec(adt, dk, p_att):
+    return FUSED_DEC_ATTN and fused_relattn(adt, dk, p_att)
 
 
 def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_res, s_res):
@@ -291,17 +281,25 @@ def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_
     dev, adt = ln.device, ln.dtype
     R = B * Tq
     scale = dk ** -0.5
-    if _fused_dec_self(mem, adt, dk, p_att):
-        qkv = _e((R, 3 * d), adt, dev)
-        K.linear(ln, w.Wqkv, qkv, bias=w.bqkv)
+    if _fused_dec(adt, dk, p_att):
+        if mem is None:
+            qkv = _e((R, 3 * d), adt, dev)
+            K.linear(ln, w.Wqkv, qkv, bias=w.bqkv)
+            q, k, v, kv = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], None
+        else:
+            qkv = None
+            q = _e((R, d), adt, dev)
+            K.linear(ln, w.Wq, q, bias=w.bq)
+            kv = _e((B * Tk, 2 * d), adt, dev)
+            K.linear(mem, w.Wkv, kv, bias=w.bkv)
+            k, v = kv[:, :d], kv[:, d:]
         stats = _e((B * H * Tq * 2,), F32, dev)
         ctx = _e((R, d), adt, dev)
-        q = qkv[:, :d]
-        K.relattn_fwd(q, q, qkv[:, d:2 * d], qkv[:, 2 * d:], _zero_pos(Tq, d, dev, adt), B, H, Tq, mask, msb,
-                      msq, scale, stats, ctx)
+        K.attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx)
         out = _e((R, d), F32, dev)
         K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
-        return out, SimpleNamespace(qkv=qkv, q=None, kv=None, P=None, Praw=None, ctx=ctx, stats=stats)
+        return out, SimpleNamespace(qkv=qkv, q=q if mem is not None else None, kv=kv, P=None, Praw=None, ctx=ctx,
+                                    stats=stats)
     if mem is None:
         qkv = _e((R, 3 * d), adt, dev)
         K.linear(ln, w.Wqkv, qkv, bias=w.bqkv)
@@ -341,17 +339,24 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
     K.gemm(gb.t(), sv.ctx, g.Wo, beta=1.0, split_k=0, rowsum=g.bo, group=True)
     dctx = _e((R, d), adt, dev)
     K.gemm(gb, w.Wo, dctx)
-    if getattr(sv, "stats", None) is not None:  # fused self-attention (mha_forward)
-        dqkv = _e((R, 3 * d), adt, dev)
-        q = sv.qkv[:, :d]
-        dbd = _e((B, H, Tq, ldS), adt, dev)  # gradient of the (zero) positional term: unused
+    if getattr(sv, "stats", None) is not None:  # fused attention (mha_forward)
         Dbuf = _e((B * H * Tq,), F32, dev)
-        K.relattn_bwd(q, q, sv.qkv[:, d:2 * d], sv.qkv[:, 2 * d:], _zero_pos(Tq, d, dev, adt), B, H, Tq, mask,
-                      msb, msq, scale, sv.stats, sv.ctx, dctx, Dbuf, dqkv[:, :d], dbd, ldS, dqkv[:, d:2 * d],
-                      dqkv[:, 2 * d:])
         dln = _e((R, d), adt, dev)
-        K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
-        K.gemm(dqkv, w.Wqkv, dln)
+        if mem is None:
+            dqkv = _e((R, 3 * d), adt, dev)
+            K.attn_bwd(sv.qkv[:, :d], sv.qkv[:, d:2 * d], sv.qkv[:, 2 * d:], B, H, Tq, Tk, mask, msb, msq, scale,
+                       sv.stats, sv.ctx, dctx, Dbuf, dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:])
+            K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
+            K.gemm(dqkv, w.Wqkv, dln)
+            return dln
+        dq = _e((R, d), adt, dev)
+        dkv = _e((B * Tk, 2 * d), adt, dev)
+        K.attn_bwd(sv.q, sv.kv[:, :d], sv.kv[:, d:], B, H, Tq, Tk, mask, msb, msq, scale, sv.stats, sv.ctx, dctx,
+                   Dbuf, dq, dkv[:, :d], dkv[:, d:])
+        K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq, group=True)
+        K.gemm(dq, w.Wq, dln)
+        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
+        K.gemm(dkv, w.Wkv, dmem, beta=1.0)
         return dln
     dctx4 = _heads(dctx, B, Tq, H, dk)
     if mem is None:

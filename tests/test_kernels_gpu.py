@@ -309,47 +309,59 @@ def test_gemm_dw_group_bit_identical(R, monkeypatch):
             close(db, db0.double() + dy.double().sum(0), 1e-5, "grouped db")
 
 
-@pytest.mark.parametrize("masked", [True, False])
-def test_decoder_self_attention_fused_matches_materialised(masked, monkeypatch):
-    """Decoder self-attention on the fused relative-position kernels with a zero positional
-    table (functional.mha_forward / mha_backward, LASR_FUSED_DEC_SELF) against the
-    materialised-score path on the same inputs: causal + key-padding mask (U2) or none
-    (Paraformer's parallel decoder), B 32, L+1 = 41, d 256, 4 heads, bf16."""
+@pytest.mark.parametrize("kind", ["self-masked", "self-nomask", "source"])
+def test_decoder_attention_fused_matches_materialised(kind, monkeypatch):
+    """Decoder attention on the fused kernels without the positional term (lasr_attn_fwd /
+    lasr_attn_bwd through functional.mha_forward / mha_backward, LASR_FUSED_DEC_ATTN)
+    against the materialised-score path on the same inputs: self attention with the causal +
+    key-padding mask (U2) or none (Paraformer's parallel decoder), and source attention over
+    an encoder output (Tq 41 != Tk 249, key padding); B 32, d 256, 4 heads, bf16."""
     from types import SimpleNamespace as NS
 
     from liteasr_amd.nets import functional as Fn
 
-    g = torch.Generator().manual_seed(41 + masked)
-    B, T, d, H = 32, 41, 256, 4
-    R = B * T
+    g = torch.Generator().manual_seed(len(kind))
+    B, Tq, d, H = 32, 41, 256, 4
+    Tk = Tq if kind != "source" else 249
+    R = B * Tq
+    sc = lambda *shape, f=0.08: (torch.randn(*shape, generator=g) * f)  # noqa: E731
     ln = torch.randn(R, d, generator=g).to(DEV, torch.bfloat16)
     x_in = torch.randn(R, d, generator=g).to(DEV)
-    w = NS(Wqkv=(torch.randn(3 * d, d, generator=g) * 0.08).to(DEV, torch.bfloat16),
-           bqkv=torch.randn(3 * d, generator=g).to(DEV) * 0.1,
-           Wo=(torch.randn(d, d, generator=g) * 0.06).to(DEV, torch.bfloat16),
-           bo=torch.randn(d, generator=g).to(DEV) * 0.1)
     gb = torch.randn(R, d, generator=g).to(DEV, torch.bfloat16)
-    if masked:
-        lens = torch.randint(5, T + 1, (B,), generator=g)
-        j = torch.arange(T)
-        m = (j[None, None, :] > j[None, :, None]) | (j[None, None, :] >= lens[:, None, None])
-        mask, msb, msq = m.to(torch.uint8).to(DEV), T * T, T
+    w = NS(Wo=sc(d, d).to(DEV, torch.bfloat16), bo=sc(d, f=0.1).to(DEV))
+    if kind == "source":
+        mem = torch.randn(B * Tk, d, generator=g).to(DEV, torch.bfloat16)
+        w.Wq, w.bq = sc(d, d).to(DEV, torch.bfloat16), sc(d, f=0.1).to(DEV)
+        w.Wkv, w.bkv = sc(2 * d, d).to(DEV, torch.bfloat16), sc(2 * d, f=0.1).to(DEV)
+        lens = torch.randint(150, Tk + 1, (B,), generator=g)
+        m = torch.arange(Tk)[None, :] >= lens[:, None]
+        mask, msb, msq = m.to(torch.uint8).to(DEV), Tk, 0
     else:
-        mask, msb, msq = None, 0, 0
+        mem = None
+        w.Wqkv, w.bqkv = sc(3 * d, d).to(DEV, torch.bfloat16), sc(3 * d, f=0.1).to(DEV)
+        if kind == "self-masked":
+            lens = torch.randint(5, Tq + 1, (B,), generator=g)
+            j = torch.arange(Tq)
+            m = (j[None, None, :] > j[None, :, None]) | (j[None, None, :] >= lens[:, None, None])
+            mask, msb, msq = m.to(torch.uint8).to(DEV), Tq * Tq, Tq
+        else:
+            mask, msb, msq = None, 0, 0
     res = {}
     for fused in (False, True):
-        monkeypatch.setattr(Fn, "FUSED_DEC_SELF", fused)
-        grads = NS(Wqkv=torch.zeros(3 * d, d, device=DEV), bqkv=torch.zeros(3 * d, device=DEV),
-                   Wo=torch.zeros(d, d, device=DEV), bo=torch.zeros(d, device=DEV))
-        out, sv = Fn.mha_forward(ln, None, w, B, T, T, H, mask, msb, msq, x_in, 0.0, 0, 0.0, 0)
+        monkeypatch.setattr(Fn, "FUSED_DEC_ATTN", fused)
+        grads = NS(**{k: torch.zeros_like(v, dtype=torch.float32) for k, v in vars(w).items()})
+        dmem = torch.zeros(B * Tk, d, device=DEV) if mem is not None else None
+        out, sv = Fn.mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, 0.0, 0, 0.0, 0)
         assert (sv.stats is not None) == fused
-        dln = Fn.mha_backward(gb, ln, None, sv, w, grads, B, T, T, H, mask, msb, msq, 0.0, 0, None)
+        dln = Fn.mha_backward(gb, ln, mem, sv, w, grads, B, Tq, Tk, H, mask, msb, msq, 0.0, 0, dmem)
         torch.cuda.synchronize()
-        res[fused] = (out.float(), dln.float(), grads)
-    (o0, d0, g0), (o1, d1, g1) = res[False], res[True]
+        res[fused] = (out.float(), dln.float(), dmem, grads)
+    (o0, d0, m0, g0), (o1, d1, m1, g1) = res[False], res[True]
     close(o1, o0, 1e-2, "out")
     close(d1, d0, 2e-2, "dln")
-    for k in ("Wqkv", "bqkv", "Wo", "bo"):
+    if m0 is not None:
+        close(m1, m0, 2e-2, "dmem")
+    for k in vars(g0):
         close(getattr(g1, k), getattr(g0, k), 2e-2, k)
 
 
