@@ -150,6 +150,9 @@ class FusedEncoderModel(LiteasrModel):
         d = enc.h_dim
         pos = torch.empty(T, d, dtype=self.compute_dtype, device=xs.device)
         K.pe_fwd(None, T, T, d, enc.pe.table(T), 1.0, pos, env.p_pos, env.seed + 4)
+        pp = FN.pos_projections(pos, [layer.weights().att.Wpos for layer in enc.enc_layers]) \
+            if FN.BATCH_POS_PROJ else None
+        env.pos_proj = {id(layer): p for layer, p in zip(enc.enc_layers, pp)} if pp else None
         for j, layer in enumerate(enc.enc_layers):
             x = self._cut(x, j)
             x = FN.ConformerLayerFn.apply(x, pos, layer.final_norm.weight, layer, env)

@@ -156,7 +156,33 @@ def fused_relattn(adt, dk, p_att):
     return FUSED_RELATTN and adt == torch.bfloat16 and dk in (32, 64) and p_att == 0.0
 
 
-def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res):
+BATCH_POS_PROJ = os.environ.get("LASR_BATCH_POS_PROJ", "1") != "0"
+
+
+def pos_projections(pos, Ws):
+    """p_j = pos @ Wpos_j^T of every encoder layer in ONE batched GEMM (positional_encoding +
+    attention.py:95 linear_pos; the table is the same for all layers): the layers' weights
+    sit at a constant stride in the flat parameter store, so they form one strided batch.
+    None when they do not (the layers then project their own)."""
+    n = len(Ws)
+    if n < 2 or not all(W.is_contiguous() for W in Ws):
+        return None
+    base = Ws[0].untyped_storage().data_ptr()
+    if any(W.untyped_storage().data_ptr() != base for W in Ws):
+        return None
+    offs = [W.storage_offset() for W in Ws]
+    st = offs[1] - offs[0]
+    if st <= 0 or any(offs[j] - offs[0] != j * st for j in range(n)):
+        return None
+    dout, din = Ws[0].shape
+    Wt = torch.as_strided(Ws[0], (n, din, dout), (st, 1, din), offs[0])  # W_j^T
+    T = pos.shape[0]
+    out = _e((n, T, dout), pos.dtype, pos.device)
+    K.gemm(pos.unsqueeze(0).expand(n, T, din), Wt, out)
+    return [out[j] for j in range(n)]
+
+
+def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None):
     B, T, H = env.B, env.T, env.H
     d = ln.shape[1]
     dk = d // H
@@ -165,8 +191,9 @@ def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res):
     scale = dk ** -0.5
     qkv = _e((M, 3 * d), adt, dev)
     K.linear(ln, w.Wqkv, qkv, bias=w.bqkv)
-    p = _e((T, d), adt, dev)
-    K.linear(pos, w.Wpos, p)
+    if p is None:  # else precomputed for all layers at once (pos_projections)
+        p = _e((T, d), adt, dev)
+        K.linear(pos, w.Wpos, p)
     qu = _e((M, d), adt, dev)
     qv = _e((M, d), adt, dev)
     K.qbias_fwd(qkv, B, T, H, dk, w.u, w.v, qu, qv)
@@ -537,7 +564,9 @@ class ConformerLayerFn(torch.autograd.Function):
                                  _seed(s, 1), x0, 0.5, pd, _seed(s, 2))
         # (b) relative-position MHSA
         ln_b, _, mb, rb = ln_forward(x1, w.ln_b.g, w.ln_b.b, adt)
-        x2, svb = relmha_forward(ln_b, pos, w.att, env, x1, pat, _seed(s, 3), pd, _seed(s, 4))
+        pp = getattr(env, "pos_proj", None)
+        x2, svb = relmha_forward(ln_b, pos, w.att, env, x1, pat, _seed(s, 3), pd, _seed(s, 4),
+                                 p=pp.get(id(layer)) if pp else None)
         # (c) convolution module
         ln_c, _, mc, rc = ln_forward(x2, w.ln_c.g, w.ln_c.b, adt)
         x3, svc = conv_forward(ln_c, w.conv, env, x2, pd, _seed(s, 5), tr)
