@@ -105,7 +105,9 @@ def _worker(rank, world, port, q):
         bn.fill_(float(rank + 20))
         ddp._sync_buffers()
         res["bn_after_sync"] = float(bn[0])
-        q.put((rank, res))
+        # by value: a torch tensor through the queue is a shared-memory handle that dies with
+        # this process, which may exit before the parent unpickles it
+        q.put((rank, {k: (v.numpy().copy() if isinstance(v, torch.Tensor) else v) for k, v in res.items()}))
     finally:
         dist.destroy_process_group()
 
@@ -122,7 +124,8 @@ def test_flat_ddp_gloo_world2():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=240) for _ in procs)
+    out = {r: {k: (torch.from_numpy(v) if hasattr(v, "dtype") and hasattr(v, "shape") else v) for k, v in d.items()}
+           for r, d in (q.get(timeout=240) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
