@@ -192,6 +192,12 @@ int lasr_layernorm_fwd(const void* x, int x_dtype, int64_t rows, int D, const fl
                        const float* beta, float eps, void* y, int y_dtype, float* mean,
                        float* rstd, void* y2, int y2_dtype, float p2, uint64_t seed2,
                        void* stream);
+/* Two chained LayerNorms per row (a Conformer layer's final norm, then the next layer's
+ * first norm: liteasr/nets/conformer_layer.py:147, :130): y = LN1(x) fp32 + (mean1, rstd1),
+ * z = LN2(y) bf16 + (mean2, rstd2); bit-identical to two lasr_layernorm_fwd calls. */
+int lasr_layernorm2_fwd(const float* x, int64_t rows, int D, const float* g1, const float* b1,
+                        const float* g2, const float* b2, float eps, float* y, float* mean1,
+                        float* rstd1, void* z, float* mean2, float* rstd2, void* stream);
 int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype, int64_t rows,
                        int D, const float* gamma, const float* mean, const float* rstd,
                        const void* dres, int dres_dtype, void* dx, int dx_dtype,

@@ -133,6 +133,7 @@ SIGNATURES = {
     "lasr_ffn_fwd": [C.POINTER(FfnArgs), _p],
     "lasr_ffn_bwd_dx": [C.POINTER(FfnArgs), _p],
     "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
+    "lasr_layernorm2_fwd": [_p, _l, _i, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _p],
     "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],
     "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,
                            _p, _i, _f, _f, _u, _p],

@@ -49,10 +49,12 @@ __global__ void embed_pe_fwd_kernel(const int32_t* ids, int R, int L, int D, con
 // every row with that id and adds it to dE[id].  The rows holding the id are found in
 // parallel (ballot compaction, row order kept); the sum runs over 4 row groups x 8
 // accumulators per column and is combined in a fixed order (run-to-run identical).
+constexpr int EMB_EC = 4;  // 64-column chunks per pass of embed_bwd_kernel
+
 template <typename TD>
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int R, int D, const TD* dy,
                                                         float xscale, DropCfg d, float* dE) {
-  extern __shared__ int sid[];  // R ids, up to R matching rows, 256 partial sums
+  extern __shared__ int sid[];  // R ids, up to R matching rows, 4 x EMB_EC x 64 partial sums
   __shared__ int wcnt[4];
   int* rows = sid + R;
   for (int i = threadIdx.x; i < R; i += blockDim.x) sid[i] = ids[i];
@@ -75,30 +77,45 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
     n += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
     __syncthreads();
   }
-  // 4 row groups x 64 columns per pass, fixed-order combine
+  // 4 row groups x 64 columns per chunk, EC chunks (EC * 64 columns) per pass so a frequent
+  // id's long row list is walked once per pass with EC x 8 independent loads in flight (a
+  // frequent id, e.g. the eos padding, has hundreds of rows: the latency chain, not
+  // bandwidth, bounds this block); per column the same summation order as one chunk a pass
   const uint32_t key = d.p > 0.f ? drop_key(d) : 0u;
-  float* part = reinterpret_cast<float*>(rows + R);  // [4][64]
-  for (int c0 = 0; c0 < D; c0 += 64) {
-    const int c = c0 + lane;
-    // 8 independent loads in flight per step (a frequent id, e.g. the eos padding, has
-    // hundreds of rows: the latency chain, not bandwidth, bounds this block)
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (c < D) {
-      for (int q0 = w; q0 < n; q0 += 32) {
+  float* part = reinterpret_cast<float*>(rows + R);  // [4][EC * 64]
+  for (int c0 = 0; c0 < D; c0 += 64 * EMB_EC) {
+    float a[EMB_EC][8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int q = q0 + 4 * u;
-          if (q < n) {
-            const int64_t e = (int64_t)rows[q] * D + c;
-            a[u] += to_f(dy[e]) * drop_mul_k(d, key, (uint64_t)e);
+    for (int cc = 0; cc < EMB_EC; ++cc)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[cc][u] = 0.f;
+    for (int q0 = w; q0 < n; q0 += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + 4 * u;
+        if (q < n) {
+          const int64_t rb = (int64_t)rows[q] * D;
+#pragma unroll
+          for (int cc = 0; cc < EMB_EC; ++cc) {
+            const int c = c0 + 64 * cc + lane;
+            if (c < D) a[cc][u] += to_f(dy[rb + c]) * drop_mul_k(d, key, (uint64_t)(rb + c));
           }
         }
       }
     }
-    part[w * 64 + lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+    for (int cc = 0; cc < EMB_EC; ++cc)
+      part[w * 64 * EMB_EC + 64 * cc + lane] =
+          ((a[cc][0] + a[cc][1]) + (a[cc][2] + a[cc][3])) + ((a[cc][4] + a[cc][5]) + (a[cc][6] + a[cc][7]));
     __syncthreads();
-    if (w == 0 && c < D)
-      dE[(int64_t)id * D + c] += (((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane]) * xscale;
+    if (w == 0) {
+#pragma unroll
+      for (int cc = 0; cc < EMB_EC; ++cc) {
+        const int c = c0 + 64 * cc + lane, o = 64 * cc + lane, S = 64 * EMB_EC;
+        if (c < D)
+          dE[(int64_t)id * D + c] += (((part[o] + part[S + o]) + part[2 * S + o]) + part[3 * S + o]) * xscale;
+      }
+    }
     __syncthreads();
   }
 }
@@ -171,7 +188,7 @@ extern "C" int lasr_embed_bwd(const int32_t* ids, int R, int D, const void* dy, 
   LASR_CHECK_ARG(R <= 16384, "lasr_embed_bwd: R=%d > 16384", R);  // 2 R ints of LDS
   DropCfg d = mkdrop(p, seed);
   hipStream_t st = (hipStream_t)stream;
-  const size_t shm = ((size_t)2 * R + 256) * sizeof(int);
+  const size_t shm = ((size_t)2 * R + 256 * EMB_EC) * sizeof(int);
   if (dydt == LASR_F32) embed_bwd_kernel<float><<<R, 256, shm, st>>>(ids, R, D, (const float*)dy, xscale, d, dE);
   else embed_bwd_kernel<bf16_t><<<R, 256, shm, st>>>(ids, R, D, (const bf16_t*)dy, xscale, d, dE);
   return lasr_check_launch("embed_bwd");

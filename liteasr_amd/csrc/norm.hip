@@ -50,6 +50,54 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, i
   }
 }
 
+// Two chained LayerNorms of one row (a Conformer layer's final norm and the next layer's
+// first norm, conformer_layer.py:147 -> :130): y = LN1(x) stored fp32 (the layer output),
+// z = LN2(y) stored bf16, each with its row statistics.  LN2 reads the fp32 y it just wrote,
+// so z and its statistics are bit-identical to a separate lasr_layernorm_fwd on y.
+template <int NPL>
+__global__ __launch_bounds__(256) void ln2_fwd_kernel(const float* __restrict__ x, int64_t rows,
+                                                      const float* __restrict__ g1, const float* __restrict__ b1,
+                                                      const float* __restrict__ g2, const float* __restrict__ b2,
+                                                      float eps, float* __restrict__ y, float* __restrict__ mean1,
+                                                      float* __restrict__ rstd1, bf16_t* __restrict__ z,
+                                                      float* __restrict__ mean2, float* __restrict__ rstd2) {
+  constexpr int D = NPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int c0 = lane * NPL;
+  float v[NPL], g[NPL], b[NPL];
+  ldv<NPL>(x + row * D + c0, v);
+  ldv<NPL>(g1 + c0, g);
+  ldv<NPL>(b1 + c0, b);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) s += v[i];
+    const float mu = wave_sum(s) * (1.f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) { const float dv = v[i] - mu; q += dv * dv; }
+    const float var = wave_sum(q) * (1.f / D);
+    const float rs = rsqrtf(var + eps);
+    float o[NPL];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) o[i] = (v[i] - mu) * rs * g[i] + b[i];
+    if (pass == 0) {
+      if (lane == 0) { mean1[row] = mu; rstd1[row] = rs; }
+      stv<NPL>(y + row * D + c0, o);
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) v[i] = o[i];
+      ldv<NPL>(g2 + c0, g);
+      ldv<NPL>(b2 + c0, b);
+    } else {
+      if (lane == 0) { mean2[row] = mu; rstd2[row] = rs; }
+      stv<NPL>(z + row * D + c0, o);
+    }
+  }
+}
+
 // Backward: LnbCfg::WAVES waves per block, each LN_ROWS_PER_BLOCK / WAVES rows; the
 // block's dgamma/dbeta partials are combined in fixed order through LDS (deterministic).
 template <int NPL>
@@ -190,6 +238,27 @@ extern "C" int lasr_layernorm_fwd(const void* x, int x_dtype, int64_t rows, int 
     default: lasr_set_error("lasr_layernorm_fwd: D=%d unsupported", D); return LASR_ERR_INVALID;
   }
   return lasr_check_launch("layernorm_fwd");
+}
+
+extern "C" int lasr_layernorm2_fwd(const float* x, int64_t rows, int D, const float* g1, const float* b1,
+                                   const float* g2, const float* b2, float eps, float* y, float* mean1,
+                                   float* rstd1, void* z, float* mean2, float* rstd2, void* stream) {
+  LASR_CHECK_ARG(D == 256 || D == 512 || D == 128 || D == 64, "lasr_layernorm2_fwd: D=%d unsupported", D);
+  LASR_CHECK_ARG(ln_aligned(x, D, LASR_F32) && ln_aligned(y, D, LASR_F32) && ln_aligned(z, D, LASR_BF16) &&
+                     ln_aligned(g1, D, LASR_F32) && ln_aligned(b1, D, LASR_F32) && ln_aligned(g2, D, LASR_F32) &&
+                     ln_aligned(b2, D, LASR_F32),
+                 "lasr_layernorm2_fwd: misaligned row pointer");
+  if (rows <= 0) return LASR_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned nb = (unsigned)cdiv(rows, LN_WAVES);
+#define LN2(NPL) ln2_fwd_kernel<NPL><<<nb, LN_WAVES * 64, 0, st>>>(x, rows, g1, b1, g2, b2, eps, y, mean1, rstd1, \
+                                                                  (bf16_t*)z, mean2, rstd2)
+  if (D == 64) LN2(1);
+  else if (D == 128) LN2(2);
+  else if (D == 256) LN2(4);
+  else LN2(8);
+#undef LN2
+  return lasr_check_launch("layernorm2_fwd");
 }
 
 // Backward dispatch: x/dy dtypes in {f32,bf16}; dres (f32/bf16/none), dx f32/bf16, gb bf16/f32.

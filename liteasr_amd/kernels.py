@@ -402,6 +402,13 @@ def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd, y2=None, p2=0.0, seed2=0):
            stream())
 
 
+def layernorm2_fwd(x, g1, b1, g2, b2, eps, y, mean1, rstd1, z, mean2, rstd2):
+    """y = LN1(x) (fp32), z = LN2(y) (bf16), one launch (lasr_layernorm2_fwd)."""
+    rows, D = x.shape
+    N.call("lasr_layernorm2_fwd", ptr(x), rows, D, ptr(g1), ptr(b1), ptr(g2), ptr(b2), eps, ptr(y), ptr(mean1),
+           ptr(rstd1), ptr(z), ptr(mean2), ptr(rstd2), stream())
+
+
 def layernorm_bwd(x, dy, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, gb=None,
                   bscale=1.0, bp=0.0, bseed=0):
     rows, D = x.shape

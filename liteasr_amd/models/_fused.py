@@ -153,9 +153,17 @@ class FusedEncoderModel(LiteasrModel):
         pp = FN.pos_projections(pos, [layer.weights().att.Wpos for layer in enc.enc_layers]) \
             if FN.BATCH_POS_PROJ else None
         env.pos_proj = {id(layer): p for layer, p in zip(enc.enc_layers, pp)} if pp else None
-        for j, layer in enumerate(enc.enc_layers):
+        layers = list(enc.enc_layers)
+        env.pre_ln = None
+        for j, layer in enumerate(layers):
             x = self._cut(x, j)
+            if j + 1 < len(layers):
+                wn = layers[j + 1].weights().ln_a
+                env.next_ln = (layers[j + 1], wn.g, wn.b)
+            else:
+                env.next_ln = None
             x = FN.ConformerLayerFn.apply(x, pos, layer.final_norm.weight, layer, env)
+        env.next_ln = env.pre_ln = None
         x = self._cut(x, len(enc.enc_layers))
         return x, prep, env
 

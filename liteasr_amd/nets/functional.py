@@ -157,6 +157,8 @@ def fused_relattn(adt, dk, p_att):
 
 
 BATCH_POS_PROJ = os.environ.get("LASR_BATCH_POS_PROJ", "1") != "0"
+# a layer's final norm and the next layer's first norm in one launch (lasr_layernorm2_fwd)
+FUSED_LN2 = os.environ.get("LASR_FUSED_LN2", "1") != "0"
 
 
 def pos_projections(pos, Ws):
@@ -559,7 +561,12 @@ class ConformerLayerFn(torch.autograd.Function):
         adt = env.adt
         x0 = x0.contiguous()
         # (a) macaron FFN, scale 0.5
-        ln_a, _, ma, ra = ln_forward(x0, w.ln_a.g, w.ln_a.b, adt)
+        pre = getattr(env, "pre_ln", None)  # this layer's first norm, computed by the previous layer
+        if pre is not None and pre[0] == id(layer) and pre[1] == x0.data_ptr():
+            ln_a, ma, ra = pre[2:]
+            env.pre_ln = None
+        else:
+            ln_a, _, ma, ra = ln_forward(x0, w.ln_a.g, w.ln_a.b, adt)
         x1, za, ha = ffn_forward(ln_a, w.ffm.W1, w.ffm.b1, w.ffm.W2, w.ffm.b2, ACT_SWISH, pff,
                                  _seed(s, 1), x0, 0.5, pd, _seed(s, 2))
         # (b) relative-position MHSA
@@ -574,11 +581,20 @@ class ConformerLayerFn(torch.autograd.Function):
         ln_d, _, md, rd = ln_forward(x3, w.ln_d.g, w.ln_d.b, adt)
         x4, zd, hd = ffn_forward(ln_d, w.ff.W1, w.ff.b1, w.ff.W2, w.ff.b2, ACT_SWISH, pff,
                                  _seed(s, 6), x3, 0.5, pd, _seed(s, 7))
-        # final LN -> next layer's residual stream (fp32)
+        # final LN -> next layer's residual stream (fp32); with the next layer's first norm
+        # chained in the same launch when the encoder loop names it (env.next_ln)
         x5 = _e(x4.shape, F32, x4.device)
         mf = _e(x4.shape[0], F32, x4.device)
         rf = _e(x4.shape[0], F32, x4.device)
-        K.layernorm_fwd(x4, w.ln_f.g, w.ln_f.b, LN_EPS, x5, mf, rf)
+        nxt = getattr(env, "next_ln", None)
+        if FUSED_LN2 and nxt is not None and adt == torch.bfloat16:
+            z = _e(x4.shape, adt, x4.device)
+            m2 = _e(x4.shape[0], F32, x4.device)
+            r2 = _e(x4.shape[0], F32, x4.device)
+            K.layernorm2_fwd(x4, w.ln_f.g, w.ln_f.b, nxt[1], nxt[2], LN_EPS, x5, mf, rf, z, m2, r2)
+            env.pre_ln = (id(nxt[0]), x5.data_ptr(), z, m2, r2)
+        else:
+            K.layernorm_fwd(x4, w.ln_f.g, w.ln_f.b, LN_EPS, x5, mf, rf)
         if torch.is_grad_enabled() or anchor.requires_grad:
             ctx.sv = SimpleNamespace(x=(x0, x1, x2, x3, x4), ln=(ln_a, ln_b, ln_c, ln_d),
                                      st=((ma, ra), (mb, rb), (mc, rc), (md, rd), (mf, rf)),

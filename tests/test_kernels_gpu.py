@@ -419,6 +419,27 @@ def test_layernorm(D, dtype):
     close(db, dy.double().sum(0), 1e-5, "ln dbeta")
 
 
+@pytest.mark.parametrize("D", [256, 512])
+def test_layernorm2_chained_bit_exact(D):
+    """lasr_layernorm2_fwd (a layer's final norm chained with the next layer's first norm)
+    gives the same bits as two lasr_layernorm_fwd launches: y fp32 + stats, z bf16 + stats."""
+    kn = K()
+    rows = 1001
+    g = torch.Generator().manual_seed(D)
+    x = (torch.randn(rows, D, generator=g) * 3 + 0.5).to(DEV)
+    g1, b1, g2, b2 = (torch.randn(D, generator=g).to(DEV) for _ in range(4))
+    y0, m0, r0 = torch.empty(rows, D, device=DEV), torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    z0 = torch.empty(rows, D, device=DEV, dtype=torch.bfloat16)
+    m0b, r0b = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    kn.layernorm_fwd(x, g1, b1, 1e-12, y0, m0, r0)
+    kn.layernorm_fwd(y0, g2, b2, 1e-12, z0, m0b, r0b)
+    y1, m1, r1 = torch.empty_like(y0), torch.empty_like(m0), torch.empty_like(r0)
+    z1, m1b, r1b = torch.empty_like(z0), torch.empty_like(m0b), torch.empty_like(r0b)
+    kn.layernorm2_fwd(x, g1, b1, g2, b2, 1e-12, y1, m1, r1, z1, m1b, r1b)
+    for a, b in ((y0, y1), (m0, m1), (r0, r1), (z0, z1), (m0b, m1b), (r0b, r1b)):
+        assert torch.equal(a, b)
+
+
 def test_colsum():
     kn = K()
     x = torch.randn(1000, 300, device=DEV).bfloat16()
