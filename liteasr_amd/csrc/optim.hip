@@ -9,13 +9,31 @@
 
 constexpr int SQ_CHUNK = 16384;  // elements per partial
 
+// One partial per SQ_CHUNK elements.  Full chunks: 16-B loads, all 16 per thread issued
+// before the sums (4 accumulators, fixed order); the ragged last chunk: scalar loads.
 __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* g, int64_t n, float* ws) {
   __shared__ float red[32];
   const int64_t base = (int64_t)blockIdx.x * SQ_CHUNK;
   float s = 0.f;
-  for (int64_t i = base + threadIdx.x; i < base + SQ_CHUNK && i < n; i += 256) {
-    const float v = g[i];
-    s += v * v;
+  if (base + SQ_CHUNK <= n && (((uintptr_t)g) & 15) == 0) {
+    constexpr int NV = SQ_CHUNK / (256 * 4);
+    float4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = *(const float4*)(g + base + ((int64_t)k * 256 + threadIdx.x) * 4);
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      a[0] += v[k].x * v[k].x;
+      a[1] += v[k].y * v[k].y;
+      a[2] += v[k].z * v[k].z;
+      a[3] += v[k].w * v[k].w;
+    }
+    s = (a[0] + a[1]) + (a[2] + a[3]);
+  } else {
+    for (int64_t i = base + threadIdx.x; i < base + SQ_CHUNK && i < n; i += 256) {
+      const float v = g[i];
+      s += v * v;
+    }
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) ws[blockIdx.x] = s;
