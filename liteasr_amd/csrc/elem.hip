@@ -83,6 +83,57 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
   // bandwidth, bounds this block); per column the same summation order as one chunk a pass
   const uint32_t key = d.p > 0.f ? drop_key(d) : 0u;
   float* part = reinterpret_cast<float*>(rows + R);  // [4][EC * 64]
+  if ((D & 1) == 0) {
+    // even D: a lane takes a column PAIR (one 4/8-B load, one dropout draw for both halves,
+    // as the forward drew them); per column the same order as below, so the same bits
+    constexpr int PC = EMB_EC / 2, S = 64 * EMB_EC;
+    for (int c0 = 0; c0 < D; c0 += S) {
+      float a[PC][2][8];
+#pragma unroll
+      for (int pc = 0; pc < PC; ++pc)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[pc][0][u] = a[pc][1][u] = 0.f;
+      for (int q0 = w; q0 < n; q0 += 32) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int q = q0 + 4 * u;
+          if (q < n) {
+            const int64_t rb = (int64_t)rows[q] * D;
+#pragma unroll
+            for (int pc = 0; pc < PC; ++pc) {
+              const int c = c0 + 128 * pc + 2 * lane;
+              if (c < D) {
+                float v2[2];
+                ldv<2>(dy + rb + c, v2);
+                const uint32_t bits = drop_bits(key, (uint64_t)(rb + c) >> 1);
+                a[pc][0][u] += v2[0] * ((bits & 0xFFFFu) >= d.thr ? d.scale : 0.f);
+                a[pc][1][u] += v2[1] * ((bits >> 16) >= d.thr ? d.scale : 0.f);
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int pc = 0; pc < PC; ++pc)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          part[w * S + 128 * pc + 2 * lane + j] = ((a[pc][j][0] + a[pc][j][1]) + (a[pc][j][2] + a[pc][j][3])) +
+                                                  ((a[pc][j][4] + a[pc][j][5]) + (a[pc][j][6] + a[pc][j][7]));
+      __syncthreads();
+      if (w == 0) {
+#pragma unroll
+        for (int pc = 0; pc < PC; ++pc)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int o = 128 * pc + 2 * lane + j, c = c0 + o;
+            if (c < D)
+              dE[(int64_t)id * D + c] += (((part[o] + part[S + o]) + part[2 * S + o]) + part[3 * S + o]) * xscale;
+          }
+      }
+      __syncthreads();
+    }
+    return;
+  }
   for (int c0 = 0; c0 < D; c0 += 64 * EMB_EC) {
     float a[EMB_EC][8];
 #pragma unroll
