@@ -92,6 +92,16 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(RSegs a) {
       const float4 v = *(const float4*)(src + (int64_t)p * g.N);
       acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
     }
+    float* o4 = n + 4 <= g.split ? g.out0 + n : (n >= g.split ? g.out1 + (n - g.split) : nullptr);
+    if (o4 && ((uintptr_t)o4 & 15) == 0) {  // the 4 columns in one aligned output run: 16-B RMW
+      float4 r = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      if (g.accumulate) {
+        const float4 c = *(const float4*)o4;
+        r = make_float4(c.x + acc[0], c.y + acc[1], c.z + acc[2], c.w + acc[3]);
+      }
+      *(float4*)o4 = r;
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float* o = n + q < g.split ? g.out0 + n + q : g.out1 + (n + q - g.split);
