@@ -6,7 +6,7 @@
 #include "common.h"
 
 constexpr int LN_WAVES = 4;           // forward: one row per wave
-constexpr int LN_ROWS_PER_BLOCK = 32;  // backward: rows per block (one partial row each)
+constexpr int LN_ROWS_PER_BLOCK = 16;  // backward: rows per block (one partial row each; 16: one row per wave, 2 blocks per CU)
 
 // Lane l owns the NPL contiguous columns [l*NPL, (l+1)*NPL) of a row (vector loads).
 template <int NPL, typename TX, typename TY, typename TY2>

@@ -412,7 +412,7 @@ def layernorm2_fwd(x, g1, b1, g2, b2, eps, y, mean1, rstd1, z, mean2, rstd2):
 def layernorm_bwd(x, dy, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, gb=None,
                   bscale=1.0, bp=0.0, bseed=0):
     rows, D = x.shape
-    nblk = (rows + 31) // 32  # LN_ROWS_PER_BLOCK (norm.hip)
+    nblk = (rows + 15) // 16  # LN_ROWS_PER_BLOCK (norm.hip)
     defer = _DEFER.depth and dgamma is not None and dbeta is not None
     if defer:
         ws = torch.empty(nblk * 2 * D, dtype=torch.float32, device=x.device)
