@@ -78,7 +78,35 @@ __global__ __launch_bounds__(256) void adam_kernel(float* p, TL* plp, const floa
   const float bc2 = 1.f - powf(beta2, step);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  auto upd = [&](float gi, float pi, float& mi, float& vi) {
+    gi *= coef;
+    if (wd != 0.f) gi += wd * pi;
+    mi = mi + (1.f - beta1) * (gi - mi);  // lerp, as torch.optim.Adam
+    vi = vi * beta2 + (1.f - beta2) * gi * gi;
+    return pi - step_size * mi / (sqrtf(vi) / bc2s + eps);
+  };
+  // 16-B accesses, 4 parameters per thread and iteration (the same per-element arithmetic)
+  const bool vec = ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&
+                   (((uintptr_t)plp) & (4 * sizeof(TL) - 1)) == 0;
+  int64_t done = 0;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+      const float4 g4 = ((const float4*)g)[i], p4 = ((const float4*)p)[i];
+      float4 m4 = ((float4*)m)[i], v4 = ((float4*)v)[i];
+      float o[4];
+      o[0] = upd(g4.x, p4.x, m4.x, v4.x);
+      o[1] = upd(g4.y, p4.y, m4.y, v4.y);
+      o[2] = upd(g4.z, p4.z, m4.z, v4.z);
+      o[3] = upd(g4.w, p4.w, m4.w, v4.w);
+      ((float4*)m)[i] = m4;
+      ((float4*)v)[i] = v4;
+      ((float4*)p)[i] = make_float4(o[0], o[1], o[2], o[3]);
+      if (plp) stv<4>(plp + 4 * i, o);
+    }
+    done = n4 * 4;
+  }
+  for (int64_t i = done + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float gi = g[i] * coef;
     float pi = p[i];
     if (wd != 0.f) gi += wd * pi;

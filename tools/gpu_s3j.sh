@@ -9,4 +9,4 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline --steps 40 > $
 python3 -c "import json;d=json.load(open('$OUT/b.json'));print(d['ms_per_step'], d['value'])"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/tr -o run -- python3 $R/bench.py --no-cpu-baseline --no-roofline --steps 5 --warmup 3 > $OUT/tr.log 2>&1 || exit 1
-python3 $R/tools/step_summary.py $OUT/tr/run_results.db 5 > $OUT/summary.txt && head -3 $OUT/summary.txt && grep -E "embed_bwd|sumsq|adam" $OUT/summary.txt
+python3 $R/tools/step_summary.py $OUT/tr/run_results.db 5 > $OUT/summary.txt && head -3 $OUT/summary.txt && grep -E "adam|ln_bwd|reduce_multi" $OUT/summary.txt
