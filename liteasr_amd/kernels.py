@@ -107,7 +107,12 @@ _GROUP_TILES = {(64, 64): (64, 64), (64, 128): (128, 128), (128, 64): (128, 128)
 # a lone launch (fewer fp32 partial slabs to write and reduce); 128 x 128 groups keep half
 # (tools: LASR_DW_GROUP_SPLIT_DIV overrides both)
 _DIV_ENV = os.environ.get("LASR_DW_GROUP_SPLIT_DIV")
-DW_GROUP_SPLIT_DIV = {(64, 64): 4, (128, 128): 2} if _DIV_ENV is None else int(_DIV_ENV)
+if _DIV_ENV is None:
+    DW_GROUP_SPLIT_DIV = {(64, 64): 4, (128, 128): 2}
+elif "," in _DIV_ENV:  # "d64,d128": one divisor per group tile
+    DW_GROUP_SPLIT_DIV = dict(zip([(64, 64), (128, 128)], map(int, _DIV_ENV.split(","))))
+else:
+    DW_GROUP_SPLIT_DIV = int(_DIV_ENV)
 
 
 def _group_div(key):
