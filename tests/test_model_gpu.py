@@ -378,6 +378,44 @@ def test_graphed_step_matches_eager():
     assert o1.device_state() == o2.device_state()
 
 
+def test_graphed_step_survives_workspace_growth():
+    """The captured graphs address the shared kernel scratch buffer (kernels.WS); an eager
+    call that needs more scratch replaces that buffer. GraphedTrainStep keeps the captured
+    one alive, so replays after the growth leave live tensors alone (memory of the replaced
+    buffer's size handed out again and filled with NaN stays NaN) and still match the eager
+    steps bit for bit."""
+    from liteasr_amd import kernels as K
+    from liteasr_amd.graph_step import GraphedTrainStep
+
+    batches = [[t.cuda() for t in O.synthetic_batch(3, 120, 6, 30, seed=20 + i)] for i in range(3)]
+    m1, c1, o1 = _graph_setup(0.1)
+    eager = []
+    for b in batches:
+        l = c1(m1, *b)
+        l.backward()
+        o1.clip_and_step(5.0)
+        o1.zero_grad()
+        eager.append(l.item())
+    m2, c2, o2 = _graph_setup(0.1)
+    gs = GraphedTrainStep(m2, c2, o2, batches[0], clip=5.0, warmup=1)
+    graphed = [gs(batches[0]).item()]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    old = K.WS.buf[dev.index]
+    n_old = old.numel()
+    del old
+    grown = K.WS.get(n_old * 4, dev)  # what a longer eager batch would do
+    assert grown.numel() > n_old and K.WS.buf[dev.index] is grown
+    grown.fill_(float("nan"))
+    reuse = torch.full((n_old,), float("nan"), device=dev)  # may land on a freed block
+    graphed += [gs(b).item() for b in batches[1:]]
+    torch.cuda.synchronize()
+    # the replays write their scratch into the captured buffer, never into live tensors
+    assert torch.isnan(reuse).all() and torch.isnan(grown).all()
+    assert graphed == eager, (graphed, eager)
+    assert torch.equal(m1.store.flat, m2.store.flat)
+    del reuse
+
+
 def _ddp_graph_worker(rank, world, port, q):
     try:
         import torch.distributed as dist
