@@ -132,6 +132,7 @@ int decode(Cursor& c, const Header& h, TO* out, int64_t max_rows, int64_t ld) {
   const int64_t cols = h.cols > 0 ? h.cols : (h.kind == LASR_ARK_FV || h.kind == LASR_ARK_DV ? h.rows : 0);
   const bool vec = h.kind == LASR_ARK_FV || h.kind == LASR_ARK_DV;
   if (vec) {  // one row of length rows
+    if (max_rows <= 0) return 0;  // "at most max_rows rows": none
     c.pos = h.data_pos;
     if (h.kind == LASR_ARK_FV) {
       std::vector<float> buf(cols);
