@@ -463,8 +463,8 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
 }
 
 // ------------------------------- BatchNorm ---------------------------------------
-// 1024 threads = BNF_C channels x BNF_G partial-groups, combined exactly in double (fixed
-// order), then one thread per channel finalises.
+// 1024 threads = BNF_C channels x BNF_G partial-groups, combined in double by a fixed
+// pairwise tree, then one thread per channel finalises.
 constexpr int BNF_C = 16, BNF_G = 1024 / BNF_C;
 __global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
     const float* stats, int nparts, int C, float eps, float momentum, const float* gamma,
@@ -498,10 +498,16 @@ __global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
   sn[ty][tx] = n;
   smu[ty][tx] = s;
   __syncthreads();
-  n = 0.0;
-  s = 0.0;
-#pragma unroll
-  for (int g = 0; g < BNF_G; ++g) { n += sn[g][tx]; s += smu[g][tx]; }
+  // fixed pairwise tree over the partial groups (6 LDS steps instead of a 64-long chain)
+  for (int w = BNF_G / 2; w >= 1; w >>= 1) {
+    if (ty < w) {
+      sn[ty][tx] += sn[ty + w][tx];
+      smu[ty][tx] += smu[ty + w][tx];
+    }
+    __syncthreads();
+  }
+  n = sn[0][tx];
+  s = smu[0][tx];
   const double mu = n > 0.0 ? s / n : 0.0;
   double m2 = 0.0;
   if (c < C)
@@ -512,10 +518,12 @@ __global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
     }
   sm2[ty][tx] = m2;
   __syncthreads();
+  for (int w = BNF_G / 2; w >= 1; w >>= 1) {
+    if (ty < w) sm2[ty][tx] += sm2[ty + w][tx];
+    __syncthreads();
+  }
   if (ty != 0 || c >= C) return;
-  m2 = 0.0;
-#pragma unroll
-  for (int g = 0; g < BNF_G; ++g) m2 += sm2[g][tx];
+  m2 = sm2[0][tx];
   const float var = (float)(m2 / n);
   const float rs = rsqrtf(var + eps);
   mean[c] = (float)mu;
