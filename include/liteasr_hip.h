@@ -122,46 +122,6 @@ int lasr_gemm_force_ksub(int ksub);
  * them (lasr_reduce_multi). */
 int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* stream);
 
-/* FFN data gradient through the activation with the gate recomputed (liteasr/nets/
- * feed_forward.py:18-19 backward): dz = (gb @ W2) * act'(ln @ W1^T + b1) * keep * scale,
- * keep / scale = the fc1 forward's dropout draws (lasr_gemm epilogue, element m*F + f, same
- * (p1, seed1, step counter)).  The forward then stores only h = drop(act(u)).  ln, gb [M, D],
- * W1 [F, D], W2 [D, F], dz [M, F] bf16; b1 [F] fp32; D % 32 == 0, F % 128 == 0, 16-B aligned. */
-typedef struct lasr_ffn_dz_args {
-  int M, D, F, act;
-  const void* ln; const void* W1; const float* b1;
-  const void* gb; const void* W2;
-  float p1; uint64_t seed1;
-  void* dz;
-} lasr_ffn_dz_args;
-int lasr_ffn_dz(const lasr_ffn_dz_args* args, void* stream);
-/* ---- fused position-wise feed-forward chains (liteasr/nets/feed_forward.py:18-19 in the
- * Conformer residual branches, conformer_layer.py:37-47,58-66) --------------------------
- * fwd:    u = x W1^T + b1 ; z = act'(u) * keep1 (the gate) ; h = drop1(act(u)) ;
- *         out = res + res_scale * drop2(h W2^T + b2)
- *         x = LN output [M, D] bf16, z / h [M, F] bf16 (kept for the backward; F <= 2048),
- *         out [M, D] fp32 (res nullable: out = res_scale * ...).
- * bwd_dx: dz = (x W2) * z * scale1 ; dx = dz W1
- *         x = gb, the gradient of the FFN output [M, D] bf16; z = the forward's gate [M, F]
- *         bf16 in; dz [M, F] bf16 and dx [M, D] bf16 out.
- * W1 [F, D], W2 [D, F] bf16 (working copies), b1 [F], b2 [D] fp32; D in {256, 512},
- * F % 128 == 0, every pointer 16-B aligned, rows dense.  act: LASR_ACT_SWISH / _RELU.
- * Dropout masks: same (seed, step counter, element index) function as lasr_gemm's
- * epilogue (index m*F + f for drop1, m*D + n for drop2). */
-typedef struct lasr_ffn_args {
-  int M, D, F, act;
-  const void* x;
-  const void* W1; const float* b1;
-  const void* W2; const float* b2;
-  float p1; uint64_t seed1;
-  float p2; uint64_t seed2;
-  const float* res; float res_scale;
-  void* z; void* h; float* out;
-  void* dz; void* dx;
-} lasr_ffn_args;
-int lasr_ffn_fwd(const lasr_ffn_args* args, void* stream);
-int lasr_ffn_bwd_dx(const lasr_ffn_args* args, void* stream);
-
 /* Batched partial reductions (one launch for a backward node's deferred parameter
  * gradients): out[n] (+)= sum_p part[p*N + n], n < split -> out0[n], else out1[n-split].
  * Summation order per segment as the single-launch kernels (lasr_reduce_cols for P > 64,

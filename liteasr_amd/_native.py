@@ -48,22 +48,6 @@ class GemmArgs(C.Structure):
     ]
 
 
-class FfnArgs(C.Structure):
-    """Mirror of ``lasr_ffn_args``."""
-
-    _fields_ = [
-        ("M", _i), ("D", _i), ("F", _i), ("act", _i),
-        ("x", _p),
-        ("W1", _p), ("b1", _p),
-        ("W2", _p), ("b2", _p),
-        ("p1", _f), ("seed1", _u),
-        ("p2", _f), ("seed2", _u),
-        ("res", _p), ("res_scale", _f),
-        ("z", _p), ("h", _p), ("out", _p),
-        ("dz", _p), ("dx", _p),
-    ]
-
-
 class Conv2Args(C.Structure):
     """Mirror of ``lasr_conv2_args``."""
 
@@ -78,18 +62,6 @@ class Conv2Args(C.Structure):
 
 
 CONV2_FWD, CONV2_DW, CONV2_DX = 0, 1, 2
-
-
-class FfnDzArgs(C.Structure):
-    """Mirror of ``lasr_ffn_dz_args``."""
-
-    _fields_ = [
-        ("M", _i), ("D", _i), ("F", _i), ("act", _i),
-        ("ln", _p), ("W1", _p), ("b1", _p),
-        ("gb", _p), ("W2", _p),
-        ("p1", _f), ("seed1", _u),
-        ("dz", _p),
-    ]
 
 
 class CifArgs(C.Structure):
@@ -130,8 +102,6 @@ SIGNATURES = {
                          _p, _p, _p, _i, _i, _p, _p, _l, _p],
     "lasr_reduce_multi": [C.POINTER(ReduceSeg), _i, _p],
     "lasr_dropout_scale": [_f],
-    "lasr_ffn_fwd": [C.POINTER(FfnArgs), _p],
-    "lasr_ffn_bwd_dx": [C.POINTER(FfnArgs), _p],
     "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
     "lasr_layernorm2_fwd": [_p, _l, _i, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _p],
     "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],
@@ -152,7 +122,6 @@ SIGNATURES = {
     "lasr_conv1_fwd": [_p, _i, _i, _i, _i, _p, _p, _p, _i, _p],
     "lasr_conv1_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _l, _p],
     "lasr_conv2_gemm": [C.POINTER(Conv2Args), _p],
-    "lasr_ffn_dz": [C.POINTER(FfnDzArgs), _p],
     "lasr_cif_fwd": [C.POINTER(CifArgs), _p],
     "lasr_cif_bwd": [C.POINTER(CifArgs), _p],
     "lasr_glancing_mix": [_l, _i, _p, _p, _p, _p, _p, _i, _p],

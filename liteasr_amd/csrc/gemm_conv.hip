@@ -118,34 +118,3 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   }
   return LASR_OK;
 }
-
-// ============== FFN data gradient with the gate recomputed (G_FFN instance) ==============
-// dz = (gb @ W2) * act'(ln @ W1^T + b1) * keep * scale in one kernel: the fc1 product is
-// recomputed per tile (K = D, phase 1) instead of the forward storing the [M, F] gate and the
-// backward reading it back (liteasr/nets/feed_forward.py:18-19 backward).
-extern "C" int lasr_ffn_dz(const lasr_ffn_dz_args* a, void* stream) {
-  LASR_CHECK_ARG(a != nullptr, "lasr_ffn_dz: null args");
-  LASR_CHECK_ARG(a->M > 0 && a->D > 0 && a->D % 32 == 0 && a->F % 128 == 0,
-                 "lasr_ffn_dz: needs M > 0, D % 32 == 0, F % 128 == 0");
-  LASR_CHECK_ARG(a->act == LASR_ACT_SWISH || a->act == LASR_ACT_RELU || a->act == LASR_ACT_NONE,
-                 "lasr_ffn_dz: act must be SWISH, RELU or NONE");
-  LASR_CHECK_ARG(a->ln && a->W1 && a->b1 && a->gb && a->W2 && a->dz && aligned16(a->ln) && aligned16(a->W1) &&
-                     aligned16(a->b1) && aligned16(a->gb) && aligned16(a->W2) && aligned16(a->dz),
-                 "lasr_ffn_dz: null or unaligned pointer");
-  GemmP p;
-  memset(&p, 0, sizeof(p));
-  p.batch = 1; p.batch_div = 1; p.alpha = 1.f; p.res_scale = 1.f; p.split_k = 1;
-  p.M = a->M; p.N = a->F; p.K = a->D; p.kchunk = a->D;
-  p.A = a->gb; p.lda_m = a->D; p.lda_k = 1;
-  p.B = a->W2; p.ldb_n = 1; p.ldb_k = a->F;
-  p.C = a->dz; p.ldc = a->F; p.c_vec = 1; p.epi_mode = 0;
-  p.A1 = a->ln; p.lda1 = a->D; p.B1 = a->W1; p.ldb1 = a->D; p.bias1 = a->b1;
-  p.gate_act = a->act; p.k1 = a->D;
-  p.drop = mkdrop(0.f, 0);  // the epilogue stores (gb W2) * gate as is
-  p.gdrop = mkdrop(a->p1, a->seed1);
-  p.gate_scale = p.gdrop.p > 0.f ? p.gdrop.scale : 1.f;
-  dim3 grid((unsigned)(a->F / 128), (unsigned)cdiv(a->M, 128), 1);
-  LASR_CHECK_ARG(grid.y <= 65535, "lasr_ffn_dz: grid too large");
-  gemm_bf16_glds_kernel<128, 128, true, false, bf16_t, 3, 2, G_FFN><<<grid, 256, 0, (hipStream_t)stream>>>(p);
-  return lasr_check_launch("lasr_ffn_dz");
-}

@@ -25,7 +25,7 @@ struct ConvG {
   const bf16_t* zero;   // G_DX: >= 32 zero bf16 (taps that fall outside dy2)
 };
 typedef ConvG ConvGeom;
-enum { G_LIN = 0, G_FWD = 1, G_DW = 2, G_DX = 3, G_FFN = 4 };
+enum { G_LIN = 0, G_FWD = 1, G_DW = 2, G_DX = 3 };
 
 struct GemmP {
   int M, N, K, batch, batch_div;
@@ -67,19 +67,6 @@ struct GemmP {
   int v4;  // direct epilogue: 4-wide C/zout/aux/res/bias/ws access allowed (host-checked)
   int zout_mode;  // 0: zout = pre-activation; 1: zout = act'(pre-activation) * keep (gate)
   ConvGeom cv;    // implicit-GEMM instances of the subsampling conv2 only (G != 0)
-  // G_FFN (FFN data gradient with the gate recomputed): phase 1 accumulates
-  // u = A1 @ B1^T over k1 (A1 [M, k1], B1 [N, k1], both K-contiguous), the gate
-  // act'(u + bias1) * keep(drop) * gate_scale stays in registers; phase 2 accumulates A @ B
-  // (B N-contiguous) and the epilogue stores (A @ B) * gate.
-  const void* A1;
-  int64_t lda1;
-  const void* B1;
-  int64_t ldb1;
-  const float* bias1;
-  int gate_act;
-  int k1;
-  float gate_scale;
-  DropCfg gdrop;  // the gate's dropout draws (the epilogue's own `drop` stays off)
 };
 
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
@@ -648,41 +635,6 @@ struct ConvRowsDW {  // G_DW B operand: tile [32 k][R_TILE n] of im2col(y1), k =
   }
 };
 
-// G_FFN phase boundary: acc holds u = A1 @ B1^T as C^T fragments (lane: row (l & 15), four
-// consecutive columns 4 (l >> 4) + e).  gate = act'(u + bias1) * keep * gate_scale, with the
-// forward's dropout keep draws (element index m * N + n, the fc1 epilogue's); acc is cleared
-// for phase 2.
-template <int BM, int BN>
-LASR_DEV void ffn_gate(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], f32x4 (&gate)[BM / 32][BN / 32], int m0,
-                       int n0, int wr, int wc, int lane) {
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  const bool drop = p.gdrop.p > 0.f;
-  const uint32_t key = drop ? drop_key(p.gdrop) : 0u;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wc * WN + j * 16 + 4 * (lane >> 4);
-    float b[4];
-    ldv<4>(p.bias1 + n, b);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wr * WM + i * 16 + (lane & 15);
-      const uint32_t km = drop ? drop_keep_mask<4>(p.gdrop, key, (uint64_t)m * p.N + n) : 0xFu;
-      f32x4 g;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float u = acc[i][j][e] + b[e];
-        float d;
-        if (p.gate_act == LASR_ACT_SWISH) d = swish_grad(u);
-        else if (p.gate_act == LASR_ACT_RELU) d = u > 0.f ? 1.f : 0.f;
-        else d = 1.f;
-        g[e] = (km >> e) & 1u ? d * p.gate_scale : 0.f;
-      }
-      gate[i][j] = g;
-      acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-  }
-}
-
 // KS: 32-deep k sub-tiles per ring stage (G_LIN only).  KS = 2 makes the stage 64 deep: one
 // counted wait + barrier per 64 k and twice the DMA bytes per issue (the guide's "fix BK first").
 // XCD-aware (bijective) remap of tile `orig` among `nwg` tiles: tiles that share an XCD (the
@@ -697,7 +649,7 @@ LASR_DEV int xcd_remap(int orig, int nwg) {
 template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int G, int KS>
 LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const int zz) {
   static_assert(G == G_LIN || (G == G_DW ? (!AKC && !BKC) : (AKC && (G == G_FWD) == BKC)),
-                "gather / FFN instance operand orientation");
+                "gather instance operand orientation");
   static_assert(KS == 1 || (KS == 2 && G == G_LIN), "k sub-tiles: generic instances only");
   constexpr int BK = 32;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
@@ -729,9 +681,7 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
 
   // full 32-deep tiles go through the glds ring; a ragged last tile is handled after the
   // loop (ordinary loads inside the loop would make hipcc drain the ring with vmcnt(0))
-  // G_FFN: k1/32 phase-1 tiles, then K/32 phase-2 tiles (host-checked multiples of 32)
-  const int nk1 = G == G_FFN ? p.k1 / BK : 0;
-  const int nfull = ((kend - kbeg) > 0 ? (kend - kbeg) / BK : 0) + nk1;
+  const int nfull = (kend - kbeg) > 0 ? (kend - kbeg) / BK : 0;
   [[maybe_unused]] ConvRowsKC<BM> ga;
   [[maybe_unused]] ConvRowsDW<BN> gb;
   if constexpr (G == G_FWD) ga.init_fwd(p.cv, m0, p.M, tid);
@@ -746,14 +696,6 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
       for (int u = 0; u < KS; ++u) {
         glds_tile<BM, AKC>(A, lda, m0, p.M, k0 + u * BK, dst + u * TILE, tid);
         glds_tile<BN, BKC>(B, ldb, n0, p.N, k0 + u * BK, dst + u * TILE + BM * BK, tid);
-      }
-    } else if constexpr (G == G_FFN) {
-      if (t < nk1) {
-        glds_tile<BM, true>((const bf16_t*)p.A1, p.lda1, m0, p.M, t * BK, dst, tid);
-        glds_tile<BN, true>((const bf16_t*)p.B1, p.ldb1, n0, p.N, t * BK, dst + BM * BK, tid);
-      } else {
-        glds_tile<BM, true>(A, lda, m0, p.M, (t - nk1) * BK, dst, tid);
-        glds_tile<BN, false>(B, ldb, n0, p.N, (t - nk1) * BK, dst + BM * BK, tid);
       }
     } else if constexpr (G == G_FWD) {
       const int C = p.cv.C, tap = k0 / C, kh = tap / 3, kw = tap - 3 * kh;
@@ -773,7 +715,7 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
       glds_tile<BN, false>(B + (kh * 3 + kw) * C, ldb, n0, p.N, cin, dst + BM * BK, tid);
     }
   };
-  auto compute = [&](const bf16_t* cur, bool b_kc = false) {
+  auto compute = [&](const bf16_t* cur) {
     bf16x8 af[FM], bfr[FN];
     v2i ra[2 * FM], rb[2 * FN];
 #pragma unroll
@@ -781,30 +723,17 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
       if constexpr (AKC) af[i] = frag<BM, true>(cur, wr * WM + i * 16, lane);
       else frag_tr_raw<BM>(cur, wr * WM + i * 16, lane, ra + 2 * i);
     }
-    if constexpr (G == G_FFN) {  // phase 1 reads a K-contiguous B image
-      if (b_kc) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = frag<BN, true>(cur + BM * BK, wc * WN + j * 16, lane);
-      } else {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) frag_tr_raw<BN>(cur + BM * BK, wc * WN + j * 16, lane, rb + 2 * j);
-        tie_lgkm<2 * FN>(rb);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = frag_from_raw(rb + 2 * j);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if constexpr (BKC) bfr[j] = frag<BN, true>(cur + BM * BK, wc * WN + j * 16, lane);
-        else frag_tr_raw<BN>(cur + BM * BK, wc * WN + j * 16, lane, rb + 2 * j);
-      }
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (BKC) bfr[j] = frag<BN, true>(cur + BM * BK, wc * WN + j * 16, lane);
+      else frag_tr_raw<BN>(cur + BM * BK, wc * WN + j * 16, lane, rb + 2 * j);
     }
     if constexpr (!AKC) {
       tie_lgkm<2 * FM>(ra);
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[i] = frag_from_raw(ra + 2 * i);
     }
-    if constexpr (!BKC && G != G_FFN) {
+    if constexpr (!BKC) {
       tie_lgkm<2 * FN>(rb);
 #pragma unroll
       for (int j = 0; j < FN; ++j) bfr[j] = frag_from_raw(rb + 2 * j);
@@ -833,19 +762,13 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   for (int t = 0; t < S - 1; ++t)
     if (t < nst) issue(t);
 
-  [[maybe_unused]] f32x4 gate[G == G_FFN ? FM : 1][G == G_FFN ? FN : 1];
   for (int kt = 0; kt < nst; ++kt) {
     const int after = min(S - 2, nst - 1 - kt);  // stages issued after kt (still in flight)
     wait_ring<S, GL * KS>(after);
     lds_barrier();
     if (kt + S - 1 < nst) issue(kt + S - 1);
-    if constexpr (G == G_FFN) {
-      compute(smem + (kt % S) * STAGE, kt < nk1);
-      if (kt == nk1 - 1) ffn_gate<BM, BN>(p, acc, gate, m0, n0, wr, wc, lane);
-    } else {
 #pragma unroll
-      for (int u = 0; u < KS; ++u) compute(smem + (kt % S) * STAGE + u * TILE);
-    }
+    for (int u = 0; u < KS; ++u) compute(smem + (kt % S) * STAGE + u * TILE);
     if constexpr (!AKC)
       if (do_rs)
 #pragma unroll
@@ -863,12 +786,6 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
       if constexpr (!AKC)
         if (do_rs) rowsum_tile<BM>(smem, tid, rs);
     }
-  }
-  if constexpr (G == G_FFN) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] *= gate[i][j];
   }
   if (G == G_LIN && nfull < nk) {  // ragged tail: register loader with zero fill (conv: host-checked K % 32 == 0)
     __syncthreads();

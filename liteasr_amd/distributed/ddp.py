@@ -45,10 +45,16 @@ class FlatReducer:
         self.world = dist.get_world_size(process_group)
         self.enabled = True
         units = self._units()
-        # buckets in backward order: group consecutive units until >= bucket_bytes
+        # buckets in backward order: group consecutive units until >= bucket_bytes; a bucket
+        # is one contiguous slice of the flat buffer, so a unit that does not touch the
+        # bucket's current range (the Paraformer's heads sit after its decoder in memory
+        # but complete before the encoder) starts a new bucket
         self.buckets: List[List[_Unit]] = []
         cur, size = [], 0
         for u in units:
+            if cur and not (u.lo == max(v.hi for v in cur) or u.hi == min(v.lo for v in cur)):
+                self.buckets.append(cur)
+                cur, size = [], 0
             cur.append(u)
             size += (u.hi - u.lo) * 4
             if size >= bucket_bytes:
@@ -69,16 +75,15 @@ class FlatReducer:
             if isinstance(mod, _Bound):
                 mod._ready_hook = self._on_ready
         model.encoder._after_norm_hook = self._on_ready
+        model._unit_hook = self._on_ready  # units that are not _Bound modules (model.unit_ready)
 
     def _units(self):
-        """Hook units (module prefix -> flat range) in the order backward completes them."""
-        st, m = self.store, self.model
-        enc, dec = m.encoder, m.decoder
-        order = [("ctc", m.ctc), ("decoder", dec), ("encoder.after_norm", None)]
-        order += [(l._pfx, l) for l in reversed(list(enc.enc_layers))]
-        order += [("encoder.embed", enc.embed)]
+        """Hook units (module prefix -> flat range) in the order backward completes them;
+        the model names them (``reducer_units``: U2's CTC head / decoder / encoder, the
+        Paraformer's decoder / embedding / predictor / encoder)."""
+        st = self.store
         units, covered = [], set()
-        for name, _ in order:
+        for name in self.model.reducer_units():
             names = [n for n in st.names if n == name or n.startswith(name + ".")]
             assert names, name
             lo = min(st.offsets[n] for n in names)
@@ -141,7 +146,6 @@ class FlatReducer:
         return self.store.grad[lo:hi]
 
     def _launch(self, bi):
-        K.join_side()  # node-end gradient work forked to the side stream (kernels.py)
         g = self._slice(self.buckets[bi])
         if g.is_cuda and dist.get_backend(self.pg) == "nccl":
             w = dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)

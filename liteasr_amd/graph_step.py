@@ -83,7 +83,6 @@ class GraphedTrainStep:
     def _fwd_bwd(self):
         loss = self.crit(self.model, *self.static)
         loss.backward()
-        K.join_side()
         return loss
 
     def _update(self):
@@ -159,7 +158,6 @@ class GraphedTrainStep:
                         g = torch.cuda.CUDAGraph()
                         with torch.cuda.graph(g, pool=pool, capture_error_mode=_MODE):
                             out = fn()
-                            K.join_side()  # a capture must rejoin every stream it forked
                         if i == 0:
                             self.loss = out
                             pool = g.pool()

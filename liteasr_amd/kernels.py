@@ -134,40 +134,6 @@ def _flush_gemm_group():
     # the operand references in q die here, after the launches were enqueued
 
 
-# Side stream: the node-end work of a backward node (its grouped dW GEMMs and the
-# reduction launch) only produces parameter gradients, which nothing reads until the
-# optimizer / the DDP bucket exchange, so it is forked to a second stream and overlaps the
-# next node's backward.  join_side() makes the current stream wait for it (optimizer, DDP
-# bucket launch, end of the backward, end of a captured graph segment); the tensors it
-# touches stay referenced until then.  Opt-in (LASR_SIDE_STREAM=1): measured slower on
-# MI355X, 13.64 vs 13.08 ms per graphed small-config step (the forked dW groups and the next
-# node's GEMMs contend for the same CUs and L2).
-SIDE_STREAM = os.environ.get("LASR_SIDE_STREAM", "0") == "1"
-_SIDE = {}
-_KEEP = []
-_PENDING = [False]
-
-
-def _side_stream(device):
-    idx = torch.device(device).index
-    if idx is None:
-        idx = torch.cuda.current_device()
-    if idx not in _SIDE:
-        _SIDE[idx] = torch.cuda.Stream(device=idx)
-    return _SIDE[idx]
-
-
-def join_side():
-    """The current stream waits for the node-end work forked to the side stream(s)."""
-    if _PENDING[0]:
-        cur = torch.cuda.current_stream()
-        for st in _SIDE.values():
-            if st.device == cur.device:
-                cur.wait_stream(st)
-        _PENDING[0] = False
-        _KEEP.clear()
-
-
 def _flush_node_end(segs):
     if _DEFER.gemms:
         _flush_gemm_group()
@@ -181,17 +147,6 @@ def _flush_node_end(segs):
 def flush_reductions():
     segs, _DEFER.segs = _DEFER.segs, []
     if not segs and not _DEFER.gemms:
-        return
-    dev = segs[0][0].device if segs else _DEFER.gemms[0][2][0].device
-    if SIDE_STREAM and dev.type == "cuda":
-        keep = [t for seg in segs for t in seg[:5] if isinstance(t, torch.Tensor)]
-        keep += [t for _, _, refs in _DEFER.gemms for t in refs]
-        side = _side_stream(dev)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            _flush_node_end(segs)
-        _KEEP.extend(keep)
-        _PENDING[0] = True
         return
     _flush_node_end(segs)
     # the partial buffers are released here; the caching allocator hands their memory only
@@ -316,7 +271,9 @@ def gemm(
             # partials-only launch (split_k = -1) into a buffer that lives until the flush
             nrs = sp * M if rowsum is not None else 0
             part = torch.empty(sp * M * Nn + nrs, dtype=torch.float32, device=c.device)
-            args.split_k = -sp if grouped else -1
+            # the explicit slice count on both paths: `part` is sized for sp slices, and a
+            # re-derived auto split (-1) could differ from sp after the group adjustment
+            args.split_k = -sp
             args.workspace, args.workspace_bytes = ptr(part), part.numel() * 4
             if grouped:
                 key = _GROUP_TILES[(tm.value, tn.value)]
@@ -345,50 +302,6 @@ def linear(x, w, out, bias=None, **kw):
 def dropout_scale(p: float) -> float:
     """Multiplier of kept elements at drop probability p (1 when p <= 0)."""
     return float(N.load().lasr_dropout_scale(float(p))) if p > 0 else 1.0
-
-
-# --------------------------------------------------------- fused FFN chains ---
-def ffn_supported(x, W1):
-    """Shapes / dtypes the fused chains (ffn.hip) take: bf16, D in {256, 512}, F % 128 == 0."""
-    F, D = W1.shape
-    return x.dtype == torch.bfloat16 and D in (256, 512) and F % 128 == 0 and F <= 2048
-
-
-def _ffn_args(M, D, F, act, x, W1, W2, **kw):
-    for t in (x, W1, W2):
-        assert t.is_contiguous() and t.dtype == torch.bfloat16, "ffn operands: contiguous bf16"
-    a = N.FfnArgs()
-    a.M, a.D, a.F, a.act = M, D, F, act
-    a.x, a.W1, a.W2 = ptr(x), ptr(W1), ptr(W2)
-    a.b1, a.b2 = ptr(kw.get("b1")), ptr(kw.get("b2"))
-    a.p1, a.seed1 = float(kw.get("p1", 0.0)), int(kw.get("seed1", 0)) & 0xFFFFFFFFFFFFFFFF
-    a.p2, a.seed2 = float(kw.get("p2", 0.0)), int(kw.get("seed2", 0)) & 0xFFFFFFFFFFFFFFFF
-    a.res, a.res_scale = ptr(kw.get("res")), float(kw.get("res_scale", 1.0))
-    for k in ("z", "h", "out", "dz", "dx"):
-        setattr(a, k, ptr(kw.get(k)))
-    return a
-
-
-def ffn_fwd(ln, W1, b1, W2, b2, act, p1, seed1, res, res_scale, p2, seed2, z, h, out):
-    """z = ln W1^T + b1; h = drop1(act(z)); out = res + res_scale * drop2(h W2^T + b2)
-    in one launch (lasr_ffn_fwd); the [M, F] intermediate never round-trips HBM."""
-    M, D = ln.shape
-    F = W1.shape[0]
-    assert W1.shape == (F, D) and W2.shape == (D, F) and z.shape == h.shape == (M, F) and out.shape == (M, D)
-    assert out.dtype == torch.float32 and (res is None or (res.dtype == torch.float32 and res.is_contiguous()))
-    a = _ffn_args(M, D, F, act, ln, W1, W2, b1=b1, b2=b2, p1=p1, seed1=seed1, p2=p2, seed2=seed2,
-                  res=res, res_scale=res_scale, z=z, h=h, out=out)
-    N.call("lasr_ffn_fwd", C.byref(a), stream())
-
-
-def ffn_bwd_dx(gb, W1, W2, z, act, p1, seed1, dz, dx):
-    """dz = (gb W2) * act'(z) * drop1; dx = dz W1 in one launch (lasr_ffn_bwd_dx)."""
-    M, D = gb.shape
-    F = W1.shape[0]
-    assert W1.shape == (F, D) and W2.shape == (D, F) and z.shape == dz.shape == (M, F) and dx.shape == (M, D)
-    assert z.is_contiguous() and dz.is_contiguous() and dx.is_contiguous() and dx.dtype == torch.bfloat16
-    a = _ffn_args(M, D, F, act, gb, W1, W2, p1=p1, seed1=seed1, z=z, dz=dz, dx=dx)
-    N.call("lasr_ffn_bwd_dx", C.byref(a), stream())
 
 
 def colsum(x2d: torch.Tensor, out: torch.Tensor, accumulate=True):
@@ -824,18 +737,3 @@ def glancing_mix(replace, a, b, out, out2=None, backward=False):
     rows, D = out.shape
     N.call("lasr_glancing_mix", rows, D, ptr(replace), ptr(a), ptr(b), ptr(out), ptr(out2), int(backward),
            stream())
-
-
-def ffn_dz(ln, W1, b1, gb, W2, act, p1, seed1, dz):
-    """dz = (gb @ W2) * act'(ln @ W1^T + b1) * keep * scale (lasr_ffn_dz; the fc1 forward's
-    dropout draws for (p1, seed1))."""
-    M, D = ln.shape
-    F_ = W1.shape[0]
-    for t in (ln, W1, gb, W2, dz):
-        assert t.dtype == torch.bfloat16 and t.is_contiguous()
-    assert tuple(W2.shape) == (D, F_) and tuple(gb.shape) == (M, D) and tuple(dz.shape) == (M, F_)
-    a = N.FfnDzArgs()
-    a.M, a.D, a.F, a.act = M, D, F_, act
-    a.ln, a.W1, a.b1, a.gb, a.W2 = ptr(ln), ptr(W1), ptr(b1), ptr(gb), ptr(W2)
-    a.p1, a.seed1, a.dz = p1, int(seed1) & 0xFFFFFFFFFFFFFFFF, ptr(dz)
-    N.call("lasr_ffn_dz", C.byref(a), stream())

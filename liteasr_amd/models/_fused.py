@@ -83,6 +83,26 @@ class FusedEncoderModel(LiteasrModel):
     def flat_parameters(self):
         return self.store
 
+    # ------------------------------------------------------ data-parallel units
+    _unit_hook = None
+
+    def reducer_units(self):
+        """Parameter-prefix units in the order the fused backward completes them (the
+        bucket order of distributed.ddp.FlatReducer): the heads, then the encoder top-down.
+        Every name must fire a ready hook (a _Bound module's on_grads_ready, the encoder's
+        after_norm_ready, or unit_ready)."""
+        enc = self.encoder
+        return (self._head_units() + ["encoder.after_norm"] + [l._pfx for l in reversed(list(enc.enc_layers))]
+                + ["encoder.embed"])
+
+    def _head_units(self):
+        return ["ctc", "decoder"]
+
+    def unit_ready(self, name):
+        """A reducer unit that is not a _Bound module has its gradients complete."""
+        if self._unit_hook is not None:
+            self._unit_hook(name)
+
     # ------------------------------------------------------------- bookkeeping
     def get_pred_len(self, xlens) -> Tensor:
         """liteasr/models/u2.py:319-321."""

@@ -94,6 +94,10 @@ class Paraformer(FusedEncoderModel):
         self.last_glance = None
         self._finalize()
 
+    def _head_units(self):
+        """ParaformerHeadsFn.backward order: decoder, target embedding, predictor."""
+        return ["decoder", "embed", "predictor"]
+
     def embed_weight(self):
         return self.store.view("embed.weight")
 

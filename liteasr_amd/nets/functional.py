@@ -57,79 +57,30 @@ def ln_forward(x, g, b, adt, y2=False, p2=0.0, seed2=0):
     return y, yd, mean, rstd
 
 
-# The single-launch FFN chains of ffn.hip: correct (tests/test_kernels_gpu.py::
-# test_ffn_fused_chains) but slower than the two GEMMs at the step's shapes,
-# so off unless LASR_FUSED_FFN=1.
-FUSED_FFN = os.environ.get("LASR_FUSED_FFN", "0") == "1"
-
-
-def _fused_ffn(x, W1):
-    return FUSED_FFN and K.ffn_supported(x, W1)
-
-
-# FFN data gradient with the gate recomputed (lasr_ffn_dz): the forward stores only h and the
-# backward recomputes u = ln W1^T per tile instead of writing and re-reading an [M, F] gate.
-# Correct (tests/test_kernels_gpu.py::test_ffn_dz_recomputed_gate) but slower at the step's
-# shapes (60 us vs 33.5 us for the stored-gate dX GEMM), so opt-in with
-# LASR_FFN_GATE_RECOMPUTE=1.
-GATE_STORE = os.environ.get("LASR_FFN_GATE_RECOMPUTE", "0") != "1"
-
-
-class _GateRecompute:
-    """ffn_forward's stand-in for the stored gate: the backward recomputes it from ln, W1, b1."""
-
-    __slots__ = ("b1",)
-
-    def __init__(self, b1):
-        self.b1 = b1
-
-
-def _recompute_gate(ln, W1):
-    M, D = ln.shape
-    F_ = W1.shape[0]
-    return (not GATE_STORE and ln.dtype == torch.bfloat16 and D % 32 == 0 and F_ % 128 == 0
-            and ln.is_contiguous() and W1.is_contiguous())
-
-
 def ffn_forward(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res):
-    """Returns (out, g, h).  g is what the backward needs for act' and the dropout keep:
-    either the stored gate act'(u) * keep (fc1 epilogue, zout_mode 1; fp32 build) or a
-    _GateRecompute marker (bf16 build: lasr_ffn_dz recomputes u in the backward)."""
+    """Returns (out, g, h).  g is the gate act'(u) * keep the backward needs, stored in the
+    compute dtype by the fc1 epilogue (zout_mode 1): h = drop(act(u)) and g come out of the
+    same launch, and the backward's dz GEMM multiplies by g (no recompute of u)."""
     M = ln.shape[0]
     dev, adt = ln.device, ln.dtype
     h = _e((M, W1.shape[0]), adt, dev)
     out = _e((M, W2.shape[0]), F32, dev)
-    if _fused_ffn(ln, W1):  # one launch: the [M, F] intermediate stays on chip (ffn.hip)
-        g = _e((M, W1.shape[0]), adt, dev)
-        K.ffn_fwd(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res, g, h, out)
-        return out, g, h
-    if _recompute_gate(ln, W1):
-        g = _GateRecompute(b1)
-        K.linear(ln, W1, h, bias=b1, act=act, drop_p=p_ff, drop_seed=s_ff)
-    else:
-        g = _e((M, W1.shape[0]), adt, dev)
-        K.linear(ln, W1, h, bias=b1, act=act, zout=g, zout_mode=1, drop_p=p_ff, drop_seed=s_ff)
+    g = _e((M, W1.shape[0]), adt, dev)
+    K.linear(ln, W1, h, bias=b1, act=act, zout=g, zout_mode=1, drop_p=p_ff, drop_seed=s_ff)
     K.linear(h, W2, out, bias=b2, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res)
     return out, g, h
 
 
 def ffn_backward(gb, ln, g, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
     """gb: gradient of the FFN output (after the residual-branch dropout/scale); g: the
-    forward's gate act'(z) * keep, or the marker to recompute it."""
+    forward's stored gate act'(z) * keep."""
     M = gb.shape[0]
     dev, adt = gb.device, gb.dtype
     K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0, rowsum=gb2, group=True)
     dz = _e((M, W1.shape[0]), adt, dev)
     dln = _e((M, W1.shape[1]), adt, dev)
-    if isinstance(g, _GateRecompute):
-        K.ffn_dz(ln, W1, g.b1, gb, W2, act, p_ff, s_ff, dz)
-    elif _fused_ffn(gb, W1):  # dz and dln in one launch (ffn.hip)
-        K.ffn_bwd_dx(gb, W1, W2, g, act, p_ff, s_ff, dz, dln)
-        K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1, group=True)
-        return dln
-    else:
-        # dz = (gb W2) * scale * g: the dropout scale as alpha, the gate as aux
-        K.gemm(gb, W2, dz, alpha=K.dropout_scale(p_ff), aux=g, aux_act=ACT_GATE)
+    # dz = (gb W2) * scale * g: the dropout scale as alpha, the gate as aux
+    K.gemm(gb, W2, dz, alpha=K.dropout_scale(p_ff), aux=g, aux_act=ACT_GATE)
     K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1, group=True)
     K.gemm(dz, W1, dln)
     return dln
@@ -464,9 +415,9 @@ def conv_backward(gb, ln, sv, w, g, env):
 
 
 def _conv2_implicit(adt, C):
-    """conv2 on the implicit-GEMM instances (bf16 build, C % 128 == 0); LASR_CONV2_IM2COL=1
-    keeps the explicit im2col path (A/B measurements)."""
-    return adt == torch.bfloat16 and C % 128 == 0 and os.environ.get("LASR_CONV2_IM2COL", "0") != "1"
+    """conv2 on the implicit-GEMM instances (bf16 build, C % 128 == 0); the fp32 parity build
+    and other widths take explicit im2col + the GEMM."""
+    return adt == torch.bfloat16 and C % 128 == 0
 
 
 # ============================================================ autograd nodes ====
@@ -542,7 +493,6 @@ class EmbedFn(torch.autograd.Function):
             K.gemm(dy2, w.W2p, dcol)
             K.col2im(dcol, sv.y1, dy1)
         K.conv1_bwd(sv.xs, dy1, g.W1, g.b1)
-        K.join_side()  # end of the backward: every gradient complete on the current stream
         mod.on_grads_ready()
         return None, None, None, None
 
@@ -892,6 +842,7 @@ class ParaformerHeadsFn(torch.autograd.Function):
         g_emb, g_cif = _e((R, d), F32, dev), _e((R, d), F32, dev)
         K.glancing_mix(sv.rep, dmix, None, g_emb, g_cif, backward=True)
         K.embed_bwd(sv.ys_in, g_emb, math.sqrt(d), model.embed_grad(), sv.p_pos, env.seed + 5)
+        model.unit_ready("embed")
         # ---- CIF backward -> predictor logits / encoder output
         dz = _e(M, F32, dev)
         dh_cif = _e((B, T, d), F32, dev)

@@ -56,7 +56,6 @@ class Adam(LiteasrOptimizer):
 
     def clip_and_step(self, max_norm: float):
         """clip_grad_norm_(max_norm) + NaN-skip + Adam step, fused, no host sync."""
-        K.join_side()  # gradient reductions still running on the side stream
         mode, lr, factor, dim, warm = self._lr_args()
         g = self.param_groups[0]
         b1, b2 = g["betas"]
@@ -67,7 +66,6 @@ class Adam(LiteasrOptimizer):
         self.clip_and_step(self.max_norm)
 
     def zero_grad(self):
-        K.join_side()
         grad = self.store.ensure_grad()
         K.fill(grad, 0.0)
 

@@ -180,3 +180,90 @@ def test_bench_spawns_one_process_per_rank():
     import bench
 
     assert bench.spawn_ranks(3, argv=["--x", "1"], target=_spawn_target) == 0
+
+
+def _tiny_paraformer():
+    from liteasr_amd.models.paraformer import Paraformer, ParaformerConfig
+    from liteasr_amd.utils.cfg import resolve_self
+
+    c = ParaformerConfig(input_dim=40, vocab_size=20, enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_layers=2,
+                         dec_dim=32, dec_ff_dim=64, dec_attn_heads=4, dec_layers=2)
+    resolve_self(c)
+    return Paraformer(c)
+
+
+def _fire_units(model, rank):
+    """Stand-in backward: every reducer unit gets (rank+1)*(i+1) and fires its hook the way
+    the fused nodes do (_Bound.on_grads_ready, encoder.after_norm_ready, model.unit_ready)."""
+    from liteasr_amd.nets.modules import _Bound
+
+    st = model.store
+    grad = st.ensure_grad()
+    mods = {m._pfx: m for m in model.modules() if isinstance(m, _Bound)}
+    for i, name in enumerate(model.reducer_units()):
+        for n in st.names:
+            if n == name or n.startswith(name + "."):
+                o, k = st.offsets[n], st.shapes[n].numel()
+                grad[o:o + k] += (rank + 1) * (i + 1)
+        if name == "encoder.after_norm":
+            model.encoder.after_norm_ready()
+        elif name in mods:
+            mods[name].on_grads_ready()
+        else:
+            model.unit_ready(name)
+
+
+def _paraformer_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from liteasr_amd.distributed.ddp import DistributedDataParallel
+
+        torch.manual_seed(200 + rank)
+        model = _tiny_paraformer()
+        ddp = DistributedDataParallel(model, bucket_cap_mb=0.02)
+        red = ddp.reducer
+        model.store.ensure_grad().zero_()
+        red._reset()
+        red.record = []
+        _fire_units(model, rank)
+        rec = list(red.record)
+        for bi in red.record:
+            red.launch(bi)
+        red.record = None
+        red.wait()
+        q.put((rank, {"units": model.reducer_units(), "nbuckets": len(red.buckets), "record": rec,
+                      "grad": model.store.grad.numpy().copy(), "flat": model.store.flat.numpy().copy()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flat_ddp_paraformer_gloo_world2():
+    """DDP over the Paraformer (predictor, target embedding, no CTC head): every
+    parameter sits in a reducer unit, every unit's hook completes its bucket, gradients
+    average over the two ranks."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_paraformer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a, b = out[0], out[1]
+    assert a["units"][:4] == ["decoder", "embed", "predictor", "encoder.after_norm"]
+    assert a["nbuckets"] >= 2 and a["record"] == list(range(a["nbuckets"]))
+    assert (a["flat"] == b["flat"]).all()
+    g = torch.from_numpy(a["grad"])
+    assert torch.equal(g, torch.from_numpy(b["grad"]))
+    nz = g[g != 0]
+    assert nz.numel() == g.numel() - int((g == 0).sum())
+    assert torch.allclose(nz / 1.5, torch.round(nz / 1.5))  # ((0+1) i + (1+1) i) / 2

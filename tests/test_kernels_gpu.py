@@ -1072,101 +1072,3 @@ def test_ctc_against_reference_golden_full_size(name):
     err_ours = (gg - g64).abs().max().item() / m
     assert err_ours <= max(2e-3, 1.5 * err_ref), (err_ours, err_ref)
     close(gg, gold, err_ref + err_ours + 1e-6, "ctc grad vs reference golden")
-
-
-@pytest.mark.parametrize("M,D,F,act,p", [(77, 256, 2048, "swish", 0.1), (200, 256, 2048, "swish", 0.0),
-                                         (33, 256, 512, "relu", 0.1), (96, 512, 2048, "swish", 0.1),
-                                         (64, 512, 1024, "relu", 0.0), (1312, 256, 2048, "relu", 0.1)])
-def test_ffn_fused_chains(M, D, F, act, p):
-    """ffn.hip (one launch per direction) vs the two-GEMM path it replaces (same kernels'
-    epilogue semantics: bias, gate act'(u) * keep, Swish/ReLU, dropout index m*F+f /
-    m*D+n, residual; gate aux with the dropout scale), and vs a float64 reference at p = 0.
-    Rows not a multiple of the 32-row block exercise the clamped tail."""
-    from liteasr_amd import _native as Nn
-    from liteasr_amd._native import ACT_RELU, ACT_SWISH
-
-    kn = K()
-    a = ACT_SWISH if act == "swish" else ACT_RELU
-    g = torch.Generator().manual_seed(M + D + F)
-    bf = torch.bfloat16
-    ln = torch.randn(M, D, generator=g).to(bf)
-    W1 = (torch.randn(F, D, generator=g) * D ** -0.5).to(bf)
-    b1 = torch.randn(F, generator=g) * 0.1
-    W2 = (torch.randn(D, F, generator=g) * F ** -0.5).to(bf)
-    b2 = torch.randn(D, generator=g) * 0.1
-    res = torch.randn(M, D, generator=g)
-    gb = torch.randn(M, D, generator=g).to(bf)
-    d = lambda t: t.to(DEV).contiguous()
-    ln_d, W1_d, W2_d, b1_d, b2_d, res_d, gb_d = map(d, (ln, W1, W2, b1, b2, res, gb))
-    z = torch.empty(M, F, dtype=bf, device=DEV)
-    h = torch.empty_like(z)
-    out = torch.empty(M, D, device=DEV)
-    kn.ffn_fwd(ln_d, W1_d, b1_d, W2_d, b2_d, a, p, 11, res_d, 0.5, p, 12, z, h, out)
-    z2, h2, out2 = torch.empty_like(z), torch.empty_like(h), torch.empty_like(out)
-    kn.linear(ln_d, W1_d, h2, bias=b1_d, act=a, zout=z2, zout_mode=1, drop_p=p, drop_seed=11)
-    kn.linear(h2, W2_d, out2, bias=b2_d, res=res_d, res_scale=0.5, drop_p=p, drop_seed=12)
-    torch.cuda.synchronize()
-    assert torch.equal(z, z2), "gate differs from the fc1 GEMM's zout_mode-1 output"
-    assert torch.equal(h, h2), "activation / dropout differs from the fc1 GEMM epilogue"
-    close(out, out2, 2e-5, "ffn out vs two-GEMM path")  # chunk-rotated sum order
-    dz = torch.empty_like(z)
-    dx = torch.empty(M, D, dtype=bf, device=DEV)
-    kn.ffn_bwd_dx(gb_d, W1_d, W2_d, z, a, p, 11, dz, dx)
-    dz2, dx2 = torch.empty_like(dz), torch.empty_like(dx)
-    kn.gemm(gb_d, W2_d, dz2, alpha=kn.dropout_scale(p), aux=z2, aux_act=Nn.ACT_GATE)
-    kn.gemm(dz2, W1_d, dx2)
-    torch.cuda.synchronize()
-    assert torch.equal(dz, dz2), "dz differs from the dX GEMM with activation-gradient aux"
-    close(dx, dx2, 1e-2, "ffn dx vs two-GEMM path")  # bf16 output: last-bit rounding only
-    if p == 0.0:
-        x64 = ln.double()
-        z64 = x64 @ W1.double().t() + b1.double()
-        act64 = (lambda t: t * torch.sigmoid(t)) if act == "swish" else torch.relu
-        o64 = res.double() + 0.5 * (act64(z64) @ W2.double().t() + b2.double())
-        close(out, o64, 1e-2, "ffn out vs float64")
-        dact = (torch.sigmoid(z64) * (1 + z64 * (1 - torch.sigmoid(z64)))) if act == "swish" else (z64 > 0).double()
-        close(z, dact, 2e-2, "ffn gate vs float64")
-        dz64 = (gb.double() @ W2.double()) * z.cpu().double()  # the saved bf16 gate, as used
-        close(dz, dz64, 2e-2, "ffn dz vs float64")
-        close(dx, dz.cpu().double() @ W1.double(), 2e-2, "ffn dx vs float64 (of the bf16 dz)")
-
-
-@pytest.mark.parametrize("M,D,F,act,p", [(7968, 256, 2048, "swish", 0.1), (300, 256, 512, "relu", 0.0),
-                                         (130, 512, 2048, "swish", 0.3), (64, 64, 256, "relu", 0.1)])
-def test_ffn_dz_recomputed_gate(M, D, F, act, p):
-    """lasr_ffn_dz (fc1 product recomputed per tile) == the stored-gate path (fc1 epilogue
-    writes act'(u)*keep, the fc2 dX GEMM multiplies by it) up to the gate's bf16 rounding, and
-    matches a float64 reference built from the forward's own dropout mask (the kept h)."""
-    from liteasr_amd import _native as Nn
-
-    kn = K()
-    g = torch.Generator(device="cpu").manual_seed(M + D)
-    bf = torch.bfloat16
-    ln = torch.randn(M, D, generator=g).to(bf).to(DEV)
-    w1 = (torch.randn(F, D, generator=g) / D ** 0.5).to(bf).to(DEV)
-    b1 = (torch.randn(F, generator=g) * 0.1).to(DEV)
-    w2 = (torch.randn(D, F, generator=g) / F ** 0.5).to(bf).to(DEV)
-    gb = torch.randn(M, D, generator=g).to(bf).to(DEV)
-    a = Nn.ACT_SWISH if act == "swish" else Nn.ACT_RELU
-    seed = 1234
-    h = torch.empty(M, F, device=DEV, dtype=bf)
-    gate = torch.empty_like(h)
-    kn.linear(ln, w1, h, bias=b1, act=a, zout=gate, zout_mode=1, drop_p=p, drop_seed=seed)
-    dz_old = torch.empty(M, F, device=DEV, dtype=bf)
-    kn.gemm(gb, w2, dz_old, alpha=kn.dropout_scale(p), aux=gate, aux_act=Nn.ACT_GATE)
-    dz = torch.empty_like(dz_old)
-    kn.ffn_dz(ln, w1, b1, gb, w2, a, p, seed, dz)
-    torch.cuda.synchronize()
-    close(dz, dz_old, 1e-2, "ffn_dz vs stored gate")
-    # float64 reference: u, act', the forward's keep (h != 0 where act(u) != 0)
-    u = ln.double() @ w1.double().t() + b1.double()
-    if act == "swish":
-        s = torch.sigmoid(u)
-        d = s * (1 + u * (1 - s))
-        hv = u * s
-    else:
-        d = (u > 0).double()
-        hv = torch.relu(u)
-    keep = ((h.double() != 0) | (hv.abs() < 1e-30)).double() if p > 0 else torch.ones_like(u)
-    ref = (gb.double() @ w2.double()) * d * keep * (kn.dropout_scale(p) if p > 0 else 1.0)
-    close(dz, ref, 8e-3, "ffn_dz vs fp64")
