@@ -61,26 +61,38 @@ def cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
-def run_case(cfg_o, B, T, L, dtype, chunk=0, ctc_weight=0.3, seed=0, training=True, round_bf16=False):
+def run_case(cfg_o, B, T, L, dtype, chunk=0, ctc_weight=0.3, seed=0, training=True, round_bf16=False,
+             emulate=False):
+    """One training step of liteasr_amd on the GPU against the oracle on the same seeded
+    weights and batch.  emulate=True: the oracle is oracle/u2_bf16.py (float64 with the bf16
+    build's roundings) instead of the plain fp64 oracle; weights and features are then
+    bf16-representable on both sides."""
     from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
     from liteasr_amd.optims.noam import Noam, NoamConfig
 
     params = O.init_params(cfg_o, seed=seed + 11)
     buffers = O.init_buffers(cfg_o)
     batch = O.synthetic_batch(B, T, L, cfg_o["vocab_size"], seed=seed)
-    if round_bf16:  # both sides see the same bf16-representable weights and features
+    if round_bf16 or emulate:  # both sides see the same bf16-representable weights and features
         params = {k: (v.bfloat16().float() if v.is_floating_point() else v) for k, v in params.items()}
         batch = (batch[0].bfloat16().float(),) + tuple(batch[1:])
-    # oracle in fp64
     p64 = {k: v.double() for k, v in params.items()}
     b64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in buffers.items()}
     xs, xlens, ys, ylens = batch
-    with torch.no_grad():
-        ha_o, hc_o, _, _ = O.u2_forward(xs.double(), xlens, ys, ylens, p64, cfg_o, {k: v.clone() for k, v in b64.items()},
-                                        training, chunk)
-    loss_o, grads_o, new_o, _, norm_o = O.train_step(p64, b64, (xs.double(), xlens, ys, ylens), cfg_o,
-                                                       ctc_weight=ctc_weight, smoothing=0.1, clip=5.0,
-                                                       model_dim=cfg_o["enc_dim"], chunk=chunk, training=training)
+    new_o = norm_o = None
+    if emulate:
+        from oracle import u2_bf16 as E
+
+        loss_o, _, _, grads_o, ha_o, hc_o = E.loss_and_grads(p64, b64, (xs.double(), xlens, ys, ylens), cfg_o,
+                                                             ctc_weight=ctc_weight, smoothing=0.1, chunk=chunk,
+                                                             training=training)
+    else:
+        with torch.no_grad():
+            ha_o, hc_o, _, _ = O.u2_forward(xs.double(), xlens, ys, ylens, p64, cfg_o,
+                                            {k: v.clone() for k, v in b64.items()}, training, chunk)
+        loss_o, grads_o, new_o, _, norm_o = O.train_step(p64, b64, (xs.double(), xlens, ys, ylens), cfg_o,
+                                                           ctc_weight=ctc_weight, smoothing=0.1, clip=5.0,
+                                                           model_dim=cfg_o["enc_dim"], chunk=chunk, training=training)
     # liteasr_amd on the GPU
     model = build(cfg_o, dtype, chunk)
     missing, unexpected = model.load_state_dict({**params, **buffers}, strict=False)
@@ -175,6 +187,33 @@ def test_parity_bf16(cfg, B, T, L):
     _check_bf16(run_case(cfg, B, T, L, "bf16", round_bf16=True))
 
 
+# ---- the bf16 build against the bf16-emulating oracle (oracle/u2_bf16.py): same roundings,
+# so the remaining difference is fp32-vs-fp64 accumulation plus the rare bf16 rounding-boundary
+# straddle.  Bars (every tensor, ReLU-gated ones included): gradients 1e-2 of max, logits
+# 1e-2 of max, loss 1e-4 relative.  Measured worst values: DESIGN.md §2 (tools/bf16_errs.py).
+EMU_GRAD, EMU_LOGIT, EMU_LOSS = 1e-2, 1e-2, 1e-4
+
+
+def emu_errors(r):
+    """(loss rel, h_attn, h_ctc, worst (err, name) over the gradients) of an emulate=True case."""
+    lg, lo = r["loss"]
+    g, go = r["grads"]
+    errs, _ = grad_errs(g, go)
+    return (abs(lg - lo) / abs(lo), rel(*r["h_attn"]), rel(*r["h_ctc"]), max((v, k) for k, v in errs.items()))
+
+
+def _check_emulated(r):
+    loss, ha, hc, worst = emu_errors(r)
+    assert loss <= EMU_LOSS, r["loss"]
+    assert ha < EMU_LOGIT and hc < EMU_LOGIT, (ha, hc)
+    assert worst[0] < EMU_GRAD, worst
+
+
+@pytest.mark.parametrize("cfg,B,T,L", [(TINY, 3, 130, 8), (SMALL, 2, 210, 12)])
+def test_parity_bf16_emulated(cfg, B, T, L):
+    _check_emulated(run_case(cfg, B, T, L, "bf16", emulate=True))
+
+
 # d_k 32 with the streaming chunk mask (config 4's attention shape) through the fused kernels
 LARGE_HEADS = O.default_cfg(enc_dim=128, enc_heads=4, enc_ff=256, enc_layers=2, dec_dim=128, dec_heads=4,
                             dec_ff=256, dec_layers=1, vocab_size=30)
@@ -214,6 +253,36 @@ def test_parity_large_width_chunk_fp32():
 def test_parity_large_width_chunk_bf16():
     """Config 4's shape (d 512, 16 heads, chunk 16) in the bf16 build (fused d_k 32 attention)."""
     _check_bf16(run_case(LARGE, 2, 200, 10, "bf16", chunk=16, round_bf16=True))
+
+
+def test_parity_large_width_chunk_bf16_emulated():
+    """Config 4's layer shape (d 512, 16 heads, d_k 32, chunk 16) in the bf16 build against
+    the bf16-emulating oracle."""
+    _check_emulated(run_case(LARGE, 2, 200, 10, "bf16", chunk=16, emulate=True))
+
+
+# BASELINE config 2's whole model (12 encoder / 6 decoder layers, d 256, ff 2048, V 4233) at
+# its real utterance length T 1000 (T' 249), two utterances
+CONFIG2 = O.default_cfg()
+
+
+def test_parity_config2_full_model_fp32():
+    """liteasr/models/u2.py:116-159 -> criterions/hybrid_ctc_attn.py:39-79 at config 2's
+    full shape, fp32 build vs the fp64 oracle (loss 1e-5 relative, logits and every
+    gradient 2e-4 of max; the subsampling convs' ReLU-kink bar as in test_parity_fp32)."""
+    _check_fp32(run_case(CONFIG2, 2, 1000, 40, "fp32"), 2e-4)
+
+
+def test_parity_config2_full_model_bf16_emulated():
+    """Config 2's full model in the default bf16 build (fused attention, bf16 GEMMs, the
+    kernels the bench times) against the bf16-emulating oracle."""
+    _check_emulated(run_case(CONFIG2, 2, 1000, 40, "bf16", emulate=True))
+
+
+def test_parity_config5_long_bf16_emulated():
+    """BASELINE config 5's shape: T 4000 (T' 999), CTC-only (w 1.0: the decoder runs and gets
+    zero gradient), label length 150, full depth, one utterance pair."""
+    _check_emulated(run_case(CONFIG2, 2, 4000, 150, "bf16", ctc_weight=1.0, emulate=True))
 
 
 def test_parity_full_depth_fp32():

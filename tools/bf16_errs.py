@@ -1,5 +1,7 @@
-"""Measure the bf16 build's per-tensor gradient errors against the fp64 oracle run on the
-same bf16-rounded weights and features (for setting tests/test_model_gpu.py bounds)."""
+"""Measured per-tensor errors of the bf16 build against the bf16-emulating oracle
+(oracle/u2_bf16.py) and, for comparison, against the plain fp64 oracle on the same
+bf16-rounded weights and features (tests/test_model_gpu.py bars).
+    python tools/bf16_errs.py [case ...]   -> gpurun_out/bf16_errs.json"""
 import json
 import os
 import sys
@@ -8,25 +10,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import test_model_gpu as T  # noqa: E402
-from oracle import u2_oracle as O  # noqa: E402
 
 cases = {
-    "tiny": (T.TINY, 3, 130, 8, 0),
-    "small2": (T.SMALL, 2, 210, 12, 0),
-    "dk32_chunk": (T.LARGE_HEADS, 2, 150, 6, 8),
-    "d512_h16_chunk": (O.default_cfg(enc_dim=512, enc_heads=16, enc_ff=2048, enc_layers=2, dec_dim=512, dec_heads=16,
-                                     dec_ff=2048, dec_layers=1, vocab_size=4233), 2, 200, 10, 16),
+    "tiny": (T.TINY, 3, 130, 8, 0, 0.3),
+    "small2": (T.SMALL, 2, 210, 12, 0, 0.3),
+    "d512_h16_chunk": (T.LARGE, 2, 200, 10, 16, 0.3),
+    "config2_full": (T.CONFIG2, 2, 1000, 40, 0, 0.3),
+    "config5_long": (T.CONFIG2, 2, 4000, 150, 0, 1.0),
 }
+sel = sys.argv[1:] or list(cases)
 out = {}
-for name, (cfg, B, Tx, L, chunk) in cases.items():
-    for rnd in (False, True):
-        r = T.run_case(cfg, B, Tx, L, "bf16", chunk=chunk, round_bf16=rnd)
+for name in sel:
+    cfg, B, Tx, L, chunk, w = cases[name]
+    for emu in (True, False):
+        r = T.run_case(cfg, B, Tx, L, "bf16", chunk=chunk, ctc_weight=w, round_bf16=True, emulate=emu)
         g, go = r["grads"]
         errs, floor = T.grad_errs(g, go)
-        worst = sorted(((v, k) for k, v in errs.items()), reverse=True)[:4]
-        coss = min((T.cos(g[k], go[k]), k) for k in go if go[k].abs().max().item() > floor)
+        worst = sorted(((v, k) for k, v in errs.items()), reverse=True)[:5]
+        gated = max((v, k) for k, v in errs.items() if T.relu_gated(k))
         lg, lo = r["loss"]
-        out[f"{name}_round{int(rnd)}"] = dict(loss_rel=abs(lg - lo) / abs(lo), h_attn=T.rel(*r["h_attn"]),
-                                              h_ctc=T.rel(*r["h_ctc"]), worst=worst, min_cos=coss)
-        print(name, rnd, json.dumps(out[f"{name}_round{int(rnd)}"]), flush=True)
+        key = f"{name}_{'emulated' if emu else 'fp64'}"
+        out[key] = dict(loss_rel=abs(lg - lo) / abs(lo), h_attn=T.rel(*r["h_attn"]), h_ctc=T.rel(*r["h_ctc"]),
+                        worst=worst, worst_relu_gated=gated)
+        print(key, json.dumps(out[key]), flush=True)
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 json.dump(out, open(os.path.join(ROOT, "gpurun_out", "bf16_errs.json"), "w"), indent=1)
