@@ -68,6 +68,102 @@ def synthetic(cfgd, rank, dev):
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 
 
+def _rows(cfgd):
+    """B * T' (the encoder's GEMM rows)."""
+    T1 = (cfgd["T"] - 3) // 2 + 1
+    return cfgd["B"] * ((T1 - 3) // 2 + 1)
+
+
+def build_key():
+    """Identity of the HIP library a PMC pass measured: sha256 of libliteasr_hip.so (first
+    16 hex digits).  Committed PMC byte counts are used only while the library is the same
+    build, so a kernel change that keeps its template name cannot reuse stale bytes."""
+    import hashlib
+
+    path = os.path.join(ROOT, "liteasr_amd", "lib", "libliteasr_hip.so")
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def family_case(cfgd, dev):
+    """The dominant kernel family of the step (profiles/r03 step summary: the GEMMs whose
+    output is d = 256 columns wide, 64 x 64 tiles, ~2.4 ms of the ~12 ms step): one Conformer
+    layer's ten of them, issued through the product's own calls (kernels.linear /
+    kernels.gemm: same planner, tiles and epilogues as nets/functional.py):
+      forward, fp32 residual out = res + s * (X W^T + b)   (liteasr/nets/conformer_layer.py:37-78)
+        fc2 of both FFNs (K = ff), linear_o (K = d), pointwise_conv2 (K = d)
+      backward, bf16 data gradients dX = dY W           (the same layers' input gradients)
+        fc1 of both FFNs (K = ff), linear_o (K = d), the fused q/k/v (K = 3d),
+        pointwise_conv2 (K = d), pointwise_conv1 (K = 2d).
+    Algorithmic bytes per launch: A [M, K] and W [d, K] bf16 read once, the output written
+    once (fp32 forward + the fp32 residual read once; bf16 backward), bias fp32."""
+    import torch
+
+    from liteasr_amd import kernels as K
+
+    M, D, F = _rows(cfgd), cfgd["d"], cfgd["ff"]
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(7)
+
+    def rn(*shape, dt=bf, scale=1.0):
+        return (torch.randn(*shape, device=dev, generator=g) * scale).to(dt)
+
+    res = rn(M, D, dt=torch.float32)
+    insts = []
+
+    def fwd(name, Kd, count):
+        x, w, b = rn(M, Kd), rn(D, Kd, scale=Kd ** -0.5), rn(D, dt=torch.float32, scale=0.02)
+        out = torch.empty(M, D, device=dev)
+        scale = 0.5 if name.startswith("fc2") else 1.0
+        fn = lambda: K.linear(x, w, out, bias=b, res=res, res_scale=scale, drop_p=0.1, drop_seed=5)  # noqa: E731
+        insts.append(dict(name=name, M=M, N=D, K=Kd, count=count, launch=fn, plan=(x, w.t(), out),
+                          bytes=2.0 * (M * Kd + D * Kd) + 4.0 * M * D * 2 + 4.0 * D, flops=2.0 * M * D * Kd))
+
+    def dx(name, Kd, count):
+        dy, w = rn(M, Kd), rn(Kd, D, scale=Kd ** -0.5)
+        out = torch.empty(M, D, device=dev, dtype=bf)
+        fn = lambda: K.gemm(dy, w, out)  # noqa: E731
+        insts.append(dict(name=name, M=M, N=D, K=Kd, count=count, launch=fn, plan=(dy, w, out),
+                          bytes=2.0 * (M * Kd + D * Kd) + 2.0 * M * D, flops=2.0 * M * D * Kd))
+
+    fwd("fc2 fwd (+res)", F, 2)
+    fwd("linear_o fwd (+res)", D, 1)
+    fwd("pointwise_conv2 fwd (+res)", D, 1)
+    dx("fc1 dX", F, 2)
+    dx("linear_o dX", D, 1)
+    dx("qkv dX", 3 * D, 1)
+    dx("pointwise_conv2 dX", D, 1)
+    dx("pointwise_conv1 dX", 2 * D, 1)
+    for it in insts:
+        a_, b_, c_ = it["plan"]
+        tm, tn, sp = K.gemm_plan(a_, b_, c_)
+        it["tile"] = f"{tm}x{tn}" + (f" split {sp}" if sp > 1 else "")
+    return insts
+
+
+def family_roofline(cfgd, dev, iters=50):
+    """Per-instance average launch time (HIP events on the launch stream, `iters` back-to-back
+    launches) and the family aggregate: sum over one layer's launches of algorithmic bytes /
+    sum of their times, against the 8 TB/s HBM peak (every instance's byte time exceeds its
+    flop time at 2.5 PFLOP/s: bound hbm)."""
+    insts = family_case(cfgd, dev)
+    rows, tb, tt, tf = [], 0.0, 0.0, 0.0
+    for it in insts:
+        sec = _time_case(it["launch"], iters)
+        bound, ach, peak, unit = _roof(it["flops"], it["bytes"], sec)
+        rows.append({"name": it["name"], "shape": f"M={it['M']} N={it['N']} K={it['K']}", "tile": it["tile"],
+                     "per_layer": it["count"], "avg_launch_us": round(sec * 1e6, 2),
+                     "algorithmic_bytes": it["bytes"], "GBps": round(it["bytes"] / sec / 1e9, 1),
+                     "frac": round(it["bytes"] / sec / 1e9 / PEAK_HBM_GBS, 4), "bound": bound})
+        tb += it["count"] * it["bytes"]
+        tt += it["count"] * sec
+        tf += it["count"] * it["flops"]
+    return rows, tb, tt, tf
+
+
 def roofline_case(cfgd, dev):
     """The dominant kernel family of the step (rocprof): the weight-gradient GEMMs (both
     operands M/N-contiguous, LDS transposed reads, split-K fp32 partials).  In the step they
@@ -115,7 +211,8 @@ def roofline_case(cfgd, dev):
     S, minb = {(64, 64): (3, 3), (128, 128): (2, 2)}[(tm, tn)]
     splits = sorted({-x[1].split_k for x in q})
     meta = {"kernel": f"gemm_dw_group_kernel<{tm}, {tn}, {S}, {minb}>",
-            "shape": f"{len(q)} problems: 2x (M={F} N={D}) + 2x (M={D} N={F}), K={rows}, split_k={splits}"}
+            "shape": f"{len(q)} problems: 2x (M={F} N={D}) + 2x (M={D} N={F}), K={rows}, split_k={splits}",
+            "build": build_key()}
     return launch, flops, bytes_, meta
 
 
@@ -144,7 +241,8 @@ def hottest_case(cfgd, dev):
     flops = 2.0 * M * F * D
     bytes_ = 2.0 * (M * D + F * D) + 2 * 2.0 * M * F + 4.0 * F
     meta = {"kernel": "gemm_bf16_glds_kernel<128, 256, true, true, unsigned short, 3, 2, 0, 1>",
-            "shape": f"M={M} N={F} K={D} bias+swish+gate+dropout", "grid": [F // 256, -(-M // 128), 1]}
+            "shape": f"M={M} N={F} K={D} bias+swish+gate+dropout", "grid": [F // 256, -(-M // 128), 1],
+            "build": build_key()}
     return launch, flops, bytes_, meta
 
 
@@ -171,15 +269,7 @@ def _roof(flops, bytes_, sec):
     return "mfma", flops / sec / 1e12, PEAK_BF16_TFLOPS, "TFLOP/s"
 
 
-def dominant_kernel_roofline(cfgd, dev, iters=50):
-    """Average launch duration of the dominant kernel measured live with HIP events on the
-    stream it is launched on; bound = whichever of FLOP time (dense bf16 MFMA peak) and
-    byte time (HBM peak) is larger for its algorithmic work."""
-    import torch
-
-    from liteasr_amd import kernels as K
-
-    launch, flops, bytes_, meta = roofline_case(cfgd, dev)
+def _case_entry(launch, flops, bytes_, meta, iters):
     sec = _time_case(launch, iters)
     bound, ach, peak, unit = _roof(flops, bytes_, sec)
     traffic = pmc_traffic(meta)
@@ -187,38 +277,128 @@ def dominant_kernel_roofline(cfgd, dev, iters=50):
            "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
            "traffic": traffic["bytes_per_launch"] if traffic else None,
            "algorithmic_bytes_per_launch": bytes_, "algorithmic_flops_per_launch": flops,
-           "avg_launch_us": round(sec * 1e6, 2),
-           "achieved_tflops": round(flops / sec / 1e12, 2)}
+           "avg_launch_us": round(sec * 1e6, 2), "achieved_tflops": round(flops / sec / 1e12, 2)}
     if traffic:
         out["traffic_source"] = traffic["source"]
-    launch, flops, bytes_, meta = hottest_case(cfgd, dev)
-    sec = _time_case(launch, iters)
-    bound, ach, peak, unit = _roof(flops, bytes_, sec)
-    traffic = pmc_traffic(meta)
-    out["hottest_instance"] = {
-        "kernel": meta["kernel"], "shape": meta["shape"], "bound": bound, "achieved": round(ach, 2), "peak": peak,
-        "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic["bytes_per_launch"] if traffic else None,
-        "algorithmic_bytes_per_launch": bytes_, "algorithmic_flops_per_launch": flops,
-        "avg_launch_us": round(sec * 1e6, 2), "achieved_tflops": round(flops / sec / 1e12, 2)}
     return out
 
 
+def dominant_kernel_roofline(cfgd, dev, iters=50):
+    """`roofline` = the dominant kernel family (family_case), measured live with HIP events
+    on the stream the kernels are launched on; `traffic` = HBM bytes per layer's set of
+    launches from the committed PMC passes of the same library build (pmc_traffic).
+    Secondary entries: the grouped FFN weight-gradient launch (`dw_group`) and the single
+    hottest GEMM instance, the FFN fc1 forward (`hottest_instance`)."""
+    rows, tb, tt, tf = family_roofline(cfgd, dev, iters)
+    ach = tb / tt / 1e9
+    fam_meta = family_meta(cfgd)
+    traffic = pmc_traffic(fam_meta)
+    out = {"kernel": fam_meta["kernel"], "shape": fam_meta["shape"], "bound": "hbm", "achieved": round(ach, 2),
+           "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+           "traffic": traffic["bytes_per_launch"] if traffic else None,
+           "per": "one Conformer layer's launches of the family (10); achieved = algorithmic bytes / summed "
+                  "launch time",
+           "algorithmic_bytes_per_launch": tb, "algorithmic_flops_per_launch": tf,
+           "avg_launch_us": round(tt / sum(r["per_layer"] for r in rows) * 1e6, 2),
+           "layer_set_us": round(tt * 1e6, 2), "achieved_tflops": round(tf / tt / 1e12, 2),
+           "instances": rows}
+    if traffic:
+        out["traffic_source"] = traffic["source"]
+    else:
+        out["traffic_note"] = f"no PMC pass for library build {build_key()}"
+    out["dw_group"] = _case_entry(*roofline_case(cfgd, dev), iters)
+    out["hottest_instance"] = _case_entry(*hottest_case(cfgd, dev), iters)
+    return out
+
+
+def family_meta(cfgd):
+    M, D, F = _rows(cfgd), cfgd["d"], cfgd["ff"]
+    return {"kernel": "gemm_bf16_glds_kernel", "family": "N = d output GEMMs (64x64 tiles)",
+            "shape": f"one layer: 2x fc2 fwd M={M} N={D} K={F} +res, linear_o / pw2 fwd K={D} +res, "
+                     f"2x fc1 dX K={F}, dX K={D},{3 * D},{D},{2 * D}", "build": build_key()}
+
+
+def ctc_roofline(cfgd, dev, iters=20):
+    """SURVEY §8(d) / BASELINE.md §3: the fused log-softmax + CTC (hybrid_ctc_attn.py:67-75)
+    at the config's shape with bf16 logits, three kernels timed live: the row log-sum-exp +
+    gather (lasr_ctc_fwd with alpha = NULL), the alpha / beta lattice recursion
+    (lasr_ctc_lattice: serial in T', alpha and beta side by side), and the gradient
+    softmax - gamma (lasr_ctc_bwd).  Algorithmic bytes = read the logits once + write the
+    gradient once, 2 * B * T' * V * 2 B (bf16; BASELINE.md quotes 4 B for fp32 logits)."""
+    import torch
+
+    from liteasr_amd import _native as Nn
+    from liteasr_amd import kernels as K
+    from liteasr_amd.utils.synthetic import synthetic_batch
+
+    B, L, V_ = cfgd["B"], cfgd["L"], V
+    T1 = (cfgd["T"] - 3) // 2 + 1
+    Tp = (T1 - 3) // 2 + 1
+    xs, xlens, ys, ylens = synthetic_batch(B, cfgd["T"], L, V_, seed=99)
+    ilen = (((xlens - 1) // 2 - 1) // 2).to(torch.int32).to(dev)
+    tlen = ylens.to(torch.int32).to(dev)
+    tgt = ys.clamp(min=0).to(torch.int32).to(dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    logits = K.padded_rows(B * Tp, V_, torch.bfloat16, dev).view(B, Tp, V_)
+    logits.copy_(torch.randn(B, Tp, V_, device=dev, generator=g))
+    f32 = dict(dtype=torch.float32, device=dev)
+    S = 2 * L + 1
+    lse, lp = torch.empty(B * Tp, **f32), torch.empty(B * Tp * (L + 1), **f32)
+    alpha, beta, nll = torch.empty(B * Tp * S, **f32), torch.empty(B * Tp * S, **f32), torch.empty(B, **f32)
+    grad = K.padded_rows(B * Tp, V_, torch.bfloat16, dev).view(B, Tp, V_)
+    st = K.stream()
+
+    def gather():
+        K.ctc_fwd(logits, tgt, ilen, tlen, lse, lp, None, nll)
+
+    def lattice():
+        Nn.call("lasr_ctc_lattice", B, Tp, L, K.ptr(tgt), K.ptr(ilen), K.ptr(tlen), K.ptr(lp), K.ptr(alpha),
+                K.ptr(beta), K.ptr(nll), st)
+
+    def gradk():
+        K.ctc_bwd(logits, tgt, ilen, tlen, lse, lp, alpha, nll, beta, grad, 1.0 / B, beta_ready=True)
+
+    gather()
+    lattice()
+    tg, tl, tr = _time_case(gather, iters), _time_case(lattice, iters), _time_case(gradk, iters)
+    tot = tg + tl + tr
+    byt = 2.0 * B * Tp * V_ * 2
+    return {"kernels": ["ctc_lse_gather_kernel", "ctc_alpha_beta_kernel", "ctc_grad_kernel"],
+            "shape": f"B={B} T'={Tp} V={V_} L={L} (S=2L+1={S}), bf16 logits",
+            "gather_us": round(tg * 1e6, 2), "lattice_us": round(tl * 1e6, 2), "grad_us": round(tr * 1e6, 2),
+            "total_us": round(tot * 1e6, 2), "algorithmic_bytes": byt,
+            "achieved": round(byt / tot / 1e9, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(byt / tot / 1e9 / PEAK_HBM_GBS, 4),
+            "alpha_beta_us_per_step": round(tl / Tp * 1e6, 4),
+            "note": "frac over the three kernels; the lattice recursion is latency-bound (serial in T')"}
+
+
 def pmc_traffic(meta):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/*/roofline_pmc.json, written by tools/pmc_traffic.py: separate FETCH_SIZE and
-    WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), matched on kernel
-    and shape; None when absent."""
+    """HBM bytes per launch (per layer's set, for the family) from the committed rocprofv3 PMC
+    passes (profiles/*/roofline_pmc*.json, written by tools/pmc_traffic.py: separate
+    FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), matched
+    on kernel, shape AND library build (build_key); None when no pass matches this build."""
     import glob
     import json
 
-    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*",
-                                              "roofline_pmc*.json")), reverse=True):
+    key = build_key()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "roofline_pmc*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if d.get("kernel") == meta["kernel"] and d.get("shape") == meta["shape"]:
-            return {"bytes_per_launch": d["hbm_bytes_per_launch"], "source": os.path.relpath(path)}
+        if d.get("kernel") == meta["kernel"] and d.get("shape") == meta["shape"] and d.get("build") == key:
+            return {"bytes_per_launch": d["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+    return None
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
     return None
 
 
@@ -256,6 +436,7 @@ def cpu_baseline(cfgd_name, budget_s=25.0):
         if el + el / steps > budget_s or (steps >= 3 and el >= 12.0):
             break
     return {"value": round(Bs * steps / el, 3), "unit": "utterances/sec", "cores": n, "kind": "port",
+            "cpu_model": _cpu_model(),
             "sample": f"oracle (torch CPU fp32) {cfgd_name} U2, B={Bs} T={cfgd['T']} L={cfgd['L']}, dropout 0.1, "
                       f"{steps} timed step(s) = {el:.1f} s after 1 warm-up ({warm:.1f} s)"}
 
@@ -319,8 +500,9 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", type=int, default=0, metavar="N",
                     help="only launch the roofline kernel N times (for rocprofv3 --pmc passes)")
-    ap.add_argument("--roofline-case", default="dw", choices=["dw", "hot"],
-                    help="--roofline-only: the dominant-family kernel (dw) or the hottest instance (hot)")
+    ap.add_argument("--roofline-case", default="family", choices=["family", "dw", "hot"],
+                    help="--roofline-only: the dominant kernel family (one layer's set), the grouped "
+                         "weight-gradient launch (dw) or the hottest instance (hot)")
     args = ap.parse_args()
 
     import torch
@@ -328,8 +510,21 @@ def main():
 
     if args.roofline_only:
         torch.cuda.set_device(0)
-        case = roofline_case if args.roofline_case == "dw" else hottest_case
-        launch, flops, bytes_, meta = case(CONFIGS[args.config], torch.device("cuda", 0))
+        if args.roofline_case == "family":
+            cfgd = CONFIGS[args.config]
+            insts = family_case(cfgd, torch.device("cuda", 0))
+            meta = family_meta(cfgd)
+            bytes_ = sum(it["count"] * it["bytes"] for it in insts)
+            flops = sum(it["count"] * it["flops"] for it in insts)
+            meta["dispatches_per_launch"] = sum(it["count"] for it in insts)
+
+            def launch():
+                for it in insts:
+                    for _ in range(it["count"]):
+                        it["launch"]()
+        else:
+            case = roofline_case if args.roofline_case == "dw" else hottest_case
+            launch, flops, bytes_, meta = case(CONFIGS[args.config], torch.device("cuda", 0))
         for _ in range(args.roofline_only):
             launch()
         torch.cuda.synchronize()
@@ -434,6 +629,7 @@ def main():
         }
         if not args.no_roofline:
             out["roofline"] = dominant_kernel_roofline(cfgd, dev)
+            out["ctc"] = ctc_roofline(cfgd, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.config)
         print(json.dumps(out), flush=True)

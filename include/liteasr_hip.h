@@ -183,10 +183,15 @@ int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_d
  * ---------------------------------------------------------------------- */
 /* beta (optional, [B][T][2*Lmax+1]): when given, the forward also runs the beta
  * recursion, concurrently with alpha; pass beta_ready = 1 to lasr_ctc_bwd then.
- * 2*Lmax+1 <= 1024 (one lattice state per thread). */
+ * 2*Lmax+1 <= 1024 (one lattice state per thread).  alpha == NULL runs only the first
+ * stage (row log-sum-exp over V and the gather of the blank / target log-probs into lp);
+ * lasr_ctc_lattice then runs the second (the serial-in-T alpha (+ beta) recursion over lp
+ * and nll), so the two stages can be timed or scheduled apart. */
 int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, int64_t ld, const int32_t* targets,
                  int Lmax, const int32_t* ilen, const int32_t* tlen, float* lse, float* lp,
                  float* alpha, float* beta, float* nll, void* stream);
+int lasr_ctc_lattice(int B, int T, int Lmax, const int32_t* targets, const int32_t* ilen, const int32_t* tlen,
+                     const float* lp, float* alpha, float* beta, float* nll, void* stream);
 int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, int64_t ld, const int32_t* targets,
                  int Lmax, const int32_t* ilen, const int32_t* tlen, const float* lse,
                  const float* lp, const float* alpha, const float* nll, float* beta,

@@ -109,6 +109,7 @@ SIGNATURES = {
                            _p, _i, _f, _f, _u, _p],
     "lasr_branch_grad": [_p, _i, _l, _p, _i, _f, _f, _u, _p],
     "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p],
+    "lasr_ctc_lattice": [_i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "lasr_ctc_bwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _i, _p, _i, _f, _p, _p],
     "lasr_lsm_kl_fwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _p],
     "lasr_lsm_kl_bwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _i, _f, _p, _p],

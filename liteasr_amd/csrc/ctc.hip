@@ -308,9 +308,17 @@ extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, in
   else
     ctc_lse_gather_kernel<bf16_t><<<B * T, 256, 0, st>>>((const bf16_t*)logits, B, T, V, ld, targets, Lmax, ilen, tlen, lse, lp);
   int rc = lasr_check_launch("ctc_lse_gather");
-  if (rc) return rc;
+  if (rc || !alpha) return rc;  // alpha == NULL: the log-softmax / gather stage only
+  return lasr_ctc_lattice(B, T, Lmax, targets, ilen, tlen, lp, alpha, beta, nll, stream);
+}
+
+extern "C" int lasr_ctc_lattice(int B, int T, int Lmax, const int32_t* targets, const int32_t* ilen,
+                                const int32_t* tlen, const float* lp, float* alpha, float* beta, float* nll,
+                                void* stream) {
+  LASR_CHECK_ARG(B > 0 && T > 0 && Lmax >= 0 && 2 * Lmax + 1 <= 1024, "lasr_ctc_lattice: bad sizes");
+  LASR_CHECK_ARG(lp && alpha && nll, "lasr_ctc_lattice: lp / alpha / nll");
   const int Smax = 2 * Lmax + 1;
-  ctc_alpha_beta_kernel<<<beta ? 2 * B : B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(
+  ctc_alpha_beta_kernel<<<beta ? 2 * B : B, ctc_block(Smax), 2 * Smax * sizeof(float), (hipStream_t)stream>>>(
       B, T, Lmax, targets, ilen, tlen, lp, alpha, nll, beta);
   return lasr_check_launch("ctc_alpha_beta");
 }

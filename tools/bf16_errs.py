@@ -26,12 +26,14 @@ for name in sel:
         r = T.run_case(cfg, B, Tx, L, "bf16", chunk=chunk, ctc_weight=w, round_bf16=True, emulate=emu)
         g, go = r["grads"]
         errs, floor = T.grad_errs(g, go)
+        errs = {k: v for k, v in errs.items() if not k.endswith(T.NOISE)}
+        noise = T.emu_errors(r)[3] if emu else None
         worst = sorted(((v, k) for k, v in errs.items()), reverse=True)[:5]
         gated = max((v, k) for k, v in errs.items() if T.relu_gated(k))
         lg, lo = r["loss"]
         key = f"{name}_{'emulated' if emu else 'fp64'}"
         out[key] = dict(loss_rel=abs(lg - lo) / abs(lo), h_attn=T.rel(*r["h_attn"]), h_ctc=T.rel(*r["h_ctc"]),
-                        worst=worst, worst_relu_gated=gated)
+                        worst=worst, worst_relu_gated=gated, worst_incl_zero_grad_tensors=noise)
         print(key, json.dumps(out[key]), flush=True)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 json.dump(out, open(os.path.join(ROOT, "gpurun_out", "bf16_errs.json"), "w"), indent=1)

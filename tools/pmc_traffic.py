@@ -28,9 +28,15 @@ if __name__ == "__main__":
     f = per_dispatch(dbf, "FETCH_SIZE", meta["kernel"])
     w = per_dispatch(dbw, "WRITE_SIZE", meta["kernel"])
     assert f and w, "no dispatches of the roofline kernel in the PMC databases"
-    fk, wk = statistics.median(f), statistics.median(w)
-    out = {"kernel": meta["kernel"], "shape": meta["shape"], "launches": [len(f), len(w)],
-           "FETCH_SIZE_kB_median": fk, "WRITE_SIZE_kB_median": wk,
+    per = meta.get("dispatches_per_launch", 1)
+    if per > 1:  # a family: one "launch" = a layer's set of dispatches; total over the run / sets
+        n = meta["launches"]
+        assert len(f) == len(w) == n * per, (len(f), len(w), n, per)
+        fk, wk = sum(f) / n, sum(w) / n
+    else:
+        fk, wk = statistics.median(f), statistics.median(w)
+    out = {"kernel": meta["kernel"], "shape": meta["shape"], "build": meta.get("build"), "launches": [len(f), len(w)],
+           "FETCH_SIZE_kB_per_launch": fk, "WRITE_SIZE_kB_per_launch": wk,
            "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
            "algorithmic_bytes_per_launch": meta["algorithmic_bytes_per_launch"],
            "note": "FETCH_SIZE doubled (gfx950 wide-read correction); kB = 1024 B"}
