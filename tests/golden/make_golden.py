@@ -31,6 +31,10 @@ Fixtures
                   their torch.Generator seed (a checksum is stored to detect drift)
   host_policies.npz  SeqBatch / FrameBatch grouping of synthetic length lists (incl. the
                   oversize-utterance edge), Trigger firing sequences, Vocab lookups
+  transducer.npz  tiny Transducer (Conformer encoder, LSTM decoder, joint): init state_dict,
+                  batch (one empty transcript), encoder / decoder outputs, joint logits and every
+                  gradient of the RNN-T loss (oracle/rnnt_ref.py) backpropagated through the
+                  reference model
   spec_aug.npz    the reference SpecAugment (utils/transform/spec_augment.py) on seeded
                   inputs: global random/numpy seeds per case, input regenerated from its own
                   PCG64 seed, the augmented output, and one random.random() /
@@ -525,9 +529,55 @@ def gen_paraformer():
     save("paraformer.npz", **arrs)
 
 
+def gen_transducer():
+    """Tiny Transducer (liteasr/models/transducer.py; Conformer encoder d 32 x 2 with relative
+    PE and Swish, LSTM decoder dec_dim 16 / 48 units x 2 layers, joint 24, V 20, F 40), seed-42
+    init state_dict, a batch with an empty transcript: the encoder output, the decoder
+    output, the joint logits h_jnt (B, T', Lmax+1, V) and every parameter gradient of the
+    RNN-T loss backpropagated through the REFERENCE model.  The loss and its logits
+    gradient come from oracle/rnnt_ref.py (the reference's loss is the absent warp-transducer
+    package, rnnt.py:28,33: that part is unpinned; the model forward / backward is the
+    reference's own)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import rnnt_ref
+    from liteasr.models.transducer import DecoderArch as TDA
+    from liteasr.models.transducer import EncoderArch as TEA
+    from liteasr.models.transducer import Transducer
+
+    cfg = types.SimpleNamespace(joint_dim=24, dropout_rate=0.0, enc_arch=TEA.Conformer, use_rel=True, input_dim=40,
+                                enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_dropout_rate=0.0,
+                                enc_pos_dropout_rate=0.0, enc_attn_dropout_rate=0.0, enc_ff_dropout_rate=0.0,
+                                enc_layers=2, activation="swish", dec_arch=TDA.LSTM, vocab_size=20, dec_dim=16,
+                                dec_units=48, dec_dropout_rate=0.0, dec_layers=2)
+    torch.manual_seed(42)
+    model = Transducer(cfg)
+    model.train()
+    init = {k: v.clone() for k, v in model.state_dict().items() if not k.endswith(".pe.pe")}
+    g = torch.Generator().manual_seed(5)
+    xl, yl = [120, 97, 64], [5, 3, 0]
+    xlens, ylens = torch.tensor(xl), torch.tensor(yl)
+    B, Tx, L, V = 3, max(xl), max(yl), 20
+    xs = torch.randn(B, Tx, 40, generator=g).masked_fill(padding_mask(xlens).unsqueeze(-1), 0.0)
+    ys = torch.randint(1, V, (B, L), generator=g).masked_fill(padding_mask(ylens), -1)
+    rec = {}
+    enc_fwd, dec_fwd = model.encoder.forward, model.decoder.forward
+    model.encoder.forward = lambda *a, **k: rec.setdefault("h_enc", enc_fwd(*a, **k))
+    model.decoder.forward = lambda *a, **k: rec.setdefault("h_dec", dec_fwd(*a, **k))
+    h_jnt = model(xs, xlens, ys, ylens)
+    plen = model.get_pred_len(xlens)
+    loss, nll, dz = rnnt_ref.rnnt_batch(h_jnt.detach().double().numpy(), ys.clamp(min=0).numpy(), plen.numpy(),
+                                        ylens.numpy())
+    h_jnt.backward(torch.from_numpy(dz).float())
+    arrs = {"xs": xs, "xlens": xlens, "ys": ys, "ylens": ylens, "h_enc": rec["h_enc"].detach(),
+            "h_dec": rec["h_dec"].detach(), "h_jnt": h_jnt.detach(), "loss": np.array(loss), "nll": nll}
+    arrs.update({"init." + k: v for k, v in init.items()})
+    arrs.update({"grad." + n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+    save("transducer.npz", **arrs)
+
+
 GENERATORS = dict(relshift=gen_relshift, lengths=gen_lengths, ctc_kl=gen_ctc_kl, u2_step=gen_u2_step,
                   decode=gen_decode, loader=gen_loader, spec_aug=gen_spec_aug, ctc_large=gen_ctc_large,
-                  host_policies=gen_host_policies, paraformer=gen_paraformer)
+                  host_policies=gen_host_policies, paraformer=gen_paraformer, transducer=gen_transducer)
 
 if __name__ == "__main__":
     # python tests/golden/make_golden.py [name ...]   (default: all)

@@ -349,3 +349,34 @@ def test_paraformer_oracle_matches_reference(case):
     for k, v in gold.items():
         err = (p[k].grad.double() - v.double()).abs().max().item() / max(v.abs().max().item(), floor)
         assert err < 1e-4, (k, err)
+
+
+TRANSDUCER_GOLDEN = O.default_cfg(enc_dim=32, enc_heads=4, enc_ff=64, enc_layers=2, vocab_size=20, input_dim=40,
+                                  dec_layers=2, dec_units=48)
+
+
+def test_transducer_oracle_matches_reference():
+    """oracle/transducer_ref.py (encoder + LSTM prediction network + joint) against the
+    reference Transducer's own run (transducer.npz): encoder / decoder outputs and the joint
+    logits 1e-5; every parameter gradient of the RNN-T loss (the loss and its logits gradient
+    from oracle/rnnt_ref.py in both runs) 1e-4 of the tensor's max."""
+    from oracle import rnnt_ref
+    from oracle import transducer_ref as TR
+
+    d = load("transducer.npz")
+    params, buffers = _golden_params(d, "init.")
+    leaf = {k: v.double().requires_grad_() for k, v in params.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in buffers.items()}
+    hj, he, hd = TR.transducer_forward(d["xs"].double(), d["xlens"], d["ys"], d["ylens"], leaf, TRANSDUCER_GOLDEN,
+                                       b64, True)
+    assert rel(he, d["h_enc"]) < 1e-5 and rel(hd, d["h_dec"]) < 1e-5 and rel(hj, d["h_jnt"]) < 1e-5
+    plen = O.pred_len(d["xlens"])
+    loss, nll, dz = rnnt_ref.rnnt_batch(hj.detach().numpy(), d["ys"].clamp(min=0).numpy(), plen.numpy(),
+                                        d["ylens"].numpy())
+    assert abs(loss - d["loss"].item()) <= 1e-5 * abs(loss)
+    hj.backward(torch.from_numpy(dz))
+    gmax = max(v.abs().max().item() for k, v in d.items() if k.startswith("grad."))
+    for k, v in leaf.items():
+        ref = d["grad." + k].double()
+        g = v.grad if v.grad is not None else torch.zeros_like(v)
+        assert (g - ref).abs().max().item() <= 1e-4 * max(ref.abs().max().item(), 1e-3 * gmax), k
