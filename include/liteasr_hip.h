@@ -31,7 +31,9 @@ extern "C" {
 enum { LASR_F32 = 0, LASR_BF16 = 1, LASR_I32 = 2, LASR_I64 = 3, LASR_U8 = 4 };
 enum { LASR_OK = 0, LASR_ERR_INVALID = -1, LASR_ERR_LAUNCH = -2 };
 enum { LASR_ACT_NONE = 0, LASR_ACT_RELU = 1, LASR_ACT_SWISH = 2,
-       LASR_ACT_GATE = 3 /* aux_act only: multiply by the aux value itself */ };
+       LASR_ACT_GATE = 3 /* aux_act only: multiply by the aux value itself */,
+       LASR_ACT_TANH = 4 /* act: tanh; aux_act: multiply by 1 - aux^2 (aux = a stored tanh
+                            output: the Transducer joint, liteasr/models/transducer.py:202) */ };
 
 const char* lasr_last_error(void);
 int lasr_version(void);
@@ -394,7 +396,9 @@ int lasr_cast(const void* src, int sdt, void* dst, int ddt, int64_t n, void* str
 int lasr_scale_add(const void* a, int adt, const void* b, int bdt, float sa, float sb,
                    void* out, int odt, int64_t n, void* stream); /* out = sa*a + sb*b */
 /* Decoder embedding + absolute PE (liteasr/nets/transformer_decoder.py:77-78,
- * positional_encoding.py:49-56): y[r,:] = E[ids[r],:]*xscale + pe[r % L,:], dropout. */
+ * positional_encoding.py:49-56): y[r,:] = E[ids[r],:]*xscale + pe[r % L,:], dropout; pe may
+ * be NULL (plain embedding lookup).  lasr_embed_bwd: dE[ids[r]] += the rows' gradients; a
+ * row with a negative id contributes nothing (nn.Embedding padding_idx). */
 int lasr_embed_pe_fwd(const int32_t* ids, int R, int L, int D, const float* E,
                       const float* pe, float xscale, float p, uint64_t seed, void* y, int ydt,
                       void* stream);
@@ -403,6 +407,45 @@ int lasr_embed_bwd(const int32_t* ids, int R, int D, const void* dy, int dydt, f
 /* y = x*xscale (+ pe[t]) with dropout; rows = B*T, row r uses pe row r % T. */
 int lasr_pe_fwd(const void* x, int xdt, int64_t rows, int T, int D, const float* pe,
                 float xscale, float p, uint64_t seed, void* y, int ydt, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Transducer (liteasr/models/transducer.py) and the RNN-T loss (liteasr/criterions/rnnt.py:
+ * warp-transducer RNNTLoss(blank) / warp_rnnt.rnnt_loss(reduction="mean"), both on the raw
+ * joint logits with the log-softmax fused).  Lattice rows are (b, t, u) with u fastest:
+ * row = (b*T + t)*U1 + u, U1 = Lmax + 1; logits / grad rows start at row*ld (ld >= V).
+ * targets [B, Lmax] int32 (labels at u < tlen[b]); ilen / tlen [B] int32.
+ * fwd: lse [rows], lp [rows][2] = (log p(blank), log p(next label)), alpha / beta
+ *      [B][T][U1] (log space, beta includes the node's own emission) and nll [B]
+ *      (= -log P(y|x); +inf when ilen = 0).  U1 <= 1024.
+ * bwd: grad[row] = g * (softmax * occ - blank / label occupancies) for rows inside
+ *      (ilen[b], tlen[b] + 1), 0 elsewhere; g = gscale * (*gdev if gdev) (the batch mean:
+ *      gscale = 1/B).
+ * ---------------------------------------------------------------------- */
+int lasr_rnnt_fwd(const void* logits, int ldt, int B, int T, int U1, int V, int64_t ld, const int32_t* targets,
+                  int Lmax, const int32_t* ilen, const int32_t* tlen, int blank, float* lse, float* lp,
+                  float* alpha, float* beta, float* nll, void* stream);
+int lasr_rnnt_bwd(const void* logits, int ldt, int B, int T, int U1, int V, int64_t ld, const int32_t* targets,
+                  int Lmax, const int32_t* ilen, const int32_t* tlen, int blank, const float* lse, const float* lp,
+                  const float* alpha, const float* beta, const float* nll, void* grad, int gdt, float gscale,
+                  const float* gdev, void* stream);
+/* Joint (transducer.py:199-203): z[(b*T + t)*U1 + u][j] = tanh(e[b*T + t][j] + d[u*B + b][j]),
+ * e = lin_enc(h_enc) [B*T][J], d = lin_dec(h_dec) [U1*B][J] (time-major rows), fp32; J % 8 == 0.
+ * lasr_joint_reduce: the joint inputs' gradients from dz (the tanh input gradient, rows as
+ * z): de[b*T + t] = sum_u dz, dd[u*B + b] = sum_t dz, fixed summation order. */
+int lasr_joint_fwd(const float* e, const float* d, int B, int T, int U1, int J, void* z, int zdt, void* stream);
+int lasr_joint_reduce(const void* dz, int dzdt, int B, int T, int U1, int J, void* de, void* dd, int odt,
+                      void* stream);
+/* LSTMCell gate arithmetic (liteasr/nets/rnn_decoder.py:21-24,49-67; torch gate order i, f,
+ * g, o) around the per-step recurrent GEMM: gates [B][ldg >= 4H] fp32 pre-activations
+ * (x W_ih^T + b_ih + h W_hh^T), plus bias [4H] (nullable: b_hh) added by the cell; c_prev
+ * NULL = zero state.  fwd writes c_out [B][H] fp32 and h_out [B][ldh].  bwd: dh = dh_out
+ * (+ dh_rec, fp32), dc = dc_next + ..., writes the gate pre-activation gradients dgates
+ * [B][lddg] and dc_prev (nullable). */
+int lasr_lstm_cell_fwd(const float* gates, int64_t ldg, const float* bias, const float* c_prev, int B, int H,
+                       float* c_out, void* h_out, int hdt, int64_t ldh, void* stream);
+int lasr_lstm_cell_bwd(const float* gates, int64_t ldg, const float* bias, const float* c, const float* c_prev,
+                       const void* dh_out, int dhdt, int64_t lddh, const float* dh_rec, const float* dc_next, int B,
+                       int H, void* dgates, int gdt, int64_t lddg, float* dc_prev, void* stream);
 
 /* ------------------------------------------------------------------------
  * U2 bookkeeping (liteasr/models/u2.py:319-358, liteasr/utils/mask.py:8-90,

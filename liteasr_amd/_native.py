@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get(
 )
 
 F32, BF16, I32, I64, U8 = 0, 1, 2, 3, 4
-ACT_NONE, ACT_RELU, ACT_SWISH, ACT_GATE = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_SWISH, ACT_GATE, ACT_TANH = 0, 1, 2, 3, 4
 
 _p = C.c_void_p
 _i = C.c_int
@@ -110,6 +110,12 @@ SIGNATURES = {
     "lasr_branch_grad": [_p, _i, _l, _p, _i, _f, _f, _u, _p],
     "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "lasr_ctc_lattice": [_i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
+    "lasr_rnnt_fwd": [_p, _i, _i, _i, _i, _i, _l, _p, _i, _p, _p, _i, _p, _p, _p, _p, _p, _p],
+    "lasr_rnnt_bwd": [_p, _i, _i, _i, _i, _i, _l, _p, _i, _p, _p, _i, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p],
+    "lasr_joint_fwd": [_p, _p, _i, _i, _i, _i, _p, _i, _p],
+    "lasr_joint_reduce": [_p, _i, _i, _i, _i, _i, _p, _p, _i, _p],
+    "lasr_lstm_cell_fwd": [_p, _l, _p, _p, _i, _i, _p, _p, _i, _l, _p],
+    "lasr_lstm_cell_bwd": [_p, _l, _p, _p, _p, _p, _i, _l, _p, _p, _i, _i, _p, _i, _l, _p, _p],
     "lasr_ctc_bwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _i, _p, _i, _f, _p, _p],
     "lasr_lsm_kl_fwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _p],
     "lasr_lsm_kl_bwd": [_p, _i, _i, _i, _l, _p, _i, _f, _p, _p, _i, _f, _p, _p],

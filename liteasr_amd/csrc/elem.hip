@@ -40,7 +40,7 @@ __global__ void embed_pe_fwd_kernel(const int32_t* ids, int R, int L, int D, con
   const int64_t n = (int64_t)R * D;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(e / D), c = (int)(e - (int64_t)r * D);
-    const float v = E[(int64_t)ids[r] * D + c] * xscale + pe[(int64_t)(r % L) * D + c];
+    const float v = E[(int64_t)ids[r] * D + c] * xscale + (pe ? pe[(int64_t)(r % L) * D + c] : 0.f);
     y[e] = from_f<TY>(v * drop_mul(d, (uint64_t)e));
   }
 }
@@ -60,6 +60,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
   for (int i = threadIdx.x; i < R; i += blockDim.x) sid[i] = ids[i];
   __syncthreads();
   const int r = blockIdx.x, id = sid[r];
+  if (id < 0) return;  // a negative id contributes nothing (padding_idx rows, rnn_decoder.py:20)
   int earlier = 0;
   for (int k = threadIdx.x; k < r; k += blockDim.x) earlier |= sid[k] == id;
   if (__syncthreads_or(earlier)) return;  // not the first occurrence (uniform)

@@ -287,9 +287,13 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
     rc = lasr_check_launch("lasr_gemm/splitk_reduce");
   }
   if (rc || !a->rowsum || rs_fused) return rc;
-  // unfused: rowsum of A[M, K] (lda_m == 1) = column sums of the [K, M] matrix, ld lda_k
-  return lasr_colsum(a->A, a->in_dtype, a->K, a->M, a->lda_k, a->rowsum, 1, (float*)a->workspace,
-                     a->workspace_bytes / 4, stream);
+  // unfused: rowsum of A[M, K] (lda_m == 1) = column sums of the [K, M] matrix, ld lda_k.
+  // Its scratch starts after the split-K partials (which a partials-only call leaves in the
+  // workspace for the caller's reduction: they must not be overwritten).
+  const int64_t used = split > 1 ? (int64_t)split * batch * a->M * a->N : 0;
+  LASR_CHECK_ARG(a->workspace && a->workspace_bytes / 4 > used, "lasr_gemm: no workspace left for the rowsum");
+  return lasr_colsum(a->A, a->in_dtype, a->K, a->M, a->lda_k, a->rowsum, 1, (float*)a->workspace + used,
+                     a->workspace_bytes / 4 - used, stream);
 }
 
 

@@ -98,6 +98,13 @@ LASR_DEV void epi_core(const GemmP& p, uint64_t dbase, float (&v)[N], const floa
       } else if (p.act == LASR_ACT_RELU) {
 #pragma unroll
         for (int q = 0; q < N; ++q) g[q] = v[q] > 0.f ? 1.f : 0.f;
+      } else if (p.act == LASR_ACT_TANH) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+          v[q] = tanhf(v[q]);
+          g[q] = 1.f - v[q] * v[q];
+        }
+        acted = true;
       } else {
 #pragma unroll
         for (int q = 0; q < N; ++q) g[q] = 1.f;
@@ -118,6 +125,9 @@ LASR_DEV void epi_core(const GemmP& p, uint64_t dbase, float (&v)[N], const floa
   } else if (p.act == LASR_ACT_RELU) {
 #pragma unroll
     for (int q = 0; q < N; ++q) v[q] = fmaxf(v[q], 0.f);
+  } else if (p.act == LASR_ACT_TANH) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = tanhf(v[q]);
   }
   if (has_aux) {
     if (p.aux_act == LASR_ACT_GATE) {
@@ -126,6 +136,9 @@ LASR_DEV void epi_core(const GemmP& p, uint64_t dbase, float (&v)[N], const floa
     } else if (p.aux_act == LASR_ACT_RELU) {
 #pragma unroll
       for (int q = 0; q < N; ++q) v[q] *= auxv[q] > 0.f ? 1.f : 0.f;
+    } else if (p.aux_act == LASR_ACT_TANH) {  // aux = the stored tanh output y: tanh' = 1 - y^2
+#pragma unroll
+      for (int q = 0; q < N; ++q) v[q] *= 1.f - auxv[q] * auxv[q];
     } else {
 #pragma unroll
       for (int q = 0; q < N; ++q) v[q] *= swish_grad(auxv[q]);

@@ -269,7 +269,8 @@ def gemm(
             grouped = (tm.value, tn.value) in _GROUP_TILES and (fl.value & 5) == 5
         if sp > 1:
             # partials-only launch (split_k = -1) into a buffer that lives until the flush
-            nrs = sp * M if rowsum is not None else 0
+            # rowsum partials (fused) or the column-sum scratch (unfused, fp32 operands)
+            nrs = (sp + 128) * M if rowsum is not None else 0
             part = torch.empty(sp * M * Nn + nrs, dtype=torch.float32, device=c.device)
             # the explicit slice count on both paths: `part` is sized for sp slices, and a
             # re-derived auto split (-1) could differ from sp after the group adjustment

@@ -87,12 +87,15 @@ def RG(x):
 
 class ActGate(torch.autograd.Function):
     """h = act(u) (rounded by the caller); du = bf16(dh * bf16(act'(u))) -- the fc1 epilogue
-    stores the gate act'(u) * keep in bf16 and the dz GEMM multiplies by it (dropout 0)."""
+    stores the gate act'(u) * keep in bf16 and the dz GEMM multiplies by it (dropout 0).
+    `gate` (optional): use this stored gate instead of act'(u) -- a test feeds the kernel's
+    own ReLU gate so that a pre-activation within accumulation error of zero (a kink the
+    two sides may resolve differently) cannot decide a gradient comparison."""
 
     @staticmethod
-    def forward(ctx, u, act):
+    def forward(ctx, u, act, gate=None):
         ctx.save_for_backward(u)
-        ctx.act = act
+        ctx.act, ctx.gate = act, gate
         if act == "swish":
             return u * torch.sigmoid(u)
         return F.relu(u)
@@ -100,12 +103,14 @@ class ActGate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh):
         (u,) = ctx.saved_tensors
-        if ctx.act == "swish":
+        if ctx.gate is not None:
+            gate = ctx.gate.to(u.dtype).view_as(u)
+        elif ctx.act == "swish":
             s = torch.sigmoid(u)
             gate = s * (1 + u * (1 - s))
         else:
             gate = (u > 0).to(u.dtype)
-        return bf16(dh * bf16(gate)), None
+        return bf16(dh * bf16(gate)), None, None
 
 
 def _relshift_index(T):
@@ -204,9 +209,13 @@ def subsample(x, p, name):
     return linear(y.transpose(1, 2).reshape(B, T, C * Fp), p, name + ".out")
 
 
-def ffn(x_ln, p, name, act):
-    """PositionwiseFeedForward (liteasr/nets/feed_forward.py:18-19), swish.py:14-16."""
-    h = R(ActGate.apply(linear(x_ln, p, name + ".fc1"), act))
+def ffn(x_ln, p, name, act, gate=None, pre=None):
+    """PositionwiseFeedForward (liteasr/nets/feed_forward.py:18-19), swish.py:14-16.  `gate`:
+    see ActGate; `pre` (a list) receives the fc1 pre-activation."""
+    u = linear(x_ln, p, name + ".fc1")
+    if pre is not None:
+        pre.append(u.detach())
+    h = R(ActGate.apply(u, act, gate))
     return linear(h, p, name + ".fc2")
 
 
