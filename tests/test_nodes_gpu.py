@@ -189,15 +189,17 @@ def test_decoder_layer_node_config2():
     y = y64 + E.G(E.mha(E.RG(E.layer_norm(y64, leaf, n + ".self_attn_norm")), None, smask, leaf, n + ".self_attn", H))
     y = y + E.G(E.mha(E.RG(E.layer_norm(y, leaf, n + ".src_attn_norm")), m64, mm, leaf, n + ".src_attn", H))
     # the ReLU gate the kernel stored (act'(u), bf16 0/1) drives the oracle's FFN backward;
-    # the gate itself must equal the oracle's relu'(u) wherever |u| is not within 1e-4 of
-    # the largest pre-activation (kinks the two accumulation orders may resolve differently)
+    # the gate itself must equal the oracle's relu'(u) wherever |u| exceeds 2e-3 of the
+    # largest pre-activation: u reaches the two sides through bf16-rounded LayerNorm /
+    # attention outputs whose rare rounding straddles move it by ~1e-3 (measured: flips only
+    # at |u| <= 0.0045 of max |u| = 5.2)
     gate = sv.layers[0].z.double().cpu().view(B, L1, -1)
     pre = []
     y = y + E.G(E.ffn(E.RG(E.layer_norm(y, leaf, n + ".feed_forward_norm")), leaf, n + ".feed_forward", "relu",
                       gate=gate, pre=pre))
     u = pre[0]
     flip = (gate > 0) != (u > 0)
-    assert (u[flip].abs() <= 1e-4 * u.abs().max()).all(), u[flip].abs().max()
+    assert (u[flip].abs() <= 2e-3 * u.abs().max()).all(), u[flip].abs().max()
     out = E.RG(E.linear(E.RG(E.layer_norm(y, leaf, "decoder.after_norm")), leaf, "decoder.linear_out"))
     out.backward(dlog.double().view(B, L1, V))
     gmax = max(v.grad.abs().max().item() for v in leaf.values() if v.grad is not None)
