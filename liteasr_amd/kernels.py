@@ -738,3 +738,48 @@ def glancing_mix(replace, a, b, out, out2=None, backward=False):
     rows, D = out.shape
     N.call("lasr_glancing_mix", rows, D, ptr(replace), ptr(a), ptr(b), ptr(out), ptr(out2), int(backward),
            stream())
+
+
+# ------------------------------------------------------------------ transducer ---
+def rnnt_fwd(logits, targets, ilen, tlen, blank, lse, lp, alpha, beta, nll):
+    """RNN-T lattice forward (lasr_rnnt_fwd): logits [B, T, U1, V] (rows unit-stride, evenly
+    spaced), targets int32 [B, Lmax >= U1-1], ilen / tlen int32 [B]."""
+    B, T, U1, V = logits.shape
+    N.call("lasr_rnnt_fwd", ptr(logits), dt(logits), B, T, U1, V, _rows_ld(logits, 3), ptr(targets), targets.shape[1],
+           ptr(ilen), ptr(tlen), blank, ptr(lse), ptr(lp), ptr(alpha), ptr(beta), ptr(nll), stream())
+
+
+def rnnt_bwd(logits, targets, ilen, tlen, blank, lse, lp, alpha, beta, nll, grad, gscale, gdev=None):
+    B, T, U1, V = logits.shape
+    ld = _rows_ld(logits, 3)
+    assert grad.shape == logits.shape and _rows_ld(grad, 3) == ld
+    N.call("lasr_rnnt_bwd", ptr(logits), dt(logits), B, T, U1, V, ld, ptr(targets), targets.shape[1], ptr(ilen),
+           ptr(tlen), blank, ptr(lse), ptr(lp), ptr(alpha), ptr(beta), ptr(nll), ptr(grad), dt(grad), gscale,
+           ptr(gdev), stream())
+
+
+def joint_fwd(e, d, B, T, U1, z):
+    """z[(b T + t) U1 + u] = tanh(e[b T + t] + d[u B + b]) (lasr_joint_fwd); e, d fp32."""
+    J = e.shape[1]
+    assert e.is_contiguous() and d.is_contiguous() and z.is_contiguous() and e.dtype == d.dtype == torch.float32
+    N.call("lasr_joint_fwd", ptr(e), ptr(d), B, T, U1, J, ptr(z), dt(z), stream())
+
+
+def joint_reduce(dz, B, T, U1, de, dd):
+    J = dz.shape[1]
+    assert dz.is_contiguous() and de.is_contiguous() and dd.is_contiguous() and de.dtype == dd.dtype
+    N.call("lasr_joint_reduce", ptr(dz), dt(dz), B, T, U1, J, ptr(de), ptr(dd), dt(de), stream())
+
+
+def lstm_cell_fwd(gates, bias, c_prev, c_out, h_out):
+    """gates [B, >=4H] fp32 (row stride any), h_out [B, H] (row stride any)."""
+    B, H = c_out.shape
+    N.call("lasr_lstm_cell_fwd", ptr(gates), gates.stride(0), ptr(bias), ptr(c_prev), B, H, ptr(c_out), ptr(h_out),
+           dt(h_out), h_out.stride(0), stream())
+
+
+def lstm_cell_bwd(gates, bias, c, c_prev, dh_out, dh_rec, dc_next, dgates, dc_prev):
+    B, H = c.shape
+    N.call("lasr_lstm_cell_bwd", ptr(gates), gates.stride(0), ptr(bias), ptr(c), ptr(c_prev), ptr(dh_out),
+           dt(dh_out) if dh_out is not None else 0, dh_out.stride(0) if dh_out is not None else 0, ptr(dh_rec),
+           ptr(dc_next), B, H, ptr(dgates), dt(dgates), dgates.stride(0), ptr(dc_prev), stream())

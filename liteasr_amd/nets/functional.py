@@ -27,7 +27,7 @@ from types import SimpleNamespace
 import torch
 
 from .. import kernels as K
-from .._native import ACT_GATE, ACT_NONE, ACT_RELU, ACT_SWISH
+from .._native import ACT_GATE, ACT_NONE, ACT_RELU, ACT_SWISH, ACT_TANH
 
 F32 = torch.float32
 LN_EPS = 1e-12
@@ -986,6 +986,178 @@ class EncoderOutFn(torch.autograd.Function):
         enc.after_norm_ready()
         ctx.sv = None
         return dx, None, None, None
+
+
+# ============================================================== transducer ======
+def lstm_layer_fwd(X, w, B, U1, H, adt, p_out, seed):
+    """One LSTMCell layer over U1 time-major steps (liteasr/nets/rnn_decoder.py:49-80):
+    G = X W_ih^T + b_ih for all steps in one GEMM, then per step G[t] += h_{t-1} W_hh^T (GEMM,
+    beta 1) and the cell kernel (b_hh added there).  X [U1*B, in] (compute dtype).  Returns
+    (Y [U1*B, H] the output sequence after the layer's dropout, saved state)."""
+    dev = X.device
+    G = _e((U1, B, 4 * H), F32, dev)
+    K.linear(X, w.Wih, G.view(U1 * B, 4 * H), bias=w.bih)
+    hs = _e((U1 + 1, B, H), adt, dev)  # hs[0] = zero state, hs[t+1] = h_t
+    K.fill(hs[0], 0.0)
+    cs = _e((U1, B, H), F32, dev)
+    for t in range(U1):
+        if t > 0:
+            K.gemm(hs[t], w.Whh.t(), G[t], beta=1.0)
+        K.lstm_cell_fwd(G[t], w.bhh, cs[t - 1] if t > 0 else None, cs[t], hs[t + 1])
+    Y = hs[1:].reshape(U1 * B, H)
+    if p_out > 0:
+        Yd = _e((U1 * B, H), adt, dev)
+        K.pe_fwd(Y, U1 * B, 1, H, None, 1.0, Yd, p_out, seed)
+        Y = Yd
+    return Y, SimpleNamespace(X=X, G=G, hs=hs, cs=cs)
+
+
+def lstm_layer_bwd(dY, sv, w, g, B, U1, H, adt, p_out, seed):
+    """Backward of lstm_layer_fwd: dY [U1*B, H] fp32 gradient of the output sequence ->
+    parameter gradients into g, returns dX [U1*B, in] fp32.  Per step (reversed) the cell
+    kernel forms the gate gradients dG[t] and dc, and dh_{t-1} = dG[t] W_hh (GEMM); the
+    weight gradients are one GEMM each over all U1*B rows (dW_hh against hs[0:U1], the
+    states each step consumed)."""
+    dev = dY.device
+    if p_out > 0:
+        dYd = _e(dY.shape, F32, dev)
+        K.branch_grad(dY, dYd, 1.0, p_out, seed)
+        dY = dYd
+    dG = _e((U1, B, 4 * H), adt, dev)
+    dh_rec = _e((B, H), F32, dev)
+    dcs = [_e((B, H), F32, dev), _e((B, H), F32, dev)]
+    dY3 = dY.view(U1, B, H)
+    for t in range(U1 - 1, -1, -1):
+        last = t == U1 - 1
+        K.lstm_cell_bwd(sv.G[t], w.bhh, sv.cs[t], sv.cs[t - 1] if t > 0 else None, dY3[t],
+                        None if last else dh_rec, None if last else dcs[(t + 1) & 1], dG[t],
+                        dcs[t & 1] if t > 0 else None)
+        if t > 0:
+            K.gemm(dG[t], w.Whh, dh_rec)
+    dG2 = dG.view(U1 * B, 4 * H)
+    K.gemm(dG2.t(), sv.hs[:U1].reshape(U1 * B, H), g.Whh, beta=1.0, split_k=0, rowsum=g.bhh)
+    K.gemm(dG2.t(), sv.X, g.Wih, beta=1.0, split_k=0, rowsum=g.bih)
+    dX = _e((U1 * B, sv.X.shape[1]), F32, dev)
+    K.gemm(dG2, w.Wih, dX)
+    return dX
+
+
+class TransducerHeadsFn(torch.autograd.Function):
+    """Everything of Transducer.forward after the conformer layers (liteasr/models/
+    transducer.py:106-121,199-203): encoder after_norm, lin_enc, the prediction network
+    (nets/rnn_decoder.py:69-80: embedding with padding_idx 0, LSTMCell layers, dropouts),
+    lin_dec, z = tanh(enc + dec) (csrc/rnnt.hip joint_tanh_fwd), lin_jnt.  ids: the
+    decoder input ys_in time-major [U1*B] int32.  Returns h_jnt as [B*T'*U1, V] rows."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, model, env, ids, U1):
+        dev, adt = x.device, env.adt
+        enc, dec, jp = model.encoder, model.decoder, model.joint_params
+        B, T = env.B, env.T
+        M, R = B * T, U1 * B
+        tr = env.training
+        x = x.contiguous()
+        we = enc.after_norm_weights()
+        h, _, me, re = ln_forward(x, we.g, we.b, adt)
+        wj = jp.weights()
+        J = wj.We.shape[0]
+        e = _e((M, J), F32, dev)
+        K.linear(h, wj.We, e, bias=wj.be)
+        # prediction network
+        wd = dec.weights()
+        p = dec.rates.drop if tr else 0.0
+        emb = _e((R, dec.h_dim), adt, dev)
+        K.embed_pe_fwd(ids, U1, wd.E, None, 1.0, emb, p, env.seed + 6)
+        Xl, layers = emb, []
+        for i, lw in enumerate(wd.layers):
+            Xl, lsv = lstm_layer_fwd(Xl, lw, B, U1, dec.h_units, adt, p, env.seed + 7 + i)
+            layers.append(lsv)
+        d = _e((R, J), F32, dev)
+        K.linear(Xl, wj.Wd, d)
+        z = _e((M * U1, J), adt, dev)
+        K.joint_fwd(e, d, B, T, U1, z)
+        V = wj.Wj.shape[0]
+        out = K.padded_rows(M * U1, V, adt, dev)
+        K.linear(z, wj.Wj, out, bias=wj.bj)
+        ids_bwd = ids.masked_fill(ids == 0, -1)  # padding_idx 0: no embedding gradient
+        ctx.sv = SimpleNamespace(x=x, h=h, me=me, re=re, z=z, Y=Xl, layers=layers, ids=ids_bwd, dims=(B, T, U1, J),
+                                 p=p)
+        ctx.model, ctx.env = model, env
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        sv, model, env = ctx.sv, ctx.model, ctx.env
+        enc, dec, jp = model.encoder, model.decoder, model.joint_params
+        B, T, U1, J = sv.dims
+        M, R = B * T, U1 * B
+        dev, adt = sv.x.device, env.adt
+        wj, gj = jp.weights(), jp.grads()
+        g_out = _rows2d(g_out, M * U1)
+        # lin_jnt
+        K.gemm(g_out.t(), sv.z, gj.Wj, beta=1.0, split_k=0, rowsum=gj.bj)
+        model.unit_ready("lin_jnt")
+        dz = _e((M * U1, J), adt, dev)
+        K.gemm(g_out, wj.Wj, dz, aux=sv.z, aux_act=ACT_TANH)
+        de, dd = _e((M, J), adt, dev), _e((R, J), adt, dev)
+        K.joint_reduce(dz, B, T, U1, de, dd)
+        # lin_dec and the prediction network
+        K.gemm(dd.t(), sv.Y, gj.Wd, beta=1.0, split_k=0)
+        model.unit_ready("lin_dec")
+        dY = _e((R, dec.h_units), F32, dev)
+        K.gemm(dd, wj.Wd, dY)
+        wd, gd = dec.weights(), dec.grads()
+        for i in range(len(wd.layers) - 1, -1, -1):
+            dY = lstm_layer_bwd(dY, sv.layers[i], wd.layers[i], gd.layers[i], B, U1, dec.h_units, adt, sv.p,
+                                env.seed + 7 + i)
+        if sv.p > 0:
+            dE = _e(dY.shape, F32, dev)
+            K.branch_grad(dY, dE, 1.0, sv.p, env.seed + 6)
+            dY = dE
+        K.embed_bwd(sv.ids, dY, 1.0, gd.E)
+        dec.on_grads_ready()
+        # lin_enc
+        K.gemm(de.t(), sv.h, gj.We, beta=1.0, split_k=0, rowsum=gj.be)
+        model.unit_ready("lin_enc")
+        dh = _e((M, sv.h.shape[1]), F32, dev)
+        K.gemm(de, wj.We, dh)
+        # encoder after_norm
+        we, ge = enc.after_norm_weights(), enc.after_norm_grads()
+        dx = _e(sv.x.shape, F32, dev)
+        K.layernorm_bwd(sv.x, dh, we.g, sv.me, sv.re, dx, ge.g, ge.b)
+        enc.after_norm_ready()
+        ctx.sv = None
+        return dx, None, None, None, None, None
+
+
+class RNNTLossFn(torch.autograd.Function):
+    """RNNTLoss (liteasr/criterions/rnnt.py:53-72): batch mean of -log P(y|x) over the raw
+    joint logits [B, T, U1, V] with the log-softmax fused (csrc/rnnt.hip); the backward
+    writes d loss / d logits scaled by the incoming device gradient, no host sync."""
+
+    @staticmethod
+    def forward(ctx, logits, targets, ilen, tlen, blank):
+        dev = logits.device
+        B, T, U1, V = logits.shape
+        rows = B * T * U1
+        lse, lp = _e(rows, F32, dev), _e(rows * 2, F32, dev)
+        alpha, beta, nll = _e(rows, F32, dev), _e(rows, F32, dev), _e(B, F32, dev)
+        K.rnnt_fwd(logits, targets, ilen, tlen, blank, lse, lp, alpha, beta, nll)
+        loss = _e(1, F32, dev)
+        K.loss_combine(nll, 1.0 / B, None, 0.0, loss)
+        ctx.sv = (logits, targets, ilen, tlen, blank, lse, lp, alpha, beta, nll)
+        ctx.nll = nll
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, targets, ilen, tlen, blank, lse, lp, alpha, beta, nll = ctx.sv
+        B, T, U1, V = logits.shape
+        grad = K.padded_rows(B * T * U1, V, logits.dtype, logits.device).view(B, T, U1, V)
+        K.rnnt_bwd(logits, targets, ilen, tlen, blank, lse, lp, alpha, beta, nll, grad, 1.0 / B,
+                   gdev=g.contiguous().float())
+        ctx.sv = None
+        return grad, None, None, None, None
 
 
 # ================================================================ inference ===

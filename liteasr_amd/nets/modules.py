@@ -501,3 +501,62 @@ class Predictor(_Bound):
         return self._cached("g", lambda: SimpleNamespace(Wc=self._g("conv.weight"), bc=self._g("conv.bias"),
                                                          Wl=self._g("lin.weight"), bl=self._g("lin.bias")))
 
+
+
+class LSTMCell(nn.LSTMCell):
+    """torch.nn.LSTMCell parameter container (weight_ih, weight_hh, bias_ih, bias_hh; gate
+    order i, f, g, o) of liteasr/nets/rnn_decoder.py:21-24; the arithmetic runs in
+    csrc/rnnt.hip (lstm_cell_fwd / bwd) around the host's recurrent GEMMs."""
+
+    seed = 0
+
+    def flat_groups(self):
+        return []
+
+
+class RNNDecoder(_Bound):
+    """liteasr/nets/rnn_decoder.py:10-80 (the Transducer's prediction network): Embedding
+    (padding_idx 0) -> dropout -> n_layer LSTMCells, dropout after each cell's output."""
+
+    def __init__(self, i_dim, h_dim, h_units, n_layer, dropout_rate):
+        super().__init__()
+        self.embed = nn.Embedding(i_dim, h_dim, padding_idx=0)
+        self.dropout_embed = nn.Dropout(dropout_rate)
+        self.dec_layers = nn.ModuleList([LSTMCell(h_dim, h_units)] +
+                                        [LSTMCell(h_units, h_units) for _ in range(1, n_layer)])
+        self.dropout_dec = nn.ModuleList([nn.Dropout(dropout_rate) for _ in range(n_layer)])
+        self.h_dim, self.h_units, self.n_layer = h_dim, h_units, n_layer
+        self.rates = SimpleNamespace(drop=dropout_rate, pos=0.0, self_att=0.0, src_att=0.0, ff=0.0)
+
+    def weights(self):
+        return self._cached("w", lambda: SimpleNamespace(
+            E=self._p("embed.weight"),
+            layers=[SimpleNamespace(Wih=self._w(f"dec_layers.{i}.weight_ih"), Whh=self._w(f"dec_layers.{i}.weight_hh"),
+                                    bih=self._p(f"dec_layers.{i}.bias_ih"), bhh=self._p(f"dec_layers.{i}.bias_hh"))
+                    for i in range(self.n_layer)]))
+
+    def grads(self):
+        return self._cached("g", lambda: SimpleNamespace(
+            E=self._g("embed.weight"),
+            layers=[SimpleNamespace(Wih=self._g(f"dec_layers.{i}.weight_ih"), Whh=self._g(f"dec_layers.{i}.weight_hh"),
+                                    bih=self._g(f"dec_layers.{i}.bias_ih"), bhh=self._g(f"dec_layers.{i}.bias_hh"))
+                    for i in range(self.n_layer)]))
+
+
+class Joint(_Bound):
+    """Transducer.joint's projections (liteasr/models/transducer.py:91-95,199-203) as one
+    bound view bundle over the top-level lin_enc / lin_dec / lin_jnt parameters."""
+
+    def __init__(self, owner):
+        super().__init__()
+        object.__setattr__(self, "_owner", owner)  # not a submodule: keys stay top-level
+
+    def weights(self):
+        return self._cached("w", lambda: SimpleNamespace(
+            We=self._w("lin_enc.weight"), be=self._p("lin_enc.bias"), Wd=self._w("lin_dec.weight"),
+            Wj=self._w("lin_jnt.weight"), bj=self._p("lin_jnt.bias")))
+
+    def grads(self):
+        return self._cached("g", lambda: SimpleNamespace(
+            We=self._g("lin_enc.weight"), be=self._g("lin_enc.bias"), Wd=self._g("lin_dec.weight"),
+            Wj=self._g("lin_jnt.weight"), bj=self._g("lin_jnt.bias")))

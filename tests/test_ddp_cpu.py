@@ -213,7 +213,18 @@ def _fire_units(model, rank):
             model.unit_ready(name)
 
 
-def _paraformer_worker(rank, world, port, q):
+def _tiny_transducer():
+    from liteasr_amd.models.transducer import Transducer, TransducerConfig
+    from liteasr_amd.utils.cfg import resolve_self
+
+    c = TransducerConfig(input_dim=40, vocab_size=20, enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_layers=2,
+                         activation="swish", enc_arch="conformer", dec_dim=16, dec_units=48, dec_layers=2,
+                         joint_dim=24)
+    resolve_self(c)
+    return Transducer(c)
+
+
+def _paraformer_worker(rank, world, port, q, make=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -221,7 +232,7 @@ def _paraformer_worker(rank, world, port, q):
         from liteasr_amd.distributed.ddp import DistributedDataParallel
 
         torch.manual_seed(200 + rank)
-        model = _tiny_paraformer()
+        model = (make or _tiny_paraformer)()
         ddp = DistributedDataParallel(model, bucket_cap_mb=0.02)
         red = ddp.reducer
         model.store.ensure_grad().zero_()
@@ -239,10 +250,12 @@ def _paraformer_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_flat_ddp_paraformer_gloo_world2():
-    """DDP over the Paraformer (predictor, target embedding, no CTC head): every
-    parameter sits in a reducer unit, every unit's hook completes its bucket, gradients
-    average over the two ranks."""
+@pytest.mark.parametrize("which", ["paraformer", "transducer"])
+def test_flat_ddp_other_heads_gloo_world2(which):
+    """DDP over the Paraformer (predictor, target embedding, no CTC head) and the
+    Transducer (joint projections, LSTM prediction network): every parameter sits in a
+    reducer unit, every unit's hook completes its bucket, gradients average over the two
+    ranks."""
     import socket
 
     s = socket.socket()
@@ -251,7 +264,8 @@ def test_flat_ddp_paraformer_gloo_world2():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_paraformer_worker, args=(r, 2, port, q)) for r in range(2)]
+    make = _tiny_paraformer if which == "paraformer" else _tiny_transducer
+    procs = [ctx.Process(target=_paraformer_worker, args=(r, 2, port, q, make)) for r in range(2)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=240) for _ in procs)
@@ -259,7 +273,8 @@ def test_flat_ddp_paraformer_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     a, b = out[0], out[1]
-    assert a["units"][:4] == ["decoder", "embed", "predictor", "encoder.after_norm"]
+    heads = {"paraformer": ["decoder", "embed", "predictor"], "transducer": ["lin_jnt", "lin_dec", "decoder", "lin_enc"]}
+    assert a["units"][:len(heads[which]) + 1] == heads[which] + ["encoder.after_norm"]
     assert a["nbuckets"] >= 2 and a["record"] == list(range(a["nbuckets"]))
     assert (a["flat"] == b["flat"]).all()
     g = torch.from_numpy(a["grad"])
