@@ -530,7 +530,7 @@ def gen_paraformer():
 
 
 def gen_transducer():
-    """Tiny Transducer (liteasr/models/transducer.py; Conformer encoder d 32 x 2 with relative
+    """Tiny Transducer (liteasr/models/transducer.py; Conformer encoder d 64 x 2 with relative
     PE and Swish, LSTM decoder dec_dim 16 / 48 units x 2 layers, joint 24, V 20, F 40), seed-42
     init state_dict, a batch with an empty transcript: the encoder output, the decoder
     output, the joint logits h_jnt (B, T', Lmax+1, V) and every parameter gradient of the
@@ -545,7 +545,7 @@ def gen_transducer():
     from liteasr.models.transducer import Transducer
 
     cfg = types.SimpleNamespace(joint_dim=24, dropout_rate=0.0, enc_arch=TEA.Conformer, use_rel=True, input_dim=40,
-                                enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_dropout_rate=0.0,
+                                enc_dim=64, enc_ff_dim=128, enc_attn_heads=4, enc_dropout_rate=0.0,
                                 enc_pos_dropout_rate=0.0, enc_attn_dropout_rate=0.0, enc_ff_dropout_rate=0.0,
                                 enc_layers=2, activation="swish", dec_arch=TDA.LSTM, vocab_size=20, dec_dim=16,
                                 dec_units=48, dec_dropout_rate=0.0, dec_layers=2)

@@ -217,7 +217,7 @@ def _tiny_transducer():
     from liteasr_amd.models.transducer import Transducer, TransducerConfig
     from liteasr_amd.utils.cfg import resolve_self
 
-    c = TransducerConfig(input_dim=40, vocab_size=20, enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_layers=2,
+    c = TransducerConfig(input_dim=40, vocab_size=20, enc_dim=64, enc_ff_dim=128, enc_attn_heads=4, enc_layers=2,
                          activation="swish", enc_arch="conformer", dec_dim=16, dec_units=48, dec_layers=2,
                          joint_dim=24)
     resolve_self(c)

@@ -351,7 +351,7 @@ def test_paraformer_oracle_matches_reference(case):
         assert err < 1e-4, (k, err)
 
 
-TRANSDUCER_GOLDEN = O.default_cfg(enc_dim=32, enc_heads=4, enc_ff=64, enc_layers=2, vocab_size=20, input_dim=40,
+TRANSDUCER_GOLDEN = O.default_cfg(enc_dim=64, enc_heads=4, enc_ff=128, enc_layers=2, vocab_size=20, input_dim=40,
                                   dec_layers=2, dec_units=48)
 
 
