@@ -166,6 +166,44 @@ int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype,
                        float* dgamma, float* dbeta, float* workspace, int64_t ws_floats,
                        void* gb, int gb_dtype, float bscale, float bp, uint64_t bseed,
                        void* stream);
+/* ------------------------------------------------------------------------
+ * Full-row GEMM with the LayerNorm in its epilogue: the residual projections of a
+ * Conformer layer and the following sub-block's norm (liteasr/nets/conformer_layer.py:37-78
+ * residual adds, layer_norm.py:20), and their backward (the input-gradient GEMM of a
+ * sub-block's first projection + that norm's backward).  Tiles of 32 rows x all D columns
+ * (D = 256 or 512), K % 64 == 0, bf16 A/W with 16-B aligned rows; every [M, D] buffer
+ * below is contiguous.  Outputs are bit-identical to the two-launch path they replace
+ * (lasr_gemm with its res epilogue + lasr_layernorm_fwd / lasr_layernorm2_fwd; lasr_gemm
+ * to a bf16 dln + lasr_layernorm_bwd).
+ *  lasr_linear_res_ln:    A [M, K], W [D, K] (nn.Linear weight):
+ *    out = res + res_scale * dropout(A W^T + bias)   (fp32; dropout = lasr_gemm's, one
+ *                                                    draw per column pair of row-major out)
+ *    y1 = LN1(out) (y1_dtype) + mean1 / rstd1; if gamma2: y1 must be fp32 and
+ *    y2 = LN2(y1) (bf16) + mean2 / rstd2 (the chained norms of lasr_layernorm2_fwd).
+ *  lasr_linear_dx_ln_bwd: A = dY [M, K], W [K, D]:  dln = bf16(dY W), then
+ *    dx = LN1'(dln; x, gamma1, mean1, rstd1) (+ dres), gb = bscale * dropmask(bp, bseed) * dx
+ *    (bf16, optional), and part = the dgamma / dbeta partial rows [cdiv(M, 16)][2 D]
+ *    exactly as lasr_layernorm_bwd's workspace holds them (dgamma = columns [0, D), dbeta =
+ *    [D, 2D)); with dgamma and dbeta set they are also reduced into them (+=) as
+ *    lasr_layernorm_bwd does, else the caller reduces them (lasr_reduce_multi).
+ * ---------------------------------------------------------------------- */
+typedef struct lasr_row_ln_args {
+  int M, D, K;
+  const void* A; int64_t lda;
+  const void* W; int64_t ldw;
+  const float* gamma1; const float* beta1; float eps;
+  float* mean1; float* rstd1;
+  /* forward */
+  const float* bias; const float* res; float res_scale; float drop_p; uint64_t drop_seed;
+  float* out; void* y1; int y1_dtype;
+  const float* gamma2; const float* beta2; void* y2; float* mean2; float* rstd2;
+  /* backward */
+  const float* x; const float* dres; float* dx; void* gb; float bscale; float bp; uint64_t bseed;
+  float* part; float* dgamma; float* dbeta;
+} lasr_row_ln_args;
+int lasr_linear_res_ln(const lasr_row_ln_args* args, void* stream);
+int lasr_linear_dx_ln_bwd(const lasr_row_ln_args* args, void* stream);
+
 /* gb = scale * dropmask(seed) * dx  (residual-branch gradient, standalone form). */
 int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_dtype,
                      float scale, float p, uint64_t seed, void* stream);

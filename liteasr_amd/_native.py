@@ -75,6 +75,21 @@ class CifArgs(C.Structure):
     ]
 
 
+class RowLnArgs(C.Structure):
+    """Mirror of ``lasr_row_ln_args``."""
+
+    _fields_ = [
+        ("M", _i), ("D", _i), ("K", _i),
+        ("A", _p), ("lda", _l), ("W", _p), ("ldw", _l),
+        ("gamma1", _p), ("beta1", _p), ("eps", _f), ("mean1", _p), ("rstd1", _p),
+        ("bias", _p), ("res", _p), ("res_scale", _f), ("drop_p", _f), ("drop_seed", _u),
+        ("out", _p), ("y1", _p), ("y1_dtype", _i),
+        ("gamma2", _p), ("beta2", _p), ("y2", _p), ("mean2", _p), ("rstd2", _p),
+        ("x", _p), ("dres", _p), ("dx", _p), ("gb", _p), ("bscale", _f), ("bp", _f), ("bseed", _u),
+        ("part", _p), ("dgamma", _p), ("dbeta", _p),
+    ]
+
+
 class ReduceSeg(C.Structure):
     """Mirror of ``lasr_reduce_seg``."""
 
@@ -101,6 +116,8 @@ SIGNATURES = {
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
                          _p, _p, _p, _i, _i, _p, _p, _l, _p],
     "lasr_reduce_multi": [C.POINTER(ReduceSeg), _i, _p],
+    "lasr_linear_res_ln": [C.POINTER(RowLnArgs), _p],
+    "lasr_linear_dx_ln_bwd": [C.POINTER(RowLnArgs), _p],
     "lasr_dropout_scale": [_f],
     "lasr_colsum": [_p, _i, _l, _l, _l, _p, _i, _p, _l, _p],
     "lasr_layernorm2_fwd": [_p, _l, _i, _p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _p, _p],

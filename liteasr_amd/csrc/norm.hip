@@ -4,6 +4,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "ln_math.h"
 
 constexpr int LN_WAVES = 4;           // forward: one row per wave
 constexpr int LN_ROWS_PER_BLOCK = 16;  // backward: rows per block (one partial row each; 16: one row per wave, 2 blocks per CU)
@@ -25,19 +26,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, i
   ldv<NPL>(x + row * D + c0, v);
   ldv<NPL>(gamma + c0, g);
   ldv<NPL>(beta + c0, b);
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPL; ++i) s += v[i];
-  const float mu = wave_sum(s) * (1.f / D);
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPL; ++i) { const float dv = v[i] - mu; q += dv * dv; }
-  const float var = wave_sum(q) * (1.f / D);
-  const float rs = rsqrtf(var + eps);
+  float o[NPL], mu, rs;
+  ln_fwd_row<D, NPL>(v, g, b, eps, o, mu, rs);
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
-  float o[NPL];
-#pragma unroll
-  for (int i = 0; i < NPL; ++i) o[i] = (v[i] - mu) * rs * g[i] + b[i];
   stv<NPL>(y + row * D + c0, o);
   if (y2) {
     if (d2.p > 0.f) {
@@ -72,18 +63,8 @@ __global__ __launch_bounds__(256) void ln2_fwd_kernel(const float* __restrict__ 
   ldv<NPL>(b1 + c0, b);
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) s += v[i];
-    const float mu = wave_sum(s) * (1.f / D);
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) { const float dv = v[i] - mu; q += dv * dv; }
-    const float var = wave_sum(q) * (1.f / D);
-    const float rs = rsqrtf(var + eps);
-    float o[NPL];
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) o[i] = (v[i] - mu) * rs * g[i] + b[i];
+    float o[NPL], mu, rs;
+    ln_fwd_row<D, NPL>(v, g, b, eps, o, mu, rs);
     if (pass == 0) {
       if (lane == 0) { mean1[row] = mu; rstd1[row] = rs; }
       stv<NPL>(y + row * D + c0, o);
@@ -131,25 +112,16 @@ __global__ __launch_bounds__(1024) void ln_bwd_kernel(const TX* __restrict__ x,
     const int64_t row = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK + w * RPW + rr;
     if (row < rows) {
       const float mu = mean[row], rs = rstd[row];
-      float xv[NPL], d[NPL], g[NPL];
+      float xv[NPL], d[NPL];
       ldv<NPL>(x + row * D + c0, xv);
       ldv<NPL>(dy + row * D + c0, d);
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < NPL; ++i) {
-        xv[i] = (xv[i] - mu) * rs;  // x-hat
-        pg[i] += d[i] * xv[i];
-        pb[i] += d[i];
-        g[i] = d[i] * gm[i];
-        s1 += g[i];
-        s2 += g[i] * xv[i];
-      }
-      s1 = wave_sum(s1) * (1.f / D);
-      s2 = wave_sum(s2) * (1.f / D);
       float o[NPL], r[NPL];
-      if (dres) ldv<NPL>(dres + row * D + c0, r);
-#pragma unroll
-      for (int i = 0; i < NPL; ++i) o[i] = rs * (g[i] - s1 - xv[i] * s2) + (dres ? r[i] : 0.f);
+      if (dres) {
+        ldv<NPL>(dres + row * D + c0, r);
+        ln_bwd_row<D, NPL, true>(xv, d, gm, mu, rs, r, pg, pb, o);
+      } else {
+        ln_bwd_row<D, NPL, false>(xv, d, gm, mu, rs, r, pg, pb, o);
+      }
       stv<NPL>(dx + row * D + c0, o);
       if (gb) {
         float dm[NPL];

@@ -347,6 +347,70 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, gb=Non
         _defer(ws, nblk, 2 * D, dgamma, dbeta, split=D)
 
 
+# ------------------------------------------------- full-row GEMM + LayerNorm ---
+def _al16(t):
+    return t is None or t.data_ptr() % 16 == 0
+
+
+# The row kernel's main loop ingests the whole weight per 32-row workgroup, one workgroup per CU:
+# measured faster than GEMM + norm up to K = 768 (tools/row_ln_bench.py, profiles/r03), slower at
+# K = 2048, where the 64 x 64 GEMM's 2-3 workgroups per CU keep more of the LDS-DMA in flight.
+ROW_LN_MAX_K = int(os.environ.get("LASR_ROW_LN_MAX_K", "1024"))
+
+
+def row_ln_ok(a, w, D, max_k=None):
+    """Whether lasr_linear_res_ln / lasr_linear_dx_ln_bwd take a GEMM with A = a [M, K] and the
+    D-wide output: bf16, D in (256, 512), K % 64 == 0, unit column strides, 16-B rows; and
+    (the product policy) K <= max_k (default ROW_LN_MAX_K)."""
+    Kd = a.shape[-1]
+    return (a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and D in (256, 512) and a.dim() == 2
+            and Kd % 64 == 0 and Kd <= (ROW_LN_MAX_K if max_k is None else max_k) and a.stride(1) == 1
+            and a.stride(0) % 8 == 0 and w.is_contiguous() and _al16(a) and _al16(w))
+
+
+def linear_res_ln(x, w, out, y1, mean1, rstd1, g1, b1, eps, *, bias=None, res, res_scale=1.0, drop_p=0.0,
+                  drop_seed=0, g2=None, b2=None, y2=None, mean2=None, rstd2=None):
+    """out = res + res_scale * dropout(x @ w^T + bias) (fp32), y1 = LN1(out), optionally
+    y2 = LN2(y1): one launch (lasr_linear_res_ln), bit-identical to linear(..., res=...) +
+    layernorm_fwd / layernorm2_fwd.  x [M, K] bf16, w [D, K]; [M, D] buffers contiguous."""
+    M, Kd = x.shape
+    D = w.shape[0]
+    a = N.RowLnArgs()
+    a.M, a.D, a.K = M, D, Kd
+    a.A, a.lda, a.W, a.ldw = ptr(x), x.stride(0), ptr(w), w.stride(0)
+    a.gamma1, a.beta1, a.eps, a.mean1, a.rstd1 = ptr(g1), ptr(b1), eps, ptr(mean1), ptr(rstd1)
+    a.bias, a.res, a.res_scale, a.drop_p, a.drop_seed = ptr(bias), ptr(res), res_scale, drop_p, drop_seed
+    a.out, a.y1, a.y1_dtype = ptr(out), ptr(y1), dt(y1)
+    if g2 is not None:
+        a.gamma2, a.beta2, a.y2, a.mean2, a.rstd2 = ptr(g2), ptr(b2), ptr(y2), ptr(mean2), ptr(rstd2)
+    N.call("lasr_linear_res_ln", C.byref(a), stream())
+
+
+def linear_dx_ln_bwd(dy, w, x, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, gb=None, bscale=1.0, bp=0.0,
+                     bseed=0):
+    """dln = bf16(dy @ w) (dy [M, K] bf16, w [K, D]) and the LayerNorm backward of it in one
+    launch (lasr_linear_dx_ln_bwd): bit-identical to gemm(dy, w, dln) + layernorm_bwd(x, dln,
+    ...).  The dgamma / dbeta partials are reduced like layernorm_bwd's (deferred inside a
+    deferred_reductions block)."""
+    M, Kd = dy.shape
+    D = w.shape[1]
+    nblk = (M + 15) // 16
+    defer = _DEFER.depth and dgamma is not None and dbeta is not None
+    part = torch.empty(nblk * 2 * D, dtype=torch.float32, device=dy.device) if defer else \
+        WS.get(nblk * 2 * D, dy.device)
+    a = N.RowLnArgs()
+    a.M, a.D, a.K = M, D, Kd
+    a.A, a.lda, a.W, a.ldw = ptr(dy), dy.stride(0), ptr(w), w.stride(0)
+    a.gamma1, a.mean1, a.rstd1 = ptr(gamma), ptr(mean), ptr(rstd)
+    a.x, a.dres, a.dx, a.gb, a.bscale, a.bp, a.bseed = ptr(x), ptr(dres), ptr(dx), ptr(gb), bscale, bp, bseed
+    a.part = ptr(part)
+    if not defer:  # reduced in the same call, as layernorm_bwd's immediate path
+        a.dgamma, a.dbeta = ptr(dgamma), ptr(dbeta)
+    N.call("lasr_linear_dx_ln_bwd", C.byref(a), stream())
+    if defer:
+        _defer(part, nblk, 2 * D, dgamma, dbeta, split=D)
+
+
 def branch_grad(dx, gb, scale, p=0.0, seed=0):
     N.call("lasr_branch_grad", ptr(dx), dt(dx), dx.numel(), ptr(gb), dt(gb), scale, p, seed,
            stream())

@@ -57,33 +57,93 @@ def ln_forward(x, g, b, adt, y2=False, p2=0.0, seed2=0):
     return y, yd, mean, rstd
 
 
-def ffn_forward(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res):
+# Full-row GEMM tiles with the next LayerNorm in the epilogue (gemm_row.hip): a residual
+# projection and the norm after it, or an input-gradient GEMM and the norm backward before
+# it, in one launch, bit-identical to the two launches.  LASR_ROW_LN=0 keeps two launches
+# (benchmark A/B); shapes the kernel does not take (fp32 build, other widths) keep them too.
+ROW_LN = os.environ.get("LASR_ROW_LN", "1") != "0"
+
+
+class PostLN(SimpleNamespace):
+    """A LayerNorm to run on a residual projection's output row in the same launch:
+    g, b (its parameters), f32 (y1 stored fp32: a layer's final norm), nxt (optional
+    (g2, b2) of a chained second norm, bf16 out).  After the call: y1, m1, r1 (+ y2, m2, r2)."""
+
+
+def res_proj(x, W, bias, res, res_scale, p_res, s_res, post=None):
+    """out = res + res_scale * drop(x W^T + bias) (fp32 residual stream); when `post` names
+    the following LayerNorm and the row kernel takes the shape, the norm runs in the same
+    launch and its outputs are set on `post` (post.y1 stays None otherwise)."""
+    M, D = x.shape[0], W.shape[0]
+    dev = x.device
+    out = _e((M, D), F32, dev)
+    if post is not None:
+        post.y1 = None
+    if post is None or not ROW_LN or not K.row_ln_ok(x, W, D):
+        K.linear(x, W, out, bias=bias, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res)
+        return out
+    post.y1 = _e((M, D), F32 if post.f32 else x.dtype, dev)
+    post.m1, post.r1 = _e(M, F32, dev), _e(M, F32, dev)
+    kw = {}
+    if post.nxt is not None:
+        post.y2 = _e((M, D), x.dtype, dev)
+        post.m2, post.r2 = _e(M, F32, dev), _e(M, F32, dev)
+        kw = dict(g2=post.nxt[0], b2=post.nxt[1], y2=post.y2, mean2=post.m2, rstd2=post.r2)
+    K.linear_res_ln(x, W, out, post.y1, post.m1, post.r1, post.g, post.b, LN_EPS, bias=bias, res=res,
+                    res_scale=res_scale, drop_p=p_res, drop_seed=s_res, **kw)
+    return out
+
+
+class LnBwd(SimpleNamespace):
+    """The LayerNorm backward that consumes an input-gradient GEMM's output dln (the norm
+    in front of a sub-block, liteasr/nets/conformer_layer.py:37-66): x, g (gamma), mean,
+    rstd, dx (fp32 out), dgamma, dbeta, and optionally dres (fp32 residual gradient added),
+    gb (+ bscale, bp, bseed: the preceding branch's gradient, layernorm_bwd's gb)."""
+
+
+def dx_ln(dy, W, lnb):
+    """dln = dy @ W ([M, K] x [K, D]); with `lnb` the LayerNorm backward of dln follows (one
+    launch on the row kernel when it takes the shape) and None is returned, else dln."""
+    M, D = dy.shape[0], W.shape[1]
+    if lnb is not None and ROW_LN and K.row_ln_ok(dy, W, D) and lnb.x.dtype == F32 and lnb.dx.dtype == F32:
+        K.linear_dx_ln_bwd(dy, W, lnb.x, lnb.g, lnb.mean, lnb.rstd, lnb.dx, lnb.dgamma, lnb.dbeta,
+                           dres=lnb.dres, gb=lnb.gb, bscale=lnb.bscale, bp=lnb.bp, bseed=lnb.bseed)
+        return None
+    dln = _e((M, D), dy.dtype, dy.device)
+    K.gemm(dy, W, dln)
+    if lnb is None:
+        return dln
+    K.layernorm_bwd(lnb.x, dln, lnb.g, lnb.mean, lnb.rstd, lnb.dx, lnb.dgamma, lnb.dbeta, dres=lnb.dres,
+                    gb=lnb.gb, bscale=lnb.bscale, bp=lnb.bp, bseed=lnb.bseed)
+    return None
+
+
+def ffn_forward(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res, post=None):
     """Returns (out, g, h).  g is the gate act'(u) * keep the backward needs, stored in the
     compute dtype by the fc1 epilogue (zout_mode 1): h = drop(act(u)) and g come out of the
-    same launch, and the backward's dz GEMM multiplies by g (no recompute of u)."""
+    same launch, and the backward's dz GEMM multiplies by g (no recompute of u).  `post`:
+    the LayerNorm after the residual add (res_proj)."""
     M = ln.shape[0]
     dev, adt = ln.device, ln.dtype
     h = _e((M, W1.shape[0]), adt, dev)
-    out = _e((M, W2.shape[0]), F32, dev)
     g = _e((M, W1.shape[0]), adt, dev)
     K.linear(ln, W1, h, bias=b1, act=act, zout=g, zout_mode=1, drop_p=p_ff, drop_seed=s_ff)
-    K.linear(h, W2, out, bias=b2, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res)
+    out = res_proj(h, W2, b2, res, res_scale, p_res, s_res, post)
     return out, g, h
 
 
-def ffn_backward(gb, ln, g, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff):
+def ffn_backward(gb, ln, g, h, W1, W2, gW1, gb1, gW2, gb2, act, p_ff, s_ff, lnb=None):
     """gb: gradient of the FFN output (after the residual-branch dropout/scale); g: the
-    forward's stored gate act'(z) * keep."""
+    forward's stored gate act'(z) * keep.  Returns dln, or None when `lnb` (the norm in
+    front of the FFN) consumed it (dx_ln)."""
     M = gb.shape[0]
     dev, adt = gb.device, gb.dtype
     K.gemm(gb.t(), h, gW2, beta=1.0, split_k=0, rowsum=gb2, group=True)
     dz = _e((M, W1.shape[0]), adt, dev)
-    dln = _e((M, W1.shape[1]), adt, dev)
     # dz = (gb W2) * scale * g: the dropout scale as alpha, the gate as aux
     K.gemm(gb, W2, dz, alpha=K.dropout_scale(p_ff), aux=g, aux_act=ACT_GATE)
     K.gemm(dz.t(), ln, gW1, beta=1.0, split_k=0, rowsum=gb1, group=True)
-    K.gemm(dz, W1, dln)
-    return dln
+    return dx_ln(dz, W1, lnb)
 
 
 def _heads(t, B, T, H, dk):
@@ -135,7 +195,7 @@ def pos_projections(pos, Ws):
     return [out[j] for j in range(n)]
 
 
-def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None):
+def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None, post=None):
     B, T, H = env.B, env.T, env.H
     d = ln.shape[1]
     dk = d // H
@@ -156,8 +216,7 @@ def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None):
         ctx = _e((M, d), adt, dev)
         K.relattn_fwd(qu, qv, qkv[:, d:2 * d], qkv[:, 2 * d:], p, B, H, T, env.mask, env.msb, env.msq,
                       scale, stats, ctx)
-        out = _e((M, d), F32, dev)
-        K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+        out = res_proj(ctx, w.Wo, w.bo, x_in, 1.0, p_res, s_res, post)
         return out, SimpleNamespace(qkv=qkv, p=p, qu=qu, qv=qv, ctx=ctx, stats=stats)
     ldS = ld_scores(T)
     Sac = _e((B, H, T, ldS), F32, dev)
@@ -172,13 +231,12 @@ def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None):
     K.attn_softmax_fwd(Sac, Sbd, B, H, T, T, ldS, env.mask, env.msb, env.msq, P, p_att, s_att, Praw)
     ctx = _e((M, d), adt, dev)
     K.gemm(P[..., :T], v4, _heads(ctx, B, T, H, dk))
-    out = _e((M, d), F32, dev)
-    K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+    out = res_proj(ctx, w.Wo, w.bo, x_in, 1.0, p_res, s_res, post)
     saved = SimpleNamespace(qkv=qkv, p=p, qu=qu, qv=qv, P=P, Praw=Praw, ctx=ctx, stats=None)
     return out, saved
 
 
-def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
+def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att, lnb=None):
     B, T, H = env.B, env.T, env.H
     d = ln.shape[1]
     dk = d // H
@@ -208,9 +266,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
         K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
         K.gemm(dp.t(), pos, g.Wpos, beta=1.0, split_k=0, group=True)
         K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
-        dln = _e((M, d), adt, dev)
-        K.gemm(dqkv, w.Wqkv, dln)
-        return dln
+        return dx_ln(dqkv, w.Wqkv, lnb)
     dBD = _e((B, H, T, ldS), adt, dev)
     # materialised-score backward (fp32 build, attention dropout, other d_k)
     dctx4 = _heads(dctx, B, T, H, dk)
@@ -236,9 +292,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att):
     K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
     K.gemm(dp.t(), pos, g.Wpos, beta=1.0, split_k=0, group=True)
     K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
-    dln = _e((M, d), adt, dev)
-    K.gemm(dqkv, w.Wqkv, dln)
-    return dln
+    return dx_ln(dqkv, w.Wqkv, lnb)
 
 
 # ============================================================ plain MHA =========
@@ -375,7 +429,7 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
 
 
 # ========================================================= conformer conv =======
-def conv_forward(ln, w, env, x_in, p_res, s_res, training):
+def conv_forward(ln, w, env, x_in, p_res, s_res, training, post=None):
     B, T = env.B, env.T
     M, d = ln.shape
     dev, adt = ln.device, ln.dtype
@@ -390,13 +444,12 @@ def conv_forward(ln, w, env, x_in, p_res, s_res, training):
                   scale, shift, 1 if training else 2)
     h3 = _e((M, d), adt, dev)
     K.bn_swish_fwd(y, scale, shift, h3)
-    out = _e((M, d), F32, dev)
-    K.linear(h3, w.Wpw2, out, bias=w.bpw2, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+    out = res_proj(h3, w.Wpw2, w.bpw2, x_in, 1.0, p_res, s_res, post)
     return out, SimpleNamespace(z1=z1, y=y, mean=mean, rstd=rstd, scale=scale, shift=shift, h3=h3,
                                 training=training)
 
 
-def conv_backward(gb, ln, sv, w, g, env):
+def conv_backward(gb, ln, sv, w, g, env, lnb=None):
     B, T = env.B, env.T
     M, d = ln.shape
     dev, adt = ln.device, ln.dtype
@@ -409,9 +462,7 @@ def conv_backward(gb, ln, sv, w, g, env):
     dz1 = _e((M, 2 * d), adt, dev)
     K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
     K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0, rowsum=g.bpw1, group=True)
-    dln = _e((M, d), adt, dev)
-    K.gemm(dz1, w.Wpw1, dln)
-    return dln
+    return dx_ln(dz1, w.Wpw1, lnb)
 
 
 def _conv2_implicit(adt, C):
@@ -517,34 +568,56 @@ class ConformerLayerFn(torch.autograd.Function):
             env.pre_ln = None
         else:
             ln_a, _, ma, ra = ln_forward(x0, w.ln_a.g, w.ln_a.b, adt)
+        # every residual projection runs the following norm in its epilogue when the row
+        # kernel takes the shape (res_proj); ln_forward covers the rest
+        pb_ = PostLN(g=w.ln_b.g, b=w.ln_b.b, f32=False, nxt=None)
         x1, za, ha = ffn_forward(ln_a, w.ffm.W1, w.ffm.b1, w.ffm.W2, w.ffm.b2, ACT_SWISH, pff,
-                                 _seed(s, 1), x0, 0.5, pd, _seed(s, 2))
+                                 _seed(s, 1), x0, 0.5, pd, _seed(s, 2), post=pb_)
         # (b) relative-position MHSA
-        ln_b, _, mb, rb = ln_forward(x1, w.ln_b.g, w.ln_b.b, adt)
-        pp = getattr(env, "pos_proj", None)
-        x2, svb = relmha_forward(ln_b, pos, w.att, env, x1, pat, _seed(s, 3), pd, _seed(s, 4),
-                                 p=pp.get(id(layer)) if pp else None)
-        # (c) convolution module
-        ln_c, _, mc, rc = ln_forward(x2, w.ln_c.g, w.ln_c.b, adt)
-        x3, svc = conv_forward(ln_c, w.conv, env, x2, pd, _seed(s, 5), tr)
-        # (d) FFN, scale 0.5
-        ln_d, _, md, rd = ln_forward(x3, w.ln_d.g, w.ln_d.b, adt)
-        x4, zd, hd = ffn_forward(ln_d, w.ff.W1, w.ff.b1, w.ff.W2, w.ff.b2, ACT_SWISH, pff,
-                                 _seed(s, 6), x3, 0.5, pd, _seed(s, 7))
-        # final LN -> next layer's residual stream (fp32); with the next layer's first norm
-        # chained in the same launch when the encoder loop names it (env.next_ln)
-        x5 = _e(x4.shape, F32, x4.device)
-        mf = _e(x4.shape[0], F32, x4.device)
-        rf = _e(x4.shape[0], F32, x4.device)
-        nxt = getattr(env, "next_ln", None)
-        if FUSED_LN2 and nxt is not None and adt == torch.bfloat16:
-            z = _e(x4.shape, adt, x4.device)
-            m2 = _e(x4.shape[0], F32, x4.device)
-            r2 = _e(x4.shape[0], F32, x4.device)
-            K.layernorm2_fwd(x4, w.ln_f.g, w.ln_f.b, nxt[1], nxt[2], LN_EPS, x5, mf, rf, z, m2, r2)
-            env.pre_ln = (id(nxt[0]), x5.data_ptr(), z, m2, r2)
+        if pb_.y1 is not None:
+            ln_b, mb, rb = pb_.y1, pb_.m1, pb_.r1
         else:
-            K.layernorm_fwd(x4, w.ln_f.g, w.ln_f.b, LN_EPS, x5, mf, rf)
+            ln_b, _, mb, rb = ln_forward(x1, w.ln_b.g, w.ln_b.b, adt)
+        pp = getattr(env, "pos_proj", None)
+        pc_ = PostLN(g=w.ln_c.g, b=w.ln_c.b, f32=False, nxt=None)
+        x2, svb = relmha_forward(ln_b, pos, w.att, env, x1, pat, _seed(s, 3), pd, _seed(s, 4),
+                                 p=pp.get(id(layer)) if pp else None, post=pc_)
+        # (c) convolution module
+        if pc_.y1 is not None:
+            ln_c, mc, rc = pc_.y1, pc_.m1, pc_.r1
+        else:
+            ln_c, _, mc, rc = ln_forward(x2, w.ln_c.g, w.ln_c.b, adt)
+        pd_ = PostLN(g=w.ln_d.g, b=w.ln_d.b, f32=False, nxt=None)
+        x3, svc = conv_forward(ln_c, w.conv, env, x2, pd, _seed(s, 5), tr, post=pd_)
+        # (d) FFN, scale 0.5
+        if pd_.y1 is not None:
+            ln_d, md, rd = pd_.y1, pd_.m1, pd_.r1
+        else:
+            ln_d, _, md, rd = ln_forward(x3, w.ln_d.g, w.ln_d.b, adt)
+        # final LN -> next layer's residual stream (fp32); with the next layer's first norm
+        # chained when the encoder loop names it (env.next_ln): in fc2's epilogue, or in one
+        # lasr_layernorm2_fwd launch
+        nxt = getattr(env, "next_ln", None)
+        chain = FUSED_LN2 and nxt is not None and adt == torch.bfloat16
+        pf_ = PostLN(g=w.ln_f.g, b=w.ln_f.b, f32=True, nxt=(nxt[1], nxt[2]) if chain else None)
+        x4, zd, hd = ffn_forward(ln_d, w.ff.W1, w.ff.b1, w.ff.W2, w.ff.b2, ACT_SWISH, pff,
+                                 _seed(s, 6), x3, 0.5, pd, _seed(s, 7), post=pf_)
+        if pf_.y1 is not None:
+            x5, mf, rf = pf_.y1, pf_.m1, pf_.r1
+            if chain:
+                env.pre_ln = (id(nxt[0]), x5.data_ptr(), pf_.y2, pf_.m2, pf_.r2)
+        else:
+            x5 = _e(x4.shape, F32, x4.device)
+            mf = _e(x4.shape[0], F32, x4.device)
+            rf = _e(x4.shape[0], F32, x4.device)
+            if chain:
+                z = _e(x4.shape, adt, x4.device)
+                m2 = _e(x4.shape[0], F32, x4.device)
+                r2 = _e(x4.shape[0], F32, x4.device)
+                K.layernorm2_fwd(x4, w.ln_f.g, w.ln_f.b, nxt[1], nxt[2], LN_EPS, x5, mf, rf, z, m2, r2)
+                env.pre_ln = (id(nxt[0]), x5.data_ptr(), z, m2, r2)
+            else:
+                K.layernorm_fwd(x4, w.ln_f.g, w.ln_f.b, LN_EPS, x5, mf, rf)
         if torch.is_grad_enabled() or anchor.requires_grad:
             ctx.sv = SimpleNamespace(x=(x0, x1, x2, x3, x4), ln=(ln_a, ln_b, ln_c, ln_d),
                                      st=((ma, ra), (mb, rb), (mc, rc), (md, rd), (mf, rf)),
@@ -572,26 +645,30 @@ class ConformerLayerFn(torch.autograd.Function):
             gb = _e((M, d), adt, dev)
             K.layernorm_bwd(x4, dx5, w.ln_f.g, mf, rf, dx4, g.ln_f.g, g.ln_f.b, gb=gb, bscale=0.5,
                             bp=pd, bseed=_seed(s, 7))
-            dln = ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2,
-                               g.ff.b2, ACT_SWISH, pff, _seed(s, 6))
+            # each sub-block's input-gradient GEMM runs its norm's backward in its epilogue
+            # (dx_ln); the branch-gradient buffers are fresh: grouped dW GEMMs read them at the
+            # end of the node
             dx3 = _e((M, d), F32, dev)
-            gb = _e((M, d), adt, dev)  # fresh: grouped dW GEMMs read it at the end of the node
-            K.layernorm_bwd(x3, dln, w.ln_d.g, md, rd, dx3, g.ln_d.g, g.ln_d.b, dres=dx4, gb=gb,
-                            bscale=1.0, bp=pd, bseed=_seed(s, 5))
-            dln = conv_backward(gb, ln_c, sv.svc, w.conv, g.conv, env)
+            gb3 = _e((M, d), adt, dev)
+            ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2, g.ff.b2,
+                         ACT_SWISH, pff, _seed(s, 6),
+                         lnb=LnBwd(x=x3, g=w.ln_d.g, mean=md, rstd=rd, dx=dx3, dgamma=g.ln_d.g, dbeta=g.ln_d.b,
+                                   dres=dx4, gb=gb3, bscale=1.0, bp=pd, bseed=_seed(s, 5)))
             dx2 = _e((M, d), F32, dev)
-            gb = _e((M, d), adt, dev)  # fresh: grouped dW GEMMs read it at the end of the node
-            K.layernorm_bwd(x2, dln, w.ln_c.g, mc, rc, dx2, g.ln_c.g, g.ln_c.b, dres=dx3, gb=gb,
-                            bscale=1.0, bp=pd, bseed=_seed(s, 4))
-            dln = relmha_backward(gb, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3))
+            gb2 = _e((M, d), adt, dev)
+            conv_backward(gb3, ln_c, sv.svc, w.conv, g.conv, env,
+                          lnb=LnBwd(x=x2, g=w.ln_c.g, mean=mc, rstd=rc, dx=dx2, dgamma=g.ln_c.g, dbeta=g.ln_c.b,
+                                    dres=dx3, gb=gb2, bscale=1.0, bp=pd, bseed=_seed(s, 4)))
             dx1 = _e((M, d), F32, dev)
-            gb = _e((M, d), adt, dev)  # fresh: grouped dW GEMMs read it at the end of the node
-            K.layernorm_bwd(x1, dln, w.ln_b.g, mb, rb, dx1, g.ln_b.g, g.ln_b.b, dres=dx2, gb=gb,
-                            bscale=0.5, bp=pd, bseed=_seed(s, 2))
-            dln = ffn_backward(gb, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1,
-                               g.ffm.W2, g.ffm.b2, ACT_SWISH, pff, _seed(s, 1))
+            gb1 = _e((M, d), adt, dev)
+            relmha_backward(gb2, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3),
+                            lnb=LnBwd(x=x1, g=w.ln_b.g, mean=mb, rstd=rb, dx=dx1, dgamma=g.ln_b.g, dbeta=g.ln_b.b,
+                                      dres=dx2, gb=gb1, bscale=0.5, bp=pd, bseed=_seed(s, 2)))
             dx0 = _e((M, d), F32, dev)
-            K.layernorm_bwd(x0, dln, w.ln_a.g, ma, ra, dx0, g.ln_a.g, g.ln_a.b, dres=dx1)
+            ffn_backward(gb1, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1, g.ffm.W2, g.ffm.b2,
+                         ACT_SWISH, pff, _seed(s, 1),
+                         lnb=LnBwd(x=x0, g=w.ln_a.g, mean=ma, rstd=ra, dx=dx0, dgamma=g.ln_a.g, dbeta=g.ln_a.b,
+                                   dres=dx1, gb=None, bscale=1.0, bp=0.0, bseed=0))
         ctx.sv = None
         layer.on_grads_ready()
         return dx0, None, None, None, None
