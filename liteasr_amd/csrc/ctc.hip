@@ -13,8 +13,9 @@
 //   ctc_alpha_kernel      : one workgroup per utterance, threads over states, LDS
 //                           ping-pong across the serial t recursion.
 //   ctc_beta_kernel       : same, backward in t.
-//   ctc_grad_kernel       : one workgroup per (b,t) row: gamma from alpha+beta, then a
-//                           single coalesced write of g*(softmax - gamma) over V.
+//   ctc_grad_kernel       : one workgroup per (b,t) row: gamma from alpha+beta (summed
+//                           per distinct label once per row), then a single coalesced
+//                           write of g*(softmax - gamma) over V.
 #include "common.h"
 
 template <typename T>
@@ -218,12 +219,14 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
                                                        const float* lp, const float* alpha,
                                                        const float* beta, const float* nll,
                                                        TG* grad, float gscale, const float* gdev) {
-  // dynamic LDS: [Lmax] gamma per label position, [Lmax] labels, [(V+31)/32] label bitmap
+  // dynamic LDS: [Lmax] gamma per label position, [Lmax] labels, [(V+31)/32] label bitmap,
+  // [V] gamma per vocabulary entry (read only where the bitmap is set)
   extern __shared__ float sh[];
   __shared__ float red[32];
   float* glab = sh;
   int* lab = (int*)(sh + Lmax);
   uint32_t* bits = (uint32_t*)(sh + 2 * Lmax);
+  float* gam = sh + 2 * Lmax + (V + 31) / 32;
   const int row = blockIdx.x;
   const int b = row / T_, t = row - b * T_;
   TG* g = grad + (int64_t)row * ld;
@@ -261,16 +264,26 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
     atomicOr(&bits[tg[j] >> 5], 1u << (tg[j] & 31));
   }
   __syncthreads();
+  // gamma of each distinct label, by the thread of its first position: the positions carrying
+  // it summed in position order from 0 (the per-column loop of r02, done once per label)
+  for (int j = threadIdx.x; j < Lb; j += blockDim.x) {
+    const int c = lab[j];
+    float sub = 0.f;
+    bool first = true;
+    for (int jj = 0; jj < Lb; ++jj) {
+      if (lab[jj] != c) continue;
+      if (jj < j) { first = false; break; }
+      sub += glab[jj];
+    }
+    if (first) gam[c] = sub;
+  }
+  __syncthreads();
   const float gs = gscale * (gdev ? gdev[0] : 1.f);
   const T* x = logits + (int64_t)row * ld;
   const float l = lse[row];
   auto gamma_of = [&](int c) {
-    float sub = (c == 0) ? gb : 0.f;
-    if (c != 0 && ((bits[c >> 5] >> (c & 31)) & 1u)) {
-      for (int j = 0; j < Lb; ++j)
-        if (lab[j] == c) sub += glab[j];
-    }
-    return sub;
+    if (c == 0) return gb;
+    return ((bits[c >> 5] >> (c & 31)) & 1u) ? gam[c] : 0.f;
   };
   if (vec) {
     for (int c0 = threadIdx.x * 8; c0 < V; c0 += blockDim.x * 8) {
@@ -337,7 +350,7 @@ extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, in
     const int rc = lasr_check_launch("ctc_beta");
     if (rc) return rc;
   }
-  const size_t shm = ((size_t)2 * (Lmax > 0 ? Lmax : 1) + (V + 31) / 32) * sizeof(float);
+  const size_t shm = ((size_t)2 * (Lmax > 0 ? Lmax : 1) + (V + 31) / 32 + V) * sizeof(float);
   LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_ctc_bwd: vocab/labels too large for LDS");
 #define CTC_G(TT, TGG)                                                                      \
   ctc_grad_kernel<TT, TGG><<<B * T, 256, shm, st>>>((const TT*)logits, B, T, V, ld, targets, Lmax,\
