@@ -36,7 +36,6 @@ CONFIGS = {
 }
 V = 4233
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-PEAK_HBM_GBS = 8000.0
 
 
 def log(*a):
@@ -89,55 +88,84 @@ def build_key():
 
 
 def family_case(cfgd, dev):
-    """The dominant kernel family of the step (profiles/r03 step summary: the GEMMs whose
-    output is d = 256 columns wide, 64 x 64 tiles, ~2.4 ms of the ~12 ms step): one Conformer
-    layer's ten of them, issued through the product's own calls (kernels.linear /
-    kernels.gemm: same planner, tiles and epilogues as nets/functional.py):
-      forward, fp32 residual out = res + s * (X W^T + b)   (liteasr/nets/conformer_layer.py:37-78)
-        fc2 of both FFNs (K = ff), linear_o (K = d), pointwise_conv2 (K = d)
-      backward, bf16 data gradients dX = dY W           (the same layers' input gradients)
-        fc1 of both FFNs (K = ff), linear_o (K = d), the fused q/k/v (K = 3d),
-        pointwise_conv2 (K = d), pointwise_conv1 (K = 2d).
-    Algorithmic bytes per launch: A [M, K] and W [d, K] bf16 read once, the output written
-    once (fp32 forward + the fp32 residual read once; bf16 backward), bias fp32."""
+    """The dominant kernel family of the step (profiles/r03 step summary): the GEMMs whose
+    output is d = 256 columns wide, ~3.3 ms of the ~11.8 ms step.  One Conformer layer's
+    twelve of them, issued through the product's own calls exactly as nets/functional.py
+    issues them (same planner, tiles, epilogues and the full-row LayerNorm kernels):
+      forward, fp32 residual out = res + s * dropout(X W^T + b)   (conformer_layer.py:37-78)
+        fc2 of both FFNs (K = ff; 64 x 64 GEMM tiles: the row kernel is slower at K = 2048),
+        linear_o and pointwise_conv2 (K = d) with the next LayerNorm in the epilogue
+        (lasr_linear_res_ln: y1 = LN(out) and its row statistics written too)
+      backward, input gradients dX = dY W                         (the same layers)
+        fc1 of both FFNs (K = ff, bf16 out; the LayerNorm backward after it is a separate
+        launch), linear_o and pointwise_conv2 (K = d, bf16 out), the fused q/k/v (K = 3d) and
+        pointwise_conv1 (K = 2d) with the LayerNorm backward in the epilogue
+        (lasr_linear_dx_ln_bwd: dx = dres + LN'(dY W) and the branch gradient gb written).
+    Algorithmic bytes per launch: every operand the call reads, once, and every output it
+    writes, once (the LayerNorm gamma/beta partial rows excluded: scratch of this design)."""
     import torch
 
     from liteasr_amd import kernels as K
 
     M, D, F = _rows(cfgd), cfgd["d"], cfgd["ff"]
-    bf = torch.bfloat16
+    bf, f32 = torch.bfloat16, torch.float32
     g = torch.Generator(device=dev).manual_seed(7)
 
     def rn(*shape, dt=bf, scale=1.0):
         return (torch.randn(*shape, device=dev, generator=g) * scale).to(dt)
 
-    res = rn(M, D, dt=torch.float32)
+    def nb(*ts):
+        return float(sum(t.numel() * t.element_size() for t in ts))
+
+    gam, bet = 1.0 + rn(D, dt=f32, scale=0.1), rn(D, dt=f32, scale=0.1)
     insts = []
 
-    def fwd(name, Kd, count):
-        x, w, b = rn(M, Kd), rn(D, Kd, scale=Kd ** -0.5), rn(D, dt=torch.float32, scale=0.02)
+    def add(name, kind, Kd, count, fn, plan, rd, wr):
+        insts.append(dict(name=name, kernel=kind, M=M, N=D, K=Kd, count=count, launch=fn, plan=plan,
+                          bytes=nb(*rd) + nb(*wr), flops=2.0 * M * D * Kd))
+
+    def fwd_res(name, Kd, count):
+        x, w, b, res = rn(M, Kd), rn(D, Kd, scale=Kd ** -0.5), rn(D, dt=f32, scale=0.02), rn(M, D, dt=f32)
         out = torch.empty(M, D, device=dev)
-        scale = 0.5 if name.startswith("fc2") else 1.0
-        fn = lambda: K.linear(x, w, out, bias=b, res=res, res_scale=scale, drop_p=0.1, drop_seed=5)  # noqa: E731
-        insts.append(dict(name=name, M=M, N=D, K=Kd, count=count, launch=fn, plan=(x, w.t(), out),
-                          bytes=2.0 * (M * Kd + D * Kd) + 4.0 * M * D * 2 + 4.0 * D, flops=2.0 * M * D * Kd))
+        fn = lambda: K.linear(x, w, out, bias=b, res=res, res_scale=0.5, drop_p=0.1, drop_seed=5)  # noqa: E731
+        add(name, "gemm_bf16_glds_kernel", Kd, count, fn, (x, w.t(), out), (x, w, b, res), (out,))
+
+    def fwd_res_ln(name, Kd, count):
+        x, w, b, res = rn(M, Kd), rn(D, Kd, scale=Kd ** -0.5), rn(D, dt=f32, scale=0.02), rn(M, D, dt=f32)
+        out, y1 = torch.empty(M, D, device=dev), torch.empty(M, D, device=dev, dtype=bf)
+        m1, r1 = torch.empty(M, device=dev), torch.empty(M, device=dev)
+        fn = lambda: K.linear_res_ln(x, w, out, y1, m1, r1, gam, bet, 1e-12, bias=b, res=res,  # noqa: E731
+                                     drop_p=0.1, drop_seed=6)
+        add(name, "row_res_ln_kernel", Kd, count, fn, None, (x, w, b, res, gam, bet), (out, y1, m1, r1))
 
     def dx(name, Kd, count):
         dy, w = rn(M, Kd), rn(Kd, D, scale=Kd ** -0.5)
         out = torch.empty(M, D, device=dev, dtype=bf)
         fn = lambda: K.gemm(dy, w, out)  # noqa: E731
-        insts.append(dict(name=name, M=M, N=D, K=Kd, count=count, launch=fn, plan=(dy, w, out),
-                          bytes=2.0 * (M * Kd + D * Kd) + 2.0 * M * D, flops=2.0 * M * D * Kd))
+        add(name, "gemm_bf16_glds_kernel", Kd, count, fn, (dy, w, out), (dy, w), (out,))
 
-    fwd("fc2 fwd (+res)", F, 2)
-    fwd("linear_o fwd (+res)", D, 1)
-    fwd("pointwise_conv2 fwd (+res)", D, 1)
+    def dx_ln(name, Kd, count):
+        dy, w = rn(M, Kd), rn(Kd, D, scale=Kd ** -0.5)
+        x, dres = rn(M, D, dt=f32), rn(M, D, dt=f32)
+        mean, rstd = rn(M, dt=f32, scale=0.1), 1.0 + rn(M, dt=f32, scale=0.1).abs()
+        dxo, gb = torch.empty(M, D, device=dev), torch.empty(M, D, device=dev, dtype=bf)
+        dgam, dbet = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        fn = lambda: K.linear_dx_ln_bwd(dy, w, x, gam, mean, rstd, dxo, dgam, dbet, dres=dres, gb=gb,  # noqa: E731
+                                        bp=0.1, bseed=4)
+        add(name, "row_dx_ln_bwd_kernel", Kd, count, fn, None, (dy, w, x, gam, mean, rstd, dres), (dxo, gb, dgam, dbet))
+
+    fwd_res("fc2 fwd (+res)", F, 2)
+    fwd_res_ln("linear_o fwd (+res, +LN)", D, 1)
+    fwd_res_ln("pointwise_conv2 fwd (+res, +LN)", D, 1)
     dx("fc1 dX", F, 2)
     dx("linear_o dX", D, 1)
-    dx("qkv dX", 3 * D, 1)
     dx("pointwise_conv2 dX", D, 1)
-    dx("pointwise_conv1 dX", 2 * D, 1)
+    dx_ln("qkv dX (+LN bwd)", 3 * D, 1)
+    dx_ln("pointwise_conv1 dX (+LN bwd)", 2 * D, 1)
     for it in insts:
+        if it["plan"] is None:
+            it["tile"] = f"32x{D} row, 8 waves"
+            continue
         a_, b_, c_ = it["plan"]
         tm, tn, sp = K.gemm_plan(a_, b_, c_)
         it["tile"] = f"{tm}x{tn}" + (f" split {sp}" if sp > 1 else "")
@@ -154,7 +182,8 @@ def family_roofline(cfgd, dev, iters=50):
     for it in insts:
         sec = _time_case(it["launch"], iters)
         bound, ach, peak, unit = _roof(it["flops"], it["bytes"], sec)
-        rows.append({"name": it["name"], "shape": f"M={it['M']} N={it['N']} K={it['K']}", "tile": it["tile"],
+        rows.append({"name": it["name"], "kernel": it["kernel"], "shape": f"M={it['M']} N={it['N']} K={it['K']}",
+                     "tile": it["tile"],
                      "per_layer": it["count"], "avg_launch_us": round(sec * 1e6, 2),
                      "algorithmic_bytes": it["bytes"], "GBps": round(it["bytes"] / sec / 1e9, 1),
                      "frac": round(it["bytes"] / sec / 1e9 / PEAK_HBM_GBS, 4), "bound": bound})
@@ -240,8 +269,11 @@ def hottest_case(cfgd, dev):
 
     flops = 2.0 * M * F * D
     bytes_ = 2.0 * (M * D + F * D) + 2 * 2.0 * M * F + 4.0 * F
-    meta = {"kernel": "gemm_bf16_glds_kernel<128, 256, true, true, unsigned short, 3, 2, 0, 1>",
-            "shape": f"M={M} N={F} K={D} bias+swish+gate+dropout", "grid": [F // 256, -(-M // 128), 1],
+    tm, tn, _, fl = K.gemm_plan(ln, w1.t(), h, flags=True, bias=b1, act=ACT_SWISH, zout=g, zout_mode=1,
+                                drop_p=0.1, drop_seed=11)
+    inst = "2, 1, 0, 2, 8" if fl & 8 else "3, 2, 0, 1, 4"  # gemm_launch.h: wide 8-wave / 4-wave 32-deep
+    meta = {"kernel": f"gemm_bf16_glds_kernel<{tm}, {tn}, true, true, unsigned short, {inst}>",
+            "shape": f"M={M} N={F} K={D} bias+swish+gate+dropout", "grid": [-(-F // tn), -(-M // tm), 1],
             "build": build_key()}
     return launch, flops, bytes_, meta
 
@@ -296,7 +328,7 @@ def dominant_kernel_roofline(cfgd, dev, iters=50):
     out = {"kernel": fam_meta["kernel"], "shape": fam_meta["shape"], "bound": "hbm", "achieved": round(ach, 2),
            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
            "traffic": traffic["bytes_per_launch"] if traffic else None,
-           "per": "one Conformer layer's launches of the family (10); achieved = algorithmic bytes / summed "
+           "per": "one Conformer layer's launches of the family (12); achieved = algorithmic bytes / summed "
                   "launch time",
            "algorithmic_bytes_per_launch": tb, "algorithmic_flops_per_launch": tf,
            "avg_launch_us": round(tt / sum(r["per_layer"] for r in rows) * 1e6, 2),
@@ -313,9 +345,11 @@ def dominant_kernel_roofline(cfgd, dev, iters=50):
 
 def family_meta(cfgd):
     M, D, F = _rows(cfgd), cfgd["d"], cfgd["ff"]
-    return {"kernel": "gemm_bf16_glds_kernel", "family": "N = d output GEMMs (64x64 tiles)",
-            "shape": f"one layer: 2x fc2 fwd M={M} N={D} K={F} +res, linear_o / pw2 fwd K={D} +res, "
-                     f"2x fc1 dX K={F}, dX K={D},{3 * D},{D},{2 * D}", "build": build_key()}
+    return {"kernel": "gemm_bf16_glds_kernel + row_res_ln_kernel + row_dx_ln_bwd_kernel",
+            "family": "N = d output GEMMs (64x64 tiles and the full-row LayerNorm tiles)",
+            "shape": f"one layer: 2x fc2 fwd M={M} N={D} K={F} +res, linear_o / pw2 fwd K={D} +res +LN, "
+                     f"2x fc1 dX K={F}, linear_o / pw2 dX K={D}, qkv dX K={3 * D} +LN bwd, "
+                     f"pw1 dX K={2 * D} +LN bwd", "build": build_key()}
 
 
 def ctc_roofline(cfgd, dev, iters=20):

@@ -103,6 +103,7 @@ float lasr_dropout_scale(float p);
 #define LASR_PLAN_GLDS 1
 #define LASR_PLAN_ROWSUM_FUSED 2
 #define LASR_PLAN_KSUB2 4 /* 64-deep LDS ring stages (two 32-deep sub-tiles per wait) */
+#define LASR_PLAN_WIDE 8  /* 256 x 256 tile on 8 waves (512-thread workgroups) */
 int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k, int* flags);
 /* Tuning hook: force the bf16 LDS-DMA tile (64/128/256 x 64/128/256) of every later
  * lasr_gemm call in the process; (0, 0) restores the planner.  Benchmarks only. */
@@ -410,17 +411,19 @@ int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float eps, float 
                      float* running_var, int64_t* num_batches, float* mean, float* rstd,
                      float* scale, float* shift, int mode, void* stream);
 /* mode: 0 batch stats, 1 batch stats + running-stat update (train), 2 running stats (eval) */
-int lasr_bn_swish_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
-                      const float* shift, void* h, int hdt, void* stream);
-/* BN+Swish backward: dgamma/dbeta accumulated, dy = BN'(dh * swish'(u)).
+int lasr_bn_act_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
+                    const float* shift, void* h, int hdt, int act, void* stream);
+/* BN+activation backward: dgamma/dbeta accumulated, dy = BN'(dh * act'(u)); act is
+ * LASR_ACT_SWISH (the default conv-module activation) or LASR_ACT_RELU (encoder activation
+ * "relu", liteasr/nets/transformer_encoder.py:77-80).
  * batch_stats 1: train-mode BN (mean/rstd are the batch statistics, their gradient terms
  * included); 0: eval-mode BN (mean/rstd = running statistics, constants).
  * ws >= (ceil(rows/64)+1)*2*C floats. */
-int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt, int64_t rows, int C,
-                      const float* scale, const float* shift, const float* mean,
-                      const float* rstd, const float* gamma, float* dgamma, float* dbeta,
-                      void* dy, int dydt, float* ws, int64_t ws_floats, int batch_stats,
-                      void* stream);
+int lasr_bn_act_bwd(const void* y, int ydt, const void* dh, int hdt, int64_t rows, int C,
+                    const float* scale, const float* shift, const float* mean,
+                    const float* rstd, const float* gamma, float* dgamma, float* dbeta,
+                    void* dy, int dydt, float* ws, int64_t ws_floats, int batch_stats, int act,
+                    void* stream);
 int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int dydt, int B, int T, int C,
                         int K, const float* w, void* dz1, float* dw, float* db, float* ws,
                         int64_t ws_floats, void* stream);

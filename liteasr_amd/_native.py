@@ -155,8 +155,8 @@ SIGNATURES = {
     "lasr_glu_dwconv_fwd": [_p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _p],
     "lasr_dwconv_nparts": [_i, _i],
     "lasr_bn_finalize": [_p, _i, _i, _f, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p],
-    "lasr_bn_swish_fwd": [_p, _i, _l, _i, _p, _p, _p, _i, _p],
-    "lasr_bn_swish_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _l, _i, _p],
+    "lasr_bn_act_fwd": [_p, _i, _l, _i, _p, _p, _p, _i, _i, _p],
+    "lasr_bn_act_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _l, _i, _i, _p],
     "lasr_glu_dwconv_bwd": [_p, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _l, _p],
     "lasr_cast": [_p, _i, _p, _i, _l, _p],
     "lasr_scale_add": [_p, _i, _p, _i, _f, _f, _p, _i, _l, _p],

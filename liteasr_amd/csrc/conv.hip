@@ -538,10 +538,23 @@ __global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
   }
 }
 
-// Elementwise BN + Swish, 8 channels per thread (C % 8 == 0; the host checks).
-template <typename TY, typename TH>
-__global__ void bn_swish_fwd_kernel(const TY* y, int64_t rows, int C, const float* scale,
-                                    const float* shift, TH* h) {
+// The conv module's activation after the BatchNorm (conformer_convolution.py:56): Swish
+// (the default) or ReLU (encoder activation "relu", transformer_encoder.py:77-80).
+template <bool RELU>
+LASR_DEV float bn_act(float u) {
+  if constexpr (RELU) return fmaxf(u, 0.f);
+  else return swishf(u);
+}
+template <bool RELU>
+LASR_DEV float bn_act_grad(float u) {
+  if constexpr (RELU) return u > 0.f ? 1.f : 0.f;
+  else return swish_grad(u);
+}
+
+// Elementwise BN + activation, 8 channels per thread (C % 8 == 0; the host checks).
+template <typename TY, typename TH, bool RELU>
+__global__ void bn_act_fwd_kernel(const TY* y, int64_t rows, int C, const float* scale,
+                                  const float* shift, TH* h) {
   const int64_t n8 = rows * C / 8;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)((e * 8) % C);
@@ -550,7 +563,7 @@ __global__ void bn_swish_fwd_kernel(const TY* y, int64_t rows, int C, const floa
     ldv<8>(scale + c, sc);
     ldv<8>(shift + c, sf);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = swishf(v[q] * sc[q] + sf[q]);
+    for (int q = 0; q < 8; ++q) v[q] = bn_act<RELU>(v[q] * sc[q] + sf[q]);
     stv<8>(h + e * 8, v);
   }
 }
@@ -559,10 +572,10 @@ constexpr int BN_ROWS = 64;
 // 256 threads = BN_G row groups x BN_CP channel pairs; a block reduces BN_ROWS rows of
 // 2*BN_CP channels and combines its row groups in LDS (fixed order).
 constexpr int BN_G = 8, BN_CP = 32;
-template <typename TY, typename TH>
-__global__ __launch_bounds__(256) void bn_swish_bwd_reduce_kernel(const TY* y, const TH* dh, int64_t rows, int C,
-                                                                  const float* scale, const float* shift,
-                                                                  const float* mean, const float* rstd, float* part) {
+template <typename TY, typename TH, bool RELU>
+__global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const TY* y, const TH* dh, int64_t rows, int C,
+                                                                const float* scale, const float* shift,
+                                                                const float* mean, const float* rstd, float* part) {
   __shared__ float sp[BN_G][2][2 * BN_CP];
   const int cp = threadIdx.x % BN_CP, grp = threadIdx.x / BN_CP;
   const int c = (blockIdx.x * BN_CP + cp) * 2;
@@ -578,7 +591,7 @@ __global__ __launch_bounds__(256) void bn_swish_bwd_reduce_kernel(const TY* y, c
       ldv<2>(dh + r * C + c, gv);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const float du = gv[q] * swish_grad(yv[q] * sc[q] + sf[q]);
+        const float du = gv[q] * bn_act_grad<RELU>(yv[q] * sc[q] + sf[q]);
         s1[q] += du;
         s2[q] += du * (yv[q] - mu[q]) * rs[q];
       }
@@ -613,12 +626,12 @@ __global__ void bn_bwd_total_kernel(const float* part, int nparts, int C, float*
   dbeta[c] += s1;
   dgamma[c] += s2;
 }
-template <typename TY, typename TH, typename TD>
-__global__ void bn_swish_bwd_apply_kernel(const TY* y, const TH* dh, int64_t rows, int C,
-                                          const float* scale, const float* shift,
-                                          const float* mean, const float* rstd,
-                                          const float* gamma, const float* tot, TD* dy,
-                                          float* dgamma, float* dbeta, int batch_stats) {
+template <typename TY, typename TH, typename TD, bool RELU>
+__global__ void bn_act_bwd_apply_kernel(const TY* y, const TH* dh, int64_t rows, int C,
+                                        const float* scale, const float* shift,
+                                        const float* mean, const float* rstd,
+                                        const float* gamma, const float* tot, TD* dy,
+                                        float* dgamma, float* dbeta, int batch_stats) {
   if (blockIdx.x == 0)  // parameter gradients (the column totals are final here)
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       dbeta[c] += tot[c];
@@ -636,7 +649,7 @@ __global__ void bn_swish_bwd_apply_kernel(const TY* y, const TH* dh, int64_t row
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int c = c0 + q;
-      const float du = gv[q] * swish_grad(yv[q] * scale[c] + shift[c]);
+      const float du = gv[q] * bn_act_grad<RELU>(yv[q] * scale[c] + shift[c]);
       const float xh = (yv[q] - mean[c]) * rstd[c];
       o[q] = gamma[c] * rstd[c] * (du - tot[c] * inv_n - xh * tot[C + c] * inv_n);
     }
@@ -760,46 +773,48 @@ extern "C" int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float 
   return lasr_check_launch("bn_finalize");
 }
 
-extern "C" int lasr_bn_swish_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
-                                 const float* shift, void* h, int hdt, void* stream) {
-  LASR_CHECK_ARG(C % 8 == 0, "lasr_bn_swish_fwd: C must be a multiple of 8");
-  const int64_t n = rows * C / 8;
-  if (n == 0) return LASR_OK;
-  hipStream_t st = (hipStream_t)stream;
-#define BF(TY, TH) bn_swish_fwd_kernel<TY, TH><<<gridn(n), 256, 0, st>>>((const TY*)y, rows, C, scale, shift, (TH*)h)
+template <bool RELU>
+static void bn_act_fwd_launch(const void* y, int ydt, int64_t rows, int C, const float* scale, const float* shift,
+                              void* h, int hdt, int64_t n, hipStream_t st) {
+#define BF(TY, TH) bn_act_fwd_kernel<TY, TH, RELU><<<gridn(n), 256, 0, st>>>((const TY*)y, rows, C, scale, shift, (TH*)h)
   if (ydt == LASR_F32 && hdt == LASR_F32) BF(float, float);
   else if (ydt == LASR_F32) BF(float, bf16_t);
   else if (hdt == LASR_F32) BF(bf16_t, float);
   else BF(bf16_t, bf16_t);
 #undef BF
-  return lasr_check_launch("bn_swish_fwd");
 }
 
-extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt, int64_t rows,
-                                 int C, const float* scale, const float* shift, const float* mean,
-                                 const float* rstd, const float* gamma, float* dgamma,
-                                 float* dbeta, void* dy, int dydt, float* ws, int64_t ws_floats,
-                                 int batch_stats, void* stream) {
-  const int64_t nparts = cdiv(rows, BN_ROWS);
-  LASR_CHECK_ARG(ws_floats >= (nparts + 1) * 2 * C, "lasr_bn_swish_bwd: workspace too small");
-  LASR_CHECK_ARG(nparts <= 65535, "lasr_bn_swish_bwd: too many rows");
-  if (rows == 0) return LASR_OK;
+extern "C" int lasr_bn_act_fwd(const void* y, int ydt, int64_t rows, int C, const float* scale,
+                               const float* shift, void* h, int hdt, int act, void* stream) {
+  LASR_CHECK_ARG(C % 8 == 0, "lasr_bn_act_fwd: C must be a multiple of 8");
+  LASR_CHECK_ARG(act == LASR_ACT_SWISH || act == LASR_ACT_RELU, "lasr_bn_act_fwd: act must be SWISH or RELU");
+  const int64_t n = rows * C / 8;
+  if (n == 0) return LASR_OK;
   hipStream_t st = (hipStream_t)stream;
-  LASR_CHECK_ARG(C % 8 == 0, "lasr_bn_swish_bwd: C must be a multiple of 8");
+  if (act == LASR_ACT_RELU) bn_act_fwd_launch<true>(y, ydt, rows, C, scale, shift, h, hdt, n, st);
+  else bn_act_fwd_launch<false>(y, ydt, rows, C, scale, shift, h, hdt, n, st);
+  return lasr_check_launch("bn_act_fwd");
+}
+
+template <bool RELU>
+static int bn_act_bwd_launch(const void* y, int ydt, const void* dh, int hdt, int64_t rows, int C,
+                             const float* scale, const float* shift, const float* mean, const float* rstd,
+                             const float* gamma, float* dgamma, float* dbeta, void* dy, int dydt, float* ws,
+                             int64_t nparts, int batch_stats, hipStream_t st) {
   float* tot = ws + nparts * 2 * C;
   dim3 g((unsigned)cdiv(C, 2 * BN_CP), (unsigned)nparts);
-#define BR(TY, TH) bn_swish_bwd_reduce_kernel<TY, TH><<<g, 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, ws)
+#define BR(TY, TH) bn_act_bwd_reduce_kernel<TY, TH, RELU><<<g, 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, ws)
   if (ydt == LASR_F32 && hdt == LASR_F32) BR(float, float);
   else if (ydt == LASR_F32) BR(float, bf16_t);
   else if (hdt == LASR_F32) BR(bf16_t, float);
   else BR(bf16_t, bf16_t);
 #undef BR
-  int rc = lasr_check_launch("bn_swish_bwd/reduce");
+  int rc = lasr_check_launch("bn_act_bwd/reduce");
   if (rc) return rc;
   rc = lasr_reduce_cols(ws, (int)nparts, 2 * C, tot, nullptr, 2 * C, 0, st);
   if (rc) return rc;
   const int64_t n = rows * C / 8;
-#define BA(TY, TH, TD) bn_swish_bwd_apply_kernel<TY, TH, TD><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy, dgamma, dbeta, batch_stats)
+#define BA(TY, TH, TD) bn_act_bwd_apply_kernel<TY, TH, TD, RELU><<<gridn(n), 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, gamma, tot, (TD*)dy, dgamma, dbeta, batch_stats)
   const bool yf = ydt == LASR_F32, hf = hdt == LASR_F32, df = dydt == LASR_F32;
   if (yf && hf && df) BA(float, float, float);
   else if (yf && hf) BA(float, float, bf16_t);
@@ -810,7 +825,26 @@ extern "C" int lasr_bn_swish_bwd(const void* y, int ydt, const void* dh, int hdt
   else if (df) BA(bf16_t, bf16_t, float);
   else BA(bf16_t, bf16_t, bf16_t);
 #undef BA
-  return lasr_check_launch("bn_swish_bwd/apply");
+  return lasr_check_launch("bn_act_bwd/apply");
+}
+
+extern "C" int lasr_bn_act_bwd(const void* y, int ydt, const void* dh, int hdt, int64_t rows,
+                               int C, const float* scale, const float* shift, const float* mean,
+                               const float* rstd, const float* gamma, float* dgamma,
+                               float* dbeta, void* dy, int dydt, float* ws, int64_t ws_floats,
+                               int batch_stats, int act, void* stream) {
+  const int64_t nparts = cdiv(rows, BN_ROWS);
+  LASR_CHECK_ARG(ws_floats >= (nparts + 1) * 2 * C, "lasr_bn_act_bwd: workspace too small");
+  LASR_CHECK_ARG(nparts <= 65535, "lasr_bn_act_bwd: too many rows");
+  LASR_CHECK_ARG(act == LASR_ACT_SWISH || act == LASR_ACT_RELU, "lasr_bn_act_bwd: act must be SWISH or RELU");
+  if (rows == 0) return LASR_OK;
+  LASR_CHECK_ARG(C % 8 == 0, "lasr_bn_act_bwd: C must be a multiple of 8");
+  hipStream_t st = (hipStream_t)stream;
+  if (act == LASR_ACT_RELU)
+    return bn_act_bwd_launch<true>(y, ydt, dh, hdt, rows, C, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy,
+                                   dydt, ws, nparts, batch_stats, st);
+  return bn_act_bwd_launch<false>(y, ydt, dh, hdt, rows, C, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy,
+                                  dydt, ws, nparts, batch_stats, st);
 }
 
 extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int dydt, int B, int T,

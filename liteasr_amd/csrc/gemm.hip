@@ -21,10 +21,10 @@ int g_stages = 0;  // lasr_gemm_force_split (tuning hook)
 
 // bf16 launch table: gemm_launch.h, instantiated per operand layout in gemm_l{0..3}.hip
 template <bool AKC, bool BKC, typename TC>
-void launch_bf16(const GemmP& p, int BM, int BN, int ks, bool glds, dim3 grid, hipStream_t st);
-#define LASR_EXTERN_LAUNCH(ak, bk)                                                                    \
-  extern template void launch_bf16<ak, bk, float>(const GemmP&, int, int, int, bool, dim3, hipStream_t); \
-  extern template void launch_bf16<ak, bk, bf16_t>(const GemmP&, int, int, int, bool, dim3, hipStream_t);
+void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3 grid, hipStream_t st);
+#define LASR_EXTERN_LAUNCH(ak, bk)                                                                         \
+  extern template void launch_bf16<ak, bk, float>(const GemmP&, int, int, int, int, bool, dim3, hipStream_t); \
+  extern template void launch_bf16<ak, bk, bf16_t>(const GemmP&, int, int, int, int, bool, dim3, hipStream_t);
 LASR_EXTERN_LAUNCH(true, true)
 LASR_EXTERN_LAUNCH(true, false)
 LASR_EXTERN_LAUNCH(false, true)
@@ -32,13 +32,13 @@ LASR_EXTERN_LAUNCH(false, false)
 #undef LASR_EXTERN_LAUNCH
 
 template <typename TC>
-static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int BN, int ks, bool glds,
+static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int BN, int ks, int nw, bool glds,
                      dim3 grid, hipStream_t st) {
   if (bf16in) {
-    if (akc && bkc) launch_bf16<true, true, TC>(p, BM, BN, ks, glds, grid, st);
-    else if (akc) launch_bf16<true, false, TC>(p, BM, BN, ks, glds, grid, st);
-    else if (bkc) launch_bf16<false, true, TC>(p, BM, BN, ks, glds, grid, st);
-    else launch_bf16<false, false, TC>(p, BM, BN, ks, glds, grid, st);
+    if (akc && bkc) launch_bf16<true, true, TC>(p, BM, BN, ks, nw, glds, grid, st);
+    else if (akc) launch_bf16<true, false, TC>(p, BM, BN, ks, nw, glds, grid, st);
+    else if (bkc) launch_bf16<false, true, TC>(p, BM, BN, ks, nw, glds, grid, st);
+    else launch_bf16<false, false, TC>(p, BM, BN, ks, nw, glds, grid, st);
   } else {
     if (akc && bkc) gemm_f32_kernel<true, true, TC><<<grid, 256, 0, st>>>(p);
     else if (akc) gemm_f32_kernel<true, false, TC><<<grid, 256, 0, st>>>(p);
@@ -86,8 +86,11 @@ extern "C" int lasr_gemm_force_ksub(int ksub) {
   return LASR_OK;
 }
 
-// Tile and split-K choice for one call (shared by lasr_gemm and lasr_gemm_plan).
-static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, int* kso = nullptr) {
+// Tile and split-K choice for one call (shared by lasr_gemm and lasr_gemm_plan).  nwo: 8 for
+// an 8-wave instance (none planned today; see below), else 4.
+static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, int* kso = nullptr,
+                      int* nwo = nullptr) {
+  int nw = 4;
   const int batch = a->batch > 0 ? a->batch : 1;
   const bool bf = a->in_dtype == LASR_BF16;
   int BM = 64, BN = 64;
@@ -130,6 +133,9 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
     if (BM == 128 && BN == 128 && (a->zout || a->aux || (a->act && a->drop_p > 0.f)) && a->N >= 1024) BN = 256;
     // (FFN fc2 forward, M 7968 N 256 K 2048: 64 x 128 wins the cold-operand sweep, 24.2 vs
     // 27.6 us, but loses inside the step, 33.5 vs 24 us per launch: kept at 64 x 64)
+    // (the 8-wave 256 x 256 tile, one workgroup per CU, for the FFN fc1 forward / fc2 input
+    // gradient at K = 256: 40.8 / 38.5 vs 37.8 / 38.4 us in the step, 11.70 vs 11.59 ms/step --
+    // their time is the epilogue, which a second co-resident 4-wave workgroup overlaps)
   }
   if (!bf && autosplit) {
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
@@ -138,6 +144,7 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
   if (bf && g_tile_m) {
     BM = g_tile_m;
     BN = g_tile_n;
+    nw = 4;
   }
   if (autosplit && g_split) split = g_split;
   if (a->split_k <= -2 && plain && a->workspace) split = -a->split_k;  // explicit partials-only
@@ -152,8 +159,10 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
     const int64_t kc = split > 1 ? cdiv(a->K, split) : a->K;
     const bool small = BM * BN <= 64 * 128;
     *kso = (bf && BM < 256 && BN < 256 && ((BM == 64 && BN == 64) || kc >= 1024 || (kc >= 512 && small))) ? 2 : 1;
-    if (g_ksub) *kso = g_ksub;
+    if (nw == 8) *kso = 2;
+    else if (g_ksub) *kso = g_ksub;
   }
+  if (nwo) *nwo = nw;
   *BMo = BM;
   *BNo = BN;
   *splito = split;
@@ -176,12 +185,18 @@ static bool gemm_uses_glds(const lasr_gemm_args* a) {
 
 extern "C" int lasr_gemm_plan(const lasr_gemm_args* a, int* tile_m, int* tile_n, int* split_k, int* flags) {
   LASR_CHECK_ARG(a && tile_m && tile_n && split_k, "lasr_gemm_plan: null argument");
-  int ks = 1;
-  gemm_plan(a, tile_m, tile_n, split_k, &ks);
+  int ks = 1, nw = 4;
+  gemm_plan(a, tile_m, tile_n, split_k, &ks, &nw);
+  const bool glds = gemm_uses_glds(a);
+  if (!glds) {  // as lasr_gemm: 256-wide tiles exist only in the LDS-DMA kernel
+    *tile_m = std::min(*tile_m, 128);
+    *tile_n = std::min(*tile_n, 128);
+    nw = 4;
+  }
   if (flags) {
-    const bool glds = gemm_uses_glds(a);
     *flags = (glds ? LASR_PLAN_GLDS : 0) | (a->rowsum && glds && a->lda_k != 1 ? LASR_PLAN_ROWSUM_FUSED : 0) |
-             (glds && ks == 2 && *tile_m < 256 ? LASR_PLAN_KSUB2 : 0);
+             (glds && ks == 2 && (*tile_m < 256 || nw == 8) ? LASR_PLAN_KSUB2 : 0) |
+             (glds && nw == 8 ? LASR_PLAN_WIDE : 0);
   }
   return LASR_OK;
 }
@@ -250,8 +265,8 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
     p.epi_mode = !base_ok ? 2 : nsrc == 0 ? 0 : src_ok ? 1 : 2;
   }
 
-  int BM, BN, split, ks;
-  gemm_plan(a, &BM, &BN, &split, &ks);
+  int BM, BN, split, ks, nw;
+  gemm_plan(a, &BM, &BN, &split, &ks, &nw);
   p.split_k = split;
   const int kstep = bf ? 32 : 16;
   p.kchunk = split > 1 ? (int)(cdiv(cdiv(a->K, split), kstep) * kstep) : a->K;
@@ -267,6 +282,7 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   if (!glds) {  // 256-wide tiles exist only in the LDS-DMA kernel
     BM = std::min(BM, 128);
     BN = std::min(BN, 128);
+    nw = 4;
   }
   dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM), (unsigned)(batch * split));
   LASR_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lasr_gemm: grid too large");
@@ -276,8 +292,8 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
     p.rowsum = a->rowsum;
     if (split > 1) p.rs_ws = p.ws + (int64_t)split * batch * a->M * a->N;
   }
-  if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, ks, glds, grid, st);
-  else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, ks, glds, grid, st);
+  if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, ks, nw, glds, grid, st);
+  else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, ks, nw, glds, grid, st);
   int rc = lasr_check_launch("lasr_gemm");
   if (!rc && split > 1 && a->split_k >= 0) {
     const int64_t total = (int64_t)a->M * a->N * batch;

@@ -26,6 +26,23 @@ static GemmP conv_params(const lasr_conv2_args* a) {
   return p;
 }
 
+// The weight gradient on 256 x 256 tiles with 8 waves and 64-deep ring stages
+// (gemm_bf16_glds_kernel NW = 8) when C % 256 == 0: one 512-thread workgroup per CU, K split
+// so the 9 tiles fill the 256 CUs once (28 slices at config 2), half the LDS-DMA ingest per
+// MFMA of the 4-wave 128 x 128 tiles: 365 -> 236 us standalone, 352 -> 186 us in the step
+// (tools/conv2_bench.py, profiles/r03).  Forward and data gradient stay on the 4-wave
+// 128 x 256 tiles: their 8-wave variants (256 x 256 with 64- or 32-deep stages, 256 x 128)
+// took 265-299 / 523-529 us against 262 / 468 (their 592-tile grids run 2.3 rounds of one
+// workgroup per CU).  LASR_CONV_WIDE=0 keeps the 4-wave weight gradient (A/B).
+static int conv_wide() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("LASR_CONV_WIDE");
+    v = e && e[0] ? atoi(e) : 1;
+  }
+  return v;
+}
+
 extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   LASR_CHECK_ARG(a != nullptr, "lasr_conv2_gemm: null args");
   LASR_CHECK_ARG(a->mode == LASR_CONV2_FWD || a->mode == LASR_CONV2_DW || a->mode == LASR_CONV2_DX,
@@ -46,6 +63,7 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     LASR_CHECK_ARG(a->w2p && aligned16(a->w2p), "lasr_conv2_gemm: w2p");
   hipStream_t st = (hipStream_t)stream;
   const int BN = C % 256 == 0 ? 256 : 128;
+  const bool wide = BN == 256 && conv_wide() > 0;
   p.c_vec = 1;
   if (a->mode == LASR_CONV2_FWD) {
     LASR_CHECK_ARG(a->bias && aligned16(a->bias), "lasr_conv2_gemm: bias");
@@ -67,22 +85,29 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     p.B = a->y1; p.ldb_n = 1; p.ldb_k = 9 * C;
     p.C = a->out; p.ldc = 9 * C;
     p.epi_mode = 0; p.ws_vec = 1; p.v4 = 1;
-    const bool big = g_tile_m == 256 && C % 256 == 0;
+    const bool big = (g_tile_m == 256 || wide) && C % 256 == 0;
     const int TM = big ? 256 : 128, TN = big ? 256 : 128;
     const int64_t tiles = (int64_t)(C / TM) * (9 * C / TN);
     int split = 1;
     const int kt = (int)(kpad / 32);
     if (g_split > 0) split = g_split;
+    else if (wide)  // one 512-thread workgroup per CU: fill the 256 CUs once, no second round
+      split = (int)std::max<int64_t>(1, std::min<int64_t>(256 / tiles, kt / 16));
     else while (tiles * split < 512 && kt / (split * 2) >= 16 && split * 2 <= 64) split *= 2;
-    const int64_t need = ((int64_t)split * C * 9 * C + (a->rowsum ? (int64_t)split * C : 0)) * 4;
-    if (split > 1 && (!a->workspace || a->workspace_bytes < need || !aligned16(a->workspace))) split = 1;
+    // fewer K slices when the workspace holds fewer partial slabs (never silently one slice)
+    const int64_t per = ((int64_t)C * 9 * C + (a->rowsum ? C : 0)) * 4;
+    const int64_t fit = a->workspace && aligned16(a->workspace) ? a->workspace_bytes / per : 0;
+    if (split > fit) split = (int)std::max<int64_t>(1, fit);
     p.split_k = split;
-    p.kchunk = split > 1 ? (int)(cdiv(cdiv(kpad, split), 32) * 32) : (int)kpad;
+    p.kchunk = split > 1 ? (int)(cdiv(cdiv(kpad, split), wide ? 64 : 32) * (wide ? 64 : 32)) : (int)kpad;
+    if (split > 1) split = (int)cdiv(kpad, p.kchunk);  // no empty slice
+    p.split_k = split;
     p.ws = (float*)a->workspace;
     p.rowsum = a->rowsum;
     if (a->rowsum && split > 1) p.rs_ws = p.ws + (int64_t)split * C * 9 * C;
     dim3 grid((unsigned)(9 * C / TN), (unsigned)(C / TM), (unsigned)split);
-    if (big) gemm_bf16_glds_kernel<256, 256, false, false, float, 3, 1, G_DW><<<grid, 256, 0, st>>>(p);
+    if (wide) gemm_bf16_glds_kernel<256, 256, false, false, float, 2, 1, G_DW, 2, 8><<<grid, 512, 0, st>>>(p);
+    else if (big) gemm_bf16_glds_kernel<256, 256, false, false, float, 3, 1, G_DW><<<grid, 256, 0, st>>>(p);
     else if (g_stages >= 4) gemm_bf16_glds_kernel<128, 128, false, false, float, 4, 2, G_DW><<<grid, 256, 0, st>>>(p);
     else gemm_bf16_glds_kernel<128, 128, false, false, float, 3, 3, G_DW><<<grid, 256, 0, st>>>(p);
     int rc = lasr_check_launch("lasr_conv2_gemm/dw");

@@ -254,8 +254,8 @@ LASR_DEV int64_t dx_row(const ConvG& g, int m) {
   return ((int64_t)(b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf) * g.C;
 }
 
-template <int BM, int BN, typename TC, bool TRANS = false, int G = G_LIN>
-LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem_epi, int m0,
+template <int BM, int BN, typename TC, bool TRANS = false, int G = G_LIN, int NW = 4>
+LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)], char* smem_epi, int m0,
                             int n0, int s, int z, int z1, int z2) {
   // output-row offsets: linear (ldc, ld of the aux/res source), or the transposed-conv scatter
   // of a G_DX launch (aux = y1 shares dy1's layout)
@@ -263,18 +263,20 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
     if constexpr (G == G_DX) return dx_row(p.cv, m);
     else return (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc;
   };
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  // NW waves as 2 (rows) x NW/2 (columns); NT threads finish the staged rows
+  constexpr int NT = NW * 64, WCOLS = NW / 2;
+  constexpr int WM = BM / 2, WN = BN / WCOLS, FM = WM / 16, FN = WN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid / WCOLS, wc = wid % WCOLS;
   constexpr int LDC = BN + 4;  // +4 floats: the 4 row-groups of a write land on distinct banks
   float* cs = reinterpret_cast<float*>(smem_epi);
   const int rq = (lane >> 4) * 4, cl = lane & 15;
   const float al = alpha_of(p);
   const bool split = p.split_k > 1;
   float* wsp = split ? p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N : nullptr;
-  // A thread's 8-column slot is the same in every epilogue iteration (256 % (BN/8) == 0):
+  // A thread's 8-column slot is the same in every epilogue iteration (NT % (BN/8) == 0):
   // its bias is loaded once; the aux/res rows of a half are prefetched before the barrier.
-  constexpr int CPR = BN / 8, RPI = 256 / CPR, ITERS = WM / RPI;
+  constexpr int CPR = BN / 8, RPI = NT / CPR, ITERS = WM / RPI;
   static_assert(WM % RPI == 0, "epilogue tiling");
   const int ec8 = (tid % CPR) * 8, er0 = tid / CPR;
   const int en = n0 + ec8;
@@ -355,7 +357,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], char
       continue;
     }
     constexpr int NV = WM * BN / 8;
-    for (int v = tid; v < NV; v += 256) {
+    for (int v = tid; v < NV; v += NT) {
       const int r = v / (BN / 8), c8 = (v % (BN / 8)) * 8;
       const int m = m0 + h * WM + r, n = n0 + c8;
       if (m < p.M && n < p.N) {
@@ -500,12 +502,13 @@ LASR_DEV void epi_store4(const GemmP& p, int z1, int z2, int z, int m, int n, in
 // C^T: lane l owns row m = mb + (l & 15) and the 4 consecutive columns nb + 4 (l >> 4) + e
 // -> one 8-B (bf16) / 16-B (fp32) access per 4 outputs (a wave instruction covers 16 rows
 // x 32 / 64 contiguous bytes; the L2 merges the row segments before write-back).
-template <int BM, int BN, typename TC>
-LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32], int m0, int n0, int s,
+template <int BM, int BN, typename TC, int NW = 4>
+LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)], int m0, int n0, int s,
                                    int z, int z1, int z2) {
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int WCOLS = NW / 2;
+  constexpr int WM = BM / 2, WN = BN / WCOLS, FM = WM / 16, FN = WN / 16;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid / WCOLS, wc = wid % WCOLS;
   const float al = alpha_of(p);
   const int mr = m0 + wr * WM + (lane & 15), nc = n0 + wc * WN + 4 * (lane >> 4);
   if (p.split_k > 1) {
@@ -562,15 +565,15 @@ LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / 32
 //    zero row when that falls outside [0,T2) x [0,F2).
 //  G_DW, B = im2col(y1) [M2, 9C] with k = m2 rows (M/N-contiguous operand): every k row is a
 //    contiguous run of one tap; the row walk advances (b, t2, f2) by 32 rows per tile.
-template <int R_TILE>
+template <int R_TILE, int NT = 256>
 struct ConvRowsKC {  // G_FWD / G_DX A operand
-  static constexpr int PER = R_TILE * 4 / 256;
+  static constexpr int PER = R_TILE * 4 / NT;
   int off[PER];
   int vm[PER];  // G_DX: bit dt*2+df set when tap (dt, df) is inside dy2
   LASR_DEV void init_fwd(const ConvG& g, int row0, int R, int tid) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int P = i * 256 + tid, r = P >> 2, c = (P & 3) ^ swz(r);
+      const int P = i * NT + tid, r = P >> 2, c = (P & 3) ^ swz(r);
       const int m = min(row0 + r, R - 1);
       const int f2 = m % g.F2, t = m / g.F2, t2 = t % g.T2, b = t / g.T2;
       off[i] = ((b * g.T1 + 2 * t2) * g.F1 + 2 * f2) * g.C + c * 8;
@@ -582,7 +585,7 @@ struct ConvRowsKC {  // G_FWD / G_DX A operand
     const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int P = i * 256 + tid, r = P >> 2, c = (P & 3) ^ swz(r);
+      const int P = i * NT + tid, r = P >> 2, c = (P & 3) ^ swz(r);
       const int m = min(row0 + r, R - 1);
       const int j = m % nJ, t = m / nJ, ii = t % nI, b = t / nI;
       off[i] = ((b * g.T2 + ii) * g.F2 + j) * g.C + c * 8;
@@ -596,7 +599,7 @@ struct ConvRowsKC {  // G_FWD / G_DX A operand
     const int wid = tid >> 6;
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-      __builtin_amdgcn_global_load_lds((gptr_t)(base + off[i] + koff), (lptr_t)(dst + (i * 256 + wid * 64) * 8),
+      __builtin_amdgcn_global_load_lds((gptr_t)(base + off[i] + koff), (lptr_t)(dst + (i * NT + wid * 64) * 8),
                                        16, 0, 0);
   }
   LASR_DEV void issue_dx(const bf16_t* base, int64_t shift, int bit, const bf16_t* zero, bf16_t* dst,
@@ -604,23 +607,23 @@ struct ConvRowsKC {  // G_FWD / G_DX A operand
     const int wid = tid >> 6;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c8 = ((i * 256 + tid) & 3) * 8;
+      const int c8 = ((i * NT + tid) & 3) * 8;
       const bf16_t* src = (vm[i] >> bit) & 1 ? base + off[i] + shift : zero + c8;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * 256 + wid * 64) * 8), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * NT + wid * 64) * 8), 16, 0, 0);
     }
   }
 };
 
-template <int R_TILE>
+template <int R_TILE, int NT = 256>
 struct ConvRowsDW {  // G_DW B operand: tile [32 k][R_TILE n] of im2col(y1), k = m2
-  static constexpr int PER = R_TILE * 4 / 256, CPR = R_TILE / 8;
+  static constexpr int PER = R_TILE * 4 / NT, CPR = R_TILE / 8;
   int noff[PER], f2[PER], t2[PER], b[PER];
   LASR_DEV void init(const ConvG& g, int n0, int N, int kbeg, int tid) {
     const int tap = n0 / g.C, kh = tap / 3, kw = tap - 3 * kh;
     const int tbase = (kh * g.F1 + kw) * g.C - tap * g.C;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int P = i * 256 + tid, k = P / CPR, ps = P % CPR;
+      const int P = i * NT + tid, k = P / CPR, ps = P % CPR;
       const int ls = ((((ps >> 1) ^ htr<R_TILE>(k))) << 1) | (ps & 1);
       const int gc = min(n0 + ls * 8, ((N + 7) & ~7) - 8);
       noff[i] = tbase + gc;
@@ -638,7 +641,7 @@ struct ConvRowsDW {  // G_DW B operand: tile [32 k][R_TILE n] of im2col(y1), k =
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int rb = b[i] < g.B ? ((b[i] * g.T1 + 2 * t2[i]) * g.F1 + 2 * f2[i]) * g.C : last;
-      __builtin_amdgcn_global_load_lds((gptr_t)(base + rb + noff[i]), (lptr_t)(dst + (i * 256 + wid * 64) * 8),
+      __builtin_amdgcn_global_load_lds((gptr_t)(base + rb + noff[i]), (lptr_t)(dst + (i * NT + wid * 64) * 8),
                                        16, 0, 0);
       f2[i] += g.r32;
       t2[i] += g.q32;
@@ -659,22 +662,24 @@ LASR_DEV int xcd_remap(int orig, int nwg) {
 
 // One output tile (tx, ty) of K slice / batch index zz: the body shared by the launch-grid
 // kernel (gemm_bf16_glds_kernel) and the grouped weight-gradient kernel (gemm_dw_group_kernel).
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int G, int KS>
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int G, int KS, int NW = 4>
 LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const int zz) {
   static_assert(G == G_LIN || (G == G_DW ? (!AKC && !BKC) : (AKC && (G == G_FWD) == BKC)),
                 "gather instance operand orientation");
-  static_assert(KS == 1 || (KS == 2 && G == G_LIN), "k sub-tiles: generic instances only");
+  static_assert(KS == 1 || KS == 2, "k sub-tiles per ring stage");
+  static_assert(NW == 4 || NW == 8, "4 waves (2 x 2) or 8 waves (2 x 4)");
   constexpr int BK = 32;
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int NT = NW * 64, WCOLS = NW / 2;
+  constexpr int WM = BM / 2, WN = BN / WCOLS, FM = WM / 16, FN = WN / 16;
   constexpr int TILE = (BM + BN) * BK;  // elements per 32-deep sub-tile
   constexpr int STAGE = KS * TILE;      // elements per ring stage
-  constexpr int MAIN_BYTES = S * STAGE * 2;  // >= the rowsum combine slab (256/(BM/8) x BM floats)
+  constexpr int MAIN_BYTES = S * STAGE * 2;  // >= the rowsum combine slab (NT/(BM/8) x BM floats)
   constexpr int EPI_BYTES = WM * (BN + 4) * 4;
-  constexpr int GL = (BM + BN) * 4 / 256;  // glds per thread per k tile
+  constexpr int GL = (BM + BN) * 4 / NT;  // glds per thread per k tile
   __shared__ __attribute__((aligned(16))) char smem_epi[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
   bf16_t* smem = reinterpret_cast<bf16_t*>(smem_epi);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid / WCOLS, wc = wid % WCOLS;
 
   const int s = zz % p.split_k, z = zz / p.split_k;
   const int z1 = z / p.batch_div, z2 = z % p.batch_div;
@@ -695,27 +700,24 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   // full 32-deep tiles go through the glds ring; a ragged last tile is handled after the
   // loop (ordinary loads inside the loop would make hipcc drain the ring with vmcnt(0))
   const int nfull = (kend - kbeg) > 0 ? (kend - kbeg) / BK : 0;
-  [[maybe_unused]] ConvRowsKC<BM> ga;
-  [[maybe_unused]] ConvRowsDW<BN> gb;
+  [[maybe_unused]] ConvRowsKC<BM, NT> ga;
+  [[maybe_unused]] ConvRowsDW<BN, NT> gb;
   if constexpr (G == G_FWD) ga.init_fwd(p.cv, m0, p.M, tid);
   if constexpr (G == G_DX) ga.init_dx(p.cv, m0, p.M, tid);
   if constexpr (G == G_DW) gb.init(p.cv, n0, p.N, kbeg, tid);
-  auto issue = [&](int t) {
-    bf16_t* dst = smem + (t % S) * STAGE;
-    const int k0 = kbeg + t * (KS * BK);
+  // one 32-deep sub-tile at k0 into dst (the conv walkers keep per-position state: sub-tiles
+  // are issued in k order)
+  auto issue_sub = [&](const int k0, bf16_t* dst) {
     if (LASR_EXP & 4) return;
     if constexpr (G == G_LIN) {
-#pragma unroll
-      for (int u = 0; u < KS; ++u) {
-        glds_tile<BM, AKC>(A, lda, m0, p.M, k0 + u * BK, dst + u * TILE, tid);
-        glds_tile<BN, BKC>(B, ldb, n0, p.N, k0 + u * BK, dst + u * TILE + BM * BK, tid);
-      }
+      glds_tile<BM, AKC, NT>(A, lda, m0, p.M, k0, dst, tid);
+      glds_tile<BN, BKC, NT>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
     } else if constexpr (G == G_FWD) {
       const int C = p.cv.C, tap = k0 / C, kh = tap / 3, kw = tap - 3 * kh;
       ga.issue(A, (int64_t)(kh * p.cv.F1 + kw) * C + (k0 - tap * C), dst, tid);
-      glds_tile<BN, true>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
+      glds_tile<BN, true, NT>(B, ldb, n0, p.N, k0, dst + BM * BK, tid);
     } else if constexpr (G == G_DW) {
-      glds_tile<BM, false>(A, lda, m0, p.M, k0, dst, tid);
+      glds_tile<BM, false, NT>(A, lda, m0, p.M, k0, dst, tid);
       gb.issue(p.cv, B, dst + BM * BK, tid);
     } else {
       // class tap ti = k0 / C: (kh, kw) = (pt ? 1 : 2a, pf ? 1 : 2c), reading dy2 row (i-dt, j-df)
@@ -725,8 +727,14 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
       const int dt = pt ? 0 : a, df = pf ? 0 : c;
       const int kh = pt ? 1 : 2 * a, kw = pf ? 1 : 2 * c;
       ga.issue_dx(A, cin - (int64_t)(dt * p.cv.F2 + df) * C, dt * 2 + df, p.cv.zero, dst, tid);
-      glds_tile<BN, false>(B + (kh * 3 + kw) * C, ldb, n0, p.N, cin, dst + BM * BK, tid);
+      glds_tile<BN, false, NT>(B + (kh * 3 + kw) * C, ldb, n0, p.N, cin, dst + BM * BK, tid);
     }
+  };
+  auto issue = [&](int t) {
+    bf16_t* dst = smem + (t % S) * STAGE;
+    const int k0 = kbeg + t * (KS * BK);
+#pragma unroll
+    for (int u = 0; u < KS; ++u) issue_sub(k0 + u * BK, dst + u * TILE);
   };
   auto compute = [&](const bf16_t* cur) {
     bf16x8 af[FM], bfr[FN];
@@ -785,25 +793,24 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
     if constexpr (!AKC)
       if (do_rs)
 #pragma unroll
-        for (int u = 0; u < KS; ++u) rowsum_tile<BM>(smem + (kt % S) * STAGE + u * TILE, tid, rs);
+        for (int u = 0; u < KS; ++u) rowsum_tile<BM, NT>(smem + (kt % S) * STAGE + u * TILE, tid, rs);
   }
   if constexpr (KS > 1) {
     // leftover full sub-tile(s): the loop's last wait was vmcnt(0), so no DMA is in flight
     for (int j = nst * KS; j < nfull; ++j) {
       __syncthreads();
-      glds_tile<BM, AKC>(A, lda, m0, p.M, kbeg + j * BK, smem, tid);
-      glds_tile<BN, BKC>(B, ldb, n0, p.N, kbeg + j * BK, smem + BM * BK, tid);
+      issue_sub(kbeg + j * BK, smem);
       wait_vmcnt<0>();
       lds_barrier();
       compute(smem);
       if constexpr (!AKC)
-        if (do_rs) rowsum_tile<BM>(smem, tid, rs);
+        if (do_rs) rowsum_tile<BM, NT>(smem, tid, rs);
     }
   }
   if (G == G_LIN && nfull < nk) {  // ragged tail: register loader with zero fill (conv: host-checked K % 32 == 0)
     __syncthreads();
-    TileLoader<BM, AKC> la;
-    TileLoader<BN, BKC> lb;
+    TileLoader<BM, AKC, NT> la;
+    TileLoader<BN, BKC, NT> lb;
     const int k0 = kbeg + nfull * BK;
     la.load(A, AKC ? p.lda_m : 0, AKC ? 0 : p.lda_k, m0, p.M, k0, kend, true, tid);
     lb.load(B, BKC ? p.ldb_n : 0, BKC ? 0 : p.ldb_k, n0, p.N, k0, kend, true, tid);
@@ -812,12 +819,12 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
     __syncthreads();
     compute(smem);
     if constexpr (!AKC)
-      if (do_rs) rowsum_tile<BM>(smem, tid, rs);
+      if (do_rs) rowsum_tile<BM, NT>(smem, tid, rs);
   }
   __syncthreads();
   if constexpr (!AKC) {
     if (do_rs) {  // combine the k groups in fixed order, then one slot per row
-      constexpr int CH = BM / 8, KG = 256 / CH;
+      constexpr int CH = BM / 8, KG = NT / CH;
       float* red = reinterpret_cast<float*>(smem_epi);
       const int c = tid % CH, kg = tid / CH;
 #pragma unroll
@@ -837,8 +844,8 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   }
   // split-K partials: fp32, 16-B per lane straight from the accumulators; final outputs:
   // staged through LDS (full 256-B rows per wave store)
-  if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC>(p, acc, m0, n0, s, z, z1, z2);
-  else gemm_epilogue<BM, BN, TC, true, G>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
+  if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC, NW>(p, acc, m0, n0, s, z, z1, z2);
+  else gemm_epilogue<BM, BN, TC, true, G, NW>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
 }
 
 // Tile order of a weight-gradient GEMM (both operands [K, M] / [K, N] with K = rows): the
@@ -850,13 +857,17 @@ LASR_DEV void dw_tile_order(int wg, int nx, int ny, bool n_major, int& tx, int& 
   else { tx = wg % nx; ty = wg / nx; }
 }
 
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN, int KS = 1>
-__global__ __launch_bounds__(256, MINB) void gemm_bf16_glds_kernel(GemmP p) {
+// NW = 8: 512-thread workgroups, waves 2 (rows) x 4 (columns) over the tile (the 256 x 256
+// tiles of the large GEMMs: half the LDS-DMA ingest per MFMA of 128 x 256 at 4 waves).
+// MINB = workgroups per CU; the launch bound's second operand is waves per SIMD.
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN, int KS = 1,
+          int NW = 4>
+__global__ __launch_bounds__(NW * 64, MINB * NW / 4) void gemm_bf16_glds_kernel(GemmP p) {
   const int nx = gridDim.x, ny = gridDim.y;
   const int wg = xcd_remap(blockIdx.y * nx + blockIdx.x, nx * ny);
   int tx, ty;
   dw_tile_order(wg, nx, ny, !AKC && !BKC && G == G_LIN && p.N > p.M, tx, ty);
-  gemm_glds_tile<BM, BN, AKC, BKC, TC, S, G, KS>(p, tx, ty, blockIdx.z);
+  gemm_glds_tile<BM, BN, AKC, BKC, TC, S, G, KS, NW>(p, tx, ty, blockIdx.z);
 }
 
 // Grouped split-K weight-gradient GEMMs (partials only): up to LASR_DW_GROUP_MAX independent

@@ -1,5 +1,5 @@
 // lasr_gemm bf16 launch table, A K-contiguous x B K-contiguous instances (gemm_launch.h).
 #include "gemm_launch.h"
 
-template void launch_bf16<true, true, float>(const GemmP&, int, int, int, bool, dim3, hipStream_t);
-template void launch_bf16<true, true, bf16_t>(const GemmP&, int, int, int, bool, dim3, hipStream_t);
+template void launch_bf16<true, true, float>(const GemmP&, int, int, int, int, bool, dim3, hipStream_t);
+template void launch_bf16<true, true, bf16_t>(const GemmP&, int, int, int, int, bool, dim3, hipStream_t);

@@ -5,7 +5,8 @@
 #include "gemm_kernel.h"
 
 template <bool AKC, bool BKC, typename TC>
-void launch_bf16(const GemmP& p, int BM, int BN, int ks, bool glds, dim3 grid, hipStream_t st) {
+void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3 grid, hipStream_t st) {
+  (void)nw;  // no 8-wave generic instance is planned (gemm.hip gemm_plan)
   if constexpr (!AKC && !BKC && std::is_same<TC, float>::value) {
     // split-K weight-gradient GEMMs: one block per CU, so a deeper ring hides the latency
     const int S = g_stages;

@@ -44,17 +44,17 @@ LASR_DEV int tr_off(int k, int col) {  // element offset of (k, col), col % 4 ==
   return k * R_TILE + ((((col >> 4) ^ htr<R_TILE>(k))) << 4) + (col & 15);
 }
 
-template <int R_TILE, bool KC>
+template <int R_TILE, bool KC, int NT = 256>
 struct TileLoader {
   static constexpr int UNITS = R_TILE * 4;  // 16-B units per 32-deep k tile
-  static constexpr int PER = (UNITS + 255) / 256;
+  static constexpr int PER = (UNITS + NT - 1) / NT;
   uint4 r0[PER];
 
   LASR_DEV void load(const bf16_t* base, int64_t ld_r, int64_t ld_k, int row0, int R, int k0,
                      int kend, bool vec, int tid) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int u = tid + i * 256;
+      const int u = tid + i * NT;
       if (u < UNITS) {
         if (KC) {
           const int r = u >> 2, c = u & 3;
@@ -73,7 +73,7 @@ struct TileLoader {
   LASR_DEV void store(bf16_t* lds, int tid) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int u = tid + i * 256;
+      const int u = tid + i * NT;
       if (u < UNITS) {
         if (KC) {
           const int r = u >> 2, c = u & 3;
@@ -168,10 +168,11 @@ LASR_DEV v4i ds_b128_asm(const bf16_t* p) {
   return r;
 }
 // Row sums of an M-contiguous A tile image ([32 k][BM], tr_off layout): thread owns the 8
-// rows 8*(tid % (BM/8)).. and k rows tid / (BM/8) + j * (256 / (BM/8)).
-template <int BM>
+// rows 8*(tid % (BM/8)).. and k rows tid / (BM/8) + j * (NT / (BM/8)).
+template <int BM, int NT = 256>
 LASR_DEV void rowsum_tile(const bf16_t* tile, int tid, float* rs) {
-  constexpr int CH = BM / 8, KG = 256 / CH, KR = 32 / KG;
+  constexpr int CH = BM / 8, KG = NT / CH, KR = 32 / KG;
+  static_assert(KR >= 1 && KR <= 4 && KR * KG == 32, "rowsum_tile geometry");
   const int c = tid % CH, k0 = tid / CH;
   v4i r[KR];
 #pragma unroll
@@ -214,15 +215,16 @@ LASR_DEV bf16x8 frag_from_raw(const v2i* r) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// Issue the glds of one operand tile (R_TILE rows x 32 k) into `dst`.
-template <int R_TILE, bool KC>
+// Issue the glds of one operand tile (R_TILE rows x 32 k) into `dst` (NT threads).
+template <int R_TILE, bool KC, int NT = 256>
 LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0, bf16_t* dst,
                         int tid) {
-  constexpr int PER = R_TILE * 4 / 256;  // 16-B positions per thread
+  constexpr int PER = R_TILE * 4 / NT;  // 16-B positions per thread
+  static_assert(PER >= 1 && PER * NT == R_TILE * 4, "glds_tile: tile / thread count");
   const int wid = tid >> 6, lane = tid & 63;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int P = i * 256 + tid;  // linear 16-B position in the image
+    const int P = i * NT + tid;  // linear 16-B position in the image
     const bf16_t* src;
     if (KC) {
       const int r = P >> 2, c = (P & 3) ^ swz(r);
@@ -235,7 +237,7 @@ LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0,
       const int gc = min(row0 + ls * 8, ((R + 7) & ~7) - 8);  // host: row stride >= roundup8(R)
       src = base + (int64_t)(k0 + k) * ld + gc;
     }
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * 256 + wid * 64) * 8), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * NT + wid * 64) * 8), 16, 0, 0);
     (void)lane;
   }
 }

@@ -595,7 +595,7 @@ def _conv2(mode, y1, out, w2p=None, bias=None, dy2=None, rowsum=None):
         assert rowsum.dtype == torch.float32 and rowsum.is_contiguous() and rowsum.numel() == Cc
         a.rowsum = ptr(rowsum)
     if mode == N.CONV2_DW:
-        ws = WS.get(16 * (9 * Cc * Cc + Cc), y1.device)
+        ws = WS.get(32 * (9 * Cc * Cc + Cc), y1.device)  # K slices: <= 32 (gemm_conv.hip caps to fit)
         a.workspace, a.workspace_bytes = ptr(ws), ws.numel() * 4
     N.call("lasr_conv2_gemm", C.byref(a), stream())
 
@@ -637,19 +637,19 @@ def bn_finalize(stats, nparts, Cc, eps, momentum, gamma, beta, rmean, rvar, nbt,
            int(update), stream())
 
 
-def bn_swish_fwd(y, scale, shift, h):
+def bn_act_fwd(y, scale, shift, h, act=N.ACT_SWISH):
+    """h = act(y * scale + shift) (the conv module's BatchNorm + Swish / ReLU)."""
     rows, Cc = y.shape
-    N.call("lasr_bn_swish_fwd", ptr(y), dt(y), rows, Cc, ptr(scale), ptr(shift), ptr(h), dt(h),
-           stream())
+    N.call("lasr_bn_act_fwd", ptr(y), dt(y), rows, Cc, ptr(scale), ptr(shift), ptr(h), dt(h), act, stream())
 
 
-def bn_swish_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy, batch_stats=True):
+def bn_act_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, dy, batch_stats=True, act=N.ACT_SWISH):
     """batch_stats False: eval-mode BN (mean/rstd are the running statistics)."""
     rows, Cc = y.shape
     ws = WS.get(((rows + 63) // 64 + 1) * 2 * Cc, y.device)
-    N.call("lasr_bn_swish_bwd", ptr(y), dt(y), ptr(dh), dt(dh), rows, Cc, ptr(scale), ptr(shift),
+    N.call("lasr_bn_act_bwd", ptr(y), dt(y), ptr(dh), dt(dh), rows, Cc, ptr(scale), ptr(shift),
            ptr(mean), ptr(rstd), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dy), dt(dy), ptr(ws),
-           ws.numel(), int(bool(batch_stats)), stream())
+           ws.numel(), int(bool(batch_stats)), act, stream())
 
 
 def glu_dwconv_bwd(z1, dy, B, T, Cc, K, w, dz1, dw, db):

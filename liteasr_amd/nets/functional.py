@@ -443,7 +443,7 @@ def conv_forward(ln, w, env, x_in, p_res, s_res, training, post=None):
     K.bn_finalize(stats, nparts, d, 1e-5, 0.1, w.gamma, w.beta, w.rmean, w.rvar, w.nbt, mean, rstd,
                   scale, shift, 1 if training else 2)
     h3 = _e((M, d), adt, dev)
-    K.bn_swish_fwd(y, scale, shift, h3)
+    K.bn_act_fwd(y, scale, shift, h3, act=getattr(w, "act", ACT_SWISH))
     out = res_proj(h3, w.Wpw2, w.bpw2, x_in, 1.0, p_res, s_res, post)
     return out, SimpleNamespace(z1=z1, y=y, mean=mean, rstd=rstd, scale=scale, shift=shift, h3=h3,
                                 training=training)
@@ -457,8 +457,8 @@ def conv_backward(gb, ln, sv, w, g, env, lnb=None):
     dh3 = _e((M, d), adt, dev)
     K.gemm(gb, w.Wpw2, dh3)
     dy = _e((M, d), F32, dev)
-    K.bn_swish_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy,
-                   batch_stats=sv.training)
+    K.bn_act_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy,
+                 batch_stats=sv.training, act=getattr(w, "act", ACT_SWISH))
     dz1 = _e((M, 2 * d), adt, dev)
     K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
     K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0, rowsum=g.bpw1, group=True)

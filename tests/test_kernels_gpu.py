@@ -871,14 +871,14 @@ def test_conformer_conv_module_pieces(dtype, Cc, T):
     close(rv, bn.running_var, 1e-5, "running_var")
     assert int(nbt.item()) == 1
     h = torch.empty(B * T, Cc, device=DEV, dtype=dtype)
-    kn.bn_swish_fwd(y.view(B * T, Cc), scale, shift, h)
+    kn.bn_act_fwd(y.view(B * T, Cc), scale, shift, h)
     hr = u * torch.sigmoid(u)
     close(h, hr.transpose(1, 2).reshape(B * T, Cc), tol, "bn swish fwd")
     dh = torch.randn(B * T, Cc, device=DEV).to(dtype)
     dgm = torch.zeros(Cc, device=DEV)
     dbt = torch.zeros(Cc, device=DEV)
     dyb = torch.empty(B * T, Cc, device=DEV, dtype=torch.float32)
-    kn.bn_swish_bwd(y.view(B * T, Cc), dh, scale, shift, mean, rstd, gamma, dgm, dbt, dyb)
+    kn.bn_act_bwd(y.view(B * T, Cc), dh, scale, shift, mean, rstd, gamma, dgm, dbt, dyb)
     gy, gw_, gb_ = torch.autograd.grad(hr, (yq, bn.weight, bn.bias), dh.double().cpu().view(B, T, Cc).transpose(1, 2))
     close(dyb, gy.transpose(1, 2).reshape(B * T, Cc), 1e-4, "bn dy")
     close(dgm, gw_, 1e-4, "bn dgamma")

@@ -24,9 +24,8 @@ def main():
           f"busy {busy:.3f} ms/step, wall {wall:.3f} ms/step")
     tm, cnt = collections.Counter(), collections.Counter()
     for name, s, e in seg:
-        k = re.sub(r"\(.*", "", name).replace("void ", "")
-        if not k.strip():
-            k = "relattn_" + re.sub(r".*relattn_", "", name)[:40]
+        k = name.replace("(anonymous namespace)::", "").replace("void ", "")
+        k = re.sub(r"\(.*", "", k)
         tm[k] += e - s
         cnt[k] += 1
     print(f"{'kernel':100s} {'per step':>9s} {'us/step':>9s} {'us/launch':>9s}")
