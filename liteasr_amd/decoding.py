@@ -164,33 +164,32 @@ def pick_best(hyps, g, ctc_weight=0.5):
     return best_i
 
 
-def attention_beam_search(model, x, beam=10):
+def attention_beam_search(model, x, beam=10, trace=None):
     """u2.py:163-216: left-to-right attention beam search (memory h repeated, no memory
-    mask), max T' steps, per-step log_softmax + topk(beam) on the device, the (beam x
-    beam) score bookkeeping in float32 on the host.  The reference's decoder cache only
-    skips recomputing earlier positions; here each step reruns the causal decoder over
-    the prefix, which yields the same last-position log-probs."""
+    mask), max T' steps, the decoder advanced one position per step through its key/value
+    cache (FN.DecoderStepCache: the reference's forward_one_step cache semantics, incl. its
+    never-reordered cache of layers >= 1), per-step log_softmax + topk(beam) on the device,
+    the (beam x beam) score bookkeeping in float32 on the host.  trace (a list): per step
+    (hyps fed to the step [beam, i], log-prob top-k values [beam, beam]) for tests."""
     h, T = encode(model, x)
     dev = h.device
-    d = h.shape[1]
-    mem = h.view(1, T, d).expand(beam, T, d).reshape(beam * T, d)
     sos, eos = model.sos, model.eos
     init = np.array([0.0] + [-np.inf] * (beam - 1), dtype=np.float32)
     hyps = np.full((beam, 1), sos, dtype=np.int64)
     scores = init.reshape(beam, 1).copy()
     end = np.zeros(beam, dtype=bool)
-    mmask = _mem_mask(beam, T, dev)
+    dec = FN.DecoderStepCache(model, h, beam, T, T + 1)
+    sel_d = None
     for i in range(1, T + 1):
         if end.sum() == beam:
             break
-        ys_in = torch.from_numpy(hyps.astype(np.int32)).to(dev)
-        tri = torch.triu(torch.ones(i, i, dtype=torch.uint8, device=dev), diagonal=1)
-        dmask = tri.unsqueeze(0).expand(beam, i, i).contiguous()
-        logits = FN.decoder_logits(model, mem, ys_in, dmask, mmask, beam, i, T)
-        last = logits[i - 1:]  # rows b*i + (i-1), stride i rows
-        vals, idx, _ = K.logsoftmax_topk(last, beam, rows=beam, ld=i * logits.stride(0))
+        ids = torch.from_numpy(np.ascontiguousarray(hyps[:, -1]).astype(np.int32)).to(dev)
+        logits = dec.step(ids, i, sel_d)
+        vals, idx, _ = K.logsoftmax_topk(logits, beam)
         st = vals.cpu().numpy()
         it = idx.cpu().numpy().astype(np.int64)
+        if trace is not None:
+            trace.append((hyps.copy(), st.copy()))
         st[end] = init
         it[end] = eos
         cand = (scores + st).reshape(-1).astype(np.float32)
@@ -198,6 +197,7 @@ def attention_beam_search(model, x, beam=10):
         scores = cand[order].reshape(beam, 1)
         sel, off = order // beam, order % beam
         hyps = np.concatenate([hyps[sel], it[sel, off][:, None]], axis=1)
+        sel_d = torch.from_numpy(sel.astype(np.int64)).to(dev)
         end = hyps[:, -1] == eos
     best = int(np.argmax(scores.reshape(-1)))
     return hyps[best].tolist()

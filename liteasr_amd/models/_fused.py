@@ -166,17 +166,26 @@ class FusedEncoderModel(LiteasrModel):
         if torch.is_grad_enabled():
             self.store.ensure_grad()  # p.grad views of the flat grad buffer (once per step)
         enc.embed.repack(self.compute_dtype)
-        x = FN.EmbedFn.apply(xs.float(), enc.embed.out.weight, enc.embed, env)
         d = enc.h_dim
-        pos = torch.empty(T, d, dtype=self.compute_dtype, device=xs.device)
-        K.pe_fwd(None, T, T, d, enc.pe.table(T), 1.0, pos, env.p_pos, env.seed + 4)
-        pp = FN.pos_projections(pos, [layer.weights().att.Wpos for layer in enc.enc_layers]) \
-            if FN.BATCH_POS_PROJ else None
+        rel = getattr(enc, "use_rel", True)
+        env.abs_pe = None if rel else enc.pe.table(T)  # absolute PE: added to x in the embed node
+        x = FN.EmbedFn.apply(xs.float(), enc.embed.out.weight, enc.embed, env)
+        pos, pp = None, None
+        if rel:  # relative PE: the dropped-out table feeds every layer's positional projection
+            pos = torch.empty(T, d, dtype=self.compute_dtype, device=xs.device)
+            K.pe_fwd(None, T, T, d, enc.pe.table(T), 1.0, pos, env.p_pos, env.seed + 4)
+            pp = FN.pos_projections(pos, [layer.weights().att.Wpos for layer in enc.enc_layers]) \
+                if FN.BATCH_POS_PROJ else None
         env.pos_proj = {id(layer): p for layer, p in zip(enc.enc_layers, pp)} if pp else None
         layers = list(enc.enc_layers)
+        conformer = getattr(enc, "arch", "conformer") == "conformer"
         env.pre_ln = None
         for j, layer in enumerate(layers):
             x = self._cut(x, j)
+            if not conformer:  # Transformer layers: no final norm to chain the next first norm into
+                env.next_ln = None
+                x = FN.TransformerLayerFn.apply(x, pos, layer.feed_forward_norm.weight, layer, env)
+                continue
             if j + 1 < len(layers):
                 wn = layers[j + 1].weights().ln_a
                 env.next_ln = (layers[j + 1], wn.g, wn.b)

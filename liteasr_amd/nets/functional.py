@@ -113,9 +113,15 @@ def dx_ln(dy, W, lnb):
     K.gemm(dy, W, dln)
     if lnb is None:
         return dln
+    ln_bwd_of(dln, lnb)
+    return None
+
+
+def ln_bwd_of(dln, lnb):
+    """The LayerNorm backward `lnb` describes, on an already computed dln (the paths whose
+    input-gradient GEMM is not the row kernel's: dx_ln does both in one launch)."""
     K.layernorm_bwd(lnb.x, dln, lnb.g, lnb.mean, lnb.rstd, lnb.dx, lnb.dgamma, lnb.dbeta, dres=lnb.dres,
                     gb=lnb.gb, bscale=lnb.bscale, bp=lnb.bp, bseed=lnb.bseed)
-    return None
 
 
 def ffn_forward(ln, W1, b1, W2, b2, act, p_ff, s_ff, res, res_scale, p_res, s_res, post=None):
@@ -502,7 +508,9 @@ class EmbedFn(torch.autograd.Function):
         y2f = y2.view(B * T2, F2 * C)
         K.linear(y2f, w.Woutp, xl, bias=w.bout)
         x0 = _e((B * T2, w.d), F32, dev)
-        K.pe_fwd(xl, B * T2, T2, w.d, None, math.sqrt(w.d), x0, env.p_pos, env.seed + 1)
+        # relative PE: x * sqrt(d) (positional_encoding.py:68-75); absolute (use_rel False):
+        # x * sqrt(d) + pe[t] (:49-56); dropout either way
+        K.pe_fwd(xl, B * T2, T2, w.d, getattr(env, "abs_pe", None), math.sqrt(w.d), x0, env.p_pos, env.seed + 1)
         ctx.sv = SimpleNamespace(xs=xs, y1=y1, col=col, y2=y2, dims=(B, T1, F1, T2, F2, C), implicit=implicit)
         ctx.mod, ctx.env = mod, env
         return x0
@@ -548,6 +556,27 @@ class EmbedFn(torch.autograd.Function):
         return None, None, None, None
 
 
+def enc_attn_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None, post=None):
+    """An encoder layer's self-attention sub-block: relative-position attention
+    (attention.py:120-154) when the layer has a positional projection, else the plain
+    multi-head attention (:61-71) over the same key-padding / chunk mask (use_rel False)."""
+    if w.Wpos is not None:
+        return relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=p, post=post)
+    if post is not None:
+        post.y1 = None  # plain attention: the following norm runs on its own
+    return mha_forward(ln, None, w, env.B, env.T, env.T, env.H, env.mask, env.msb, env.msq, x_in, p_att, s_att,
+                       p_res, s_res)
+
+
+def enc_attn_backward(gb, ln, pos, sv, w, g, env, p_att, s_att, lnb):
+    if w.Wpos is not None:
+        return relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att, lnb=lnb)
+    dln = mha_backward(gb, ln, None, sv, w, g, env.B, env.T, env.T, env.H, env.mask, env.msb, env.msq, p_att, s_att,
+                       None)
+    ln_bwd_of(dln, lnb)
+    return None
+
+
 class ConformerLayerFn(torch.autograd.Function):
     """RelativeEncoderLayer.forward (liteasr/nets/conformer_layer.py:130-147), pre-norm."""
 
@@ -571,7 +600,7 @@ class ConformerLayerFn(torch.autograd.Function):
         # every residual projection runs the following norm in its epilogue when the row
         # kernel takes the shape (res_proj); ln_forward covers the rest
         pb_ = PostLN(g=w.ln_b.g, b=w.ln_b.b, f32=False, nxt=None)
-        x1, za, ha = ffn_forward(ln_a, w.ffm.W1, w.ffm.b1, w.ffm.W2, w.ffm.b2, ACT_SWISH, pff,
+        x1, za, ha = ffn_forward(ln_a, w.ffm.W1, w.ffm.b1, w.ffm.W2, w.ffm.b2, w.act, pff,
                                  _seed(s, 1), x0, 0.5, pd, _seed(s, 2), post=pb_)
         # (b) relative-position MHSA
         if pb_.y1 is not None:
@@ -580,8 +609,8 @@ class ConformerLayerFn(torch.autograd.Function):
             ln_b, _, mb, rb = ln_forward(x1, w.ln_b.g, w.ln_b.b, adt)
         pp = getattr(env, "pos_proj", None)
         pc_ = PostLN(g=w.ln_c.g, b=w.ln_c.b, f32=False, nxt=None)
-        x2, svb = relmha_forward(ln_b, pos, w.att, env, x1, pat, _seed(s, 3), pd, _seed(s, 4),
-                                 p=pp.get(id(layer)) if pp else None, post=pc_)
+        x2, svb = enc_attn_forward(ln_b, pos, w.att, env, x1, pat, _seed(s, 3), pd, _seed(s, 4),
+                                   p=pp.get(id(layer)) if pp else None, post=pc_)
         # (c) convolution module
         if pc_.y1 is not None:
             ln_c, mc, rc = pc_.y1, pc_.m1, pc_.r1
@@ -600,7 +629,7 @@ class ConformerLayerFn(torch.autograd.Function):
         nxt = getattr(env, "next_ln", None)
         chain = FUSED_LN2 and nxt is not None and adt == torch.bfloat16
         pf_ = PostLN(g=w.ln_f.g, b=w.ln_f.b, f32=True, nxt=(nxt[1], nxt[2]) if chain else None)
-        x4, zd, hd = ffn_forward(ln_d, w.ff.W1, w.ff.b1, w.ff.W2, w.ff.b2, ACT_SWISH, pff,
+        x4, zd, hd = ffn_forward(ln_d, w.ff.W1, w.ff.b1, w.ff.W2, w.ff.b2, w.act, pff,
                                  _seed(s, 6), x3, 0.5, pd, _seed(s, 7), post=pf_)
         if pf_.y1 is not None:
             x5, mf, rf = pf_.y1, pf_.m1, pf_.r1
@@ -651,7 +680,7 @@ class ConformerLayerFn(torch.autograd.Function):
             dx3 = _e((M, d), F32, dev)
             gb3 = _e((M, d), adt, dev)
             ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2, g.ff.b2,
-                         ACT_SWISH, pff, _seed(s, 6),
+                         w.act, pff, _seed(s, 6),
                          lnb=LnBwd(x=x3, g=w.ln_d.g, mean=md, rstd=rd, dx=dx3, dgamma=g.ln_d.g, dbeta=g.ln_d.b,
                                    dres=dx4, gb=gb3, bscale=1.0, bp=pd, bseed=_seed(s, 5)))
             dx2 = _e((M, d), F32, dev)
@@ -661,14 +690,77 @@ class ConformerLayerFn(torch.autograd.Function):
                                     dres=dx3, gb=gb2, bscale=1.0, bp=pd, bseed=_seed(s, 4)))
             dx1 = _e((M, d), F32, dev)
             gb1 = _e((M, d), adt, dev)
-            relmha_backward(gb2, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3),
-                            lnb=LnBwd(x=x1, g=w.ln_b.g, mean=mb, rstd=rb, dx=dx1, dgamma=g.ln_b.g, dbeta=g.ln_b.b,
-                                      dres=dx2, gb=gb1, bscale=0.5, bp=pd, bseed=_seed(s, 2)))
+            enc_attn_backward(gb2, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3),
+                              lnb=LnBwd(x=x1, g=w.ln_b.g, mean=mb, rstd=rb, dx=dx1, dgamma=g.ln_b.g, dbeta=g.ln_b.b,
+                                        dres=dx2, gb=gb1, bscale=0.5, bp=pd, bseed=_seed(s, 2)))
             dx0 = _e((M, d), F32, dev)
             ffn_backward(gb1, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1, g.ffm.W2, g.ffm.b2,
-                         ACT_SWISH, pff, _seed(s, 1),
+                         w.act, pff, _seed(s, 1),
                          lnb=LnBwd(x=x0, g=w.ln_a.g, mean=ma, rstd=ra, dx=dx0, dgamma=g.ln_a.g, dbeta=g.ln_a.b,
                                    dres=dx1, gb=None, bscale=1.0, bp=0.0, bseed=0))
+        ctx.sv = None
+        layer.on_grads_ready()
+        return dx0, None, None, None, None
+
+
+class TransformerLayerFn(torch.autograd.Function):
+    """Transformer encoder layer (enc_arch "transformer"; liteasr/nets/transformer_layer.py:
+    EncoderLayer.forward :64-76 / RelativeEncoderLayer.forward :119-136), pre-norm:
+    x1 = x0 + drop(MHA(LN_b(x0))), x2 = x1 + drop(FFN(LN_d(x1))) -- no macaron half-step,
+    no convolution module, no final norm (the encoder's after_norm follows the stack)."""
+
+    @staticmethod
+    def forward(ctx, x0, pos, anchor, layer, env):
+        w = layer.weights()
+        s = layer.seed
+        tr = env.training
+        pd = env.p_drop if tr else 0.0
+        pff = env.p_ff if tr else 0.0
+        pat = env.p_att if tr else 0.0
+        adt = env.adt
+        x0 = x0.contiguous()
+        ln_b, _, mb, rb = ln_forward(x0, w.ln_b.g, w.ln_b.b, adt)
+        pp = getattr(env, "pos_proj", None)
+        pd_ = PostLN(g=w.ln_d.g, b=w.ln_d.b, f32=False, nxt=None)
+        x1, svb = enc_attn_forward(ln_b, pos, w.att, env, x0, pat, _seed(s, 3), pd, _seed(s, 4),
+                                   p=pp.get(id(layer)) if pp else None, post=pd_)
+        if pd_.y1 is not None:
+            ln_d, md, rd = pd_.y1, pd_.m1, pd_.r1
+        else:
+            ln_d, _, md, rd = ln_forward(x1, w.ln_d.g, w.ln_d.b, adt)
+        x2, zd, hd = ffn_forward(ln_d, w.ff.W1, w.ff.b1, w.ff.W2, w.ff.b2, w.act, pff, _seed(s, 6), x1, 1.0, pd,
+                                 _seed(s, 7))
+        if torch.is_grad_enabled() or anchor.requires_grad:
+            ctx.sv = SimpleNamespace(x=(x0, x1), ln=(ln_b, ln_d), st=((mb, rb), (md, rd)), zd=zd, hd=hd, svb=svb,
+                                     pos=pos, p=(pd, pff, pat))
+        ctx.layer, ctx.env = layer, env
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        sv, layer, env = ctx.sv, ctx.layer, ctx.env
+        w, g = layer.weights(), layer.grads()
+        s = layer.seed
+        pd, pff, pat = sv.p
+        x0, x1 = sv.x
+        ln_b, ln_d = sv.ln
+        (mb, rb), (md, rd) = sv.st
+        dev, adt = dx2.device, env.adt
+        M, d = x1.shape
+        dx2 = dx2.contiguous()
+        with K.deferred_reductions():
+            gb = _e((M, d), adt, dev)
+            K.branch_grad(dx2, gb, 1.0, pd, _seed(s, 7))
+            dx1 = _e((M, d), F32, dev)
+            gb1 = _e((M, d), adt, dev)
+            ffn_backward(gb, ln_d, sv.zd, sv.hd, w.ff.W1, w.ff.W2, g.ff.W1, g.ff.b1, g.ff.W2, g.ff.b2, w.act, pff,
+                         _seed(s, 6),
+                         lnb=LnBwd(x=x1, g=w.ln_d.g, mean=md, rstd=rd, dx=dx1, dgamma=g.ln_d.g, dbeta=g.ln_d.b,
+                                   dres=dx2, gb=gb1, bscale=1.0, bp=pd, bseed=_seed(s, 4)))
+            dx0 = _e((M, d), F32, dev)
+            enc_attn_backward(gb1, ln_b, sv.pos, sv.svb, w.att, g.att, env, pat, _seed(s, 3),
+                              lnb=LnBwd(x=x0, g=w.ln_b.g, mean=mb, rstd=rb, dx=dx0, dgamma=g.ln_b.g, dbeta=g.ln_b.b,
+                                        dres=dx1, gb=None, bscale=1.0, bp=0.0, bseed=0))
         ctx.sv = None
         layer.on_grads_ready()
         return dx0, None, None, None, None
@@ -1275,3 +1367,90 @@ def decoder_logits(model, h, ys_in, dec_mask, mem_mask, B, L1, T):
     out = K.padded_rows(R, wd.Wout.shape[0], adt, dev)
     K.linear(yf, wd.Wout, out, bias=wd.bout)
     return out
+
+
+class DecoderStepCache:
+    """TransformerDecoder.forward_one_step (liteasr/nets/transformer_decoder.py:58-68,
+    DecoderLayer with cache: transformer_layer.py:27-47,179-221) for the attention beam
+    search (u2.py:163-216), eval mode, with a key/value cache per decoder layer: each step
+    runs only the new position -- its row's projections, one-query attention over the cached
+    keys, the source attention over the memory keys/values (projected ONCE per utterance:
+    the memory is the same for every beam and step), the FFN and the output projection --
+    instead of the whole prefix.
+
+    Cache semantics follow the reference exactly.  Its cache (each layer's outputs for the
+    earlier positions) is NOT reordered when the beam reorders its hypotheses; the first
+    layer recomputes its keys from the (reordered) hypothesis embeddings, while layers >= 1
+    attend to the earlier rows in the previous step's slot order.  Here: the first layer's
+    key/value cache is gathered by the beam's selection each step (identical to recomputing
+    it from the reordered embeddings: a row's projection does not depend on other rows);
+    the caches of layers >= 1 are never permuted (tests/golden/decode_cache.npz, two
+    decoder layers, pins the per-step log-probs)."""
+
+    def __init__(self, model, mem, beam, T, max_len):
+        wd = model.decoder.weights()
+        self.wd, self.beam, self.T = wd, beam, T
+        d, adt, dev = wd.d, mem.dtype, mem.device
+        self.adt, self.dev = adt, dev
+        self.kv_mem = []  # per layer [T, 2d]: linear_k / linear_v of the memory (src_attn)
+        for lw in wd.layers:
+            kv = _e((T, 2 * d), adt, dev)
+            K.linear(mem, lw.ca.Wkv, kv, bias=lw.ca.bkv)
+            self.kv_mem.append(kv)
+        n = len(wd.layers)
+        self.kc = [_e((beam, max_len, d), adt, dev) for _ in range(n)]
+        self.vc = [_e((beam, max_len, d), adt, dev) for _ in range(n)]
+
+    def _attend(self, q, k3, v3, Tk):
+        """softmax(q k^T / sqrt(dk)) v for one query row per beam: q [beam, d] (row stride
+        arbitrary), k3 / v3 [beam, >=Tk, d] views (any batch stride, 0 included)."""
+        wd, beam = self.wd, self.beam
+        H, d = wd.H, wd.d
+        dk = d // H
+        ldS = ld_scores(Tk)
+        q4 = q.unflatten(1, (H, dk)).unsqueeze(2)  # (beam, H, 1, dk)
+        k4 = k3[:, :Tk].unflatten(2, (H, dk)).permute(0, 2, 1, 3)  # (beam, H, Tk, dk)
+        v4 = v3[:, :Tk].unflatten(2, (H, dk)).permute(0, 2, 1, 3)
+        S = _e((beam, H, 1, ldS), F32, self.dev)
+        K.gemm(q4, k4.transpose(-1, -2), S[..., :Tk], alpha=dk ** -0.5)
+        P = _e((beam, H, 1, ldS), self.adt, self.dev)
+        K.attn_softmax_fwd(S, None, beam, H, 1, Tk, ldS, None, 0, 0, P)
+        ctx = _e((beam, d), self.adt, self.dev)
+        K.gemm(P[..., :Tk], v4, ctx.unflatten(1, (H, dk)).unsqueeze(2))
+        return ctx
+
+    def step(self, ids, i, sel=None):
+        """Log-probs' logits [beam, V] of step i (1-based: the new token sits at position
+        i - 1); ids int32 [beam] = each hypothesis' last token; sel (int64 device [beam],
+        optional) = the beam's selection that produced these hypotheses from the previous
+        step's slots."""
+        wd, beam, adt, dev = self.wd, self.beam, self.adt, self.dev
+        d = wd.d
+        if sel is not None and i > 1:
+            for c in (self.kc[0], self.vc[0]):
+                c[:, :i - 1] = c[:, :i - 1].index_select(0, sel)
+        y = _e((beam, d), F32, dev)
+        K.embed_pe_fwd(ids, 1, wd.E, wd.pe[i - 1:], math.sqrt(d), y, 0.0, 0)
+        for j, lw in enumerate(wd.layers):
+            l1, _, _, _ = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
+            qkv = _e((beam, 3 * d), adt, dev)
+            K.linear(l1, lw.sa.Wqkv, qkv, bias=lw.sa.bqkv)
+            self.kc[j][:, i - 1] = qkv[:, d:2 * d]
+            self.vc[j][:, i - 1] = qkv[:, 2 * d:]
+            ctx = self._attend(qkv[:, :d], self.kc[j], self.vc[j], i)
+            y1 = _e((beam, d), F32, dev)
+            K.linear(ctx, lw.sa.Wo, y1, bias=lw.sa.bo, res=y, res_scale=1.0)
+            l2, _, _, _ = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
+            q = _e((beam, d), adt, dev)
+            K.linear(l2, lw.ca.Wq, q, bias=lw.ca.bq)
+            kv = self.kv_mem[j]
+            ctx2 = self._attend(q, kv[:, :d].unsqueeze(0).expand(beam, self.T, d),
+                                kv[:, d:].unsqueeze(0).expand(beam, self.T, d), self.T)
+            y2 = _e((beam, d), F32, dev)
+            K.linear(ctx2, lw.ca.Wo, y2, bias=lw.ca.bo, res=y1, res_scale=1.0)
+            l3, _, _, _ = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)
+            y, _, _ = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, 0.0, 0, y2, 1.0, 0.0, 0)
+        yf, _, _, _ = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
+        out = K.padded_rows(beam, wd.Wout.shape[0], adt, dev)
+        K.linear(yf, wd.Wout, out, bias=wd.bout)
+        return out

@@ -229,9 +229,44 @@ KV_W = ("linear_k.weight", "linear_v.weight")
 KV_B = ("linear_k.bias", "linear_v.bias")
 
 
+def _act_code(activation):
+    """The encoder activation module -> the kernels' epilogue code (Swish or ReLU)."""
+    from .._native import ACT_RELU, ACT_SWISH
+
+    return ACT_SWISH if isinstance(activation, Swish) else ACT_RELU
+
+
+def _att_weights(layer, grad):
+    """Self-attention operand views of an encoder layer: the fused q/k/v projection, the
+    output projection and, for the relative-position attention (attention.py:74-154), the
+    positional projection and the two position biases (rel False: None)."""
+    d = layer.size
+    a = "self_attn."
+    rel = layer.rel
+    if grad:
+        return SimpleNamespace(Wqkv=layer._gg([a + n for n in QKV_W], d), bqkv=layer._gg([a + n for n in QKV_B]),
+                               Wpos=layer._g(a + "linear_pos.weight") if rel else None,
+                               u=layer._g(a + "pos_bias_u").view(-1) if rel else None,
+                               v=layer._g(a + "pos_bias_v").view(-1) if rel else None,
+                               Wo=layer._g(a + "linear_o.weight"), bo=layer._g(a + "linear_o.bias"))
+    return SimpleNamespace(Wqkv=layer._wg([a + n for n in QKV_W], d), bqkv=layer._pg([a + n for n in QKV_B]),
+                           Wpos=layer._w(a + "linear_pos.weight") if rel else None,
+                           u=layer._p(a + "pos_bias_u").view(-1) if rel else None,
+                           v=layer._p(a + "pos_bias_v").view(-1) if rel else None,
+                           Wo=layer._w(a + "linear_o.weight"), bo=layer._p(a + "linear_o.bias"))
+
+
+def _att_groups(layer):
+    a = layer._pfx + ".self_attn."
+    g = [[a + n for n in QKV_W], [a + n for n in QKV_B]]
+    return g + [[a + "pos_bias_u", a + "pos_bias_v"]] if layer.rel else g
+
+
 class RelativeEncoderLayer(_LayerCommon):
-    """Conformer RelativeEncoderLayer: liteasr/nets/conformer_layer.py:84-147 (+ the
-    EncoderLayer base of liteasr/nets/transformer_layer.py:10-27)."""
+    """Conformer encoder layer: RelativeEncoderLayer (liteasr/nets/conformer_layer.py:84-147)
+    with a RelativeMultiHeadAttention, or EncoderLayer (:10-81, use_rel False) with a plain
+    MultiHeadAttention (+ the EncoderLayer base of liteasr/nets/transformer_layer.py:10-27);
+    the FFN / conv-module activation is Swish or ReLU (transformer_encoder.py:77-80)."""
 
     def __init__(self, size, self_attn, feed_forward, feed_forward_macaron, conv, dropout_rate,
                  normalize_before=True, concat_after=False):
@@ -251,10 +286,11 @@ class RelativeEncoderLayer(_LayerCommon):
         self.final_norm = LayerNorm(size)
         self.feed_forward_scale = 0.5
         self.seed = 0
+        self.rel = isinstance(self_attn, RelativeMultiHeadAttention)
+        self.act = _act_code(feed_forward.activation)
 
     def flat_groups(self):
-        a = self._pfx + ".self_attn."
-        return [[a + n for n in QKV_W], [a + n for n in QKV_B], [a + "pos_bias_u", a + "pos_bias_v"]]
+        return _att_groups(self)
 
     def weights(self):
         return self._cached("w", self._weights)
@@ -264,18 +300,14 @@ class RelativeEncoderLayer(_LayerCommon):
 
     def _weights(self):
         d = self.size
-        a = "self_attn."
         c = "conv."
         bn = self.conv.norm
         return SimpleNamespace(
             ln_a=self._ln("feed_forward_macaron_norm"), ln_b=self._ln("self_attn_norm"),
             ln_c=self._ln("conv_norm"), ln_d=self._ln("feed_forward_norm"), ln_f=self._ln("final_norm"),
             ffm=self._ffn("feed_forward_macaron"), ff=self._ffn("feed_forward"),
-            att=SimpleNamespace(Wqkv=self._wg([a + n for n in QKV_W], d), bqkv=self._pg([a + n for n in QKV_B]),
-                                Wpos=self._w(a + "linear_pos.weight"), u=self._p(a + "pos_bias_u").view(-1),
-                                v=self._p(a + "pos_bias_v").view(-1), Wo=self._w(a + "linear_o.weight"),
-                                bo=self._p(a + "linear_o.bias")),
-            conv=SimpleNamespace(Wpw1=self._w(c + "pointwise_conv1.weight").view(2 * d, d),
+            att=_att_weights(self, False), act=self.act,
+            conv=SimpleNamespace(act=self.act, Wpw1=self._w(c + "pointwise_conv1.weight").view(2 * d, d),
                                  bpw1=self._p(c + "pointwise_conv1.bias"),
                                  wdw=self._p(c + "depthwise_conv.weight").view(d, -1),
                                  bdw=self._p(c + "depthwise_conv.bias"),
@@ -287,17 +319,13 @@ class RelativeEncoderLayer(_LayerCommon):
 
     def _grads(self):
         d = self.size
-        a = "self_attn."
         c = "conv."
         return SimpleNamespace(
             ln_a=self._ln("feed_forward_macaron_norm", True), ln_b=self._ln("self_attn_norm", True),
             ln_c=self._ln("conv_norm", True), ln_d=self._ln("feed_forward_norm", True),
             ln_f=self._ln("final_norm", True),
             ffm=self._ffn("feed_forward_macaron", True), ff=self._ffn("feed_forward", True),
-            att=SimpleNamespace(Wqkv=self._gg([a + n for n in QKV_W], d), bqkv=self._gg([a + n for n in QKV_B]),
-                                Wpos=self._g(a + "linear_pos.weight"), u=self._g(a + "pos_bias_u").view(-1),
-                                v=self._g(a + "pos_bias_v").view(-1), Wo=self._g(a + "linear_o.weight"),
-                                bo=self._g(a + "linear_o.bias")),
+            att=_att_weights(self, True),
             conv=SimpleNamespace(Wpw1=self._g(c + "pointwise_conv1.weight").view(2 * d, d),
                                  bpw1=self._g(c + "pointwise_conv1.bias"),
                                  wdw=self._g(c + "depthwise_conv.weight").view(d, -1),
@@ -305,6 +333,39 @@ class RelativeEncoderLayer(_LayerCommon):
                                  Wpw2=self._g(c + "pointwise_conv2.weight").view(d, d),
                                  bpw2=self._g(c + "pointwise_conv2.bias"),
                                  gamma=self._g(c + "norm.weight"), beta=self._g(c + "norm.bias")))
+
+
+class TransformerEncoderLayer(_LayerCommon):
+    """Transformer encoder layer (enc_arch "transformer"): EncoderLayer / RelativeEncoderLayer
+    of liteasr/nets/transformer_layer.py:10-136, pre-norm: x + drop(MHA(LN(x))), then
+    x + drop(FFN(LN(x))) with the FFN's default ReLU (feed_forward.py:11)."""
+
+    def __init__(self, size, self_attn, feed_forward, dropout_rate, normalize_before=True, concat_after=False):
+        super().__init__()
+        assert normalize_before, "only the pre-norm (default) layer is on the hot path"
+        self.self_attn = self_attn
+        self.feed_forward = feed_forward
+        self.self_attn_norm = LayerNorm(size)
+        self.feed_forward_norm = LayerNorm(size)
+        self.dropout = nn.Dropout(dropout_rate)
+        self.size = size
+        self.normalize_before = normalize_before
+        self.seed = 0
+        self.rel = isinstance(self_attn, RelativeMultiHeadAttention)
+        self.act = _act_code(feed_forward.activation)
+
+    def flat_groups(self):
+        return _att_groups(self)
+
+    def weights(self):
+        return self._cached("w", lambda: SimpleNamespace(
+            ln_b=self._ln("self_attn_norm"), ln_d=self._ln("feed_forward_norm"), ff=self._ffn("feed_forward"),
+            att=_att_weights(self, False), act=self.act))
+
+    def grads(self):
+        return self._cached("g", lambda: SimpleNamespace(
+            ln_b=self._ln("self_attn_norm", True), ln_d=self._ln("feed_forward_norm", True),
+            ff=self._ffn("feed_forward", True), att=_att_weights(self, True)))
 
 
 class DecoderLayer(_LayerCommon):
@@ -348,29 +409,45 @@ class DecoderLayer(_LayerCommon):
 
 
 class TransformerEncoder(_Bound):
-    """liteasr/nets/transformer_encoder.py:28-127 (conformer + relative PE on the HIP path)."""
+    """liteasr/nets/transformer_encoder.py:28-127: Conv2DLayer, the relative (use_rel) or
+    absolute positional encoding, n_layer Conformer (arch "conformer", Swish or ReLU) or
+    Transformer (arch "transformer") layers with relative or plain self-attention, after_norm.
+    Constructed in the reference's order (same seed -> same initial weights)."""
 
     def __init__(self, use_rel, i_dim, h_dim, ff_dim, n_head, n_layer, dropout_rate, pos_dropout_rate,
                  attn_dropout_rate, ff_dropout_rate, activation, arch):
         super().__init__()
-        if not (use_rel and arch == "conformer" and activation == "swish"):
-            raise NotImplementedError(
-                "liteasr_amd builds the Conformer + relative-PE + Swish encoder (the U2 hot path); "
-                f"got use_rel={use_rel}, arch={arch}, activation={activation}")
+        if arch not in ("conformer", "transformer") or (arch == "conformer" and activation not in ("swish", "relu")):
+            raise ValueError(f"encoder arch {arch!r} / activation {activation!r}: the reference builds "
+                             "conformer (swish | relu) and transformer")
         self.embed = Conv2DLayer(i_dim, h_dim, dropout_rate)
-        self.pe = RelativePositionalEncoding(h_dim, dropout_rate=pos_dropout_rate)
-        act = Swish()
-        self.enc_layers = nn.ModuleList([
-            RelativeEncoderLayer(
-                size=h_dim,
-                self_attn=RelativeMultiHeadAttention(n_head, h_dim, attn_dropout_rate),
-                feed_forward=PositionwiseFeedForward(h_dim, ff_dim, dropout_rate=ff_dropout_rate, activation=act),
-                feed_forward_macaron=PositionwiseFeedForward(h_dim, ff_dim, dropout_rate=ff_dropout_rate,
-                                                             activation=act),
-                conv=Convolution(h_dim, 15, activation=act),
-                dropout_rate=dropout_rate,
-            ) for _ in range(n_layer)
-        ])
+        self.use_rel = bool(use_rel)
+        pe = RelativePositionalEncoding if use_rel else PositionalEncoding
+        mha = RelativeMultiHeadAttention if use_rel else MultiHeadAttention
+        self.pe = pe(h_dim, dropout_rate=pos_dropout_rate)
+        self.arch = arch
+        if arch == "transformer":
+            self.enc_layers = nn.ModuleList([
+                TransformerEncoderLayer(
+                    size=h_dim,
+                    self_attn=mha(n_head, h_dim, attn_dropout_rate),
+                    feed_forward=PositionwiseFeedForward(h_dim, ff_dim, dropout_rate=ff_dropout_rate),
+                    dropout_rate=dropout_rate,
+                ) for _ in range(n_layer)
+            ])
+        else:
+            act = nn.ReLU() if activation == "relu" else Swish()
+            self.enc_layers = nn.ModuleList([
+                RelativeEncoderLayer(
+                    size=h_dim,
+                    self_attn=mha(n_head, h_dim, attn_dropout_rate),
+                    feed_forward=PositionwiseFeedForward(h_dim, ff_dim, dropout_rate=ff_dropout_rate, activation=act),
+                    feed_forward_macaron=PositionwiseFeedForward(h_dim, ff_dim, dropout_rate=ff_dropout_rate,
+                                                                 activation=act),
+                    conv=Convolution(h_dim, 15, activation=act),
+                    dropout_rate=dropout_rate,
+                ) for _ in range(n_layer)
+            ])
         self.after_norm = LayerNorm(h_dim)
         self.h_dim, self.n_head = h_dim, n_head
         self.rates = SimpleNamespace(drop=dropout_rate, pos=pos_dropout_rate, att=attn_dropout_rate,

@@ -141,9 +141,10 @@ def ffn(x, p: Params, name: str, act: str, drop=0.0, training=True):
     return linear(F.dropout(h, drop, training), p, name + ".fc2")
 
 
-def conv_module(x, p: Params, name: str, bn_state: Optional[dict], training=True):
+def conv_module(x, p: Params, name: str, bn_state: Optional[dict], training=True, act: str = "swish"):
     """Convolution: liteasr/nets/conformer_convolution.py:44-57 (BatchNorm1d train mode:
-    batch stats over B*T incl. padding; running stats updated, momentum 0.1, eps 1e-5)."""
+    batch stats over B*T incl. padding; running stats updated, momentum 0.1, eps 1e-5);
+    activation Swish or ReLU (transformer_encoder.py:77-80)."""
     y = x.transpose(1, 2)
     y = F.conv1d(y, p[name + ".pointwise_conv1.weight"], p[name + ".pointwise_conv1.bias"])
     y = F.glu(y, dim=1)
@@ -155,40 +156,64 @@ def conv_module(x, p: Params, name: str, bn_state: Optional[dict], training=True
     y = F.batch_norm(y, rm, rv, p[name + ".norm.weight"], p[name + ".norm.bias"], training, 0.1, 1e-5)
     if bn_state is not None and training:
         bn_state[name + ".norm.num_batches_tracked"] += 1
-    y = y * torch.sigmoid(y)
+    y = y * torch.sigmoid(y) if act == "swish" else F.relu(y)
     y = F.conv1d(y, p[name + ".pointwise_conv2.weight"], p[name + ".pointwise_conv2.bias"])
     return y.transpose(1, 2)
 
 
 def conformer_layer(x, pos, mask, p: Params, name: str, H: int, cfg, bn_state, training=True):
-    """RelativeEncoderLayer (pre-norm, macaron 0.5 scale): liteasr/nets/conformer_layer.py:130-147."""
+    """Conformer layer (pre-norm, macaron 0.5 scale): RelativeEncoderLayer
+    liteasr/nets/conformer_layer.py:130-147 (pos given) or EncoderLayer :68-81 (use_rel
+    False: plain attention); FFN and conv-module activation cfg["activation"]."""
     dr, ff_dr, at_dr = cfg["dropout"], cfg["ff_dropout"], cfg["attn_dropout"]
+    act = cfg.get("activation", "swish")
     h = layer_norm(x, p, name + ".feed_forward_macaron_norm")
-    x = x + 0.5 * F.dropout(ffn(h, p, name + ".feed_forward_macaron", "swish", ff_dr, training), dr, training)
+    x = x + 0.5 * F.dropout(ffn(h, p, name + ".feed_forward_macaron", act, ff_dr, training), dr, training)
     h = layer_norm(x, p, name + ".self_attn_norm")
     x = x + F.dropout(attention(h, h, h, mask, p, name + ".self_attn", H, pos, at_dr, training), dr, training)
     h = layer_norm(x, p, name + ".conv_norm")
-    x = x + F.dropout(conv_module(h, p, name + ".conv", bn_state, training), dr, training)
+    x = x + F.dropout(conv_module(h, p, name + ".conv", bn_state, training, act), dr, training)
     h = layer_norm(x, p, name + ".feed_forward_norm")
-    x = x + 0.5 * F.dropout(ffn(h, p, name + ".feed_forward", "swish", ff_dr, training), dr, training)
+    x = x + 0.5 * F.dropout(ffn(h, p, name + ".feed_forward", act, ff_dr, training), dr, training)
     return layer_norm(x, p, name + ".final_norm")
 
 
+def transformer_layer(x, pos, mask, p: Params, name: str, H: int, cfg, training=True):
+    """Transformer encoder layer (enc_arch "transformer", pre-norm): EncoderLayer
+    liteasr/nets/transformer_layer.py:27-76 / RelativeEncoderLayer :79-136; the FFN keeps its
+    default ReLU (feed_forward.py:11, transformer_encoder.py:58-62)."""
+    dr, ff_dr, at_dr = cfg["dropout"], cfg["ff_dropout"], cfg["attn_dropout"]
+    h = layer_norm(x, p, name + ".self_attn_norm")
+    x = x + F.dropout(attention(h, h, h, mask, p, name + ".self_attn", H, pos, at_dr, training), dr, training)
+    h = layer_norm(x, p, name + ".feed_forward_norm")
+    return x + F.dropout(ffn(h, p, name + ".feed_forward", "relu", ff_dr, training), dr, training)
+
+
 def encoder(xs, xlens, p: Params, cfg, bn_state=None, training=True, chunk: int = 0):
-    """TransformerEncoder (conformer + relative PE): liteasr/nets/transformer_encoder.py:107-127.
+    """TransformerEncoder: liteasr/nets/transformer_encoder.py:107-127 -- conformer or
+    transformer layers (cfg enc_arch), relative PE (use_rel: x * sqrt(d), the table feeds the
+    attention, positional_encoding.py:68-75) or absolute PE (x * sqrt(d) + pe, :49-56).
     chunk > 0 adds the chunk mask triangle_mask(T', stage=chunk) (config 4 oracle-by-composition)."""
     d = cfg["enc_dim"]
     x = subsample(xs, p, "encoder.embed")
     B, T, _ = x.shape
     pe = sinusoid_table(T, d, x.dtype)
-    x = F.dropout(x * math.sqrt(d), cfg["pos_dropout"], training)
-    pos = F.dropout(pe.unsqueeze(0), cfg["pos_dropout"], training)
+    if cfg.get("use_rel", True):
+        x = F.dropout(x * math.sqrt(d), cfg["pos_dropout"], training)
+        pos = F.dropout(pe.unsqueeze(0), cfg["pos_dropout"], training)
+    else:
+        x = F.dropout(x * math.sqrt(d) + pe.unsqueeze(0), cfg["pos_dropout"], training)
+        pos = None
     kmask = encoder_key_mask(xlens, xs.shape[1])  # (B, T')
     mask = kmask[:, None, :]
     if chunk > 0:
         mask = mask | triangle_mask(T, stage=chunk)[None]
     for i in range(cfg["enc_layers"]):
-        x = conformer_layer(x, pos, mask, p, f"encoder.enc_layers.{i}", cfg["enc_heads"], cfg, bn_state, training)
+        if cfg.get("enc_arch", "conformer") == "transformer":
+            x = transformer_layer(x, pos, mask, p, f"encoder.enc_layers.{i}", cfg["enc_heads"], cfg, training)
+        else:
+            x = conformer_layer(x, pos, mask, p, f"encoder.enc_layers.{i}", cfg["enc_heads"], cfg, bn_state,
+                                training)
     return layer_norm(x, p, "encoder.after_norm"), kmask
 
 
@@ -315,13 +340,23 @@ def init_params(cfg, seed: int = 42, dtype=torch.float32) -> Params:
     p["encoder.embed.conv.2.weight"] = torch.randn(d, d, 3, 3, generator=g) / math.sqrt(9 * d)
     p["encoder.embed.conv.2.bias"] = torch.randn(d, generator=g) * 0.02
     lin("encoder.embed.out", d, d * f2)
+    rel = cfg.get("use_rel", True)
+    tfm = cfg.get("enc_arch", "conformer") == "transformer"
     for i in range(cfg["enc_layers"]):
         n = f"encoder.enc_layers.{i}"
-        p[n + ".self_attn.pos_bias_u"] = torch.randn(H, d // H, generator=g) * 0.1
-        p[n + ".self_attn.pos_bias_v"] = torch.randn(H, d // H, generator=g) * 0.1
+        if rel:
+            p[n + ".self_attn.pos_bias_u"] = torch.randn(H, d // H, generator=g) * 0.1
+            p[n + ".self_attn.pos_bias_v"] = torch.randn(H, d // H, generator=g) * 0.1
         for q in ("q", "k", "v", "o"):
             lin(f"{n}.self_attn.linear_{q}", d, d)
-        lin(n + ".self_attn.linear_pos", d, d, bias=False)
+        if rel:
+            lin(n + ".self_attn.linear_pos", d, d, bias=False)
+        if tfm:  # transformer layer: attention, one FFN, two norms
+            lin(n + ".feed_forward.fc1", ff, d)
+            lin(n + ".feed_forward.fc2", d, ff)
+            ln(n + ".self_attn_norm", d)
+            ln(n + ".feed_forward_norm", d)
+            continue
         for f in ("feed_forward", "feed_forward_macaron"):
             lin(f"{n}.{f}.fc1", ff, d)
             lin(f"{n}.{f}.fc2", d, ff)
@@ -355,6 +390,8 @@ def init_params(cfg, seed: int = 42, dtype=torch.float32) -> Params:
 
 def init_buffers(cfg) -> dict:
     b = {}
+    if cfg.get("enc_arch", "conformer") == "transformer":
+        return b  # no convolution module, no BatchNorm
     for i in range(cfg["enc_layers"]):
         n = f"encoder.enc_layers.{i}.conv.norm"
         b[n + ".running_mean"] = torch.zeros(cfg["enc_dim"])

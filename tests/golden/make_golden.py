@@ -31,6 +31,12 @@ Fixtures
                   their torch.Generator seed (a checksum is stored to detect drift)
   host_policies.npz  SeqBatch / FrameBatch grouping of synthetic length lists (incl. the
                   oversize-utterance edge), Trigger firing sequences, Vocab lookups
+  decode_cache.npz tiny U2 with two decoder layers: the reference's attention beam search
+                  step by step (hyps fed to forward_one_step, the log-probs it returned,
+                  the best hypothesis): pins its never-reordered decoder cache
+  u2_variants.npz the tiny U2 of u2_step with the other encoders the reference builds
+                  (transformer layers with absolute / relative PE, conformer with absolute
+                  PE or ReLU): init state_dict, outputs, loss and every gradient
   transducer.npz  tiny Transducer (Conformer encoder, LSTM decoder, joint): init state_dict,
                   batch (one empty transcript), encoder / decoder outputs, joint logits and every
                   gradient of the RNN-T loss (oracle/rnnt_ref.py) backpropagated through the
@@ -575,9 +581,96 @@ def gen_transducer():
     save("transducer.npz", **arrs)
 
 
+def gen_decode_cache():
+    """decode_cache.npz: the reference's attention beam search (u2.py:163-216) with TWO
+    decoder layers, where its forward_one_step cache matters: the cache is never reordered
+    with the hypotheses, so layers >= 1 attend to the previous step's row order.  Per
+    utterance: the input, every step's hyps fed to forward_one_step and the log-probs it
+    returned, and the best hypothesis."""
+    torch.manual_seed(42)
+    model = U2(tiny_cfg(enc_dim=64, dec_dim=64, enc_ff_dim=256, dec_ff_dim=256, vocab_size=30, dec_layers=2))
+    with torch.no_grad():
+        model.decoder.linear_out.weight.mul_(6.0)
+    model.eval()
+    state = {k: v.clone() for k, v in model.state_dict().items() if not k.endswith(".pe.pe")}
+    g = torch.Generator().manual_seed(13)
+    arrs = {"n_utt": np.array(2)}
+    step = model.decoder.forward_one_step
+    with torch.no_grad():
+        for u, T in enumerate((120, 80)):
+            x = torch.randn(1, T, 40, generator=g)
+            trace = []
+
+            def rec(y, mask, memory, memory_mask, cache, _step=step, _t=trace):
+                logp, new = _step(y, mask, memory, memory_mask, cache)
+                _t.append((y.clone(), logp.clone()))
+                return logp, new
+
+            model.decoder.forward_one_step = rec
+            best = model.attention(x)
+            model.decoder.forward_one_step = step
+            arrs[f"u{u}.x"] = x[0]
+            arrs[f"u{u}.steps"] = np.array(len(trace))
+            for i, (y, lp) in enumerate(trace):
+                arrs[f"u{u}.hyps{i}"] = y
+                arrs[f"u{u}.logp{i}"] = lp
+            arrs[f"u{u}.attn_best"] = np.array(best, dtype=np.int64)
+    save("decode_cache.npz", **arrs, **{"init." + k: v for k, v in state.items()})
+
+
+# encoder variants the reference's U2 builds besides the default conformer + relative PE +
+# Swish (liteasr/nets/transformer_encoder.py:47-100): name -> U2Config overrides
+U2_VARIANTS = {
+    "tfm_abs": dict(enc_arch=EncoderArch.Transformer, use_rel=False),
+    "tfm_rel": dict(enc_arch=EncoderArch.Transformer, use_rel=True),
+    "cfm_abs_relu": dict(enc_arch=EncoderArch.Conformer, use_rel=False, activation="relu"),
+    "cfm_rel_relu": dict(enc_arch=EncoderArch.Conformer, use_rel=True, activation="relu"),
+}
+
+
+def gen_u2_variants():
+    """u2_variants.npz: per variant <name>.init.* (seed-42 state_dict), outputs, loss and every
+    gradient of one hybrid-loss step (w 0.3) on the u2_step batch recipe."""
+    arrs = {}
+    for name, kw in U2_VARIANTS.items():
+        torch.manual_seed(42)
+        model = U2(tiny_cfg(**kw))
+        model.train()
+        init = {k: v.clone() for k, v in model.state_dict().items() if not k.endswith(".pe.pe")}
+        g = torch.Generator().manual_seed(3)
+        B, Tx, L, V = 3, 120, 6, 20
+        xlens = torch.tensor([120, 113, 97])
+        xs = torch.randn(B, Tx, 40, generator=g).masked_fill(padding_mask(xlens).unsqueeze(-1), 0.0)
+        ylens = torch.tensor([6, 4, 2])
+        ys = torch.randint(1, V - 1, (B, L), generator=g).masked_fill(padding_mask(ylens), -1)
+        rec = {}
+
+        class _Rec:  # one forward only (BN running stats must be updated exactly once)
+            def __call__(self, *a):
+                rec["out"] = model(*a)
+                return rec["out"]
+
+            def get_pred_len(self, xl):
+                return model.get_pred_len(xl)
+
+            def get_target(self, y, yl):
+                return model.get_target(y, yl)
+
+        loss = _crit(V, 0.3)(_Rec(), xs, xlens, ys, ylens)
+        h_attn, h_ctc = rec["out"]
+        loss.backward()
+        arrs.update({f"{name}.xs": xs, f"{name}.xlens": xlens, f"{name}.ys": ys, f"{name}.ylens": ylens,
+                     f"{name}.h_attn": h_attn.detach(), f"{name}.h_ctc": h_ctc.detach(),
+                     f"{name}.loss": loss.detach()})
+        arrs.update({f"{name}.init.{k}": v for k, v in init.items()})
+        arrs.update({f"{name}.grad.{n}": p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+    save("u2_variants.npz", **arrs)
+
+
 GENERATORS = dict(relshift=gen_relshift, lengths=gen_lengths, ctc_kl=gen_ctc_kl, u2_step=gen_u2_step,
                   decode=gen_decode, loader=gen_loader, spec_aug=gen_spec_aug, ctc_large=gen_ctc_large,
-                  host_policies=gen_host_policies, paraformer=gen_paraformer, transducer=gen_transducer)
+                  host_policies=gen_host_policies, paraformer=gen_paraformer, transducer=gen_transducer,
+                  u2_variants=gen_u2_variants, decode_cache=gen_decode_cache)
 
 if __name__ == "__main__":
     # python tests/golden/make_golden.py [name ...]   (default: all)

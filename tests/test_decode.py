@@ -171,6 +171,38 @@ def test_u2_decode_against_reference():
 
 
 @pytest.mark.gpu
+def test_attention_beam_decoder_cache_against_reference():
+    """The attention beam search with TWO decoder layers (tests/golden/decode_cache.npz, the
+    reference's own u2.py:163-216 run step by step): at every step the hypotheses fed to the
+    decoder are the reference's, and the top-k log-probs of the KV-cached decoder step equal
+    the reference's forward_one_step log-probs (its never-reordered cache of layers >= 1
+    included) within 1e-4; the best hypothesis is identical.  fp32 build."""
+    from liteasr_amd import decoding as D
+    from liteasr_amd.models.u2 import U2, U2Config
+    from liteasr_amd.utils.cfg import resolve_self
+
+    d = np.load(os.path.join(os.path.dirname(GOLD), "decode_cache.npz"))
+    c = U2Config(input_dim=40, vocab_size=30, enc_dim=64, enc_ff_dim=256, enc_attn_heads=4, enc_layers=2,
+                 dec_dim=64, dec_ff_dim=256, dec_attn_heads=4, dec_layers=2, compute_dtype="fp32")
+    resolve_self(c)
+    m = U2(c)
+    sd = {k[5:]: torch.from_numpy(np.array(v)) for k, v in d.items() if k.startswith("init.")}
+    m.load_state_dict(sd, strict=False)
+    m = m.cuda().eval()
+    for u in range(int(d["n_utt"])):
+        x = torch.from_numpy(d[f"u{u}.x"]).unsqueeze(0).cuda()
+        trace = []
+        with torch.no_grad():
+            best = D.attention_beam_search(m, x, beam=10, trace=trace)
+        assert best == d[f"u{u}.attn_best"].tolist(), u
+        assert len(trace) == int(d[f"u{u}.steps"]), (u, len(trace))
+        for i, (hyps, vals) in enumerate(trace):
+            assert np.array_equal(hyps, d[f"u{u}.hyps{i}"]), (u, i)
+            ref = np.sort(d[f"u{u}.logp{i}"], axis=-1)[:, ::-1][:, :10]
+            assert np.allclose(vals, ref, atol=1e-4, rtol=0), (u, i, np.abs(vals - ref).max())
+
+
+@pytest.mark.gpu
 def test_graphed_encode_matches_eager():
     """hipGraph-replayed batch-1 encoder == eager launches, bit for bit, across replays with
     new contents and after a weight update (re-capture)."""

@@ -34,7 +34,9 @@ def build(cfg_o, dtype, chunk=0, dropout=0.0):
     c = U2Config(input_dim=cfg_o["input_dim"], vocab_size=cfg_o["vocab_size"], enc_dim=cfg_o["enc_dim"],
                  enc_ff_dim=cfg_o["enc_ff"], enc_attn_heads=cfg_o["enc_heads"], enc_layers=cfg_o["enc_layers"],
                  dec_dim=cfg_o["dec_dim"], dec_ff_dim=cfg_o["dec_ff"], dec_attn_heads=cfg_o["dec_heads"],
-                 dec_layers=cfg_o["dec_layers"], dropout_rate=dropout, compute_dtype=dtype, chunk_size=chunk)
+                 dec_layers=cfg_o["dec_layers"], dropout_rate=dropout, compute_dtype=dtype, chunk_size=chunk,
+                 enc_arch=cfg_o.get("enc_arch", "conformer"), use_rel=cfg_o.get("use_rel", True),
+                 activation=cfg_o.get("activation", "swish"))
     resolve_self(c)
     return U2(c)
 
@@ -304,6 +306,59 @@ def test_parity_config5_long_bf16_emulated():
     """BASELINE config 5's shape: T 4000 (T' 999), CTC-only (w 1.0: the decoder runs and gets
     zero gradient), label length 150, full depth, one utterance pair."""
     _check_emulated(run_case(CONFIG2, 2, 4000, 150, "bf16", ctc_weight=1.0, emulate=True))
+
+
+# The other encoders the reference's U2 builds (liteasr/nets/transformer_encoder.py:47-100;
+# the oracle restatement is pinned to the reference's run by
+# tests/test_oracle_golden.py::test_u2_encoder_variants_against_reference)
+ENC_VARIANTS = {
+    "tfm_abs": dict(enc_arch="transformer", use_rel=False),
+    "tfm_rel": dict(enc_arch="transformer", use_rel=True),
+    "cfm_abs_relu": dict(enc_arch="conformer", use_rel=False, activation="relu"),
+    "cfm_rel_relu": dict(enc_arch="conformer", use_rel=True, activation="relu"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(ENC_VARIANTS))
+def test_parity_encoder_variants_fp32(name):
+    """fp32 build vs the fp64 oracle, tiny widths (materialised attention): the bars of
+    test_parity_fp32 (the ReLU conformer's conv-module / FFN kinks share the embed convs' bar)."""
+    cfg = dict(TINY, **ENC_VARIANTS[name])
+    r = run_case(cfg, 3, 130, 8, "fp32")
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 1e-5 * abs(lo), r["loss"]
+    assert rel(*r["h_attn"]) < 2e-4 and rel(*r["h_ctc"]) < 2e-4
+    g, go = r["grads"]
+    errs, _ = grad_errs(g, go)
+    kink = {k for k in errs if k.startswith("encoder.embed.conv.")}
+    worst = max((v, k) for k, v in errs.items() if k not in kink)
+    assert worst[0] < 2e-4, worst
+    assert max(errs[k] for k in kink) < 2e-2, {k: errs[k] for k in kink}
+
+
+@pytest.mark.parametrize("name", sorted(ENC_VARIANTS))
+def test_parity_encoder_variants_bf16(name):
+    """bf16 build at the small config's widths (d 256, 4 heads: d_k 64, the fused attention
+    kernels -- with the positional term for use_rel, without it for the absolute PE) vs the
+    fp64 oracle fed the same bf16-rounded weights: the bf16 bars of test_parity_bf16, every
+    ReLU-activated encoder tensor counted as ReLU-gated.  The ReLU conformer's cosine bar is
+    0.99: its conv module applies ReLU right after a BatchNorm (inputs ~N(0, 1) per channel,
+    so a large share of them sits within bf16 rounding of the kink; measured worst 0.996,
+    conv_norm.weight), while its fp32 build holds 2e-4 (test_parity_encoder_variants_fp32)."""
+    cfg = dict(SMALL, **ENC_VARIANTS[name])
+    r = run_case(cfg, 2, 210, 12, "bf16", round_bf16=True)
+    relu_enc = cfg.get("activation") == "relu" or cfg["enc_arch"] == "transformer"
+    lg, lo = r["loss"]
+    assert abs(lg - lo) <= 5e-3 * abs(lo), r["loss"]
+    assert rel(*r["h_attn"]) < 2e-2 and rel(*r["h_ctc"]) < 2e-2
+    g, go = r["grads"]
+    errs, floor = grad_errs(g, go)
+    for k in go:
+        gated = relu_gated(k) or (relu_enc and k.startswith("encoder.enc_layers."))
+        if go[k].abs().max().item() > floor:
+            bar = (0.99 if cfg.get("activation") == "relu" else 0.998) if gated else 0.999
+            assert cos(g[k], go[k]) >= bar, k
+        assert errs[k] < (0.35 if gated else 5e-2), (k, errs[k])
 
 
 def test_parity_full_depth_fp32():

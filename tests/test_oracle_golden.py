@@ -148,6 +148,57 @@ def test_u2_step_against_reference():
             assert int(v) == int(ref), k
 
 
+# the other encoders the reference's U2 builds (tests/golden/make_golden.py U2_VARIANTS):
+# golden prefix -> oracle cfg keys
+U2_VARIANT_CFG = {
+    "tfm_abs": dict(enc_arch="transformer", use_rel=False),
+    "tfm_rel": dict(enc_arch="transformer", use_rel=True),
+    "cfm_abs_relu": dict(enc_arch="conformer", use_rel=False, activation="relu"),
+    "cfm_rel_relu": dict(enc_arch="conformer", use_rel=True, activation="relu"),
+}
+
+
+def variant_case(name):
+    """(golden dict, cfg, fp64 params, fp64 buffers, batch) of one u2_variants.npz entry."""
+    d = {k[len(name) + 1:]: v for k, v in load("u2_variants.npz").items() if k.startswith(name + ".")}
+    params, buffers = _golden_params(d, "init.")
+    cfg = dict(TINY_GOLDEN, **U2_VARIANT_CFG[name])
+    p64 = {k: v.double() for k, v in params.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in buffers.items()}
+    return d, cfg, p64, b64, (d["xs"].double(), d["xlens"], d["ys"], d["ylens"])
+
+
+@pytest.mark.parametrize("name", sorted(U2_VARIANT_CFG))
+def test_u2_encoder_variants_against_reference(name):
+    """Transformer encoder layers (absolute / relative PE) and the conformer with absolute PE or
+    ReLU (liteasr/nets/transformer_encoder.py:47-100, transformer_layer.py:10-136): the oracle's
+    restatement reproduces the reference's outputs, loss and every gradient."""
+    d, cfg, p64, b64, batch = variant_case(name)
+    assert set(p64) == {k[len("init."):] for k in d if k.startswith("init.") and "running_" not in k
+                        and "num_batches" not in k}
+    with torch.no_grad():
+        ha, hc, _, _ = O.u2_forward(*batch, p64, cfg, {k: v.clone() for k, v in b64.items()}, True)
+    assert rel(ha, d["h_attn"]) < 1e-5
+    assert rel(hc, d["h_ctc"]) < 1e-5
+    loss, grads, _, _, _ = O.train_step(p64, b64, batch, cfg, model_dim=32)
+    assert abs(loss.item() - d["loss"].item()) <= 1e-5 * abs(d["loss"].item())
+    gmax = max(v.abs().max().item() for k, v in d.items() if k.startswith("grad."))
+    for k, g in grads.items():
+        ref = d["grad." + k].double()
+        err = (g - ref).abs().max().item() / max(ref.abs().max().item(), 1e-3 * gmax)
+        assert err < 1e-4, (k, err)
+
+
+def test_u2_encoder_variant_init_keys():
+    """The oracle's init_params produces exactly the reference's state_dict keys and shapes per
+    variant (so the GPU tests can load oracle weights into liteasr_amd's U2)."""
+    for name in U2_VARIANT_CFG:
+        d, cfg, p64, b64, _ = variant_case(name)
+        mine = O.init_params(cfg)
+        assert {k: tuple(v.shape) for k, v in mine.items()} == {k: tuple(v.shape) for k, v in p64.items()}, name
+        assert set(O.init_buffers(cfg)) == set(b64), name
+
+
 def _golden_step_inputs():
     d = load("u2_step.npz")
     params, buffers = _golden_params(d, "init.")
@@ -222,6 +273,26 @@ def test_liteasr_amd_init_matches_reference():
     d = load("u2_step.npz")
     c = U2Config(input_dim=40, vocab_size=20, enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_layers=2,
                  dec_dim=32, dec_ff_dim=64, dec_attn_heads=4, dec_layers=1)
+    resolve_self(c)
+    torch.manual_seed(42)
+    m = U2(c)
+    sd = {k: v for k, v in m.state_dict().items() if not k.endswith(".pe.pe")}
+    ref = {k[5:]: v for k, v in d.items() if k.startswith("init.")}
+    assert set(sd) == set(ref)
+    for k in ref:
+        assert torch.equal(sd[k].to(ref[k].dtype), ref[k]), k
+
+
+@pytest.mark.parametrize("name", sorted(U2_VARIANT_CFG))
+def test_liteasr_amd_init_matches_reference_variants(name):
+    """The same for the other encoders: identical keys and bit-identical seed-42 weights."""
+    from liteasr_amd.models.u2 import U2, U2Config
+    from liteasr_amd.utils.cfg import resolve_self
+
+    d, cfg, _, _, _ = variant_case(name)
+    c = U2Config(input_dim=40, vocab_size=20, enc_dim=32, enc_ff_dim=64, enc_attn_heads=4, enc_layers=2,
+                 dec_dim=32, dec_ff_dim=64, dec_attn_heads=4, dec_layers=1, enc_arch=cfg["enc_arch"],
+                 use_rel=cfg["use_rel"], activation=cfg.get("activation", "swish"))
     resolve_self(c)
     torch.manual_seed(42)
     m = U2(c)

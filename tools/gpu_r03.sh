@@ -18,6 +18,7 @@ for s in $STEPS; do
     conv) cd "$R" && for v in ${CONV_VARIANTS:-0 1}; do LASR_CONV_WIDE=$v run timeout -k 10 120 python3 tools/conv2_bench.py >> "$OUT/conv2_bench.json" 2>> "$OUT/conv2_bench.err"; done
           run timeout -k 10 60 python3 -c "import torch; a=torch.load('/tmp/conv2_dw_0.pt'); b=torch.load('/tmp/conv2_dw_1.pt'); print('dw rel', ((a['dw']-b['dw']).abs().max()/a['dw'].abs().max()).item(), 'db rel', ((a['db']-b['db']).abs().max()/a['db'].abs().max()).item())" >> "$OUT/conv2_bench.json" ;;
     benchab) cd "$R" && for v in ${WIDE_VARIANTS:-0 1}; do LASR_GEMM_WIDE=$v run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/bench_wide$v.json" 2> "$OUT/bench_wide$v.err"; done ;;
+    variants) cd "$R" && run timeout -k 10 400 python -u -m pytest tests/test_model_gpu.py -m gpu -q --timeout 200 --timeout-method thread -k "variants" -s > "$OUT/variants.log" 2>&1 ;;
     kgpu) cd "$R" && run timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_nodes_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/kgpu.log" 2>&1 ;;
     smoke) cd "$R" && run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) cd "$R" && run timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
