@@ -237,9 +237,15 @@ def roofline_case(cfgd, dev):
     flops = sum(2.0 * a.shape[0] * a.shape[1] * b.shape[1] for a, b, _, _ in probs)
     bytes_ = sum(2.0 * (a.numel() + b.numel()) + 4.0 * c.numel() for a, b, c, _ in probs)
     tm, tn = q[0][0]
-    S, minb = {(64, 64): (3, 3), (128, 128): (2, 2)}[(tm, tn)]
+    # the group key is the planner's family; lasr_gemm_dw_group (gemm.hip) runs the FFN-sized
+    # family on 8-wave 256 x 128 tiles unless LASR_DW_WIDE=0
+    if (tm, tn) == (128, 128) and os.environ.get("LASR_DW_WIDE", "1") != "0":
+        kname = "gemm_dw_group_kernel<256, 128, 3, 1, 8>"
+    else:
+        S, minb = {(64, 64): (3, 3), (128, 128): (2, 2)}[(tm, tn)]
+        kname = f"gemm_dw_group_kernel<{tm}, {tn}, {S}, {minb}, 4>"
     splits = sorted({-x[1].split_k for x in q})
-    meta = {"kernel": f"gemm_dw_group_kernel<{tm}, {tn}, {S}, {minb}>",
+    meta = {"kernel": kname,
             "shape": f"{len(q)} problems: 2x (M={F} N={D}) + 2x (M={D} N={F}), K={rows}, split_k={splits}",
             "build": build_key()}
     return launch, flops, bytes_, meta

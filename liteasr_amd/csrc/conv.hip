@@ -89,15 +89,25 @@ __global__ void conv1_bwd_reduce_kernel(const float* part, int nparts, int C, fl
 // (their 8x10 weights in registers) and a strided set of output columns f1, so every
 // y1 / dy1 access is one 16-B (bf16) vector and a wave covers whole 512-B channel rows.
 // Same per-output arithmetic order as the scalar kernels above.
+constexpr int C1V_ROWS = 32;  // (b,t1) rows per vectorised conv1-bwd block
+constexpr int C1F_ROWS = 8;   // (b,t1) rows per vectorised conv1-fwd block
+
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restrict__ x, int T_, int F,
-                                                           int C, int T1, int F1, const float* w,
+                                                           int C, int T1, int F1, int nrows, const float* w,
                                                            const float* bias, T* y1) {
-  extern __shared__ float xs[];  // the 3 contiguous input rows 2*t1 .. 2*t1+2
-  const int bt = blockIdx.x;
-  const int b = bt / T1, t1 = bt - b * T1;
-  const float* src = x + ((int64_t)b * T_ + 2 * t1) * F;
-  for (int i = threadIdx.x; i < 3 * F; i += 256) xs[i] = src[i];
+  // C1F_ROWS output rows (b, t1) per block: the 72 weights and 8 biases a thread keeps in
+  // registers are loaded once per block, not once per row; the 3 input rows of each output
+  // row are staged in LDS.  Each output: bias + sum over the 9 taps in order, then ReLU.
+  extern __shared__ float xs[];  // C1F_ROWS x 3F
+  const int r0 = blockIdx.x * C1F_ROWS;
+  const int nr = min(C1F_ROWS, nrows - r0);
+  for (int i = threadIdx.x; i < nr * 3 * F; i += 256) {
+    const int rr = i / (3 * F), q = i - rr * 3 * F;
+    const int r = r0 + rr;
+    const int b = r / T1, t1 = r - b * T1;
+    xs[i] = x[((int64_t)b * T_ + 2 * t1) * F + q];
+  }
   const int CG = C >> 3, cg = threadIdx.x % CG, fg = threadIdx.x / CG, NFG = 256 / CG;
   const int c0 = cg * 8;
   float wr[8][9], bv[8];
@@ -108,26 +118,28 @@ __global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restri
     for (int k = 0; k < 9; ++k) wr[q][k] = w[(c0 + q) * 9 + k];
   }
   __syncthreads();
-  T* out = y1 + (int64_t)bt * F1 * C + c0;
-  for (int f1 = fg; f1 < F1; f1 += NFG) {
-    float xv[9];
+  for (int rr = 0; rr < nr; ++rr) {
+    const float* xr = xs + rr * 3 * F;
+    T* out = y1 + (int64_t)(r0 + rr) * F1 * C + c0;
+    for (int f1 = fg; f1 < F1; f1 += NFG) {
+      float xv[9];
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
+      for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xs[kh * F + 2 * f1 + kw];
-    float o[8];
+        for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xr[kh * F + 2 * f1 + kw];
+      float o[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float acc = bv[q];
+      for (int q = 0; q < 8; ++q) {
+        float acc = bv[q];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) acc += wr[q][k] * xv[k];
-      o[q] = fmaxf(acc, 0.f);
+        for (int k = 0; k < 9; ++k) acc += wr[q][k] * xv[k];
+        o[q] = fmaxf(acc, 0.f);
+      }
+      st8(out + (int64_t)f1 * C, o);
     }
-    st8(out + (int64_t)f1 * C, o);
   }
 }
 
-constexpr int C1V_ROWS = 32;  // (b,t1) rows per vectorised conv1-bwd block
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_bwd_v8_kernel(const float* __restrict__ x, int T_, int F,
                                                            int C, int T1, int F1, int nrows,
@@ -667,10 +679,13 @@ extern "C" int lasr_conv1_fwd(const float* x, int B, int T, int F, int C, const 
   const size_t shm = (size_t)(3 * F + 10 * C) * sizeof(float);
   LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_conv1_fwd: too much LDS");
   hipStream_t st = (hipStream_t)stream;
-  if (C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)y1 & 15) == 0) {
-    const size_t shv = (size_t)3 * F * sizeof(float);
-    if (dt == LASR_F32) conv1_fwd_v8_kernel<float><<<B * T1, 256, shv, st>>>(x, T, F, C, T1, F1, w, bias, (float*)y1);
-    else conv1_fwd_v8_kernel<bf16_t><<<B * T1, 256, shv, st>>>(x, T, F, C, T1, F1, w, bias, (bf16_t*)y1);
+  if (C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)y1 & 15) == 0 &&
+      (size_t)C1F_ROWS * 3 * F * sizeof(float) <= 64 * 1024) {
+    const size_t shv = (size_t)C1F_ROWS * 3 * F * sizeof(float);
+    const int nrows = B * T1;
+    const unsigned nb = (unsigned)cdiv(nrows, C1F_ROWS);
+    if (dt == LASR_F32) conv1_fwd_v8_kernel<float><<<nb, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, w, bias, (float*)y1);
+    else conv1_fwd_v8_kernel<bf16_t><<<nb, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, w, bias, (bf16_t*)y1);
     return lasr_check_launch("conv1_fwd");
   }
   if (dt == LASR_F32) conv1_fwd_kernel<float><<<B * T1, 256, shm, st>>>(x, T, F, C, T1, F1, w, bias, (float*)y1);

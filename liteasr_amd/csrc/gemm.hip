@@ -314,6 +314,15 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
 
 
 // ---------------------------------------------------------------------------------------
+static int dw_wide() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("LASR_DW_WIDE");
+    v = e && e[0] ? atoi(e) : 1;
+  }
+  return v;
+}
+
 // Grouped split-K weight gradients (partials only): the deferred dW GEMMs of one backward
 // node in one launch.  Every problem must be what lasr_gemm would run as a partials-only
 // (split_k = -1) LDS-DMA launch with 64-deep stages, A M-contiguous and B N-contiguous
@@ -343,7 +352,17 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     // third less LDS-DMA ingest per output, and a tile's shape does not change any output's
     // summation order (k order within the slice); the group's many problems and K slices
     // keep the chip full (grouped FFN dW of a layer: 77 -> 57 us per launch)
-    if (((BM == 128 && BN == 64) || (BM == 64 && BN == 128)) && a->M >= 128 && a->N >= 128) BM = BN = 128;
+    if (((BM == 128 && BN == 64) || (BM == 64 && BN == 128)) && a->M >= 128 && a->N >= 128) {
+      BM = BN = 128;
+      // 256 x 128 tiles on 8 waves, one workgroup per CU, the same K slices (one tile for
+      // the whole group): 0.25 fewer LDS-DMA bytes per MFMA than the 4-wave 128 x 128 tile;
+      // 11.84 -> 11.63-11.70 ms/step on two boxes (profiles/r03/dw_group_ab.json; 256 x 256
+      // with twice the slices, and a 2-stage ring, measured no better).  LASR_DW_WIDE=0: A/B.
+      if (dw_wide() && a->M >= 256 && a->N >= 256) {
+        BM = 256;
+        BN = 128;
+      }
+    }
     LASR_CHECK_ARG(i == 0 || (BM == BM0 && BN == BN0), "lasr_gemm_dw_group: problems plan different tiles");
     BM0 = BM;
     BN0 = BN;

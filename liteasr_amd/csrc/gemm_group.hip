@@ -7,6 +7,8 @@ int launch_dw_group(const DwGroupP& g, int BM, int BN, int blocks, hipStream_t s
   else if (BM == 64 && BN == 128) gemm_dw_group_kernel<64, 128, 3, 2><<<blocks, 256, 0, st>>>(g);
   else if (BM == 128 && BN == 64) gemm_dw_group_kernel<128, 64, 3, 2><<<blocks, 256, 0, st>>>(g);
   else if (BM == 128 && BN == 128) gemm_dw_group_kernel<128, 128, 2, 2><<<blocks, 256, 0, st>>>(g);
+  // 8 waves (512 threads), one workgroup per CU
+  else if (BM == 256 && BN == 128) gemm_dw_group_kernel<256, 128, 3, 1, 8><<<blocks, 512, 0, st>>>(g);
   else return -1;
   return 0;
 }

@@ -890,8 +890,8 @@ struct DwGroupP {
   float* rs_ws[LASR_DW_GROUP_MAX];  // null: no fused bias rowsum
 };
 
-template <int BM, int BN, int S, int MINB>
-__global__ __launch_bounds__(256, MINB) void gemm_dw_group_kernel(DwGroupP g) {
+template <int BM, int BN, int S, int MINB, int NW = 4>
+__global__ __launch_bounds__(NW * 64, MINB * NW / 4) void gemm_dw_group_kernel(DwGroupP g) {
   const int blk = blockIdx.x;
   int i = 0;
   for (int j = 1; j < g.n; ++j)
@@ -910,7 +910,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_dw_group_kernel(DwGroupP g) {
   const int wg = xcd_remap(local % ntile, ntile);
   int tx, ty;
   dw_tile_order(wg, ntx, nty, p.N > p.M, tx, ty);
-  gemm_glds_tile<BM, BN, false, false, float, S, G_LIN, 2>(p, tx, ty, local / ntile);
+  gemm_glds_tile<BM, BN, false, false, float, S, G_LIN, 2, NW>(p, tx, ty, local / ntile);
 }
 
 // ============================ fp32 MFMA kernel ===================================

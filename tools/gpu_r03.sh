@@ -21,6 +21,7 @@ for s in $STEPS; do
     variants) cd "$R" && run timeout -k 10 400 python -u -m pytest tests/test_model_gpu.py -m gpu -q --timeout 200 --timeout-method thread -k "variants" -s > "$OUT/variants.log" 2>&1 ;;
     envab) cd "$R" && for v in ${AB_VALUES:-0 1}; do env ${AB_VAR}=$v timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/bench_${AB_VAR}_$v.json" 2> "$OUT/bench_${AB_VAR}_$v.err" || exit 1; done ;;
     model) cd "$R" && run timeout -k 10 500 python -u -m pytest tests/test_model_gpu.py tests/test_trainer_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/model.log" 2>&1 ;;
+    conv1) cd "$R" && run timeout -k 10 120 python3 tools/conv1_bench.py > "$OUT/conv1_bench.json" 2> "$OUT/conv1_bench.err" ;;
     kgpu) cd "$R" && run timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_nodes_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/kgpu.log" 2>&1 ;;
     smoke) cd "$R" && run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) cd "$R" && run timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
