@@ -96,7 +96,10 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
   int BM = 64, BN = 64;
   int split = a->split_k > 0 ? a->split_k : 1;
   const bool plain = !a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f;
-  const bool autosplit = a->split_k <= 0 && plain && a->workspace;
+  // split_k <= 0 asks for an automatic split; with an epilogue (the small-grid long-K GEMMs,
+  // kernels.gemm) the fixed-order split-K reduction applies it (splitk_reduce_kernel:
+  // bias, activation, aux, dropout, residual, beta -- the same per-element arithmetic)
+  const bool autosplit = a->split_k <= 0 && !a->zout && a->workspace;
   const int kt = (int)cdiv(a->K, 32);
   if (bf && autosplit && kt >= 16) {
     // long-K (weight-gradient) GEMMs: big tiles, fill the chip with K slices instead
@@ -114,7 +117,8 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
       BN = a->M >= a->N ? 128 : 64;
     }
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
-    const int64_t target = very_long ? 256 : 512;
+    // epilogue GEMMs (small grids, long K: the decoder's K = 2048 projections) fill one round
+    const int64_t target = very_long || !plain ? 256 : 512;
     while (nb * split < target && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
   } else if (bf) {
     const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
@@ -149,7 +153,7 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
   if (autosplit && g_split) split = g_split;
   if (a->split_k <= -2 && plain && a->workspace) split = -a->split_k;  // explicit partials-only
   const int64_t rs_floats = a->rowsum ? (int64_t)split * a->M : 0;
-  if (split > 1 && (!plain || !a->workspace ||
+  if (split > 1 && ((!plain && !autosplit) || !a->workspace ||
                     a->workspace_bytes < ((int64_t)split * batch * a->M * a->N + rs_floats) * 4))
     split = 1;
   // ring depth of the LDS-DMA kernel: 64-deep stages (two 32-deep sub-tiles per counted
@@ -347,7 +351,10 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     LASR_CHECK_ARG(gemm_uses_glds(a), "lasr_gemm_dw_group: operands not LDS-DMA eligible");
     int BM, BN, split, ks;
     gemm_plan(a, &BM, &BN, &split, &ks);
-    LASR_CHECK_ARG(split > 1 && ks == 2, "lasr_gemm_dw_group: plan is not a split-K 64-deep launch");
+    // the group kernel runs 64-deep ring stages; a lone 32-deep launch gives the same bits
+    // (the sub-tiles keep their images and order: test_gemm_ksub2_bit_identical), so a
+    // short-K plan (e.g. the decoder's FFN weights, K = B*(L+1)) groups too
+    LASR_CHECK_ARG(split > 1, "lasr_gemm_dw_group: plan is not a split-K launch");
     // the FFN-sized problems (64 x 128 / 128 x 64 plans) run on 128 x 128 group tiles: a
     // third less LDS-DMA ingest per output, and a tile's shape does not change any output's
     // summation order (k order within the slice); the group's many problems and K slices

@@ -115,6 +115,11 @@ else:
     DW_GROUP_SPLIT_DIV = int(_DIV_ENV)
 
 
+# GEMMs whose 64 x 64 grid cannot fill half the chip and whose K is long are split over K
+# (lasr_gemm autosplit; the split-K reduction applies the epilogue).  LASR_SMALL_GRID_SPLIT=0: off.
+SMALL_GRID_SPLIT = os.environ.get("LASR_SMALL_GRID_SPLIT", "1") != "0"
+
+
 def _group_div(key):
     d = DW_GROUP_SPLIT_DIV
     return d.get(key, 1) if isinstance(d, dict) else d
@@ -235,6 +240,11 @@ def gemm(
     args.drop_p, args.drop_seed = drop_p, drop_seed
     if res is not None:
         args.res, args.res_dtype, args.ldres, args.res_scale = ptr(res), dt(res), res.stride(0), res_scale
+    auto_split = (split_k == 1 and SMALL_GRID_SPLIT and rowsum is None and zout is None and not group
+                  and a.dtype == torch.bfloat16 and z1 * z2 == 1 and K >= 1024
+                  and ((M + 63) // 64) * ((Nn + 63) // 64) < 128)
+    if auto_split:  # small grid, long K (the decoder's B*(L+1)-row GEMMs): split K, reduce with the epilogue
+        split_k = 0
     args.split_k = split_k
     if rowsum is not None:
         # fused bias gradient rowsum[m] += sum_k a[m, k] (fp32, a M-contiguous)
@@ -252,21 +262,21 @@ def gemm(
         if plan_only == "flags":
             return tm.value, tn.value, sp.value, fl.value
         return tm.value, tn.value, sp.value
-    if (_DEFER.depth and split_k == 0 and beta in (0.0, 1.0) and alpha == 1.0 and alpha_dev is None
+    if (_DEFER.depth and split_k == 0 and not auto_split and beta in (0.0, 1.0) and alpha == 1.0 and alpha_dev is None
             and bias is None and act == N.ACT_NONE and zout is None and aux is None and res is None
             and drop_p <= 0.0 and z1 * z2 == 1 and c.dtype == torch.float32 and c.is_contiguous()):
         tm, tn, sp, fl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(sp), C.byref(fl))
         sp = sp.value
         grouped = (group and DW_GROUP and (tm.value, tn.value) in _GROUP_TILES
-                   and (fl.value & 5) == 5 and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16)
+                   and (fl.value & 1) and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16)
         div = _group_div(_GROUP_TILES[(tm.value, tn.value)]) if grouped else 1
         if grouped and (div > 1 or sp < 2):
             # short K too (the positional-projection weight, K = T'): two slices join the group
             sp = max(2, sp // max(1, div))
             args.split_k = -sp
             N.call("lasr_gemm_plan", C.byref(args), C.byref(tm), C.byref(tn), C.byref(C.c_int()), C.byref(fl))
-            grouped = (tm.value, tn.value) in _GROUP_TILES and (fl.value & 5) == 5
+            grouped = (tm.value, tn.value) in _GROUP_TILES and bool(fl.value & 1)
         if sp > 1:
             # partials-only launch (split_k = -1) into a buffer that lives until the flush
             # rowsum partials (fused) or the column-sum scratch (unfused, fp32 operands)

@@ -799,7 +799,12 @@ def test_conv2_implicit_gemm(B, T, Fd, Cc, ref64):
     col = torch.empty(M2, 9 * Cc, device=DEV, dtype=bf)
     kn.im2col(y1, col)
     y2e = torch.empty_like(y2)
-    kn.linear(col, w2p, y2e, bias=b2, act=Nn.ACT_RELU)
+    small_grid = kn.SMALL_GRID_SPLIT
+    kn.SMALL_GRID_SPLIT = False  # the reference GEMM in one K pass (no small-grid split)
+    try:
+        kn.linear(col, w2p, y2e, bias=b2, act=Nn.ACT_RELU)
+    finally:
+        kn.SMALL_GRID_SPLIT = small_grid
     assert torch.equal(y2.view(torch.int16), y2e.view(torch.int16)), "conv2 fwd != im2col + GEMM"
     # backward operands: dy2 with its zero tail
     rows = kn.conv2_dy2_rows(M2)

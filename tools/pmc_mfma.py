@@ -31,7 +31,7 @@ def main(path):
     for d, c in rows.items():
         if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
             continue
-        k = name[d].split("(")[0][:90]
+        k = name[d].replace("(anonymous namespace)::", "").split("(")[0][:90]
         per[k][0] += 1
         per[k][1] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
         per[k][2] += c["GRBM_GUI_ACTIVE"] / 8.0

@@ -14,19 +14,21 @@ import statistics
 import sys
 
 
-def per_dispatch(db, counter, kernel):
-    """Summed counter value per dispatch of `kernel` (rocprofv3 counters_collection view)."""
+def per_dispatch(db, counter, kernels):
+    """Summed counter value per dispatch of any kernel whose name contains one of `kernels`
+    (rocprofv3 counters_collection view), in dispatch order."""
     c = sqlite3.connect(db)
-    q = ("select dispatch_id, sum(value) from counters_collection "
-         "where counter_name = ? and instr(kernel_name, ?) > 0 group by dispatch_id")
-    return [v for _, v in c.execute(q, (counter, kernel))]
+    q = ("select dispatch_id, kernel_name, sum(value) from counters_collection "
+         "where counter_name = ? group by dispatch_id order by dispatch_id")
+    return [v for _, name, v in c.execute(q, (counter,)) if any(k in name for k in kernels)]
 
 
 if __name__ == "__main__":
     dbf, dbw, metaf, outf = sys.argv[1:5]
     meta = json.loads(open(metaf).read().strip().splitlines()[-1])
-    f = per_dispatch(dbf, "FETCH_SIZE", meta["kernel"])
-    w = per_dispatch(dbw, "WRITE_SIZE", meta["kernel"])
+    names = meta.get("match") or [meta["kernel"]]  # a family lists its kernels' names
+    f = per_dispatch(dbf, "FETCH_SIZE", names)
+    w = per_dispatch(dbw, "WRITE_SIZE", names)
     assert f and w, "no dispatches of the roofline kernel in the PMC databases"
     per = meta.get("dispatches_per_launch", 1)
     if per > 1:  # a family: one "launch" = a layer's set of dispatches; total over the run / sets
