@@ -334,7 +334,7 @@ def dominant_kernel_roofline(cfgd, dev, iters=50):
     out = {"kernel": fam_meta["kernel"], "shape": fam_meta["shape"], "bound": "hbm", "achieved": round(ach, 2),
            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
            "traffic": traffic["bytes_per_launch"] if traffic else None,
-           "per": "one Conformer layer's launches of the family (12); achieved = algorithmic bytes / summed "
+           "per": "one Conformer layer's launches of the family (10); achieved = algorithmic bytes / summed "
                   "launch time",
            "algorithmic_bytes_per_launch": tb, "algorithmic_flops_per_launch": tf,
            "avg_launch_us": round(tt / sum(r["per_layer"] for r in rows) * 1e6, 2),
@@ -352,6 +352,7 @@ def dominant_kernel_roofline(cfgd, dev, iters=50):
 def family_meta(cfgd):
     M, D, F = _rows(cfgd), cfgd["d"], cfgd["ff"]
     return {"kernel": "gemm_bf16_glds_kernel + row_res_ln_kernel + row_dx_ln_bwd_kernel",
+            "match": ["gemm_bf16_glds_kernel", "row_res_ln_kernel", "row_dx_ln_bwd_kernel"],
             "family": "N = d output GEMMs (64x64 tiles and the full-row LayerNorm tiles)",
             "shape": f"one layer: 2x fc2 fwd M={M} N={D} K={F} +res, linear_o / pw2 fwd K={D} +res +LN, "
                      f"2x fc1 dX K={F}, linear_o / pw2 dX K={D}, qkv dX K={3 * D} +LN bwd, "
@@ -657,7 +658,8 @@ def main():
                        "per_gpu_batch": cfgd["B"], "seq_len": cfgd["T"], "label_len": cfgd["L"],
                        "ctc_weight": cfgd["w"], "dropout": args.dropout, "chunk_size": cfgd["chunk"],
                        "parallelism": f"dp{world}", "launch": "hipgraph" if args.graph == "on" else "eager",
-                       "ranks_seen": world, "rank_launcher": launcher,
+                       "ranks_seen": dist.get_world_size() if dist.is_initialized() else world,
+                       "rank_launcher": launcher,
                        "allreduce": None if not use_ddp else
                        {"backend": dist.get_backend(), "buckets": len(net.reducer.buckets),
                         "bucket_mb": 25, "overlap": args.overlap == "on" and args.graph == "on" or args.graph == "off",
