@@ -33,9 +33,13 @@ class FusedEncoderModel(LiteasrModel):
         for i, layer in enumerate(self.encoder.enc_layers):
             groups += layer.flat_groups()
             layer.seed = 1000 + 16 * i
+        dgroups = getattr(self.decoder, "flat_groups", None)  # Transformer decoders: cross-layer K/V
         for i, layer in enumerate(self.decoder.dec_layers):
-            groups += layer.flat_groups()
+            if dgroups is None:
+                groups += layer.flat_groups()
             layer.seed = 5000 + 16 * i
+        if dgroups is not None:
+            groups += dgroups()
         self.store = FlatParams(self, groups, self.compute_dtype)
         for mod in self.modules():
             if isinstance(mod, _Bound):

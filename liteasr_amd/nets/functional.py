@@ -159,8 +159,10 @@ def _heads(t, B, T, H, dk):
 
 
 def _slot(t, B, T, nslot, k, H, dk):
-    """Slot k of a fused [B*T, nslot*H*dk] projection as (B, H, T, dk)."""
-    return t.view(B, T, nslot, H, dk)[:, :, k].permute(0, 2, 1, 3)
+    """Slot k of a fused [B*T, nslot*H*dk] projection (row stride arbitrary) as (B, H, T, dk)."""
+    if t.is_contiguous():
+        return t.view(B, T, nslot, H, dk)[:, :, k].permute(0, 2, 1, 3)
+    return t.unflatten(0, (B, T)).unflatten(2, (nslot, H, dk))[:, :, k].permute(0, 2, 1, 3)
 
 
 # ============================================================ rel-pos MHSA ======
@@ -314,8 +316,10 @@ def _fused_dec(adt, dk, p_att):
     return FUSED_DEC_ATTN and fused_relattn(adt, dk, p_att)
 
 
-def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_res, s_res):
-    """Decoder self (mem None) / source attention (liteasr/nets/attention.py:61-71)."""
+def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_res, s_res, kv=None):
+    """Decoder self (mem None) / source attention (liteasr/nets/attention.py:61-71).  kv: the
+    memory's key/value projection [B*Tk, 2d] already computed (decoder_layers_fwd batches it
+    over the layers); None computes it here."""
     d = ln.shape[1]
     dk = d // H
     dev, adt = ln.device, ln.dtype
@@ -330,8 +334,9 @@ def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_
             qkv = None
             q = _e((R, d), adt, dev)
             K.linear(ln, w.Wq, q, bias=w.bq)
-            kv = _e((B * Tk, 2 * d), adt, dev)
-            K.linear(mem, w.Wkv, kv, bias=w.bkv)
+            if kv is None:
+                kv = _e((B * Tk, 2 * d), adt, dev)
+                K.linear(mem, w.Wkv, kv, bias=w.bkv)
             k, v = kv[:, :d], kv[:, d:]
         stats = _e((B * H * Tq * 2,), F32, dev)
         ctx = _e((R, d), adt, dev)
@@ -350,8 +355,9 @@ def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_
     else:
         q = _e((R, d), adt, dev)
         K.linear(ln, w.Wq, q, bias=w.bq)
-        kv = _e((B * Tk, 2 * d), adt, dev)
-        K.linear(mem, w.Wkv, kv, bias=w.bkv)
+        if kv is None:
+            kv = _e((B * Tk, 2 * d), adt, dev)
+            K.linear(mem, w.Wkv, kv, bias=w.bkv)
         q4 = _heads(q, B, Tq, H, dk)
         k4 = _slot(kv, B, Tk, 2, 0, H, dk)
         v4 = _slot(kv, B, Tk, 2, 1, H, dk)
@@ -369,7 +375,11 @@ def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_
     return out, SimpleNamespace(qkv=qkv, q=q, kv=kv, P=P, Praw=Praw, ctx=ctx, stats=None)
 
 
-def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_att, dmem):
+def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_att, dmem, dkv=None):
+    """dkv: [B*Tk, 2d] destination of the key/value projection's gradient, whose weight /
+    memory gradients the caller then computes (decoder_layers_bwd, batched over the layers);
+    None computes them here (dmem accumulates)."""
+    own_kv = dkv is None
     d = ln.shape[1]
     dk = d // H
     dev, adt = ln.device, ln.dtype
@@ -390,13 +400,15 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
             K.gemm(dqkv, w.Wqkv, dln)
             return dln
         dq = _e((R, d), adt, dev)
-        dkv = _e((B * Tk, 2 * d), adt, dev)
+        if own_kv:
+            dkv = _e((B * Tk, 2 * d), adt, dev)
         K.attn_bwd(sv.q, sv.kv[:, :d], sv.kv[:, d:], B, H, Tq, Tk, mask, msb, msq, scale, sv.stats, sv.ctx, dctx,
                    Dbuf, dq, dkv[:, :d], dkv[:, d:])
         K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq, group=True)
         K.gemm(dq, w.Wq, dln)
-        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
-        K.gemm(dkv, w.Wkv, dmem, beta=1.0)
+        if own_kv:
+            K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
+            K.gemm(dkv, w.Wkv, dmem, beta=1.0)
         return dln
     dctx4 = _heads(dctx, B, Tq, H, dk)
     if mem is None:
@@ -410,7 +422,8 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
         k4 = _slot(sv.kv, B, Tk, 2, 0, H, dk)
         v4 = _slot(sv.kv, B, Tk, 2, 1, H, dk)
         dq = _e((R, d), adt, dev)
-        dkv = _e((B * Tk, 2 * d), adt, dev)
+        if own_kv:
+            dkv = _e((B * Tk, 2 * d), adt, dev)
         dq4 = _heads(dq, B, Tq, H, dk)
         dk4 = _slot(dkv, B, Tk, 2, 0, H, dk)
         dv4 = _slot(dkv, B, Tk, 2, 1, H, dk)
@@ -429,8 +442,9 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
     else:
         K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq, group=True)
         K.gemm(dq, w.Wq, dln)
-        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
-        K.gemm(dkv, w.Wkv, dmem, beta=1.0)
+        if own_kv:
+            K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
+            K.gemm(dkv, w.Wkv, dmem, beta=1.0)
     return dln
 
 
@@ -784,13 +798,18 @@ def decoder_layers_fwd(dec, wd, y, h, B, L1, T, masks, p, adt, seed_shift=0):
     pd, pff, pat, pca = p
     R = B * L1
     layers_sv = []
+    # every layer's source attention projects the same memory: its keys / values for all
+    # layers are one GEMM against the cross-layer [n_layer * 2d, d] matrix (decoder_kv_groups)
+    kvm = _e((B * T, len(wd.layers) * 2 * wd.d), adt, y.device)
+    K.linear(h, wd.kv_all.W, kvm, bias=wd.kv_all.b)
     for i, lw in enumerate(wd.layers):
         s = dec.dec_layers[i].seed + seed_shift
         l1, _, m1, r1 = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
         y1, sa = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, smask, smsb, smsq, y, pat, _seed(s, 1), pd,
                              _seed(s, 2))
         l2, _, m2, r2 = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
-        y2, ca = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, mmask, T, 0, y1, pca, _seed(s, 3), pd, _seed(s, 4))
+        y2, ca = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, mmask, T, 0, y1, pca, _seed(s, 3), pd, _seed(s, 4),
+                             kv=kvm[:, 2 * wd.d * i: 2 * wd.d * (i + 1)])
         l3, _, m3, r3 = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)
         y3, z, hh = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, pff, _seed(s, 5), y2, 1.0, pd,
                                 _seed(s, 6))
@@ -816,6 +835,7 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
     K.gemm(g_attn, wd.Wout, dyf)
     dy = _e((R, d), F32, dev)
     K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
+    dkvm = _e((B * T, len(wd.layers) * 2 * d), adt, dev)  # the batched memory K/V's gradient
     for i in range(len(wd.layers) - 1, -1, -1):
         lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
         s = dec.dec_layers[i].seed + sv.seed_shift
@@ -831,7 +851,8 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
         gb = _e((R, d), adt, dev)
         K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb, bscale=1.0, bp=pd,
                         bseed=_seed(s, 4))
-        dln = mha_backward(gb, l2, h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, mmask, T, 0, pca, _seed(s, 3), dh)
+        dln = mha_backward(gb, l2, h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, mmask, T, 0, pca, _seed(s, 3), dh,
+                           dkv=dkvm[:, 2 * d * i: 2 * d * (i + 1)])
         dy1 = _e((R, d), F32, dev)
         gb = _e((R, d), adt, dev)
         K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb, bscale=1.0, bp=pd,
@@ -841,6 +862,8 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
         dy0 = _e((R, d), F32, dev)
         K.layernorm_bwd(y0, dln, lw.ln1.g, m1, r1, dy0, lg.ln1.g, lg.ln1.b, dres=dy1)
         dy = dy0
+    K.gemm(dkvm.t(), h, gd.kv_all.W, beta=1.0, split_k=0, rowsum=gd.kv_all.b, group=True)
+    K.gemm(dkvm, wd.kv_all.W, dh, beta=1.0)
     return dy
 
 

@@ -386,10 +386,13 @@ class DecoderLayer(_LayerCommon):
         self.src_attn_norm = LayerNorm(size)
         self.seed = 0
 
-    def flat_groups(self):
+    def flat_groups(self, kv=True):
+        """kv False: the source attention's key/value weights are grouped by the decoder
+        across its layers instead (decoder_kv_groups)."""
         s = self._pfx + ".self_attn."
         c = self._pfx + ".src_attn."
-        return [[s + n for n in QKV_W], [s + n for n in QKV_B], [c + n for n in KV_W], [c + n for n in KV_B]]
+        g = [[s + n for n in QKV_W], [s + n for n in QKV_B]]
+        return g + [[c + n for n in KV_W], [c + n for n in KV_B]] if kv else g
 
     def _w_all(self, grad):
         d = self.size
@@ -466,6 +469,30 @@ class TransformerEncoder(_Bound):
         return SimpleNamespace(g=self._g("after_norm.weight"), b=self._g("after_norm.bias"))
 
 
+def decoder_kv_groups(dec):
+    """Flat-store groups of a decoder: each layer's own, plus ALL layers' source-attention
+    linear_k / linear_v weights (and biases) back to back -- one [n_layer * 2d, d] matrix, so
+    the memory's keys/values of every layer are ONE GEMM over the encoder output (the memory
+    is the same for all layers) and their input gradients one K = n_layer * 2d GEMM
+    (nets/functional.py decoder_layers_fwd / _bwd).  Each layer's [2d, d] block stays a
+    contiguous view."""
+    gs = []
+    for layer in dec.dec_layers:
+        gs += layer.flat_groups(kv=False)
+    pf = [layer._pfx + ".src_attn." for layer in dec.dec_layers]
+    return gs + [[p + n for p in pf for n in KV_W], [p + n for p in pf for n in KV_B]]
+
+
+def decoder_kv_all(dec, grad):
+    """The cross-layer source-attention key/value matrix and bias (decoder_kv_groups)."""
+    pf = ["dec_layers.%d.src_attn." % i for i in range(len(dec.dec_layers))]
+    wn = [p + n for p in pf for n in KV_W]
+    bn = [p + n for p in pf for n in KV_B]
+    if grad:
+        return SimpleNamespace(W=dec._gg(wn, dec.h_dim), b=dec._gg(bn))
+    return SimpleNamespace(W=dec._wg(wn, dec.h_dim), b=dec._pg(bn))
+
+
 class TransformerDecoder(_Bound):
     """liteasr/nets/transformer_decoder.py:13-93."""
 
@@ -495,16 +522,21 @@ class TransformerDecoder(_Bound):
     def grads(self):
         return self._cached("g", self._grads)
 
+    def flat_groups(self):
+        return decoder_kv_groups(self)
+
     def _weights(self):
         return SimpleNamespace(d=self.h_dim, H=self.n_head, E=self._p("embed.weight"),
                                pe=self.pe.table(1), layers=[l._w_all(False) for l in self.dec_layers],
                                ln_f=SimpleNamespace(g=self._p("after_norm.weight"), b=self._p("after_norm.bias")),
-                               Wout=self._w("linear_out.weight"), bout=self._p("linear_out.bias"))
+                               Wout=self._w("linear_out.weight"), bout=self._p("linear_out.bias"),
+                               kv_all=decoder_kv_all(self, False))
 
     def _grads(self):
         return SimpleNamespace(E=self._g("embed.weight"), layers=[l._w_all(True) for l in self.dec_layers],
                                ln_f=SimpleNamespace(g=self._g("after_norm.weight"), b=self._g("after_norm.bias")),
-                               Wout=self._g("linear_out.weight"), bout=self._g("linear_out.bias"))
+                               Wout=self._g("linear_out.weight"), bout=self._g("linear_out.bias"),
+                               kv_all=decoder_kv_all(self, True))
 
 
 class CTC(_Bound):
@@ -545,17 +577,20 @@ class ParallelDecoder(_Bound):
         self.rates = SimpleNamespace(drop=dropout_rate, self_att=self_attn_dropout_rate, src_att=src_attn_dropout_rate,
                                      ff=ff_dropout_rate)
 
+    def flat_groups(self):
+        return decoder_kv_groups(self)
+
     def weights(self):
         return self._cached("w", lambda: SimpleNamespace(
             d=self.h_dim, H=self.n_head, layers=[l._w_all(False) for l in self.dec_layers],
             ln_f=SimpleNamespace(g=self._p("after_norm.weight"), b=self._p("after_norm.bias")),
-            Wout=self._w("linear_out.weight"), bout=self._p("linear_out.bias")))
+            Wout=self._w("linear_out.weight"), bout=self._p("linear_out.bias"), kv_all=decoder_kv_all(self, False)))
 
     def grads(self):
         return self._cached("g", lambda: SimpleNamespace(
             layers=[l._w_all(True) for l in self.dec_layers],
             ln_f=SimpleNamespace(g=self._g("after_norm.weight"), b=self._g("after_norm.bias")),
-            Wout=self._g("linear_out.weight"), bout=self._g("linear_out.bias")))
+            Wout=self._g("linear_out.weight"), bout=self._g("linear_out.bias"), kv_all=decoder_kv_all(self, True)))
 
 
 class Predictor(_Bound):
