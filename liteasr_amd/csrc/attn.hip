@@ -127,12 +127,13 @@ __global__ __launch_bounds__(256) void attn_softmax_fwd_kernel(
   const float inv = 1.f / wave_sum(sum);
   TP* pr = P + row * ldS;
   TP* prr = Praw ? Praw + row * ldS : nullptr;
+  const uint32_t key = drop_key_if(d);
 #pragma unroll
   for (int k = 0; k < SM_MAXC; ++k) {
     const int j = lane + 64 * k;
     if (j < Tk) {
       const float p = v[k] * inv;
-      pr[j] = from_f<TP>(p * drop_mul(d, (uint64_t)row * Tk + j));
+      pr[j] = from_f<TP>(p * drop_mul_if(d, key, (uint64_t)row * Tk + j));
       if (prr) prr[j] = from_f<TP>(p);
     } else if (j < ldS) {
       pr[j] = from_f<TP>(0.f);
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(
   const float* gr = dPd + row * ldS;
   float p[SM_MAXC], g[SM_MAXC];
   float s = 0.f;
+  const uint32_t key = drop_key_if(d);
 #pragma unroll
   for (int k = 0; k < SM_MAXC; ++k) {
     const int j = lane + 64 * k;
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(
     g[k] = 0.f;
     if (j < Tk) {
       p[k] = to_f(pr[j]);
-      g[k] = gr[j] * drop_mul(d, (uint64_t)row * Tk + j);
+      g[k] = gr[j] * drop_mul_if(d, key, (uint64_t)row * Tk + j);
       s += p[k] * g[k];
     }
   }

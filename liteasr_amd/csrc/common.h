@@ -237,7 +237,13 @@ LASR_DEV void drop_mul_n(const DropCfg& d, uint32_t key, uint64_t idx0, float* m
 #pragma unroll
   for (int q = 0; q < N; ++q) m[q] *= d.scale;
 }
-// Multiplier for element idx; 1 when dropout is off.
+// Key / multiplier pair for loops: take the key once before the loop (drop_key reads the
+// device step counter; inside a loop with stores that load is re-issued every iteration).
+LASR_DEV uint32_t drop_key_if(const DropCfg& d) { return d.p > 0.f ? drop_key(d) : 0u; }
+LASR_DEV float drop_mul_if(const DropCfg& d, uint32_t key, uint64_t idx) {
+  return d.p > 0.f ? drop_mul_k(d, key, idx) : 1.f;
+}
+// Multiplier for element idx; 1 when dropout is off (one element: loops use the pair above).
 LASR_DEV float drop_mul(const DropCfg& d, uint64_t idx) {
   if (d.p <= 0.f) return 1.f;
   return drop_mul_k(d, drop_key(d), idx);

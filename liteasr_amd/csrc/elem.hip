@@ -25,12 +25,13 @@ template <typename TX, typename TY>
 __global__ void pe_fwd_kernel(const TX* x, int64_t rows, int T, int D, const float* pe,
                               float xscale, DropCfg d, TY* y) {
   const int64_t n = rows * D;
+  const uint32_t key = drop_key_if(d);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = e / D;
     const int c = (int)(e - r * D);
     float v = x ? to_f(x[e]) * xscale : 0.f;
     if (pe) v += pe[(r % T) * D + c];
-    y[e] = from_f<TY>(v * drop_mul(d, (uint64_t)e));
+    y[e] = from_f<TY>(v * drop_mul_if(d, key, (uint64_t)e));
   }
 }
 
@@ -38,10 +39,11 @@ template <typename TY>
 __global__ void embed_pe_fwd_kernel(const int32_t* ids, int R, int L, int D, const float* E,
                                     const float* pe, float xscale, DropCfg d, TY* y) {
   const int64_t n = (int64_t)R * D;
+  const uint32_t key = drop_key_if(d);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(e / D), c = (int)(e - (int64_t)r * D);
     const float v = E[(int64_t)ids[r] * D + c] * xscale + (pe ? pe[(int64_t)(r % L) * D + c] : 0.f);
-    y[e] = from_f<TY>(v * drop_mul(d, (uint64_t)e));
+    y[e] = from_f<TY>(v * drop_mul_if(d, key, (uint64_t)e));
   }
 }
 

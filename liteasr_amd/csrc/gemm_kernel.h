@@ -78,11 +78,14 @@ LASR_DEV float load_any(const void* p, int dt, int64_t i) {
 // the zout values; auxv / resv are the loaded aux / res values (nullable).  Every mode
 // switch is a wave-uniform branch around its own loop (a per-element select would make
 // the compiler evaluate every activation and its derivative for every element).
+// dkey = epi_key(p), computed ONCE per thread before the output loops: drop_key reads the
+// device step counter, and a load inside the loop is re-issued and waited for on every
+// iteration (the stores in between may alias it).
 template <int N, typename ZST>
-LASR_DEV void epi_core(const GemmP& p, uint64_t dbase, float (&v)[N], const float (&auxv)[N], bool has_aux,
-                       const float (&resv)[N], bool has_res, ZST zst) {
+LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)[N], const float (&auxv)[N],
+                       bool has_aux, const float (&resv)[N], bool has_res, ZST zst) {
   const bool drop = p.drop.p > 0.f;
-  const uint32_t km = drop ? drop_keep_mask<N>(p.drop, drop_key(p.drop), dbase) : 0u;
+  const uint32_t km = drop ? drop_keep_mask<N>(p.drop, dkey, dbase) : 0u;
   bool acted = false;  // activation already applied (the gate shares the sigmoid)
   if (p.zout) {
     if (p.zout_mode == 1) {
@@ -154,9 +157,12 @@ LASR_DEV void epi_core(const GemmP& p, uint64_t dbase, float (&v)[N], const floa
   }
 }
 
+// Dropout key of a GEMM epilogue (0 without dropout).
+LASR_DEV uint32_t epi_key(const GemmP& p) { return p.drop.p > 0.f ? drop_key(p.drop) : 0u; }
+
 // Full epilogue for one output element.
 template <typename TC>
-LASR_DEV void epi_store(const GemmP& p, int z1, int z2, int z, int m, int n, float acc,
+LASR_DEV void epi_store(const GemmP& p, uint32_t dkey, int z1, int z2, int z, int m, int n, float acc,
                         float alpha_eff) {
   if (m >= p.M || n >= p.N) return;
   float v[1] = {acc * alpha_eff};
@@ -165,7 +171,7 @@ LASR_DEV void epi_store(const GemmP& p, int z1, int z2, int z, int m, int n, flo
   float a[1], r[1];
   if (p.aux) a[0] = load_any(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n);
   if (p.res) r[0] = load_any(p.res, p.res_dtype, (int64_t)m * p.ldres + n);
-  epi_core<1>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, a, p.aux != nullptr, r, p.res != nullptr,
+  epi_core<1>(p, dkey, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, a, p.aux != nullptr, r, p.res != nullptr,
               [&](const float (&zv)[1]) { ((TC*)p.zout)[cidx] = from_f<TC>(zv[0]); });
   TC* C = (TC*)p.C;
   if (p.beta != 0.f) v[0] += p.beta * to_f(C[cidx]);
@@ -195,7 +201,7 @@ LASR_DEV void st_8(T* dst, const float* v, bool vec, int cnt) {
 
 // Epilogue for 8 consecutive columns n..n+7 of row m (same order as epi_store).
 template <typename TC>
-LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, const float* acc,
+LASR_DEV void epi_store8(const GemmP& p, uint32_t dkey, int z1, int z2, int z, int m, int n, const float* acc,
                          float alpha_eff) {
   const int cnt = min(8, p.N - n);
   float v[8], t[8];
@@ -209,7 +215,7 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
   float r[8];
   if (p.aux) ld_any8(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, p.aux_vec, cnt, t);
   if (p.res) ld_any8(p.res, p.res_dtype, (int64_t)m * p.ldres + n, p.res_vec, cnt, r);
-  epi_core<8>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
+  epi_core<8>(p, dkey, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
               [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, p.c_vec, cnt); });
   TC* C = (TC*)p.C + cidx;
   if (p.beta != 0.f) {
@@ -223,12 +229,12 @@ LASR_DEV void epi_store8(const GemmP& p, int z1, int z2, int z, int m, int n, co
 // Epilogue modes 0/1: bias already in registers (bv), the one aux/res source prefetched
 // (sv, mode 1 only; N % 8 == 0 there), beta == 0; cnt < 8 only on a ragged last vector.
 template <typename TC>
-LASR_DEV void epi_fast8(const GemmP& p, int64_t cidx, int z, int m, int n, int cnt, const float* acc,
-                        float alpha_eff, const float* bv, const float (&sv)[8]) {
+LASR_DEV void epi_fast8(const GemmP& p, uint32_t dkey, int64_t cidx, int z, int m, int n, int cnt,
+                        const float* acc, float alpha_eff, const float* bv, const float (&sv)[8]) {
   float v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff + bv[q];
-  epi_core<8>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, sv, p.aux != nullptr, sv, p.res != nullptr,
+  epi_core<8>(p, dkey, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, sv, p.aux != nullptr, sv, p.res != nullptr,
               [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, true, cnt); });
   st_8((TC*)p.C + cidx, v, true, cnt);
 }
@@ -272,6 +278,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)]
   float* cs = reinterpret_cast<float*>(smem_epi);
   const int rq = (lane >> 4) * 4, cl = lane & 15;
   const float al = alpha_of(p);
+  const uint32_t dkey = epi_key(p);
   const bool split = p.split_k > 1;
   float* wsp = split ? p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N : nullptr;
   // A thread's 8-column slot is the same in every epilogue iteration (NT % (BN/8) == 0):
@@ -349,7 +356,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)]
             float a8[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + ec8 + q];
-            epi_fast8<TC>(p, crow(m) + en, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
+            epi_fast8<TC>(p, dkey, crow(m) + en, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
           }
         }
       }
@@ -370,7 +377,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)]
           else
             for (int q = 0; q < 8 && n + q < p.N; ++q) dst[q] = a8[q];
         } else {
-          epi_store8<TC>(p, z1, z2, z, m, n, a8, al);
+          epi_store8<TC>(p, dkey, z1, z2, z, m, n, a8, al);
         }
       }
     }
@@ -450,8 +457,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
 // Epilogue of 4 consecutive columns n..n+3 of row m (same order as epi_store8); cnt < 4 or
 // !vec -> element-wise tail.
 template <typename TC, bool VEC>
-LASR_DEV void epi_store4(const GemmP& p, int z1, int z2, int z, int m, int n, int cnt, const float* acc,
-                         float al) {
+LASR_DEV void epi_store4(const GemmP& p, uint32_t dkey, int z1, int z2, int z, int m, int n, int cnt,
+                         const float* acc, float al) {
   float v[4], t[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) v[q] = acc[q] * al;
@@ -485,7 +492,7 @@ LASR_DEV void epi_store4(const GemmP& p, int z1, int z2, int z, int m, int n, in
   float r[4];
   if (p.aux) ld4(p.aux, p.aux_dtype, (int64_t)m * p.ldaux + n, t);
   if (p.res) ld4(p.res, p.res_dtype, (int64_t)m * p.ldres + n, r);
-  epi_core<4>(p, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
+  epi_core<4>(p, dkey, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, t, p.aux != nullptr, r, p.res != nullptr,
               [&](const float (&zv)[4]) { st4((TC*)p.zout + cidx, zv); });
   TC* C = (TC*)p.C + cidx;
   if (p.beta != 0.f) {
@@ -510,6 +517,7 @@ LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wr = wid / WCOLS, wc = wid % WCOLS;
   const float al = alpha_of(p);
+  const uint32_t dkey = epi_key(p);
   const int mr = m0 + wr * WM + (lane & 15), nc = n0 + wc * WN + 4 * (lane >> 4);
   if (p.split_k > 1) {
     float* wsp = p.ws + ((int64_t)s * p.batch + z) * (int64_t)p.M * p.N;
@@ -539,8 +547,8 @@ LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8
       const int n = nc + j * 16;
       if (n >= p.N) continue;
       const float a[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.v4 && n + 4 <= p.N) epi_store4<TC, true>(p, z1, z2, z, m, n, 4, a, al);
-      else epi_store4<TC, false>(p, z1, z2, z, m, n, min(4, p.N - n), a, al);
+      if (p.v4 && n + 4 <= p.N) epi_store4<TC, true>(p, dkey, z1, z2, z, m, n, 4, a, al);
+      else epi_store4<TC, false>(p, dkey, z1, z2, z, m, n, min(4, p.N - n), a, al);
     }
   }
 }
@@ -978,6 +986,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
     return;
   }
   const float al = alpha_of(p);
+  const uint32_t dkey = epi_key(p);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -985,7 +994,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + wr * 32 + i * 16 + rq + e, n = n0 + wc * 32 + j * 16 + cl;
-        epi_store<TC>(p, z1, z2, z, m, n, acc[i][j][e], al);
+        epi_store<TC>(p, dkey, z1, z2, z, m, n, acc[i][j][e], al);
       }
 }
 
@@ -995,6 +1004,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
   const int64_t MN = (int64_t)p.M * p.N;
   const int64_t total = MN * p.batch;
   const float al = alpha_of(p);
+  const uint32_t dkey = epi_key(p);
   if (p.v4) {
     // 4 consecutive columns per thread (N % 4 == 0): 16-B partial loads, 4 slices in
     // flight, summed in slice order
@@ -1021,7 +1031,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
         for (int e = 0; e < 4; ++e) acc[e] += v[e];
       }
       const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
-      epi_store4<TC, true>(p, z / p.batch_div, z % p.batch_div, z, m, n, 4, acc, al);
+      epi_store4<TC, true>(p, dkey, z / p.batch_div, z % p.batch_div, z, m, n, 4, acc, al);
     }
   } else {
     for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -1030,7 +1040,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
       float acc = 0.f;
       for (int s = 0; s < p.split_k; ++s) acc += p.ws[((int64_t)s * p.batch + z) * MN + r];
       const int m = (int)(r / p.N), n = (int)(r - (int64_t)m * p.N);
-      epi_store<TC>(p, z / p.batch_div, z % p.batch_div, z, m, n, acc, al);
+      epi_store<TC>(p, dkey, z / p.batch_div, z % p.batch_div, z, m, n, acc, al);
     }
   }
   if (p.rs_ws) {  // bias-gradient partials (batch == 1)

@@ -303,8 +303,9 @@ extern "C" int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, in
 // ----------------------------- branch grad ----------------------------------------
 template <typename TI, typename TO>
 __global__ void branch_grad_kernel(const TI* dx, int64_t n, TO* gb, float scale, DropCfg d) {
+  const uint32_t key = drop_key_if(d);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    gb[i] = from_f<TO>(scale * drop_mul(d, (uint64_t)i) * to_f(dx[i]));
+    gb[i] = from_f<TO>(scale * drop_mul_if(d, key, (uint64_t)i) * to_f(dx[i]));
 }
 
 extern "C" int lasr_branch_grad(const void* dx, int dx_dtype, int64_t n, void* gb, int gb_dtype,

@@ -19,6 +19,14 @@ from ..utils.param_store import FlatParams
 from . import LiteasrModel
 
 
+def _require_hip(model, xs):
+    """The fused models run on the HIP device only: there is no CPU path (tools/step_census.py,
+    a host-only launch recorder, is the one caller that replaces this check)."""
+    if xs.device.type != "cuda":
+        raise RuntimeError(f"liteasr_amd.{type(model).__name__} runs on the HIP device only (no CPU path); "
+                           "move the model and batch to cuda")
+
+
 class FusedEncoderModel(LiteasrModel):
     """Subclasses build ``self.encoder`` (TransformerEncoder), ``self.decoder`` (with
     ``dec_layers`` and ``rates``), set ``compute_dtype``, ``chunk_size``, ``sos``/``eos``,
@@ -143,9 +151,7 @@ class FusedEncoderModel(LiteasrModel):
     def _run_encoder(self, xs, xlens, ys, ylens):
         """Bookkeeping (_prep) + Conv2DLayer/PE + conformer layers: the encoder residual
         stream x [B*T', d] fp32 (before after_norm), prep and the kernel env."""
-        if xs.device.type != "cuda":
-            raise RuntimeError(f"liteasr_amd.{type(self).__name__} runs on the HIP device only (no CPU path); "
-                               "move the model and batch to cuda")
+        _require_hip(self, xs)
         prep = self._prep(xs, xlens, ys, ylens)
         self.last_prep = prep
         enc, dec = self.encoder, self.decoder
