@@ -18,6 +18,13 @@
 
 // ================================ host launcher ==================================
 int g_stages = 0;  // lasr_gemm_force_split (tuning hook)
+// Ring depth of the 64 x 64 tiles with 64-deep stages (LASR_KS2_STAGES, read once at load;
+// 3 or 4): S - 1 stages in flight per workgroup.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && v[0] ? atoi(v) : dflt;
+}
+int g_ks2_stages = env_int("LASR_KS2_STAGES", 3);
 
 // bf16 launch table: gemm_launch.h, instantiated per operand layout in gemm_l{0..3}.hip
 template <bool AKC, bool BKC, typename TC>

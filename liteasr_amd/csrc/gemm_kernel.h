@@ -1054,5 +1054,5 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
 
 
 // host-side tuning state shared by the two launch units (gemm.hip defines it)
-extern int g_stages, g_tile_m, g_tile_n, g_split;
+extern int g_stages, g_tile_m, g_tile_n, g_split, g_ks2_stages;
 static inline bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }

@@ -26,6 +26,7 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
     else if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 2, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 3, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 3, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
+    else if (g_ks2_stages == 4) gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     return;
   }

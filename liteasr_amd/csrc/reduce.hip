@@ -1,12 +1,36 @@
 // Deterministic reduction of per-block partial sums: out[n] (+)= sum_p part[p*N + n].
 // 256-thread blocks cover 16 columns x 16 partial-groups (coalesced 64-B reads per
-// group row); each thread sums its strided partials, then a fixed-order LDS combine.
+// group row); each thread sums its strided partials (cols_psum), then a fixed-order LDS
+// combine.
 // Used by every "partials -> parameter gradient" epilogue (LayerNorm, bias colsums,
 // BatchNorm, depthwise conv, conv1, positional biases).
 #include "common.h"
 
 constexpr int RC_COLS = 16;
 constexpr int RC_GROUPS = 16;
+constexpr int RC_ACC = 8;
+
+// Column n's partials p = ty, ty + 16, ... summed into RC_ACC accumulators (accumulator k takes
+// every RC_ACC-th of them), combined by a fixed pairwise tree.  Every iteration issues its
+// RC_ACC loads together (out-of-range ones read nothing): with P = 498 (a LayerNorm's
+// 16-row blocks over B*T' = 7968 rows) a thread waits for 4 rounds of loads, not 31 serial
+// ones -- these reductions are latency-bound, the bytes are few.
+LASR_DEV float cols_psum(const float* __restrict__ part, int P, int64_t N, int64_t n, int ty) {
+  float s[RC_ACC];
+#pragma unroll
+  for (int k = 0; k < RC_ACC; ++k) s[k] = 0.f;
+  for (int p = ty; p < P; p += RC_ACC * RC_GROUPS) {
+    float v[RC_ACC];
+#pragma unroll
+    for (int k = 0; k < RC_ACC; ++k) {
+      const int q = p + k * RC_GROUPS;
+      v[k] = q < P ? part[(int64_t)q * N + n] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < RC_ACC; ++k) s[k] += v[k];
+  }
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
 
 __global__ __launch_bounds__(256) void reduce_cols_kernel(const float* __restrict__ part, int P,
                                                           int64_t N, float* out0, float* out1,
@@ -14,19 +38,7 @@ __global__ __launch_bounds__(256) void reduce_cols_kernel(const float* __restric
   __shared__ float sh[RC_GROUPS][RC_COLS + 1];
   const int tx = threadIdx.x & (RC_COLS - 1), ty = threadIdx.x / RC_COLS;
   const int64_t n = (int64_t)blockIdx.x * RC_COLS + tx;
-  // 4 independent accumulators (4 loads in flight per thread), combined in fixed order
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (n < N) {
-    int p = ty;
-    for (; p + 3 * RC_GROUPS < P; p += 4 * RC_GROUPS) {
-      s0 += part[(int64_t)p * N + n];
-      s1 += part[(int64_t)(p + RC_GROUPS) * N + n];
-      s2 += part[(int64_t)(p + 2 * RC_GROUPS) * N + n];
-      s3 += part[(int64_t)(p + 3 * RC_GROUPS) * N + n];
-    }
-    for (; p < P; p += RC_GROUPS) s0 += part[(int64_t)p * N + n];
-  }
-  sh[ty][tx] = (s0 + s1) + (s2 + s3);
+  sh[ty][tx] = n < N ? cols_psum(part, P, N, n, ty) : 0.f;
   __syncthreads();
   if (ty == 0 && n < N) {
     float t = 0.f;
@@ -54,6 +66,7 @@ int lasr_reduce_cols(const float* part, int P, int64_t N, float* out0, float* ou
 //   mode 1 (few partials, P <= 64): 4 columns per thread, partials summed in order 0..P-1
 //                                   (splitk_reduce_kernel's order)
 constexpr int RM_MAXSEG = 32;
+constexpr int RM_VEC = 2;  // mode 1: 4-column runs per thread
 struct RSeg {
   const float* part;
   float* out0;
@@ -74,55 +87,67 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(RSegs a) {
   const RSeg& g = a.s[si];
   const int b = blockIdx.x - g.blk0;
   if (g.mode == 1) {
-    const int64_t n = ((int64_t)b * 256 + threadIdx.x) * 4;
-    if (n >= g.N) return;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const float* src = g.part + n;
+    // RM_VEC runs of 4 columns per thread, 1024 columns apart (coalesced per run); every
+    // load -- the output's old value for the RMW included -- is issued before the first add,
+    // so a thread waits for one round of loads, not two
+    float acc[RM_VEC][4], c[RM_VEC][4];
+    float* o4[RM_VEC];
+    int64_t n[RM_VEC];
+#pragma unroll
+    for (int j = 0; j < RM_VEC; ++j) {
+      n[j] = ((int64_t)b * 256 * RM_VEC + j * 256 + threadIdx.x) * 4;
+      o4[j] = n[j] + 4 <= g.split ? g.out0 + n[j] : (n[j] >= g.split ? g.out1 + (n[j] - g.split) : nullptr);
+      if (o4[j] && ((uintptr_t)o4[j] & 15) != 0) o4[j] = nullptr;  // unaligned run: element-wise below
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[j][q] = c[j][q] = 0.f;
+      if (n[j] < g.N && o4[j] && g.accumulate) {
+        const float4 v = *(const float4*)o4[j];
+        c[j][0] = v.x; c[j][1] = v.y; c[j][2] = v.z; c[j][3] = v.w;
+      }
+    }
     int p = 0;
     for (; p + 4 <= g.P; p += 4) {
-      float4 v[4];
+      float4 v[RM_VEC][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(src + (int64_t)(p + u) * g.N);
+      for (int j = 0; j < RM_VEC; ++j)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc[0] += v[u].x; acc[1] += v[u].y; acc[2] += v[u].z; acc[3] += v[u].w;
-      }
+        for (int u = 0; u < 4; ++u)
+          v[j][u] = n[j] < g.N ? *(const float4*)(g.part + n[j] + (int64_t)(p + u) * g.N) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < RM_VEC; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc[j][0] += v[j][u].x; acc[j][1] += v[j][u].y; acc[j][2] += v[j][u].z; acc[j][3] += v[j][u].w;
+        }
     }
     for (; p < g.P; ++p) {
-      const float4 v = *(const float4*)(src + (int64_t)p * g.N);
-      acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
-    }
-    float* o4 = n + 4 <= g.split ? g.out0 + n : (n >= g.split ? g.out1 + (n - g.split) : nullptr);
-    if (o4 && ((uintptr_t)o4 & 15) == 0) {  // the 4 columns in one aligned output run: 16-B RMW
-      float4 r = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      if (g.accumulate) {
-        const float4 c = *(const float4*)o4;
-        r = make_float4(c.x + acc[0], c.y + acc[1], c.z + acc[2], c.w + acc[3]);
+#pragma unroll
+      for (int j = 0; j < RM_VEC; ++j) {
+        if (n[j] >= g.N) continue;
+        const float4 v = *(const float4*)(g.part + n[j] + (int64_t)p * g.N);
+        acc[j][0] += v.x; acc[j][1] += v.y; acc[j][2] += v.z; acc[j][3] += v.w;
       }
-      *(float4*)o4 = r;
-      return;
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float* o = n + q < g.split ? g.out0 + n + q : g.out1 + (n + q - g.split);
-      *o = g.accumulate ? *o + acc[q] : acc[q];
+    for (int j = 0; j < RM_VEC; ++j) {
+      if (n[j] >= g.N) continue;
+      if (o4[j]) {  // the 4 columns in one aligned output run: 16-B RMW
+        *(float4*)o4[j] = g.accumulate ? make_float4(c[j][0] + acc[j][0], c[j][1] + acc[j][1], c[j][2] + acc[j][2],
+                                                      c[j][3] + acc[j][3])
+                                       : make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+        continue;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float* o = n[j] + q < g.split ? g.out0 + n[j] + q : g.out1 + (n[j] + q - g.split);
+        *o = g.accumulate ? *o + acc[j][q] : acc[j][q];
+      }
     }
     return;
   }
   const int tx = threadIdx.x & (RC_COLS - 1), ty = threadIdx.x / RC_COLS;
   const int64_t n = (int64_t)b * RC_COLS + tx;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (n < g.N) {
-    int p = ty;
-    for (; p + 3 * RC_GROUPS < g.P; p += 4 * RC_GROUPS) {
-      s0 += g.part[(int64_t)p * g.N + n];
-      s1 += g.part[(int64_t)(p + RC_GROUPS) * g.N + n];
-      s2 += g.part[(int64_t)(p + 2 * RC_GROUPS) * g.N + n];
-      s3 += g.part[(int64_t)(p + 3 * RC_GROUPS) * g.N + n];
-    }
-    for (; p < g.P; p += RC_GROUPS) s0 += g.part[(int64_t)p * g.N + n];
-  }
-  sh[ty][tx] = (s0 + s1) + (s2 + s3);
+  sh[ty][tx] = n < g.N ? cols_psum(g.part, g.P, g.N, n, ty) : 0.f;
   __syncthreads();
   if (ty == 0 && n < g.N) {
     float t = 0.f;
@@ -148,7 +173,7 @@ extern "C" int lasr_reduce_multi(const lasr_reduce_seg* segs, int nseg, void* st
       RSeg& g = a.s[a.nseg++];
       g.part = q.part; g.out0 = q.out0; g.out1 = q.out1; g.N = q.N; g.split = split;
       g.P = q.P; g.accumulate = q.accumulate; g.mode = vec ? 1 : 0; g.blk0 = nblk;
-      const int64_t nb = vec ? cdiv(q.N / 4, 256) : cdiv(q.N, RC_COLS);
+      const int64_t nb = vec ? cdiv(q.N / 4, 256 * RM_VEC) : cdiv(q.N, RC_COLS);
       LASR_CHECK_ARG(nblk + nb < (1ll << 31), "lasr_reduce_multi: too many blocks");
       nblk += (int)nb;
     }

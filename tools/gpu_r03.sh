@@ -37,6 +37,7 @@ for s in $STEPS; do
            grep "^{" "$OUT/pmc_fetch_$c.log" | tail -1 > "$OUT/roofline_meta_$c.json"
            run python3 "$R/tools/pmc_traffic.py" "$(find "$OUT/pmc_fetch_$c" -name '*.db' | head -1)" "$(find "$OUT/pmc_write_$c" -name '*.db' | head -1)" "$OUT/roofline_meta_$c.json" "$OUT/roofline_pmc_$c.json"
          done ;;
+    pmcsave) for c in family dw hot; do cp "$OUT/roofline_pmc_$c.json" "$R/profiles/r03/roofline_pmc_${c}_$TAG.json" || exit 1; done ;;
     mfma) cd /tmp && run timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- python3 "$R/bench.py" --graph off --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > "$OUT/pmc_mfma.log" 2>&1
           run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mfma" -name '*counter_collection.csv' | head -1)" > "$OUT/pmc_mfma_summary.json" ;;
     tracelong) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_long" -o run -- python3 "$R/bench.py" --config long --no-cpu-baseline --steps 10 --warmup 3 > "$OUT/trace_long.log" 2>&1
