@@ -34,6 +34,40 @@ static GemmP conv_params(const lasr_conv2_args* a) {
 // 128 x 256 tiles: their 8-wave variants (256 x 256 with 64- or 32-deep stages, 256 x 128)
 // took 265-299 / 523-529 us against 262 / 468 (their 592-tile grids run 2.3 rounds of one
 // workgroup per CU).  LASR_CONV_WIDE=0 keeps the 4-wave weight gradient (A/B).
+// The data gradient's four output parity classes in ONE launch: class i owns the blocks
+// [start[i], start[i+1]) (starts multiples of 8: the XCD remap stays exact inside a class),
+// heaviest class (4 taps) first.  One launch of ~4.9k workgroups instead of four of ~1.2k
+// (each 2.3-2.4 rounds of the 512 resident workgroups, so every class paid its own
+// partially filled last round).  Same tiles, same k order per output: bit-identical to the
+// per-class launches.  LASR_DX_MERGED=0 launches per class (A/B).
+struct DxClasses {
+  int start[5];
+  int M[4], K[4];
+};
+
+template <int BN>
+__global__ __launch_bounds__(256, 2) void conv2_dx_kernel(GemmP p, DxClasses c) {
+  const int blk = blockIdx.x;
+  int i = 0;
+  for (int j = 1; j < 4; ++j)
+    if (blk >= c.start[j]) i = j;
+  GemmP q = p;
+  q.cv.cls = i;
+  q.M = c.M[i];
+  q.K = c.K[i];
+  q.kchunk = c.K[i];
+  const int ntx = p.N / BN, nty = (q.M + 127) / 128, ntile = ntx * nty;
+  const int local = blk - c.start[i];
+  if (local >= ntile) return;  // alignment padding
+  const int wg = xcd_remap(local, ntile);
+  gemm_glds_tile<128, BN, true, false, bf16_t, 3, G_DX, 1, 4>(q, wg % ntx, wg / ntx, 0);
+}
+
+static int env_flag_dflt(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && e[0] ? atoi(e) : dflt;
+}
+
 static int conv_wide() {
   static int v = -1;
   if (v < 0) {
@@ -73,6 +107,7 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     p.C = a->out; p.ldc = C;
     p.bias = a->bias; p.bias_vec = 1; p.act = LASR_ACT_RELU;
     p.epi_mode = 0;
+    // (64 x 256 tiles, 2366 of them: 355 vs 279 us, profiles/r03/conv2_dx_ab.json)
     dim3 grid((unsigned)(C / BN), (unsigned)cdiv(p.M, 128), 1);
     LASR_CHECK_ARG(grid.y <= 65535, "lasr_conv2_gemm: grid too large");
     if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, true, bf16_t, 3, 2, G_FWD><<<grid, 256, 0, st>>>(p);
@@ -127,6 +162,24 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   p.aux = a->y1; p.aux_dtype = LASR_BF16; p.ldaux = C; p.aux_act = LASR_ACT_RELU; p.aux_vec = 1;
   p.epi_mode = 1;
   p.cv.zero = (const bf16_t*)a->dy2 + (int64_t)g.M2 * C;
+  static const int rowtab = env_flag_dflt("LASR_DX_ROWTAB", 1), merged = env_flag_dflt("LASR_DX_MERGED", 1);
+  p.cv.rowtab = rowtab;
+  if (merged) {
+    DxClasses dc = {};
+    int nb = 0;
+    for (int cls = 0; cls < 4; ++cls) {
+      const int pt = cls >> 1, pf = cls & 1;
+      const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
+      dc.M[cls] = g.B * nI * nJ;
+      dc.K[cls] = (pt ? 1 : 2) * (pf ? 1 : 2) * C;
+      dc.start[cls] = nb;
+      nb += (int)(cdiv(cdiv(dc.M[cls], 128) * (C / BN), 8) * 8);
+    }
+    dc.start[4] = nb;
+    if (BN == 256) conv2_dx_kernel<256><<<nb, 256, 0, st>>>(p, dc);
+    else conv2_dx_kernel<128><<<nb, 256, 0, st>>>(p, dc);
+    return lasr_check_launch("lasr_conv2_gemm/dx");
+  }
   for (int cls = 0; cls < 4; ++cls) {
     const int pt = cls >> 1, pf = cls & 1;
     const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;

@@ -23,6 +23,7 @@ struct ConvG {
   int cls;              // G_DX: output parity class (t1 & 1) * 2 + (f1 & 1)
   int q32, r32;         // G_DW: 32 = q32 * F2 + r32 (row-walk increments)
   const bf16_t* zero;   // G_DX: >= 32 zero bf16 (taps that fall outside dy2)
+  int rowtab;           // G_DX: epilogue rows from the per-tile table (A/B switch)
 };
 typedef ConvG ConvGeom;
 enum { G_LIN = 0, G_FWD = 1, G_DW = 2, G_DX = 3 };
@@ -260,13 +261,16 @@ LASR_DEV int64_t dx_row(const ConvG& g, int m) {
   return ((int64_t)(b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf) * g.C;
 }
 
+// dxrow (G_DX only): the tile's BM row offsets dx_row(m0 + r), computed once per tile (two
+// integer divisions and two remainders each; per output vector they cost more VALU than the
+// epilogue arithmetic).
 template <int BM, int BN, typename TC, bool TRANS = false, int G = G_LIN, int NW = 4>
 LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)], char* smem_epi, int m0,
-                            int n0, int s, int z, int z1, int z2) {
+                            int n0, int s, int z, int z1, int z2, const int64_t* dxrow = nullptr) {
   // output-row offsets: linear (ldc, ld of the aux/res source), or the transposed-conv scatter
   // of a G_DX launch (aux = y1 shares dy1's layout)
   auto crow = [&](int m) -> int64_t {
-    if constexpr (G == G_DX) return dx_row(p.cv, m);
+    if constexpr (G == G_DX) return p.cv.rowtab ? dxrow[m - m0] : dx_row(p.cv, m);
     else return (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc;
   };
   // NW waves as 2 (rows) x NW/2 (columns); NT threads finish the staged rows
@@ -313,14 +317,14 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)]
 #pragma unroll
         for (int it = 0; it < PF; ++it) {
           const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          const int64_t ro = G == G_DX ? dx_row(p.cv, m) : (int64_t)m * src_ld;
+          const int64_t ro = G == G_DX ? (p.cv.rowtab ? dxrow[m - m0] : dx_row(p.cv, m)) : (int64_t)m * src_ld;
           ld8((const float*)src + ro + nc, sv[it]);
         }
       } else {
 #pragma unroll
         for (int it = 0; it < PF; ++it) {
           const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          const int64_t ro = G == G_DX ? dx_row(p.cv, m) : (int64_t)m * src_ld;
+          const int64_t ro = G == G_DX ? (p.cv.rowtab ? dxrow[m - m0] : dx_row(p.cv, m)) : (int64_t)m * src_ld;
           ld8((const bf16_t*)src + ro + nc, sv[it]);
         }
       }
@@ -712,6 +716,10 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   [[maybe_unused]] ConvRowsDW<BN, NT> gb;
   if constexpr (G == G_FWD) ga.init_fwd(p.cv, m0, p.M, tid);
   if constexpr (G == G_DX) ga.init_dx(p.cv, m0, p.M, tid);
+  // the epilogue's scatter rows (read after the main loop's barriers); rows past M clamped
+  [[maybe_unused]] __shared__ int64_t dxrow[G == G_DX ? BM : 1];
+  if constexpr (G == G_DX)
+    for (int r = tid; r < BM; r += NT) dxrow[r] = dx_row(p.cv, min(m0 + r, p.M - 1));
   if constexpr (G == G_DW) gb.init(p.cv, n0, p.N, kbeg, tid);
   // one 32-deep sub-tile at k0 into dst (the conv walkers keep per-position state: sub-tiles
   // are issued in k order)
@@ -853,7 +861,7 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   // split-K partials: fp32, 16-B per lane straight from the accumulators; final outputs:
   // staged through LDS (full 256-B rows per wave store)
   if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC, NW>(p, acc, m0, n0, s, z, z1, z2);
-  else gemm_epilogue<BM, BN, TC, true, G, NW>(p, acc, smem_epi, m0, n0, s, z, z1, z2);
+  else gemm_epilogue<BM, BN, TC, true, G, NW>(p, acc, smem_epi, m0, n0, s, z, z1, z2, dxrow);
 }
 
 // Tile order of a weight-gradient GEMM (both operands [K, M] / [K, N] with K = rows): the

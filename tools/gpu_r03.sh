@@ -15,6 +15,8 @@ for s in $STEPS; do
     tests) cd "$R" && run timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/tests.log" 2>&1 ;;
     testsall) cd "$R" && timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > "$OUT/tests.log" 2>&1; echo "=== rc=$?" >&2 ;;
     rowln_ab) cd "$R" && for v in 0 1; do LASR_ROW_LN=$v timeout -k 10 200 python -u -m pytest tests/test_model_gpu.py -m gpu -q --timeout 150 --timeout-method thread -k "large_width_chunk_bf16_emulated or config2_full_model_bf16_emulated" -s > "$OUT/rowln_ab_$v.log" 2>&1 || true; done ;;
+    convdx) cd "$R" && for v in ${AB_VALUES:-0 1 0 1}; do env ${AB_VAR:-LASR_DX_ROWTAB}=$v timeout -k 10 120 python3 tools/conv2_bench.py >> "$OUT/conv2_dx_ab.json" 2>> "$OUT/conv2_bench.err" || exit 1; done ;;
+    convdx_old) cd "$R" && for v in 0 1 0 1; do LASR_DX_ROWTAB=$v run timeout -k 10 120 python3 tools/conv2_bench.py >> "$OUT/conv2_dx_ab.json" 2>> "$OUT/conv2_bench.err"; done ;;
     conv) cd "$R" && for v in ${CONV_VARIANTS:-0 1}; do LASR_CONV_WIDE=$v run timeout -k 10 120 python3 tools/conv2_bench.py >> "$OUT/conv2_bench.json" 2>> "$OUT/conv2_bench.err"; done
           run timeout -k 10 60 python3 -c "import torch; a=torch.load('/tmp/conv2_dw_0.pt'); b=torch.load('/tmp/conv2_dw_1.pt'); print('dw rel', ((a['dw']-b['dw']).abs().max()/a['dw'].abs().max()).item(), 'db rel', ((a['db']-b['db']).abs().max()/a['db'].abs().max()).item())" >> "$OUT/conv2_bench.json" ;;
     benchab) cd "$R" && for v in ${WIDE_VARIANTS:-0 1}; do LASR_GEMM_WIDE=$v run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/bench_wide$v.json" 2> "$OUT/bench_wide$v.err"; done ;;
