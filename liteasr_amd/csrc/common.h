@@ -17,6 +17,14 @@ LASR_DEV bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// Two floats -> one dword of two bf16 (low = a), one v_cvt_pk_bf16_f32 (RNE, as f2bf): packing
+// two f2bf results with shifts / ors made the compiler convert, split and re-merge halves.
+typedef float lasr_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 lasr_bf2 __attribute__((ext_vector_type(2)));
+LASR_DEV uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((lasr_f2){a, b}, lasr_bf2));
+}
+
 LASR_DEV float to_f(float x) { return x; }
 LASR_DEV float to_f(bf16_t x) { return bf2f(x); }
 template <typename T> LASR_DEV T from_f(float x);
@@ -47,7 +55,7 @@ LASR_DEV void st8(float* p, const float v[8]) {
 LASR_DEV void st8(bf16_t* p, const float v[8]) {
   uint32_t w[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  for (int i = 0; i < 4; ++i) w[i] = pk_bf16(v[2 * i], v[2 * i + 1]);
   *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -91,10 +99,9 @@ LASR_DEV void stv(float* p, const float* v) {
 template <int N>
 LASR_DEV void stv(bf16_t* p, const float* v) {
   if constexpr (N == 1) p[0] = f2bf(v[0]);
-  else if constexpr (N == 2) *(uint32_t*)p = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  else if constexpr (N == 2) *(uint32_t*)p = pk_bf16(v[0], v[1]);
   else if constexpr (N == 4)
-    *(uint2*)p = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                            (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    *(uint2*)p = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
   else {
 #pragma unroll
     for (int j = 0; j < N; j += 8) st8(p + j, v + j);

@@ -205,8 +205,8 @@ LASR_DEV v2i ds_r64_asm(const bf16_t* p) {
 }
 LASR_DEV v2i pack4_bf16(const float* v) {
   v2i r;
-  r[0] = (int)((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16));
-  r[1] = (int)((uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  r[0] = (int)pk_bf16(v[0], v[1]);
+  r[1] = (int)pk_bf16(v[2], v[3]);
   return r;
 }
 

@@ -15,6 +15,9 @@ for s in $STEPS; do
     tests) cd "$R" && run timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/tests.log" 2>&1 ;;
     testsall) cd "$R" && timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > "$OUT/tests.log" 2>&1; echo "=== rc=$?" >&2 ;;
     rowln_ab) cd "$R" && for v in 0 1; do LASR_ROW_LN=$v timeout -k 10 200 python -u -m pytest tests/test_model_gpu.py -m gpu -q --timeout 150 --timeout-method thread -k "large_width_chunk_bf16_emulated or config2_full_model_bf16_emulated" -s > "$OUT/rowln_ab_$v.log" 2>&1 || true; done ;;
+    libab) cd "$R" && for v in base new base new; do lib=liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=liteasr_amd/lib/ab/libliteasr_hip_base.so
+             LITEASR_HIP_LIB=$R/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/bench_lib_$v.json" 2> "$OUT/bench_lib_$v.err" || exit 1
+             grep "^{" "$OUT/bench_lib_$v.json" >> "$OUT/libab.jsonl"; done ;;
     convdx) cd "$R" && for v in ${AB_VALUES:-0 1 0 1}; do env ${AB_VAR:-LASR_DX_ROWTAB}=$v timeout -k 10 120 python3 tools/conv2_bench.py >> "$OUT/conv2_dx_ab.json" 2>> "$OUT/conv2_bench.err" || exit 1; done ;;
     convdx_old) cd "$R" && for v in 0 1 0 1; do LASR_DX_ROWTAB=$v run timeout -k 10 120 python3 tools/conv2_bench.py >> "$OUT/conv2_dx_ab.json" 2>> "$OUT/conv2_bench.err"; done ;;
     conv) cd "$R" && for v in ${CONV_VARIANTS:-0 1}; do LASR_CONV_WIDE=$v run timeout -k 10 120 python3 tools/conv2_bench.py >> "$OUT/conv2_bench.json" 2>> "$OUT/conv2_bench.err"; done
