@@ -41,10 +41,12 @@ for s in $STEPS; do
            run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$c" -o run -- python3 "$R/bench.py" --roofline-only 20 --roofline-case $c > "$OUT/pmc_write_$c.log" 2>&1
            grep "^{" "$OUT/pmc_fetch_$c.log" | tail -1 > "$OUT/roofline_meta_$c.json"
            run python3 "$R/tools/pmc_traffic.py" "$(find "$OUT/pmc_fetch_$c" -name '*.db' | head -1)" "$(find "$OUT/pmc_write_$c" -name '*.db' | head -1)" "$OUT/roofline_meta_$c.json" "$OUT/roofline_pmc_$c.json"
+           rm -rf "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c"  # counter databases: gpurun_out stays under its cap
          done ;;
     pmcsave) for c in family dw hot; do cp "$OUT/roofline_pmc_$c.json" "$R/profiles/r03/roofline_pmc_${c}_$TAG.json" || exit 1; done ;;
     mfma) cd /tmp && run timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- python3 "$R/bench.py" --graph off --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > "$OUT/pmc_mfma.log" 2>&1
-          run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mfma" -name '*counter_collection.csv' | head -1)" > "$OUT/pmc_mfma_summary.json" ;;
+          run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mfma" -name '*counter_collection.csv' | head -1)" > "$OUT/pmc_mfma_summary.json"
+          rm -rf "$OUT/pmc_mfma" ;;
     tracelong) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_long" -o run -- python3 "$R/bench.py" --config long --no-cpu-baseline --steps 10 --warmup 3 > "$OUT/trace_long.log" 2>&1
            db=$(find "$OUT/trace_long" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_long.txt" 2>&1 ;;
     tracefam) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_family" -o run -- python3 "$R/bench.py" --roofline-only 50 --roofline-case family > "$OUT/trace_family.log" 2>&1
