@@ -62,6 +62,8 @@ def ln_forward(x, g, b, adt, y2=False, p2=0.0, seed2=0):
 # it, in one launch, bit-identical to the two launches.  LASR_ROW_LN=0 keeps two launches
 # (benchmark A/B); shapes the kernel does not take (fp32 build, other widths) keep them too.
 ROW_LN = os.environ.get("LASR_ROW_LN", "1") != "0"
+# the decoder's norms after / before its attention projections on the row kernel (A/B switch)
+DEC_ROW_LN = os.environ.get("LASR_DEC_ROW_LN", "1") != "0"
 
 
 class PostLN(SimpleNamespace):
@@ -316,10 +318,11 @@ def _fused_dec(adt, dk, p_att):
     return FUSED_DEC_ATTN and fused_relattn(adt, dk, p_att)
 
 
-def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_res, s_res, kv=None):
+def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_res, s_res, kv=None, post=None):
     """Decoder self (mem None) / source attention (liteasr/nets/attention.py:61-71).  kv: the
     memory's key/value projection [B*Tk, 2d] already computed (decoder_layers_fwd batches it
-    over the layers); None computes it here."""
+    over the layers); None computes it here.  post: the LayerNorm after the residual add, in
+    the output projection's launch when the row kernel takes it (res_proj)."""
     d = ln.shape[1]
     dk = d // H
     dev, adt = ln.device, ln.dtype
@@ -341,8 +344,7 @@ def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_
         stats = _e((B * H * Tq * 2,), F32, dev)
         ctx = _e((R, d), adt, dev)
         K.attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx)
-        out = _e((R, d), F32, dev)
-        K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+        out = res_proj(ctx, w.Wo, w.bo, x_in, 1.0, p_res, s_res, post)
         return out, SimpleNamespace(qkv=qkv, q=q if mem is not None else None, kv=kv, P=None, Praw=None, ctx=ctx,
                                     stats=stats)
     if mem is None:
@@ -370,15 +372,15 @@ def mha_forward(ln, mem, w, B, Tq, Tk, H, mask, msb, msq, x_in, p_att, s_att, p_
     K.attn_softmax_fwd(S, None, B, H, Tq, Tk, ldS, mask, msb, msq, P, p_att, s_att, Praw)
     ctx = _e((R, d), adt, dev)
     K.gemm(P[..., :Tk], v4, _heads(ctx, B, Tq, H, dk))
-    out = _e((R, d), F32, dev)
-    K.linear(ctx, w.Wo, out, bias=w.bo, res=x_in, res_scale=1.0, drop_p=p_res, drop_seed=s_res)
+    out = res_proj(ctx, w.Wo, w.bo, x_in, 1.0, p_res, s_res, post)
     return out, SimpleNamespace(qkv=qkv, q=q, kv=kv, P=P, Praw=Praw, ctx=ctx, stats=None)
 
 
-def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_att, dmem, dkv=None):
+def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_att, dmem, dkv=None, lnb=None):
     """dkv: [B*Tk, 2d] destination of the key/value projection's gradient, whose weight /
     memory gradients the caller then computes (decoder_layers_bwd, batched over the layers);
-    None computes them here (dmem accumulates)."""
+    None computes them here (dmem accumulates).  lnb: the LayerNorm in front of the attention,
+    whose backward the input-gradient GEMM runs (dx_ln; None is returned when it did)."""
     own_kv = dkv is None
     d = ln.shape[1]
     dk = d // H
@@ -391,25 +393,22 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
     K.gemm(gb, w.Wo, dctx)
     if getattr(sv, "stats", None) is not None:  # fused attention (mha_forward)
         Dbuf = _e((B * H * Tq,), F32, dev)
-        dln = _e((R, d), adt, dev)
         if mem is None:
             dqkv = _e((R, 3 * d), adt, dev)
             K.attn_bwd(sv.qkv[:, :d], sv.qkv[:, d:2 * d], sv.qkv[:, 2 * d:], B, H, Tq, Tk, mask, msb, msq, scale,
                        sv.stats, sv.ctx, dctx, Dbuf, dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:])
             K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
-            K.gemm(dqkv, w.Wqkv, dln)
-            return dln
+            return dx_ln(dqkv, w.Wqkv, lnb)
         dq = _e((R, d), adt, dev)
         if own_kv:
             dkv = _e((B * Tk, 2 * d), adt, dev)
         K.attn_bwd(sv.q, sv.kv[:, :d], sv.kv[:, d:], B, H, Tq, Tk, mask, msb, msq, scale, sv.stats, sv.ctx, dctx,
                    Dbuf, dq, dkv[:, :d], dkv[:, d:])
         K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq, group=True)
-        K.gemm(dq, w.Wq, dln)
         if own_kv:
             K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
             K.gemm(dkv, w.Wkv, dmem, beta=1.0)
-        return dln
+        return dx_ln(dq, w.Wq, lnb)
     dctx4 = _heads(dctx, B, Tq, H, dk)
     if mem is None:
         q4 = _slot(sv.qkv, B, Tq, 3, 0, H, dk)
@@ -435,17 +434,14 @@ def mha_backward(gb, ln, mem, sv, w, g, B, Tq, Tk, H, mask, msb, msq, p_att, s_a
                        msq, dS, p_att, s_att)
     K.gemm(dS[..., :Tk], k4, dq4, alpha=scale)
     K.gemm(dS[..., :Tk].transpose(-1, -2), q4, dk4, alpha=scale)
-    dln = _e((R, d), adt, dev)
     if mem is None:
         K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
-        K.gemm(dqkv, w.Wqkv, dln)
-    else:
-        K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq, group=True)
-        K.gemm(dq, w.Wq, dln)
-        if own_kv:
-            K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
-            K.gemm(dkv, w.Wkv, dmem, beta=1.0)
-    return dln
+        return dx_ln(dqkv, w.Wqkv, lnb)
+    K.gemm(dq.t(), ln, g.Wq, beta=1.0, split_k=0, rowsum=g.bq, group=True)
+    if own_kv:
+        K.gemm(dkv.t(), mem, g.Wkv, beta=1.0, split_k=0, rowsum=g.bkv, group=True)
+        K.gemm(dkv, w.Wkv, dmem, beta=1.0)
+    return dx_ln(dq, w.Wq, lnb)
 
 
 # ========================================================= conformer conv =======
@@ -802,15 +798,26 @@ def decoder_layers_fwd(dec, wd, y, h, B, L1, T, masks, p, adt, seed_shift=0):
     # layers are one GEMM against the cross-layer [n_layer * 2d, d] matrix (decoder_kv_groups)
     kvm = _e((B * T, len(wd.layers) * 2 * wd.d), adt, y.device)
     K.linear(h, wd.kv_all.W, kvm, bias=wd.kv_all.b)
+    def post_ln(ln):  # the norm after a residual projection, in its launch (res_proj)
+        return PostLN(g=ln.g, b=ln.b, f32=False, nxt=None) if DEC_ROW_LN else None
+
+    def ln_after(x, post, ln):  # post's outputs, or the norm as its own launch
+        if post is not None and post.y1 is not None:
+            return post.y1, post.m1, post.r1
+        l_, _, m_, r_ = ln_forward(x, ln.g, ln.b, adt)
+        return l_, m_, r_
+
     for i, lw in enumerate(wd.layers):
         s = dec.dec_layers[i].seed + seed_shift
         l1, _, m1, r1 = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
+        p2 = post_ln(lw.ln2)
         y1, sa = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, smask, smsb, smsq, y, pat, _seed(s, 1), pd,
-                             _seed(s, 2))
-        l2, _, m2, r2 = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
+                             _seed(s, 2), post=p2)
+        l2, m2, r2 = ln_after(y1, p2, lw.ln2)
+        p3 = post_ln(lw.ln3)
         y2, ca = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, mmask, T, 0, y1, pca, _seed(s, 3), pd, _seed(s, 4),
-                             kv=kvm[:, 2 * wd.d * i: 2 * wd.d * (i + 1)])
-        l3, _, m3, r3 = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)
+                             kv=kvm[:, 2 * wd.d * i: 2 * wd.d * (i + 1)], post=p3)
+        l3, m3, r3 = ln_after(y2, p3, lw.ln3)
         y3, z, hh = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, pff, _seed(s, 5), y2, 1.0, pd,
                                 _seed(s, 6))
         layers_sv.append(SimpleNamespace(y=(y, y1, y2), ln=(l1, l2, l3), st=((m1, r1), (m2, r2), (m3, r3)), sa=sa,
@@ -851,16 +858,22 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
         gb = _e((R, d), adt, dev)
         K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb, bscale=1.0, bp=pd,
                         bseed=_seed(s, 4))
-        dln = mha_backward(gb, l2, h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, mmask, T, 0, pca, _seed(s, 3), dh,
-                           dkv=dkvm[:, 2 * d * i: 2 * d * (i + 1)])
+        # the norms in front of the two attentions run in their input-gradient GEMMs (dx_ln)
         dy1 = _e((R, d), F32, dev)
-        gb = _e((R, d), adt, dev)
-        K.layernorm_bwd(y1, dln, lw.ln2.g, m2, r2, dy1, lg.ln2.g, lg.ln2.b, dres=dy2, gb=gb, bscale=1.0, bp=pd,
-                        bseed=_seed(s, 2))
-        dln = mha_backward(gb, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, smask, smsb, smsq, pat,
-                           _seed(s, 1), None)
+        gb1 = _e((R, d), adt, dev)
+        lnb2 = LnBwd(x=y1, g=lw.ln2.g, mean=m2, rstd=r2, dx=dy1, dgamma=lg.ln2.g, dbeta=lg.ln2.b, dres=dy2,
+                     gb=gb1, bscale=1.0, bp=pd, bseed=_seed(s, 2))
+        dln = mha_backward(gb, l2, h, ls.ca, lw.ca, lg.ca, B, L1, T, wd.H, mmask, T, 0, pca, _seed(s, 3), dh,
+                           dkv=dkvm[:, 2 * d * i: 2 * d * (i + 1)], lnb=lnb2 if DEC_ROW_LN else None)
+        if dln is not None:
+            ln_bwd_of(dln, lnb2)
         dy0 = _e((R, d), F32, dev)
-        K.layernorm_bwd(y0, dln, lw.ln1.g, m1, r1, dy0, lg.ln1.g, lg.ln1.b, dres=dy1)
+        lnb1 = LnBwd(x=y0, g=lw.ln1.g, mean=m1, rstd=r1, dx=dy0, dgamma=lg.ln1.g, dbeta=lg.ln1.b, dres=dy1,
+                     gb=None, bscale=1.0, bp=0.0, bseed=0)
+        dln = mha_backward(gb1, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, smask, smsb, smsq, pat,
+                           _seed(s, 1), None, lnb=lnb1 if DEC_ROW_LN else None)
+        if dln is not None:
+            ln_bwd_of(dln, lnb1)
         dy = dy0
     K.gemm(dkvm.t(), h, gd.kv_all.W, beta=1.0, split_k=0, rowsum=gd.kv_all.b, group=True)
     K.gemm(dkvm, wd.kv_all.W, dh, beta=1.0)

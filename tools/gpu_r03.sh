@@ -24,7 +24,8 @@ for s in $STEPS; do
           run timeout -k 10 60 python3 -c "import torch; a=torch.load('/tmp/conv2_dw_0.pt'); b=torch.load('/tmp/conv2_dw_1.pt'); print('dw rel', ((a['dw']-b['dw']).abs().max()/a['dw'].abs().max()).item(), 'db rel', ((a['db']-b['db']).abs().max()/a['db'].abs().max()).item())" >> "$OUT/conv2_bench.json" ;;
     benchab) cd "$R" && for v in ${WIDE_VARIANTS:-0 1}; do LASR_GEMM_WIDE=$v run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/bench_wide$v.json" 2> "$OUT/bench_wide$v.err"; done ;;
     variants) cd "$R" && run timeout -k 10 400 python -u -m pytest tests/test_model_gpu.py -m gpu -q --timeout 200 --timeout-method thread -k "variants" -s > "$OUT/variants.log" 2>&1 ;;
-    envab) cd "$R" && for v in ${AB_VALUES:-0 1}; do env ${AB_VAR}=$v timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/bench_${AB_VAR}_$v.json" 2> "$OUT/bench_${AB_VAR}_$v.err" || exit 1; done ;;
+    envab) cd "$R" && for v in ${AB_VALUES:-0 1}; do env ${AB_VAR}=$v timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/bench_${AB_VAR}_$v.json" 2> "$OUT/bench_${AB_VAR}_$v.err" || exit 1
+             grep "^{" "$OUT/bench_${AB_VAR}_$v.json" | sed "s/^{/{\"ab\": \"${AB_VAR}=$v\", /" >> "$OUT/envab.jsonl"; done ;;
     model) cd "$R" && run timeout -k 10 500 python -u -m pytest tests/test_model_gpu.py tests/test_trainer_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/model.log" 2>&1 ;;
     conv1) cd "$R" && run timeout -k 10 120 python3 tools/conv1_bench.py > "$OUT/conv1_bench.json" 2> "$OUT/conv1_bench.err" ;;
     kgpu) cd "$R" && run timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_nodes_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/kgpu.log" 2>&1 ;;
