@@ -296,6 +296,12 @@ constexpr int DW_WIN = DW_TT + 2 * DW_P;
 constexpr int DW_G = 4, DW_R = DW_TT / DW_G, DW_CP = 64;
 constexpr int DW_RW = DW_R + 2 * DW_P;  // rows a thread reads (window + halo)
 
+
+// A window of DW_WIN rows (from tb - DW_P) x the block's 128 channels into LDS as channel
+// pairs: src rows of stride ld (elements), channels from col0; f(row pointer, channel, v[2])
+// turns two source values into the stored pair.  vec (C % 8 == 0, 16-B aligned rows): 8
+// channels per access and every load of the thread issued before the first LDS store -- the
+// window load is the latency these kernels wait on (two blocks per CU).
 template <typename T>
 LASR_DEV float2 glu2(const T* zr, int C, int c) {  // a * sigmoid(gate) for channels c, c+1
   float a[2], gt[2];
@@ -304,11 +310,61 @@ LASR_DEV float2 glu2(const T* zr, int C, int c) {  // a * sigmoid(gate) for chan
   return make_float2(a[0] * sigmoidf_(gt[0]), a[1] * sigmoidf_(gt[1]));
 }
 
+template <int CP, typename TS, typename F>
+LASR_DEV void dw_window(const TS* src, int64_t ld, int col0, int b, int T_, int C, int tb, bool vec,
+                        float2 (*win)[CP], F f) {
+  if (vec) {
+    constexpr int CH = CP / 4, NE = DW_WIN * CH, IT = (NE + 255) / 256;
+    float v[IT][8], u[IT][8];
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+      const int e = threadIdx.x + 256 * j;
+      const int rr = e / CH, q = e % CH, t = tb - DW_P + rr, ce = blockIdx.y * 2 * CP + q * 8;
+      if (e < NE && ce < C && t >= 0 && t < T_) {
+        f.load8(src + ((int64_t)b * T_ + t) * ld + col0, ce, v[j], u[j]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[j][k] = u[j][k] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+      const int e = threadIdx.x + 256 * j;
+      if (e >= NE) continue;
+      const int rr = e / CH, q = e % CH;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) win[rr][q * 4 + k] = f.pair(v[j] + 2 * k, u[j] + 2 * k);
+    }
+    return;
+  }
+  for (int e = threadIdx.x; e < DW_WIN * CP; e += 256) {
+    const int rr = e / CP, cq = e % CP, t = tb - DW_P + rr, ce = (blockIdx.y * CP + cq) * 2;
+    float2 r = make_float2(0.f, 0.f);
+    if (ce < C && t >= 0 && t < T_) {
+      float v[2], u[2];
+      f.load2(src + ((int64_t)b * T_ + t) * ld + col0, ce, v, u);
+      r = f.pair(v, u);
+    }
+    win[rr][cq] = r;
+  }
+}
+
+// GLU of z1 rows [a | gate] (2C wide): the pair a * sigmoid(gate), glu2's arithmetic
+template <typename T>
+struct GluWin {
+  int C;
+  LASR_DEV void load8(const T* row, int ce, float* a, float* g) const { ldv<8>(row + ce, a); ldv<8>(row + C + ce, g); }
+  LASR_DEV void load2(const T* row, int ce, float* a, float* g) const { ldv<2>(row + ce, a); ldv<2>(row + C + ce, g); }
+  LASR_DEV float2 pair(const float* a, const float* g) const {
+    return make_float2(a[0] * sigmoidf_(g[0]), a[1] * sigmoidf_(g[1]));
+  }
+};
+
 template <typename T, typename TY>
 __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const T* __restrict__ z1, int T_,
                                                              int C, const float* w,
                                                              const float* bias, TY* y,
-                                                             float* stats) {
+                                                             float* stats, int vec) {
   __shared__ float sst[DW_G][3][2 * DW_CP];
   const int cp = threadIdx.x % DW_CP, grp = threadIdx.x / DW_CP;
   const int c = (blockIdx.y * DW_CP + cp) * 2;
@@ -318,11 +374,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const T* __restrict
   // the block's GLU window (DW_TT + halo rows x 128 channels), each row computed once
   __shared__ float2 win[DW_WIN][DW_CP];
   const int tb = t0 - grp * DW_R;
-  for (int e = threadIdx.x; e < DW_WIN * DW_CP; e += 256) {
-    const int rr = e / DW_CP, cq = e % DW_CP, t = tb - DW_P + rr, ce = (blockIdx.y * DW_CP + cq) * 2;
-    win[rr][cq] = (ce < C && t >= 0 && t < T_) ? glu2(z1 + ((int64_t)b * T_ + t) * 2 * C, C, ce)
-                                              : make_float2(0.f, 0.f);
-  }
+  dw_window<DW_CP>(z1, 2 * (int64_t)C, 0, b, T_, C, tb, vec != 0, win, GluWin<T>{C});
   __syncthreads();
   float2 g[DW_RW];
 #pragma unroll
@@ -766,7 +818,8 @@ extern "C" int lasr_glu_dwconv_fwd(const void* z1, int dt, int B, int T, int C, 
   const int nchunk = (int)cdiv(T, DW_TT);
   dim3 g((unsigned)(B * nchunk), (unsigned)cdiv(C, 2 * DW_CP));
   hipStream_t st = (hipStream_t)stream;
-#define GF(TT, TY) glu_dwconv_fwd_kernel<TT, TY><<<g, 256, 0, st>>>((const TT*)z1, T, C, w, bias, (TY*)y, stats_ws)
+  const int vec = C % 8 == 0 && ((uintptr_t)z1 & 15) == 0;
+#define GF(TT, TY) glu_dwconv_fwd_kernel<TT, TY><<<g, 256, 0, st>>>((const TT*)z1, T, C, w, bias, (TY*)y, stats_ws, vec)
   if (dt == LASR_F32 && ydt == LASR_F32) GF(float, float);
   else if (dt == LASR_F32) GF(float, bf16_t);
   else if (ydt == LASR_F32) GF(bf16_t, float);
