@@ -394,6 +394,8 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     blocks += (int)cdiv(nb, 8) * 8;
   }
   g.start[n] = blocks;
+  static const int slice_xcd = env_int("LASR_DW_SLICE_XCD", 1);
+  g.slice_xcd = slice_xcd;
   LASR_CHECK_ARG(launch_dw_group(g, BM0, BN0, blocks, (hipStream_t)stream) == 0,
                  "lasr_gemm_dw_group: no grouped instance for tile %dx%d", BM0, BN0);
   return lasr_check_launch("lasr_gemm_dw_group");

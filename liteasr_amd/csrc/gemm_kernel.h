@@ -904,6 +904,7 @@ struct DwGroupP {
   int64_t lda[LASR_DW_GROUP_MAX], ldb[LASR_DW_GROUP_MAX];
   float* ws[LASR_DW_GROUP_MAX];
   float* rs_ws[LASR_DW_GROUP_MAX];  // null: no fused bias rowsum
+  int slice_xcd;                    // K slices tied to XCDs (gemm_dw_group_kernel)
 };
 
 template <int BM, int BN, int S, int MINB, int NW = 4>
@@ -923,10 +924,26 @@ __global__ __launch_bounds__(NW * 64, MINB * NW / 4) void gemm_dw_group_kernel(D
   p.rowsum = g.rs_ws[i];  // only tested for null when split_k > 1: the partials go to rs_ws
   p.rs_ws = g.rs_ws[i];
   p.alpha = 1.f;
-  const int wg = xcd_remap(local % ntile, ntile);
+  // Block -> (tile, K slice).  The hardware deals blocks to the 8 XCDs round-robin (block % 8;
+  // problem ranges start at multiples of 8).  When the split divides 8 and the tiles divide
+  // evenly, K slice s lives on XCDs [s * 8/split, (s+1) * 8/split) only, each of them taking
+  // a run of consecutive tiles (consecutive tiles share the larger operand's strip): both
+  // operands of a slice are then fetched by its own XCDs only, instead of the small operand
+  // by all 8 L2s (dg.slice_xcd; LASR_DW_SLICE_XCD=0 keeps the old map).  Same tile body, same
+  // k range per (tile, slice): the partials are bit-identical either way.
+  int tile, slice;
+  const int sp = g.split[i], per = 8 / (sp > 0 ? sp : 1);
+  if (g.slice_xcd && 8 % sp == 0 && ntile % per == 0 && (ntile * sp) % 8 == 0) {
+    const int x = local & 7, q = local >> 3, run = ntile / per;  // q < run by construction
+    slice = x / per;
+    tile = (x % per) * run + q;
+  } else {
+    tile = xcd_remap(local % ntile, ntile);
+    slice = local / ntile;
+  }
   int tx, ty;
-  dw_tile_order(wg, ntx, nty, p.N > p.M, tx, ty);
-  gemm_glds_tile<BM, BN, false, false, float, S, G_LIN, 2, NW>(p, tx, ty, local / ntile);
+  dw_tile_order(tile, ntx, nty, p.N > p.M, tx, ty);
+  gemm_glds_tile<BM, BN, false, false, float, S, G_LIN, 2, NW>(p, tx, ty, slice);
 }
 
 // ============================ fp32 MFMA kernel ===================================

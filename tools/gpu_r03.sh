@@ -37,7 +37,7 @@ for s in $STEPS; do
     ddp1) cd "$R" && run timeout -k 10 300 python3 bench.py --force-ddp --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1.json" 2> "$OUT/bench_ddp1.err" ;;
     trace) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace.log" 2>&1
            db=$(find "$OUT/trace" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary.txt" 2>&1 ;;
-    pmc) for c in family dw hot; do
+    pmc) for c in ${PMC_CASES:-family dw hot}; do
            cd /tmp && run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$c" -o run -- python3 "$R/bench.py" --roofline-only 20 --roofline-case $c > "$OUT/pmc_fetch_$c.log" 2>&1
            run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$c" -o run -- python3 "$R/bench.py" --roofline-only 20 --roofline-case $c > "$OUT/pmc_write_$c.log" 2>&1
            grep "^{" "$OUT/pmc_fetch_$c.log" | tail -1 > "$OUT/roofline_meta_$c.json"
