@@ -89,7 +89,7 @@ __global__ void conv1_bwd_reduce_kernel(const float* part, int nparts, int C, fl
 // (their 8x10 weights in registers) and a strided set of output columns f1, so every
 // y1 / dy1 access is one 16-B (bf16) vector and a wave covers whole 512-B channel rows.
 // Same per-output arithmetic order as the scalar kernels above.
-constexpr int C1V_ROWS = 32;  // (b,t1) rows per vectorised conv1-bwd block
+constexpr int C1V_ROWS = 32;  // largest (b,t1) row count per vectorised conv1-bwd block (A/B)
 constexpr int C1F_ROWS = 8;   // (b,t1) rows per vectorised conv1-fwd block
 
 template <typename T>
@@ -143,12 +143,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restri
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_bwd_v8_kernel(const float* __restrict__ x, int T_, int F,
                                                            int C, int T1, int F1, int nrows,
-                                                           const T* __restrict__ dy1, float* part) {
-  extern __shared__ float sh[];  // C1V_ROWS x 3F input rows, then the 8*256 reduce slab
+                                                           const T* __restrict__ dy1, float* part, int rpb) {
+  extern __shared__ float sh[];  // rpb x 3F input rows, then the 8*256 reduce slab
   float* xs = sh;
-  float* red = sh + C1V_ROWS * 3 * F;
-  const int r0 = blockIdx.x * C1V_ROWS;
-  const int nr = min(C1V_ROWS, nrows - r0);
+  float* red = sh + rpb * 3 * F;
+  const int r0 = blockIdx.x * rpb;
+  const int nr = min(rpb, nrows - r0);
   for (int i = threadIdx.x; i < nr * 3 * F; i += 256) {
     const int rr = i / (3 * F), q = i - rr * 3 * F;
     const int r = r0 + rr;
@@ -749,15 +749,19 @@ extern "C" int lasr_conv1_bwd(const float* x, int B, int T, int F, int C, const 
                               float* dw, float* db, float* ws, int64_t ws_floats, void* stream) {
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const int nrows = B * T1;
+  // rows per block: 16 (998 blocks at config 2, four per CU: twice the loads in flight of
+  // 32-row blocks, 143 -> 108 us standalone, tools/conv1_bench.py); LASR_C1B_ROWS=32 for A/B
+  static const int rpb_env = [] { const char* e = getenv("LASR_C1B_ROWS"); return e && e[0] ? atoi(e) : C1B_ROWS; }();
+  const int rpb = rpb_env >= 8 && rpb_env <= C1V_ROWS ? rpb_env : C1B_ROWS;
   const bool vec = C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)dy1 & 15) == 0 &&
-                   (size_t)(C1V_ROWS * 3 * F + 8 * 256) * sizeof(float) <= 64 * 1024;
-  const int nparts = (int)cdiv(nrows, vec ? C1V_ROWS : C1B_ROWS);
+                   (size_t)(rpb * 3 * F + 8 * 256) * sizeof(float) <= 64 * 1024;
+  const int nparts = (int)cdiv(nrows, vec ? rpb : C1B_ROWS);
   LASR_CHECK_ARG(ws_floats >= (int64_t)(nparts + 1) * 10 * C, "lasr_conv1_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   if (vec) {
-    const size_t shv = (size_t)(C1V_ROWS * 3 * F + 8 * 256) * sizeof(float);
-    if (dt == LASR_F32) conv1_bwd_v8_kernel<float><<<nparts, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, (const float*)dy1, ws);
-    else conv1_bwd_v8_kernel<bf16_t><<<nparts, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, (const bf16_t*)dy1, ws);
+    const size_t shv = (size_t)(rpb * 3 * F + 8 * 256) * sizeof(float);
+    if (dt == LASR_F32) conv1_bwd_v8_kernel<float><<<nparts, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, (const float*)dy1, ws, rpb);
+    else conv1_bwd_v8_kernel<bf16_t><<<nparts, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, (const bf16_t*)dy1, ws, rpb);
   } else {
     const size_t shm = (size_t)C1B_ROWS * 3 * F * sizeof(float);
     if (dt == LASR_F32) conv1_bwd_kernel<float><<<nparts, 256, shm, st>>>(x, T, F, C, T1, F1, nrows, (const float*)dy1, ws);

@@ -566,7 +566,7 @@ def conv1_bwd(x, dy1, dw, db):
     B, T, F = x.shape
     Cc = dw.shape[0]
     T1 = (T - 3) // 2 + 1
-    nparts = (B * T1 + 15) // 16
+    nparts = (B * T1 + 7) // 8  # the partial rows of the smallest block lasr_conv1_bwd may use
     ws = WS.get((nparts + 1) * 10 * Cc, x.device)
     N.call("lasr_conv1_bwd", ptr(x), B, T, F, Cc, ptr(dy1), dt(dy1), ptr(dw), ptr(db), ptr(ws),
            ws.numel(), stream())
