@@ -95,13 +95,13 @@ constexpr int C1F_ROWS = 8;   // (b,t1) rows per vectorised conv1-fwd block
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restrict__ x, int T_, int F,
                                                            int C, int T1, int F1, int nrows, const float* w,
-                                                           const float* bias, T* y1) {
+                                                           const float* bias, T* y1, int rpb) {
   // C1F_ROWS output rows (b, t1) per block: the 72 weights and 8 biases a thread keeps in
   // registers are loaded once per block, not once per row; the 3 input rows of each output
   // row are staged in LDS.  Each output: bias + sum over the 9 taps in order, then ReLU.
-  extern __shared__ float xs[];  // C1F_ROWS x 3F
-  const int r0 = blockIdx.x * C1F_ROWS;
-  const int nr = min(C1F_ROWS, nrows - r0);
+  extern __shared__ float xs[];  // rpb x 3F
+  const int r0 = blockIdx.x * rpb;
+  const int nr = min(rpb, nrows - r0);
   for (int i = threadIdx.x; i < nr * 3 * F; i += 256) {
     const int rr = i / (3 * F), q = i - rr * 3 * F;
     const int r = r0 + rr;
@@ -731,13 +731,18 @@ extern "C" int lasr_conv1_fwd(const float* x, int B, int T, int F, int C, const 
   const size_t shm = (size_t)(3 * F + 10 * C) * sizeof(float);
   LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_conv1_fwd: too much LDS");
   hipStream_t st = (hipStream_t)stream;
+  static const int rpb = [] {  // rows per block (LASR_C1F_ROWS: A/B)
+    const char* e = getenv("LASR_C1F_ROWS");
+    const int v = e && e[0] ? atoi(e) : C1F_ROWS;
+    return v >= 1 && v <= 32 ? v : C1F_ROWS;
+  }();
   if (C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)y1 & 15) == 0 &&
-      (size_t)C1F_ROWS * 3 * F * sizeof(float) <= 64 * 1024) {
-    const size_t shv = (size_t)C1F_ROWS * 3 * F * sizeof(float);
+      (size_t)rpb * 3 * F * sizeof(float) <= 64 * 1024) {
+    const size_t shv = (size_t)rpb * 3 * F * sizeof(float);
     const int nrows = B * T1;
-    const unsigned nb = (unsigned)cdiv(nrows, C1F_ROWS);
-    if (dt == LASR_F32) conv1_fwd_v8_kernel<float><<<nb, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, w, bias, (float*)y1);
-    else conv1_fwd_v8_kernel<bf16_t><<<nb, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, w, bias, (bf16_t*)y1);
+    const unsigned nb = (unsigned)cdiv(nrows, rpb);
+    if (dt == LASR_F32) conv1_fwd_v8_kernel<float><<<nb, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, w, bias, (float*)y1, rpb);
+    else conv1_fwd_v8_kernel<bf16_t><<<nb, 256, shv, st>>>(x, T, F, C, T1, F1, nrows, w, bias, (bf16_t*)y1, rpb);
     return lasr_check_launch("conv1_fwd");
   }
   if (dt == LASR_F32) conv1_fwd_kernel<float><<<B * T1, 256, shm, st>>>(x, T, F, C, T1, F1, w, bias, (float*)y1);
