@@ -285,15 +285,24 @@ def hottest_case(cfgd, dev):
 
 
 def _time_case(launch, iters):
+    """Average device time of one launch(): `iters` launches captured into one hipGraph (as the
+    step runs them) and replayed between two HIP events on the launch stream.  Timing eager
+    Python launches instead would measure the host's launch rate for the short kernels (a
+    6 us GEMM behind ~10 us of ctypes marshalling)."""
     import torch
 
-    for _ in range(5):
+    for _ in range(5):  # warm-up: workspaces reach their size outside the capture
         launch()
-    st = torch.cuda.current_stream()  # lasr_* launches go to kernels.stream() == this stream
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):  # lasr_* launches go to kernels.stream() == the capture stream
+        for _ in range(iters):
+            launch()
+    g.replay()
+    st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    for _ in range(iters):
-        launch()
+    g.replay()
     e1.record(st)
     e1.synchronize()
     return e0.elapsed_time(e1) / iters * 1e-3
@@ -387,14 +396,13 @@ def ctc_roofline(cfgd, dev, iters=20):
     lse, lp = torch.empty(B * Tp, **f32), torch.empty(B * Tp * (L + 1), **f32)
     alpha, beta, nll = torch.empty(B * Tp * S, **f32), torch.empty(B * Tp * S, **f32), torch.empty(B, **f32)
     grad = K.padded_rows(B * Tp, V_, torch.bfloat16, dev).view(B, Tp, V_)
-    st = K.stream()
 
     def gather():
         K.ctc_fwd(logits, tgt, ilen, tlen, lse, lp, None, nll)
 
-    def lattice():
+    def lattice():  # the current stream at call time (the capture stream inside _time_case)
         Nn.call("lasr_ctc_lattice", B, Tp, L, K.ptr(tgt), K.ptr(ilen), K.ptr(tlen), K.ptr(lp), K.ptr(alpha),
-                K.ptr(beta), K.ptr(nll), st)
+                K.ptr(beta), K.ptr(nll), K.stream())
 
     def gradk():
         K.ctc_bwd(logits, tgt, ilen, tlen, lse, lp, alpha, nll, beta, grad, 1.0 / B, beta_ready=True)

@@ -14,13 +14,14 @@ def main(db, metaf):
     meta = json.loads(open(metaf).read().strip().splitlines()[-1])
     per, n = meta["dispatches_per_launch"], meta["launches"]
     c = sqlite3.connect(db)
+    match = meta.get("match") or [meta["kernel"]]  # a composite family lists its kernel names
     rows = [(nm, e - s) for nm, s, e in c.execute("select name, start, end from kernels order by start")
-            if meta["kernel"] in nm]
+            if any(k in nm for k in match)]
     assert len(rows) == per * n, (len(rows), per, n)
     pos = [[] for _ in range(per)]
     for i, (nm, d) in enumerate(rows):
         pos[i % per].append(d)
-    names = [rows[i][0].split("(")[0].replace("void ", "") for i in range(per)]
+    names = [rows[i][0].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "") for i in range(per)]
     out = {"sets": n, "per_set_us": sum(sum(p) for p in pos) / n / 1e3,
            "dispatch_avg_us": [round(sum(p) / len(p) / 1e3, 2) for p in pos], "kernels": names}
     print(json.dumps(out, indent=1))
