@@ -124,8 +124,11 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
       BN = a->M >= a->N ? 128 : 64;
     }
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
-    // epilogue GEMMs (small grids, long K: the decoder's K = 2048 projections) fill one round
-    const int64_t target = very_long || !plain ? 256 : 512;
+    // K-contiguous A: the small-grid long-K data GEMMs kernels.gemm splits (the decoder's
+    // K = 2048 / V projections at B*(L+1) rows): ~128+ workgroups -- fewer fp32 slabs to
+    // reduce beats filling the chip (tools/tile_ab.py at M 1312: split 4 12.5 / 13.3 us vs
+    // split 8 15.8 / 15.4 us); the weight gradients (M-contiguous A) fill one round or two
+    const int64_t target = a->lda_k == 1 ? 128 : (very_long || !plain ? 256 : 512);
     while (nb * split < target && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
   } else if (bf) {
     const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
