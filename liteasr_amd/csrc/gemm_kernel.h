@@ -82,9 +82,36 @@ LASR_DEV float load_any(const void* p, int dt, int64_t i) {
 // dkey = epi_key(p), computed ONCE per thread before the output loops: drop_key reads the
 // device step counter, and a load inside the loop is re-issued and waited for on every
 // iteration (the stores in between may alias it).
-template <int N, typename ZST>
+// Compile-time epilogue modes of the hot FFN GEMMs (host-selected by epi_code, gemm_launch.h):
+// the same per-element arithmetic as the runtime path, without its mode branches (which, with
+// the uniform values they keep live, cost SGPR spills and ~2x the VALU of the arithmetic).
+enum { EPI_RT = 0, EPI_SWISH_GATE_DROP = 1, EPI_AUX_GATE = 2 };
+
+template <int N, int EPI = EPI_RT, typename ZST>
 LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)[N], const float (&auxv)[N],
                        bool has_aux, const float (&resv)[N], bool has_res, ZST zst) {
+  if constexpr (EPI == EPI_SWISH_GATE_DROP) {
+    // zout_mode 1, Swish, dropout on; no aux, residual or beta (FFN fc1 forward)
+    const uint32_t km = drop_keep_mask<N>(p.drop, dkey, dbase);
+    float g[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const float s = sigmoidf_(v[q]);
+      g[q] = s * (1.f + v[q] * (1.f - s));
+      v[q] *= s;
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) g[q] *= (km >> q) & 1u ? 1.f : 0.f;
+    zst(g);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] *= (km >> q) & 1u ? p.drop.scale : 0.f;
+    return;
+  } else if constexpr (EPI == EPI_AUX_GATE) {
+    // v * aux (the stored gate); no activation, zout, dropout or residual (FFN fc1 dz)
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] *= auxv[q];
+    return;
+  }
   const bool drop = p.drop.p > 0.f;
   const uint32_t km = drop ? drop_keep_mask<N>(p.drop, dkey, dbase) : 0u;
   bool acted = false;  // activation already applied (the gate shares the sigmoid)
@@ -229,13 +256,13 @@ LASR_DEV void epi_store8(const GemmP& p, uint32_t dkey, int z1, int z2, int z, i
 
 // Epilogue modes 0/1: bias already in registers (bv), the one aux/res source prefetched
 // (sv, mode 1 only; N % 8 == 0 there), beta == 0; cnt < 8 only on a ragged last vector.
-template <typename TC>
+template <typename TC, int EPI = EPI_RT>
 LASR_DEV void epi_fast8(const GemmP& p, uint32_t dkey, int64_t cidx, int z, int m, int n, int cnt,
                         const float* acc, float alpha_eff, const float* bv, const float (&sv)[8]) {
   float v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = acc[q] * alpha_eff + bv[q];
-  epi_core<8>(p, dkey, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, sv, p.aux != nullptr, sv, p.res != nullptr,
+  epi_core<8, EPI>(p, dkey, ((uint64_t)z * p.M + m) * (uint64_t)p.N + n, v, sv, p.aux != nullptr, sv, p.res != nullptr,
               [&](const float (&zv)[8]) { st_8((TC*)p.zout + cidx, zv, true, cnt); });
   st_8((TC*)p.C + cidx, v, true, cnt);
 }
@@ -264,7 +291,7 @@ LASR_DEV int64_t dx_row(const ConvG& g, int m) {
 // dxrow (G_DX only): the tile's BM row offsets dx_row(m0 + r), computed once per tile (two
 // integer divisions and two remainders each; per output vector they cost more VALU than the
 // epilogue arithmetic).
-template <int BM, int BN, typename TC, bool TRANS = false, int G = G_LIN, int NW = 4>
+template <int BM, int BN, typename TC, bool TRANS = false, int G = G_LIN, int NW = 4, int EPI = EPI_RT>
 LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)], char* smem_epi, int m0,
                             int n0, int s, int z, int z1, int z2, const int64_t* dxrow = nullptr) {
   // output-row offsets: linear (ldc, ld of the aux/res source), or the transposed-conv scatter
@@ -360,7 +387,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)]
             float a8[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) a8[q] = cs[r * LDC + ec8 + q];
-            epi_fast8<TC>(p, dkey, crow(m) + en, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
+            epi_fast8<TC, EPI>(p, dkey, crow(m) + en, z, m, en, min(8, p.N - en), a8, al, bv, sv[it]);
           }
         }
       }
@@ -674,7 +701,7 @@ LASR_DEV int xcd_remap(int orig, int nwg) {
 
 // One output tile (tx, ty) of K slice / batch index zz: the body shared by the launch-grid
 // kernel (gemm_bf16_glds_kernel) and the grouped weight-gradient kernel (gemm_dw_group_kernel).
-template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int G, int KS, int NW = 4>
+template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int G, int KS, int NW = 4, int EPI = EPI_RT>
 LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const int zz) {
   static_assert(G == G_LIN || (G == G_DW ? (!AKC && !BKC) : (AKC && (G == G_FWD) == BKC)),
                 "gather instance operand orientation");
@@ -861,7 +888,7 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   // split-K partials: fp32, 16-B per lane straight from the accumulators; final outputs:
   // staged through LDS (full 256-B rows per wave store)
   if (p.split_k > 1) gemm_epilogue_direct<BM, BN, TC, NW>(p, acc, m0, n0, s, z, z1, z2);
-  else gemm_epilogue<BM, BN, TC, true, G, NW>(p, acc, smem_epi, m0, n0, s, z, z1, z2, dxrow);
+  else gemm_epilogue<BM, BN, TC, true, G, NW, EPI>(p, acc, smem_epi, m0, n0, s, z, z1, z2, dxrow);
 }
 
 // Tile order of a weight-gradient GEMM (both operands [K, M] / [K, N] with K = rows): the
@@ -877,13 +904,13 @@ LASR_DEV void dw_tile_order(int wg, int nx, int ny, bool n_major, int& tx, int& 
 // tiles of the large GEMMs: half the LDS-DMA ingest per MFMA of 128 x 256 at 4 waves).
 // MINB = workgroups per CU; the launch bound's second operand is waves per SIMD.
 template <int BM, int BN, bool AKC, bool BKC, typename TC, int S, int MINB = 3, int G = G_LIN, int KS = 1,
-          int NW = 4>
+          int NW = 4, int EPI = EPI_RT>
 __global__ __launch_bounds__(NW * 64, MINB * NW / 4) void gemm_bf16_glds_kernel(GemmP p) {
   const int nx = gridDim.x, ny = gridDim.y;
   const int wg = xcd_remap(blockIdx.y * nx + blockIdx.x, nx * ny);
   int tx, ty;
   dw_tile_order(wg, nx, ny, !AKC && !BKC && G == G_LIN && p.N > p.M, tx, ty);
-  gemm_glds_tile<BM, BN, AKC, BKC, TC, S, G, KS, NW>(p, tx, ty, blockIdx.z);
+  gemm_glds_tile<BM, BN, AKC, BKC, TC, S, G, KS, NW, EPI>(p, tx, ty, blockIdx.z);
 }
 
 // Grouped split-K weight-gradient GEMMs (partials only): up to LASR_DW_GROUP_MAX independent

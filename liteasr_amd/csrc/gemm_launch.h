@@ -4,6 +4,18 @@
 #pragma once
 #include "gemm_kernel.h"
 
+// Compile-time epilogue of the hot FFN GEMMs (gemm_kernel.h EPI_*), or EPI_RT.  Host-checked
+// against exactly the parameters the specialised path assumes; LASR_EPI_SPEC=0 disables it.
+static inline int epi_code(const GemmP& p) {
+  static const int on = [] { const char* e = getenv("LASR_EPI_SPEC"); return e && e[0] ? atoi(e) : 1; }();
+  if (!on || p.split_k > 1 || p.beta != 0.f || p.res || p.alpha_dev) return EPI_RT;
+  if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_SWISH && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
+    return EPI_SWISH_GATE_DROP;
+  if (!p.zout && p.act == LASR_ACT_NONE && p.aux && p.aux_act == LASR_ACT_GATE && p.drop.p <= 0.f && p.epi_mode == 1)
+    return EPI_AUX_GATE;
+  return EPI_RT;
+}
+
 template <bool AKC, bool BKC, typename TC>
 void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3 grid, hipStream_t st) {
   (void)nw;  // no 8-wave generic instance is planned (gemm.hip gemm_plan)
@@ -33,7 +45,23 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
   if (glds) {
     if (BM == 256 && BN == 256) gemm_bf16_glds_kernel<256, 256, AKC, BKC, TC, 3, 1><<<grid, 256, 0, st>>>(p);
     else if (BM == 256) gemm_bf16_glds_kernel<256, 128, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
-    else if (BN == 256) gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
+    else if (BN == 256) {
+      // the FFN fc1 forward (A, B K-contiguous) and its dz GEMM (B N-contiguous), bf16 out
+      const int e = epi_code(p);
+      if constexpr (AKC && BKC && std::is_same<TC, bf16_t>::value) {
+        if (e == EPI_SWISH_GATE_DROP) {
+          gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2, G_LIN, 1, 4, EPI_SWISH_GATE_DROP><<<grid, 256, 0, st>>>(p);
+          return;
+        }
+      }
+      if constexpr (AKC && !BKC && std::is_same<TC, bf16_t>::value) {
+        if (e == EPI_AUX_GATE) {
+          gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2, G_LIN, 1, 4, EPI_AUX_GATE><<<grid, 256, 0, st>>>(p);
+          return;
+        }
+      }
+      gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
+    }
     else if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
     else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
     else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
