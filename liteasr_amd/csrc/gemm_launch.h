@@ -8,7 +8,11 @@
 // against exactly the parameters the specialised path assumes; LASR_EPI_SPEC=0 disables it.
 static inline int epi_code(const GemmP& p) {
   static const int on = [] { const char* e = getenv("LASR_EPI_SPEC"); return e && e[0] ? atoi(e) : 1; }();
-  if (!on || p.split_k > 1 || p.beta != 0.f || p.res || p.alpha_dev) return EPI_RT;
+  if (!on || p.split_k > 1 || p.beta != 0.f || p.alpha_dev) return EPI_RT;
+  if (p.res) {
+    return !p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p > 0.f && p.epi_mode == 1 ? EPI_RES_DROP : EPI_RT;
+  }
+  if (!p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p <= 0.f && p.epi_mode == 0) return EPI_PLAIN;
   if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_SWISH && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
     return EPI_SWISH_GATE_DROP;
   if (!p.zout && p.act == LASR_ACT_NONE && p.aux && p.aux_act == LASR_ACT_GATE && p.drop.p <= 0.f && p.epi_mode == 1)
@@ -39,7 +43,24 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
     else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 3, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 3, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else if (g_ks2_stages == 4) gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
-    else gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2><<<grid, 256, 0, st>>>(p);
+    else {
+      // the 64 x 64 launches of the N = d family: input gradients (B N-contiguous, bf16 out) and
+      // the residual projections (fp32 out)
+      const int e = epi_code(p);
+      if constexpr (AKC && !BKC && std::is_same<TC, bf16_t>::value) {
+        if (e == EPI_PLAIN) {
+          gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2, 4, EPI_PLAIN><<<grid, 256, 0, st>>>(p);
+          return;
+        }
+      }
+      if constexpr (AKC && BKC && std::is_same<TC, float>::value) {
+        if (e == EPI_RES_DROP) {
+          gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2, 4, EPI_RES_DROP><<<grid, 256, 0, st>>>(p);
+          return;
+        }
+      }
+      gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2><<<grid, 256, 0, st>>>(p);
+    }
     return;
   }
   if (glds) {
