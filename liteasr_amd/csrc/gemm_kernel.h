@@ -85,7 +85,7 @@ LASR_DEV float load_any(const void* p, int dt, int64_t i) {
 // Compile-time epilogue modes of the hot FFN GEMMs (host-selected by epi_code, gemm_launch.h):
 // the same per-element arithmetic as the runtime path, without its mode branches (which, with
 // the uniform values they keep live, cost SGPR spills and ~2x the VALU of the arithmetic).
-enum { EPI_RT = 0, EPI_SWISH_GATE_DROP = 1, EPI_AUX_GATE = 2, EPI_PLAIN = 3, EPI_RES_DROP = 4 };
+enum { EPI_RT = 0, EPI_SWISH_GATE_DROP = 1, EPI_AUX_GATE = 2, EPI_PLAIN = 3, EPI_RES_DROP = 4, EPI_RELU_GATE_DROP = 5 };
 
 template <int N, int EPI = EPI_RT, typename ZST>
 LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)[N], const float (&auxv)[N],
@@ -110,6 +110,20 @@ LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)
     // v * aux (the stored gate); no activation, zout, dropout or residual (FFN fc1 dz)
 #pragma unroll
     for (int q = 0; q < N; ++q) v[q] *= auxv[q];
+    return;
+  } else if constexpr (EPI == EPI_RELU_GATE_DROP) {
+    // zout_mode 1, ReLU, dropout on; no aux, residual or beta (the decoder's FFN fc1 forward)
+    const uint32_t km = drop_keep_mask<N>(p.drop, dkey, dbase);
+    float g[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) g[q] = v[q] > 0.f ? 1.f : 0.f;
+#pragma unroll
+    for (int q = 0; q < N; ++q) g[q] *= (km >> q) & 1u ? 1.f : 0.f;
+    zst(g);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = fmaxf(v[q], 0.f);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] *= (km >> q) & 1u ? p.drop.scale : 0.f;
     return;
   } else if constexpr (EPI == EPI_PLAIN) {
     return;  // alpha * acc + bias only (input-gradient GEMMs)

@@ -15,6 +15,8 @@ static inline int epi_code(const GemmP& p) {
   if (!p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p <= 0.f && p.epi_mode == 0) return EPI_PLAIN;
   if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_SWISH && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
     return EPI_SWISH_GATE_DROP;
+  if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_RELU && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
+    return EPI_RELU_GATE_DROP;
   if (!p.zout && p.act == LASR_ACT_NONE && p.aux && p.aux_act == LASR_ACT_GATE && p.drop.p <= 0.f && p.epi_mode == 1)
     return EPI_AUX_GATE;
   return EPI_RT;
@@ -47,12 +49,17 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
       // the 64 x 64 launches of the N = d family: input gradients (B N-contiguous, bf16 out) and
       // the residual projections (fp32 out)
       const int e = epi_code(p);
-      if constexpr (AKC && !BKC && std::is_same<TC, bf16_t>::value) {
-        if (e == EPI_PLAIN) {
-          gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2, 4, EPI_PLAIN><<<grid, 256, 0, st>>>(p);
-          return;
-        }
+#define L64(E) gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2, 4, E><<<grid, 256, 0, st>>>(p)
+      if constexpr (AKC && std::is_same<TC, bf16_t>::value) {
+        if (e == EPI_PLAIN) { L64(EPI_PLAIN); return; }
       }
+      if constexpr (AKC && !BKC && std::is_same<TC, bf16_t>::value) {
+        if (e == EPI_AUX_GATE) { L64(EPI_AUX_GATE); return; }  // the decoder's FFN dz
+      }
+      if constexpr (AKC && BKC && std::is_same<TC, bf16_t>::value) {
+        if (e == EPI_RELU_GATE_DROP) { L64(EPI_RELU_GATE_DROP); return; }  // the decoder's FFN fc1
+      }
+#undef L64
       if constexpr (AKC && BKC && std::is_same<TC, float>::value) {
         if (e == EPI_RES_DROP) {
           gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 3, 3, G_LIN, 2, 4, EPI_RES_DROP><<<grid, 256, 0, st>>>(p);
@@ -84,7 +91,16 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
       gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
     }
     else if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
-    else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
+    else if (BM == 128) {
+      // (the q/k/v projection: bias only)
+      if constexpr (AKC && BKC && std::is_same<TC, bf16_t>::value) {
+        if (epi_code(p) == EPI_PLAIN) {
+          gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4, 3, G_LIN, 1, 4, EPI_PLAIN><<<grid, 256, 0, st>>>(p);
+          return;
+        }
+      }
+      gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
+    }
     else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
     else gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
     return;
