@@ -45,7 +45,7 @@ struct DxClasses {
   int M[4], K[4];
 };
 
-template <int BN>
+template <int BN, int EPI = EPI_RT>
 __global__ __launch_bounds__(256, 2) void conv2_dx_kernel(GemmP p, DxClasses c) {
   const int blk = blockIdx.x;
   int i = 0;
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256, 2) void conv2_dx_kernel(GemmP p, DxClasses c) 
   const int local = blk - c.start[i];
   if (local >= ntile) return;  // alignment padding
   const int wg = xcd_remap(local, ntile);
-  gemm_glds_tile<128, BN, true, false, bf16_t, 3, G_DX, 1, 4>(q, wg % ntx, wg / ntx, 0);
+  gemm_glds_tile<128, BN, true, false, bf16_t, 3, G_DX, 1, 4, EPI>(q, wg % ntx, wg / ntx, 0);
 }
 
 static int env_flag_dflt(const char* name, int dflt) {
@@ -110,7 +110,9 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     // (64 x 256 tiles, 2366 of them: 355 vs 279 us, profiles/r03/conv2_dx_ab.json)
     dim3 grid((unsigned)(C / BN), (unsigned)cdiv(p.M, 128), 1);
     LASR_CHECK_ARG(grid.y <= 65535, "lasr_conv2_gemm: grid too large");
-    if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, true, bf16_t, 3, 2, G_FWD><<<grid, 256, 0, st>>>(p);
+    if (BN == 256 && epi_code(p) == EPI_RELU)
+      gemm_bf16_glds_kernel<128, 256, true, true, bf16_t, 3, 2, G_FWD, 1, 4, EPI_RELU><<<grid, 256, 0, st>>>(p);
+    else if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, true, bf16_t, 3, 2, G_FWD><<<grid, 256, 0, st>>>(p);
     else gemm_bf16_glds_kernel<128, 128, true, true, bf16_t, 3, 3, G_FWD><<<grid, 256, 0, st>>>(p);
     return lasr_check_launch("lasr_conv2_gemm/fwd");
   }
@@ -176,7 +178,8 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
       nb += (int)(cdiv(cdiv(dc.M[cls], 128) * (C / BN), 8) * 8);
     }
     dc.start[4] = nb;
-    if (BN == 256) conv2_dx_kernel<256><<<nb, 256, 0, st>>>(p, dc);
+    if (BN == 256 && epi_code(p) == EPI_AUX_RELU) conv2_dx_kernel<256, EPI_AUX_RELU><<<nb, 256, 0, st>>>(p, dc);
+    else if (BN == 256) conv2_dx_kernel<256><<<nb, 256, 0, st>>>(p, dc);
     else conv2_dx_kernel<128><<<nb, 256, 0, st>>>(p, dc);
     return lasr_check_launch("lasr_conv2_gemm/dx");
   }

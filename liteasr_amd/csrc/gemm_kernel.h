@@ -85,7 +85,10 @@ LASR_DEV float load_any(const void* p, int dt, int64_t i) {
 // Compile-time epilogue modes of the hot FFN GEMMs (host-selected by epi_code, gemm_launch.h):
 // the same per-element arithmetic as the runtime path, without its mode branches (which, with
 // the uniform values they keep live, cost SGPR spills and ~2x the VALU of the arithmetic).
-enum { EPI_RT = 0, EPI_SWISH_GATE_DROP = 1, EPI_AUX_GATE = 2, EPI_PLAIN = 3, EPI_RES_DROP = 4, EPI_RELU_GATE_DROP = 5 };
+enum {
+  EPI_RT = 0, EPI_SWISH_GATE_DROP = 1, EPI_AUX_GATE = 2, EPI_PLAIN = 3, EPI_RES_DROP = 4, EPI_RELU_GATE_DROP = 5,
+  EPI_RELU = 6, EPI_AUX_RELU = 7
+};
 
 template <int N, int EPI = EPI_RT, typename ZST>
 LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)[N], const float (&auxv)[N],
@@ -124,6 +127,14 @@ LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)
     for (int q = 0; q < N; ++q) v[q] = fmaxf(v[q], 0.f);
 #pragma unroll
     for (int q = 0; q < N; ++q) v[q] *= (km >> q) & 1u ? p.drop.scale : 0.f;
+    return;
+  } else if constexpr (EPI == EPI_RELU) {  // bias + ReLU (subsampling conv2 forward)
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = fmaxf(v[q], 0.f);
+    return;
+  } else if constexpr (EPI == EPI_AUX_RELU) {  // * relu'(aux) (subsampling conv2 data gradient)
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] *= auxv[q] > 0.f ? 1.f : 0.f;
     return;
   } else if constexpr (EPI == EPI_PLAIN) {
     return;  // alpha * acc + bias only (input-gradient GEMMs)
@@ -1128,6 +1139,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
   }
 }
 
+
+// Compile-time epilogue of the hot FFN GEMMs (gemm_kernel.h EPI_*), or EPI_RT.  Host-checked
+// against exactly the parameters the specialised path assumes; LASR_EPI_SPEC=0 disables it.
+static inline int epi_code(const GemmP& p) {
+  static const int on = [] { const char* e = getenv("LASR_EPI_SPEC"); return e && e[0] ? atoi(e) : 1; }();
+  if (!on || p.split_k > 1 || p.beta != 0.f || p.alpha_dev) return EPI_RT;
+  if (p.res) {
+    return !p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p > 0.f && p.epi_mode == 1 ? EPI_RES_DROP : EPI_RT;
+  }
+  if (!p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p <= 0.f && p.epi_mode == 0) return EPI_PLAIN;
+  if (!p.zout && p.act == LASR_ACT_RELU && !p.aux && p.drop.p <= 0.f && p.epi_mode == 0) return EPI_RELU;
+  if (!p.zout && p.act == LASR_ACT_NONE && p.aux && p.aux_act == LASR_ACT_RELU && p.drop.p <= 0.f && p.epi_mode == 1)
+    return EPI_AUX_RELU;
+  if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_SWISH && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
+    return EPI_SWISH_GATE_DROP;
+  if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_RELU && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
+    return EPI_RELU_GATE_DROP;
+  if (!p.zout && p.act == LASR_ACT_NONE && p.aux && p.aux_act == LASR_ACT_GATE && p.drop.p <= 0.f && p.epi_mode == 1)
+    return EPI_AUX_GATE;
+  return EPI_RT;
+}
 
 // host-side tuning state shared by the two launch units (gemm.hip defines it)
 extern int g_stages, g_tile_m, g_tile_n, g_split, g_ks2_stages;

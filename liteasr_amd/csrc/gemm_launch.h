@@ -4,24 +4,6 @@
 #pragma once
 #include "gemm_kernel.h"
 
-// Compile-time epilogue of the hot FFN GEMMs (gemm_kernel.h EPI_*), or EPI_RT.  Host-checked
-// against exactly the parameters the specialised path assumes; LASR_EPI_SPEC=0 disables it.
-static inline int epi_code(const GemmP& p) {
-  static const int on = [] { const char* e = getenv("LASR_EPI_SPEC"); return e && e[0] ? atoi(e) : 1; }();
-  if (!on || p.split_k > 1 || p.beta != 0.f || p.alpha_dev) return EPI_RT;
-  if (p.res) {
-    return !p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p > 0.f && p.epi_mode == 1 ? EPI_RES_DROP : EPI_RT;
-  }
-  if (!p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p <= 0.f && p.epi_mode == 0) return EPI_PLAIN;
-  if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_SWISH && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
-    return EPI_SWISH_GATE_DROP;
-  if (p.zout && p.zout_mode == 1 && p.act == LASR_ACT_RELU && p.drop.p > 0.f && !p.aux && p.epi_mode == 0)
-    return EPI_RELU_GATE_DROP;
-  if (!p.zout && p.act == LASR_ACT_NONE && p.aux && p.aux_act == LASR_ACT_GATE && p.drop.p <= 0.f && p.epi_mode == 1)
-    return EPI_AUX_GATE;
-  return EPI_RT;
-}
-
 template <bool AKC, bool BKC, typename TC>
 void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3 grid, hipStream_t st) {
   (void)nw;  // no 8-wave generic instance is planned (gemm.hip gemm_plan)
@@ -101,7 +83,16 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
       }
       gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
     }
-    else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
+    else if (BN == 128) {
+      // (the batched attention GEMMs of the materialised path: alpha / plain)
+      if constexpr (AKC && std::is_same<TC, bf16_t>::value) {
+        if (epi_code(p) == EPI_PLAIN) {
+          gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4, 3, G_LIN, 1, 4, EPI_PLAIN><<<grid, 256, 0, st>>>(p);
+          return;
+        }
+      }
+      gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
+    }
     else gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4><<<grid, 256, 0, st>>>(p);
     return;
   }
