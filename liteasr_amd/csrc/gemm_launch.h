@@ -69,10 +69,23 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
           gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2, G_LIN, 1, 4, EPI_AUX_GATE><<<grid, 256, 0, st>>>(p);
           return;
         }
+        if (e == EPI_AUX_RELU) {  // the subsampling output projection's input gradient
+          gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2, G_LIN, 1, 4, EPI_AUX_RELU><<<grid, 256, 0, st>>>(p);
+          return;
+        }
       }
       gemm_bf16_glds_kernel<128, 256, AKC, BKC, TC, 3, 2><<<grid, 256, 0, st>>>(p);
     }
-    else if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
+    else if (BM == 128 && BN == 128) {
+      // (the CTC head and the decoder memory K/V projections: bias only)
+      if constexpr (AKC && BKC && std::is_same<TC, bf16_t>::value) {
+        if (epi_code(p) == EPI_PLAIN) {
+          gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3, 3, G_LIN, 1, 4, EPI_PLAIN><<<grid, 256, 0, st>>>(p);
+          return;
+        }
+      }
+      gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 3><<<grid, 256, 0, st>>>(p);
+    }
     else if (BM == 128) {
       // (the q/k/v projection: bias only)
       if constexpr (AKC && BKC && std::is_same<TC, bf16_t>::value) {
