@@ -277,7 +277,10 @@ def hottest_case(cfgd, dev):
     bytes_ = 2.0 * (M * D + F * D) + 2 * 2.0 * M * F + 4.0 * F
     tm, tn, _, fl = K.gemm_plan(ln, w1.t(), h, flags=True, bias=b1, act=ACT_SWISH, zout=g, zout_mode=1,
                                 drop_p=0.1, drop_seed=11)
-    inst = "2, 1, 0, 2, 8" if fl & 8 else "3, 2, 0, 1, 4"  # gemm_launch.h: wide 8-wave / 4-wave 32-deep
+    # gemm_launch.h: wide 8-wave / 4-wave 32-deep, and the compile-time epilogue it takes for this
+    # call (EPI_SWISH_GATE_DROP = 1 unless LASR_EPI_SPEC=0; the wide tile has none)
+    epi = 1 if not fl & 8 and os.environ.get("LASR_EPI_SPEC", "1") != "0" else 0
+    inst = f"2, 1, 0, 2, 8, {epi}" if fl & 8 else f"3, 2, 0, 1, 4, {epi}"
     meta = {"kernel": f"gemm_bf16_glds_kernel<{tm}, {tn}, true, true, unsigned short, {inst}>",
             "shape": f"M={M} N={F} K={D} bias+swish+gate+dropout", "grid": [-(-F // tn), -(-M // tm), 1],
             "build": build_key()}
