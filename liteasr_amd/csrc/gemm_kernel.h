@@ -814,18 +814,27 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
 #pragma unroll
     for (int u = 0; u < KS; ++u) issue_sub(k0 + u * BK, dst + u * TILE);
   };
+  // the transposed fragments' per-thread image offsets, computed once (a k step then adds
+  // only the tile's uniform LDS base: one VALU per read instead of the recomputed address)
+  [[maybe_unused]] uint32_t aoff[AKC ? 1 : FM][2], boff[BKC ? 1 : FN][2];
+  if constexpr (!AKC)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) frag_tr_offsets<BM>(wr * WM + i * 16, lane, aoff[i]);
+  if constexpr (!BKC)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) frag_tr_offsets<BN>(wc * WN + j * 16, lane, boff[j]);
   auto compute = [&](const bf16_t* cur) {
     bf16x8 af[FM], bfr[FN];
     v2i ra[2 * FM], rb[2 * FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       if constexpr (AKC) af[i] = frag<BM, true>(cur, wr * WM + i * 16, lane);
-      else frag_tr_raw<BM>(cur, wr * WM + i * 16, lane, ra + 2 * i);
+      else frag_tr_raw_at(lds_addr(cur), aoff[i], ra + 2 * i);
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       if constexpr (BKC) bfr[j] = frag<BN, true>(cur + BM * BK, wc * WN + j * 16, lane);
-      else frag_tr_raw<BN>(cur + BM * BK, wc * WN + j * 16, lane, rb + 2 * j);
+      else frag_tr_raw_at(lds_addr(cur + BM * BK), boff[j], rb + 2 * j);
     }
     if constexpr (!AKC) {
       tie_lgkm<2 * FM>(ra);

@@ -153,6 +153,22 @@ LASR_DEV void tie_lgkm(v2i* r) {
   else
     static_assert(N < 0, "tie_lgkm: unsupported count");
 }
+// Byte offsets (in the tile image) of the two halves frag_tr_raw reads for fragment rbase:
+// loop invariant per thread, so a k step adds only the uniform tile base (frag_tr_raw_at).
+template <int R_TILE>
+LASR_DEV void frag_tr_offsets(int rbase, int lane, uint32_t* o) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
+  o[0] = 2u * (uint32_t)tr_off<R_TILE>(8 * g + q, rbase + pc);
+  o[1] = 2u * (uint32_t)tr_off<R_TILE>(8 * g + 4 + q, rbase + pc);
+}
+// uniform by construction (the ring slot of a k step): readfirstlane keeps it in an SGPR
+LASR_DEV uint32_t lds_addr(const bf16_t* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lptr_t)p);
+}
+LASR_DEV void frag_tr_raw_at(uint32_t tile_base, const uint32_t* o, v2i* r) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r[0]) : "v"(tile_base + o[0]));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r[1]) : "v"(tile_base + o[1]));
+}
 // Raw halves of a transposed fragment (see frag<>): k = 8g+q and 8g+4+q rows.
 template <int R_TILE>
 LASR_DEV void frag_tr_raw(const bf16_t* tile, int rbase, int lane, v2i* r) {
@@ -235,7 +251,10 @@ LASR_DEV void glds_tile(const bf16_t* base, int64_t ld, int row0, int R, int k0,
       const int k = P / CPR, ps = P % CPR;
       const int ls = ((((ps >> 1) ^ htr<R_TILE>(k))) << 1) | (ps & 1);
       const int gc = min(row0 + ls * 8, ((R + 7) & ~7) - 8);  // host: row stride >= roundup8(R)
-      src = base + (int64_t)(k0 + k) * ld + gc;
+      // the k0 row offset is uniform (scalar multiply) and the thread's own part is loop
+      // invariant (hoisted): (k0 + k) * ld as one vector product cost three quarter-rate
+      // multiplies per load and k tile
+      src = (base + (int64_t)k0 * ld) + ((int64_t)k * ld + gc);
     }
     __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (i * NT + wid * 64) * 8), 16, 0, 0);
     (void)lane;
