@@ -14,6 +14,10 @@ Semantics kept from torch DDP: initial parameter + buffer broadcast from rank 0;
 gradient *average*; BatchNorm running stats re-broadcast from rank 0 at every forward
 (the constant positional-encoding tables are skipped -- identical on every rank);
 ``no_sync()`` skips the all-reduce for gradient accumulation (trainer.py:142-147).
+
+``comm="native"`` routes the buckets through libliteasr_comm.so (``lasr_reducer_*``,
+include/liteasr_comm.h: its own RCCL communicator and HIP stream) instead of
+``torch.distributed.all_reduce``; bucket order and finalize points are the same.
 """
 
 from __future__ import annotations
@@ -38,7 +42,8 @@ class _Unit:
 
 
 class FlatReducer:
-    def __init__(self, model, process_group=None, bucket_bytes=BUCKET_BYTES):
+    def __init__(self, model, process_group=None, bucket_bytes=BUCKET_BYTES, comm="torch"):
+        assert comm in ("torch", "native"), comm
         self.model = model
         self.store = model.store
         self.pg = process_group
@@ -70,6 +75,13 @@ class FlatReducer:
         # appended here instead of being launched; the graphed step launches them eagerly
         # between the replayed backward segments
         self.record = None
+        self.native = None
+        if comm == "native":
+            from .native_reducer import NativeReducer, unique_id
+
+            uid = unique_id(process_group)
+            spans = [(min(u.lo for u in b), max(u.hi for u in b)) for b in self.buckets]
+            self.native = NativeReducer(self.store.grad, spans, uid, self.world, dist.get_rank(process_group))
         self._reset()
         for mod in model.modules():
             if isinstance(mod, _Bound):
@@ -146,6 +158,9 @@ class FlatReducer:
         return self.store.grad[lo:hi]
 
     def _launch(self, bi):
+        if self.native is not None:  # C-ABI reducer: in-order launch on its own stream
+            self.native.mark(bi)
+            return
         g = self._slice(self.buckets[bi])
         if self.world == 1:  # the average over one rank is the identity: no collective, no RCCL kernel
             return
@@ -167,6 +182,8 @@ class FlatReducer:
     def _finalize(self):
         for bi in range(self.next_bucket, len(self.buckets)):  # units that never fired
             self._launch(bi)
+        if self.native is not None:
+            self.native.finalize()
         for w, g in self.works:
             w.wait()
             if not (g.is_cuda and dist.get_backend(self.pg) == "nccl"):
@@ -177,7 +194,7 @@ class FlatReducer:
 class DistributedDataParallel(nn.Module):
     """torch-DDP-shaped wrapper (``.module``, ``no_sync()``) around a FlatParams model."""
 
-    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_cap_mb=25, **_):
+    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_cap_mb=25, comm="torch", **_):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -192,7 +209,7 @@ class DistributedDataParallel(nn.Module):
         self._world = dist.get_world_size(process_group)
         self._sync_buffers()
         st._work_version = -1  # weights changed under the working copy
-        self.reducer = FlatReducer(module, process_group, int(bucket_cap_mb * 1024 * 1024))
+        self.reducer = FlatReducer(module, process_group, int(bucket_cap_mb * 1024 * 1024), comm=comm)
 
     def _sync_buffers(self):
         if not self._bn_buffers or self._world == 1:  # rank 0 to itself: nothing to do

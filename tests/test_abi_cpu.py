@@ -98,3 +98,22 @@ def test_decode_header_symbols_exported():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared == {"lasr_ctc_prefix_beam_search", "lasr_decode_last_error"}
     assert declared <= exported
+
+
+def test_comm_header_symbols_exported():
+    """include/liteasr_comm.h <-> libliteasr_comm.so (native bucketed reducer over RCCL) <->
+    the ctypes signature table; only the pure host size query is called (no GPU here)."""
+    hdr = os.path.join(ROOT, "include", "liteasr_comm.h")
+    so = os.path.join(ROOT, "liteasr_amd", "lib", "libliteasr_comm.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", ROOT, so], check=True, capture_output=True)
+    src = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+    declared = set(re.findall(r"\b(lasr_[a-z0-9_]+)\s*\(", src))
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert declared <= exported, declared - exported
+    from liteasr_amd.distributed import native_reducer as NR
+
+    assert set(NR._SIGS) == declared
+    L = NR.load()
+    assert L.lasr_reducer_uid_bytes() == 128  # NCCL_UNIQUE_ID_BYTES

@@ -1,0 +1,107 @@
+"""Native bucketed reducer (libliteasr_comm.so, include/liteasr_comm.h) on the GPU.
+
+World 1 only: RCCL cannot place two ranks on the one device of the test box, and the
+average over one rank is the identity, so every check is bit-exact.  The N>1 bucket logic
+(order, averaging, no_sync) is the same FlatReducer covered by the gloo tests
+(tests/test_ddp_cpu.py); this file covers the C-ABI's stream ordering, in-order launch and
+error behaviour, and that a DDP step through it equals the torch.distributed path.
+Reference mechanism: torch DDP at liteasr/trainer.py:76-88."""
+
+import os
+import random
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pg():
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        port = random.randint(20000, 40000)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    yield dist
+    dist.destroy_process_group()
+
+
+def test_reducer_in_order_launch_and_identity(pg):
+    from liteasr_amd.distributed.native_reducer import NativeReducer, unique_id
+
+    torch.cuda.set_device(0)
+    g = torch.randn(10000, device="cuda")
+    ref = g.clone()
+    r = NativeReducer(g, [(0, 3000), (3000, 7000), (7000, 10000)], unique_id(), 1, 0)
+    for step in range(2):
+        r.mark(2)
+        assert r.launched() == 0  # bucket 0 not ready: nothing may launch out of order
+        r.mark(0)
+        assert r.launched() == 1
+        r.mark(1)
+        assert r.launched() == 3
+        with pytest.raises(RuntimeError, match="marked twice"):
+            r.mark(1)
+        r.finalize()
+        torch.cuda.synchronize()
+        assert torch.equal(g, ref)
+        assert r.launched() == 0
+    # a bucket never marked is launched by finalize, on the consumer stream's order
+    g.mul_(2.0)
+    r.mark(0)
+    r.finalize()
+    torch.cuda.synchronize()
+    assert torch.equal(g, ref * 2.0)
+    with pytest.raises(RuntimeError, match="out of range"):
+        r.mark(3)
+    r.close()
+
+
+def test_reducer_rejects_bad_buckets(pg):
+    from liteasr_amd.distributed.native_reducer import NativeReducer, unique_id
+
+    g = torch.zeros(100, device="cuda")
+    uid = unique_id()
+    with pytest.raises(RuntimeError, match="overlap"):
+        NativeReducer(g, [(0, 60), (50, 100)], uid, 1, 0)
+    with pytest.raises(RuntimeError, match="outside"):
+        NativeReducer(g, [(0, 101)], uid, 1, 0)
+
+
+def test_ddp_step_native_equals_torch(pg):
+    """Eager and segmented-graph DDP steps with comm='native' (several buckets) give the
+    same losses and parameters, bit for bit, as the torch.distributed reducer."""
+    from liteasr_amd.distributed.ddp import DistributedDataParallel
+    from liteasr_amd.graph_step import GraphedTrainStep
+    from oracle import u2_oracle as O
+    from test_model_gpu import _graph_setup
+
+    torch.cuda.set_device(0)
+    out = {}
+    for comm in ("torch", "native"):
+        for mode in ("eager", "graph"):
+            m, c, o = _graph_setup(0.0)
+            net = DistributedDataParallel(m, bucket_cap_mb=0.05, comm=comm)
+            assert len(net.reducer.buckets) >= 3
+            bs = [[t.cuda() for t in O.synthetic_batch(2, 100, 5, 30, seed=80 + i)] for i in range(3)]
+            if mode == "eager":
+                losses = []
+                for b in bs:
+                    l = c(net, *b)
+                    l.backward()
+                    o.clip_and_step(5.0)
+                    o.zero_grad()
+                    losses.append(l.item())
+            else:
+                gs = GraphedTrainStep(net, c, o, bs[0], clip=5.0, warmup=1, overlap=True)
+                losses = [gs(b).item() for b in bs]
+            torch.cuda.synchronize()
+            out[comm, mode] = (losses, m.store.flat.clone())
+            if net.reducer.native is not None:
+                net.reducer.native.close()
+    for mode in ("eager", "graph"):
+        lt, ft = out["torch", mode]
+        ln, fn = out["native", mode]
+        assert lt == ln, (mode, lt, ln)
+        assert torch.equal(ft, fn), mode
