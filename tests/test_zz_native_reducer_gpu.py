@@ -1,4 +1,4 @@
-"""Native bucketed reducer (libliteasr_comm.so, include/liteasr_comm.h) on the GPU.
+"""(Named to run after the other GPU suites.) Native bucketed reducer (libliteasr_comm.so, include/liteasr_comm.h) on the GPU.
 
 World 1 only: RCCL cannot place two ranks on the one device of the test box, and the
 average over one rank is the identity, so every check is bit-exact.  The N>1 bucket logic
