@@ -444,6 +444,29 @@ def pmc_traffic(meta):
     return None
 
 
+def pmc_mfma(cfg_name):
+    """MFMA busy fraction from the committed counter pass of the same library build and config
+    (profiles/*/pmc_mfma_summary*.json, tools/pmc_mfma.py over a rocprofv3
+    SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE pass of an eager `bench.py --graph off` run);
+    None when no pass matches this build."""
+    import glob
+
+    key = build_key()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_mfma_summary*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("build") == key and d.get("config", "small") == cfg_name:
+            top = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in t.items()}
+                   for t in d.get("top_kernels", [])[:6]]
+            return {"mfma_busy_frac": round(d["mfma_util_all_kernels"], 4), "source": os.path.relpath(path, ROOT),
+                    "note": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs), cycle-weighted over "
+                            "the kernels of eager steps (counter mode serialises dispatches: a lower bound)",
+                    "top_kernels": top}
+    return None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -546,6 +569,13 @@ def main():
     ap.add_argument("--overlap", default="on", choices=["on", "off"],
                     help="N>1 graphed step: all-reduce each gradient bucket between backward segments "
                          "(on) or after the whole backward (off)")
+    ap.add_argument("--comm", default="torch", choices=["torch", "native"],
+                    help="gradient all-reduce path (N>1 or --force-ddp): torch.distributed over RCCL, or "
+                         "the C-ABI bucketed reducer libliteasr_comm.so (lasr_reducer_*, its own RCCL "
+                         "communicator and stream)")
+    ap.add_argument("--profile", action="store_true",
+                    help="roctx ranges around every fused autograd node (liteasr_amd.utils.markers); "
+                         "implies --graph off (ranges are host-side launch spans)")
     ap.add_argument("--force-ddp", action="store_true",
                     help="wrap in the DDP reducer even at N=1 (world-1 RCCL group; profiling the overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -560,6 +590,11 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.profile:
+        from liteasr_amd.utils import markers
+
+        markers.enable()
+        args.graph = "off"
     if args.roofline_only:
         torch.cuda.set_device(0)
         if args.roofline_case == "family":
@@ -613,7 +648,7 @@ def main():
     if use_ddp:
         from liteasr_amd.distributed.ddp import DistributedDataParallel
 
-        net = DistributedDataParallel(model)
+        net = DistributedDataParallel(model, comm=args.comm)
     crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=V, smoothing=0.1, ctc_weight=cfgd["w"]))
     opt = Noam(model.parameters(), NoamConfig(model_dim=cfgd["d"]))
     batch = synthetic(cfgd, rank, dev)
@@ -638,9 +673,14 @@ def main():
     if use_ddp:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step HIP events on the stream the step runs on (no host sync inside the loop): the
+    # median step beside the wall-clock mean the contract's ms_per_step reports
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         loss = step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if use_ddp:
         dist.barrier()
@@ -650,6 +690,13 @@ def main():
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
+    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    med = per_step[len(per_step) // 2] if args.steps % 2 else 0.5 * (per_step[len(per_step) // 2 - 1] +
+                                                                     per_step[len(per_step) // 2])
+    if world > 1:
+        t = torch.tensor([med], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        med = t.item()
     final_loss = loss.item()
     launcher = "bench.py spawn" if os.environ.get("LASR_BENCH_SPAWNED") else (
         "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "env")
@@ -660,6 +707,8 @@ def main():
             "metric": "utterances/sec (U2-Conformer+CTC, 80-d fbank T≈1000) at 1/2/4/8 MI355X",
             "value": round(utt, 2), "unit": "utterances/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "ms_per_step_median": round(med, 3),
+            "ms_per_step_events_min_max": [round(per_step[0], 3), round(per_step[-1], 3)],
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (SURVEY §8d: N(0,1) 80-d fbank, xlens~U[0.95T,T], random token ids), random-init weights",
             "config": {"workload": f"U2-Conformer-{args.config} hybrid CTC-attention training step "
@@ -672,7 +721,8 @@ def main():
                        "ranks_seen": dist.get_world_size() if dist.is_initialized() else world,
                        "rank_launcher": launcher,
                        "allreduce": None if not use_ddp else
-                       {"backend": dist.get_backend(), "buckets": len(net.reducer.buckets),
+                       {"backend": dist.get_backend(), "comm": args.comm, "buckets": len(net.reducer.buckets),
+                        "bucket_mb_each": [round((hi - lo) * 4 / 1e6, 2) for lo, hi in net.reducer.native_spans()],
                         "bucket_mb": 25, "overlap": args.overlap == "on" and args.graph == "on" or args.graph == "off",
                         "segments": len(step.segs) if args.graph == "on" and step.segs else None,
                         "timeline_last_step": step.overlap_report() if args.graph == "on" else None}},
@@ -680,6 +730,9 @@ def main():
             "step_mfma_frac": round(cfgd["gflop"] * utt / world / 1e3 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(final_loss, 4), "optimizer_state": st,
         }
+        if args.profile:
+            out["config"]["profile"] = "roctx ranges per fused node (eager)"
+        out["mfma_counter"] = pmc_mfma(args.config)
         if not args.no_roofline:
             out["roofline"] = dominant_kernel_roofline(cfgd, dev)
             out["ctc"] = ctc_roofline(cfgd, dev)
@@ -687,6 +740,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.config)
         print(json.dumps(out), flush=True)
     if use_ddp:
+        net.close()
         dist.destroy_process_group()
 
 

@@ -63,6 +63,19 @@ int lasr_reducer_finalize(lasr_reducer* r, hipStream_t consumer);
 /* number of buckets launched so far in the current step */
 int lasr_reducer_launched(const lasr_reducer* r);
 
+/* Abandon the current step's bookkeeping (marked flags, next bucket) without launching
+ * anything: after a backward that stopped part-way (an exception, an abandoned capture).
+ * Collectives already launched stay in flight on the reducer's stream. */
+int lasr_reducer_reset(lasr_reducer* r);
+
+/* Point the reducer at a new gradient buffer of the same numel (the caller reallocated it,
+ * e.g. a device move of the model).  Only between steps. */
+int lasr_reducer_rebind(lasr_reducer* r, float* grad, int64_t numel);
+
+/* the gradient buffer the reducer currently averages */
+const float* lasr_reducer_grad(const lasr_reducer* r);
+
+/* drains the reducer's stream (on its device), then frees it and, if owned, the communicator */
 int lasr_reducer_destroy(lasr_reducer* r);
 
 const char* lasr_comm_last_error(void);

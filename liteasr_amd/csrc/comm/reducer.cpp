@@ -40,6 +40,7 @@ struct lasr_reducer {
   bool owns_comm = false;
   int device = 0;
   float* grad = nullptr;
+  int64_t numel = 0;
   std::vector<int64_t> lo, hi;
   std::vector<char> marked;
   int next = 0;               // next bucket to launch (strict order)
@@ -49,6 +50,18 @@ struct lasr_reducer {
 };
 
 namespace {
+
+// Selects `device` for the scope and restores the caller's device afterwards.
+struct DeviceGuard {
+  int prev = -1, rc = 0;
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    rc = hipSetDevice(device) != hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 int check_buckets(int64_t numel, const int64_t* lo, const int64_t* hi, int n) {
   if (n <= 0 || !lo || !hi) return fail(-1, "no buckets");
@@ -72,8 +85,12 @@ int setup(lasr_reducer* r, int device, float* grad, int64_t numel, const int64_t
   r->grad = grad;
   r->lo.assign(lo, lo + n);
   r->hi.assign(hi, hi + n);
+  r->numel = numel;
   r->marked.assign(n, 0);
-  HIP_TRY(hipSetDevice(device));
+  // the caller's current device is restored on return (the stream and events belong to
+  // `device`, whatever device the training thread has selected)
+  DeviceGuard dg(device);
+  if (dg.rc) return fail(-2, "hipSetDevice failed");
   HIP_TRY(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
   r->ready.assign(n, nullptr);
   for (int b = 0; b < n; ++b) HIP_TRY(hipEventCreateWithFlags(&r->ready[b], hipEventDisableTiming));
@@ -89,6 +106,8 @@ int launch(lasr_reducer* r, int b) {
 }
 
 void release(lasr_reducer* r) {
+  DeviceGuard dg(r->device);  // the stream, events and communicator live on r->device
+  if (r->stream) (void)hipStreamSynchronize(r->stream);
   for (hipEvent_t e : r->ready)
     if (e) (void)hipEventDestroy(e);
   if (r->done) (void)hipEventDestroy(r->done);
@@ -182,10 +201,28 @@ int lasr_reducer_finalize(lasr_reducer* r, hipStream_t consumer) {
 
 int lasr_reducer_launched(const lasr_reducer* r) { return r ? r->next : -1; }
 
+int lasr_reducer_reset(lasr_reducer* r) {
+  if (!r) return fail(-1, "null reducer");
+  std::fill(r->marked.begin(), r->marked.end(), 0);
+  r->next = 0;
+  return 0;
+}
+
+int lasr_reducer_rebind(lasr_reducer* r, float* grad, int64_t numel) {
+  if (!r || !grad) return fail(-1, "null argument");
+  if (numel != r->numel)
+    return fail(-1, "rebind: numel " + std::to_string(numel) + " != " + std::to_string(r->numel));
+  if (r->next != 0 || std::find(r->marked.begin(), r->marked.end(), 1) != r->marked.end())
+    return fail(-1, "rebind inside a step (buckets already marked)");
+  r->grad = grad;
+  return 0;
+}
+
+const float* lasr_reducer_grad(const lasr_reducer* r) { return r ? r->grad : nullptr; }
+
 int lasr_reducer_destroy(lasr_reducer* r) {
   if (!r) return 0;
-  (void)hipStreamSynchronize(r->stream);
-  release(r);
+  release(r);  // selects r->device, drains the stream, frees events / stream / communicator
   return 0;
 }
 

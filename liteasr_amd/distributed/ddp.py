@@ -82,6 +82,10 @@ class FlatReducer:
             uid = unique_id(process_group)
             spans = [(min(u.lo for u in b), max(u.hi for u in b)) for b in self.buckets]
             self.native = NativeReducer(self.store.grad, spans, uid, self.world, dist.get_rank(process_group))
+            # multi-rank behaviour of the second communicator is checked once, at the first
+            # step with world > 1 (``_verify_native``): the pre-reduction gradient is kept
+            self._verify = self.world > 1
+            self._pre = None
         self._reset()
         for mod in model.modules():
             if isinstance(mod, _Bound):
@@ -113,11 +117,33 @@ class FlatReducer:
         units_sorted[-1].hi = st.numel
         return units
 
+    def native_spans(self):
+        """(lo, hi) element range of every bucket, in launch order."""
+        return [(min(u.lo for u in b), max(u.hi for u in b)) for b in self.buckets]
+
     def _reset(self):
         self.ready = [0] * len(self.buckets)
         self.works = []
         self.next_bucket = 0
         self.active = False
+        if self.native is not None:  # a backward abandoned part-way leaves C-side marks too
+            self.native.reset()
+
+    def _native_bound(self):
+        """The C reducer averages the buffer it was given at creation; a device move of the
+        model (ParamStore.apply) or a re-allocated gradient replaces ``store.grad``, so rebind
+        it (between steps) instead of silently averaging the old buffer."""
+        g = self.store.grad
+        if self.native.grad_ptr() != g.data_ptr():
+            if self.native.launched() or any(self.ready):
+                raise RuntimeError("FlatReducer: the flat gradient buffer was replaced inside a step")
+            self.native.rebind(g)
+
+    def close(self):
+        """Free the native reducer (its RCCL communicator and HIP stream) now, not at GC."""
+        if self.native is not None:
+            self.native.close()
+            self.native = None
 
     def _on_ready(self, mod):
         if not self.enabled:
@@ -159,6 +185,13 @@ class FlatReducer:
 
     def _launch(self, bi):
         if self.native is not None:  # C-ABI reducer: in-order launch on its own stream
+            if bi == 0 or self.native.launched() == 0:
+                self._native_bound()
+            if self._verify:
+                if self._pre is None:
+                    self._pre = {}
+                lo, hi = self.native_spans()[bi]
+                self._pre[bi] = self.store.grad[lo:hi].clone()
             self.native.mark(bi)
             return
         g = self._slice(self.buckets[bi])
@@ -183,12 +216,33 @@ class FlatReducer:
         for bi in range(self.next_bucket, len(self.buckets)):  # units that never fired
             self._launch(bi)
         if self.native is not None:
+            self._native_bound()
             self.native.finalize()
+            if self._verify and self._pre is not None:
+                self._verify_native()
         for w, g in self.works:
             w.wait()
             if not (g.is_cuda and dist.get_backend(self.pg) == "nccl"):
                 g.div_(self.world)
         self._reset()
+
+
+    def _verify_native(self):
+        """Once, at the first step with world > 1: every bucket the C reducer averaged must equal
+        a torch.distributed average of the same pre-reduction gradient (the two communicators
+        may sum in different orders: fp32 tolerance)."""
+        self._verify = False
+        pre, self._pre = self._pre, None
+        for bi, (lo, hi) in enumerate(self.native_spans()):
+            ref = pre[bi]
+            dist.all_reduce(ref, op=dist.ReduceOp.SUM, group=self.pg)
+            ref.div_(self.world)
+            got = self.store.grad[lo:hi]
+            tol = 1e-5 * max(1.0, ref.abs().max().item())
+            err = (got - ref).abs().max().item()
+            if err > tol:
+                raise RuntimeError(f"native reducer: bucket {bi} differs from torch.distributed's average "
+                                   f"by {err:.3g} (tolerance {tol:.3g})")
 
 
 class DistributedDataParallel(nn.Module):
@@ -221,6 +275,10 @@ class DistributedDataParallel(nn.Module):
         else:
             for b in self._bn_buffers:
                 dist.broadcast(b, 0, group=self.process_group)
+
+    def close(self):
+        """Release the reducer's native resources (comm="native") before interpreter teardown."""
+        self.reducer.close()
 
     def __getattr__(self, name):
         try:

@@ -35,6 +35,9 @@ _SIGS = {
     "lasr_reducer_mark_grad_ready": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "lasr_reducer_finalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "lasr_reducer_launched": (ctypes.c_int, [ctypes.c_void_p]),
+    "lasr_reducer_reset": (ctypes.c_int, [ctypes.c_void_p]),
+    "lasr_reducer_rebind": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "lasr_reducer_grad": (ctypes.c_void_p, [ctypes.c_void_p]),
     "lasr_reducer_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "lasr_comm_last_error": (ctypes.c_char_p, []),
 }
@@ -97,6 +100,19 @@ class NativeReducer:
 
     def launched(self) -> int:
         return load().lasr_reducer_launched(self._h)
+
+    def reset(self):
+        """Drop the current step's marks (an abandoned backward); launches nothing."""
+        _check(load().lasr_reducer_reset(self._h), "lasr_reducer_reset")
+
+    def grad_ptr(self) -> int:
+        return load().lasr_reducer_grad(self._h) or 0
+
+    def rebind(self, grad: torch.Tensor):
+        """Average ``grad`` from now on (same numel; between steps only)."""
+        assert grad.is_cuda and grad.dtype == torch.float32 and grad.is_contiguous()
+        _check(load().lasr_reducer_rebind(self._h, grad.data_ptr(), grad.numel()), "lasr_reducer_rebind")
+        self.grad = grad
 
     def close(self):
         if self._h:

@@ -28,6 +28,7 @@ import torch
 
 from .. import kernels as K
 from .._native import ACT_GATE, ACT_NONE, ACT_RELU, ACT_SWISH, ACT_TANH
+from ..utils.markers import ranged
 
 F32 = torch.float32
 LN_EPS = 1e-12
@@ -488,6 +489,7 @@ def _conv2_implicit(adt, C):
 
 
 # ============================================================ autograd nodes ====
+@ranged
 class EmbedFn(torch.autograd.Function):
     """Conv2DLayer (liteasr/nets/subsampling.py:42-48) + RelativePositionalEncoding's
     x*sqrt(d) and dropout (positional_encoding.py:68-75).  Channels-last throughout;
@@ -587,6 +589,7 @@ def enc_attn_backward(gb, ln, pos, sv, w, g, env, p_att, s_att, lnb):
     return None
 
 
+@ranged
 class ConformerLayerFn(torch.autograd.Function):
     """RelativeEncoderLayer.forward (liteasr/nets/conformer_layer.py:130-147), pre-norm."""
 
@@ -713,6 +716,7 @@ class ConformerLayerFn(torch.autograd.Function):
         return dx0, None, None, None, None
 
 
+@ranged
 class TransformerLayerFn(torch.autograd.Function):
     """Transformer encoder layer (enc_arch "transformer"; liteasr/nets/transformer_layer.py:
     EncoderLayer.forward :64-76 / RelativeEncoderLayer.forward :119-136), pre-norm:
@@ -880,6 +884,7 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
     return dy
 
 
+@ranged
 class HeadsFn(torch.autograd.Function):
     """Encoder after_norm (transformer_encoder.py:126), CTC head with its always-on
     input dropout (ctc.py:28-30) and the full Transformer decoder
@@ -951,6 +956,7 @@ class HeadsFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+@ranged
 class ParaformerHeadsFn(torch.autograd.Function):
     """Everything of Paraformer.forward after the conformer layers (liteasr/models/
     paraformer.py:97-113): encoder after_norm, the CIF predictor (predictor.py:24-118:
@@ -1083,6 +1089,7 @@ class ParaformerHeadsFn(torch.autograd.Function):
         return dx, None, None, None, None, None, None
 
 
+@ranged
 class ParaformerLossFn(torch.autograd.Function):
     """ParaformerLoss.__call__ (liteasr/criterions/paraformer_loss.py:39-56):
     gamma * CE(hs_attn, ys; ignore -1, mean over targets) + mean |sum_alpha - ylens|."""
@@ -1112,6 +1119,7 @@ class ParaformerLossFn(torch.autograd.Function):
         return ga, gsum, None, None, None, None, None
 
 
+@ranged
 class HybridLossFn(torch.autograd.Function):
     """HybridCTCLoss.__call__ (liteasr/criterions/hybrid_ctc_attn.py:39-79):
     ctc_weight * CTC(sum)/B + (1 - ctc_weight) * smoothed-KL(sum)/B.
@@ -1161,6 +1169,7 @@ class HybridLossFn(torch.autograd.Function):
         return ga.view(sv.shapes[0]), gc.view(sv.shapes[1]), None, None, None, None
 
 
+@ranged
 class EncoderOutFn(torch.autograd.Function):
     """Encoder after_norm (transformer_encoder.py:126) as its own autograd node, for heads
     other than U2's HeadsFn (encoder reuse, SURVEY §8 f4: Transducer / Paraformer heads
@@ -1247,6 +1256,7 @@ def lstm_layer_bwd(dY, sv, w, g, B, U1, H, adt, p_out, seed):
     return dX
 
 
+@ranged
 class TransducerHeadsFn(torch.autograd.Function):
     """Everything of Transducer.forward after the conformer layers (liteasr/models/
     transducer.py:106-121,199-203): encoder after_norm, lin_enc, the prediction network
@@ -1335,6 +1345,7 @@ class TransducerHeadsFn(torch.autograd.Function):
         return dx, None, None, None, None, None
 
 
+@ranged
 class RNNTLossFn(torch.autograd.Function):
     """RNNTLoss (liteasr/criterions/rnnt.py:53-72): batch mean of -log P(y|x) over the raw
     joint logits [B, T, U1, V] with the log-softmax fused (csrc/rnnt.hip); the backward

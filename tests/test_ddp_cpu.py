@@ -282,3 +282,54 @@ def test_flat_ddp_other_heads_gloo_world2(which):
     nz = g[g != 0]
     assert nz.numel() == g.numel() - int((g == 0).sum())
     assert torch.allclose(nz / 1.5, torch.round(nz / 1.5))  # ((0+1) i + (1+1) i) / 2
+
+
+def _spans_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bench import CONFIGS, build
+        from liteasr_amd.distributed.ddp import FlatReducer
+
+        out = {}
+        for name, model in (("tiny", _tiny()), ("small", build(CONFIGS["small"], "bf16", 0.1, "cpu"))):
+            red = FlatReducer(model, bucket_bytes=25 * 1024 * 1024 if name == "small" else 2048)
+            out[name] = (red.native_spans(), [[u.name for u in b] for b in red.buckets], model.store.numel,
+                         [str(red._slice(b).data_ptr() - model.store.grad.data_ptr() if model.store.grad is not None
+                              else "") for b in red.buckets])
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_spans_tile_flat_buffer_in_bucket_order():
+    """The (lo, hi) spans the native reducer is given (FlatReducer.native_spans) are exactly the
+    buckets' flat slices, in launch order, and tile [0, numel) with no gap or overlap; the
+    launch order is backward-completion order (heads first, subsampling last).  For the small
+    config the last bucket -- the one only the final backward segment precedes -- is the
+    subsampling alone (7.35 MB of 184.8 MB)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    p = ctx.Process(target=_spans_worker, args=(0, 1, port, q))
+    p.start()
+    out = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for name, (spans, units, numel, _) in out.items():
+        cover = sorted(spans)
+        assert cover[0][0] == 0 and cover[-1][1] == numel, name
+        for (a0, a1), (b0, b1) in zip(cover, cover[1:]):
+            assert a1 == b0, (name, a1, b0)
+        # launch order walks the flat buffer from the heads' end downwards (encoder layers are
+        # laid out 0..n-1, and backward completes n-1..0)
+        assert units[0][0] == "ctc" and units[-1][-1] == "encoder.embed", (name, units)
+    spans, units, numel, _ = out["small"]
+    assert units[-1] == ["encoder.embed"]
+    lo, hi = spans[-1]
+    assert abs((hi - lo) * 4 / 1e6 - 7.35) < 0.05 and len(spans) == 6

@@ -1,4 +1,4 @@
-"""(Named to run after the other GPU suites.) Native bucketed reducer (libliteasr_comm.so, include/liteasr_comm.h) on the GPU.
+"""Native bucketed reducer (libliteasr_comm.so, include/liteasr_comm.h) on the GPU.
 
 World 1 only: RCCL cannot place two ranks on the one device of the test box, and the
 average over one rank is the identity, so every check is bit-exact.  The N>1 bucket logic
@@ -18,13 +18,18 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def pg():
+    """A world-1 gloo group for the unique-id broadcast; destroyed only if this fixture made it
+    (the suite passes in any order next to other modules' groups)."""
     import torch.distributed as dist
 
+    made = False
     if not dist.is_initialized():
         port = random.randint(20000, 40000)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        made = True
     yield dist
-    dist.destroy_process_group()
+    if made and dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def test_reducer_in_order_launch_and_identity(pg):
@@ -34,6 +39,13 @@ def test_reducer_in_order_launch_and_identity(pg):
     g = torch.randn(10000, device="cuda")
     ref = g.clone()
     r = NativeReducer(g, [(0, 3000), (3000, 7000), (7000, 10000)], unique_id(), 1, 0)
+    try:
+        _in_order(r, g, ref)
+    finally:
+        r.close()
+
+
+def _in_order(r, g, ref):
     for step in range(2):
         r.mark(2)
         assert r.launched() == 0  # bucket 0 not ready: nothing may launch out of order
@@ -55,7 +67,22 @@ def test_reducer_in_order_launch_and_identity(pg):
     assert torch.equal(g, ref * 2.0)
     with pytest.raises(RuntimeError, match="out of range"):
         r.mark(3)
-    r.close()
+    # an abandoned step (buckets marked, backward stopped) is cleared by reset: the next
+    # step marks from scratch without "marked twice" / out-of-order errors
+    r.mark(0)
+    r.mark(1)
+    r.reset()
+    assert r.launched() == 0
+    for b in (0, 1, 2):
+        r.mark(b)
+    r.finalize()
+    torch.cuda.synchronize()
+    # rebind to a new buffer of the same size; a different size is refused
+    g2 = torch.randn_like(g)
+    r.rebind(g2)
+    assert r.grad_ptr() == g2.data_ptr()
+    with pytest.raises(RuntimeError, match="numel"):
+        r.rebind(torch.zeros(5, device="cuda"))
 
 
 def test_reducer_rejects_bad_buckets(pg):
@@ -67,6 +94,39 @@ def test_reducer_rejects_bad_buckets(pg):
         NativeReducer(g, [(0, 60), (50, 100)], uid, 1, 0)
     with pytest.raises(RuntimeError, match="outside"):
         NativeReducer(g, [(0, 101)], uid, 1, 0)
+
+
+def test_reducer_keeps_caller_device_and_follows_buffer_swap(pg):
+    """the reducer must not change the caller's current device, and a flat gradient
+    buffer replaced after wrapping (a device move re-allocates it) is rebound, not silently
+    left behind; a FlatReducer reset mid-step clears the C-side marks too."""
+    from liteasr_amd.distributed.ddp import DistributedDataParallel
+    from oracle import u2_oracle as O
+    from test_model_gpu import _graph_setup
+
+    torch.cuda.set_device(0)
+    m, c, o = _graph_setup(0.0)
+    net = DistributedDataParallel(m, bucket_cap_mb=0.05, comm="native")
+    try:
+        red = net.reducer
+        assert torch.cuda.current_device() == 0
+        b = [t.cuda() for t in O.synthetic_batch(2, 100, 5, 30, seed=81)]
+        # partial step: mark two buckets then abandon it
+        red._launch(0)
+        red.next_bucket = 1
+        red._reset()
+        assert red.native.launched() == 0
+        # replace the gradient buffer under the reducer (what ParamStore.apply does on a move)
+        old = m.store.grad.data_ptr()
+        m.store.grad = m.store.grad.clone()
+        m.store.generation += 1
+        assert m.store.grad.data_ptr() != old
+        l = c(net, *b)
+        l.backward()
+        torch.cuda.synchronize()
+        assert red.native.grad_ptr() == m.store.grad.data_ptr()
+    finally:
+        net.close()
 
 
 def test_ddp_step_native_equals_torch(pg):
@@ -98,8 +158,7 @@ def test_ddp_step_native_equals_torch(pg):
                 losses = [gs(b).item() for b in bs]
             torch.cuda.synchronize()
             out[comm, mode] = (losses, m.store.flat.clone())
-            if net.reducer.native is not None:
-                net.reducer.native.close()
+            net.close()
     for mode in ("eager", "graph"):
         lt, ft = out["torch", mode]
         ln, fn = out["native", mode]

@@ -2,7 +2,7 @@
 
   rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d D -o run \
       -- python3 bench.py --graph off --steps 3 --warmup 1 --no-cpu-baseline --no-roofline
-  python tools/pmc_mfma.py D/run_counter_collection.csv [--skip-steps-frac F]
+  python tools/pmc_mfma.py D/run_counter_collection.csv [CONFIG]
 
 Per dispatch: elapsed shader cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs,
 MI355X_MICROARCH.md "DVFS give-back"); MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES /
@@ -13,13 +13,14 @@ cycle-weighted utilisation and the top kernels by elapsed cycles.
 
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 
 SIMDS = 256 * 4
 
 
-def main(path):
+def main(path, config="small"):
     rows = defaultdict(lambda: defaultdict(float))  # dispatch id -> counter -> value
     name = {}
     with open(path) as f:
@@ -38,7 +39,11 @@ def main(path):
     busy = sum(v[1] for v in per.values())
     el = sum(v[2] for v in per.values())
     top = sorted(per.items(), key=lambda kv: -kv[1][2])[:15]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import build_key  # the library build the pass measured (bench.pmc_mfma matches on it)
+
     out = {
+        "build": build_key(), "config": config,
         "dispatches": sum(v[0] for v in per.values()),
         "mfma_util_all_kernels": busy / (el * SIMDS) if el else None,
         "elapsed_cycles_sum": el,
@@ -49,4 +54,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *(sys.argv[2:3]))
