@@ -90,6 +90,12 @@ typedef struct lasr_gemm_args {
    * separate column sum of dY (aten sum over rows in Linear's backward). */
   float* rowsum;
   int zout_mode;
+  /* per-call plan overrides (0 = the planner's choice), for A/B measurements and the
+   * bit-identity tests: the bf16 LDS-DMA tile (64/128/256 x 64/128/256) and the k depth of
+   * its ring stages (1 = 32-deep, 2 = 64-deep: two 32-deep sub-tiles per counted wait).
+   * A tile or stage depth never changes any output's summation order. */
+  int tile_m, tile_n;
+  int ksub;
 } lasr_gemm_args;
 int lasr_gemm(const lasr_gemm_args* args, void* stream);
 /* Dropout: one 32-bit counter-hash draw per element pair, 16-bit halves against
@@ -105,16 +111,6 @@ float lasr_dropout_scale(float p);
 #define LASR_PLAN_KSUB2 4 /* 64-deep LDS ring stages (two 32-deep sub-tiles per wait) */
 #define LASR_PLAN_WIDE 8  /* 256 x 256 tile on 8 waves (512-thread workgroups) */
 int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* split_k, int* flags);
-/* Tuning hook: force the bf16 LDS-DMA tile (64/128/256 x 64/128/256) of every later
- * lasr_gemm call in the process; (0, 0) restores the planner.  Benchmarks only. */
-int lasr_gemm_force_tile(int tile_m, int tile_n);
-/* Tuning hook: force the split-K factor of auto-split calls and the LDS ring depth (3..6)
- * of split-K LDS-DMA launches; (0, 0) restores the planner.  Benchmarks only. */
-int lasr_gemm_force_split(int split_k, int stages);
-/* Tuning hook: force the k depth of the bf16 LDS-DMA ring stages of every later lasr_gemm
- * call (1 = 32-deep stages, 2 = 64-deep: two 32-deep sub-tiles per counted wait + barrier);
- * 0 restores the planner.  Benchmarks only. */
-int lasr_gemm_force_ksub(int ksub);
 
 /* Grouped split-K weight gradients (liteasr/trainer.py:142 loss.backward: the per-module
  * weight gradients of one Conformer layer / the decoder): n <= 8 independent partials-only

@@ -45,6 +45,7 @@ class GemmArgs(C.Structure):
         ("split_k", _i), ("workspace", _p), ("workspace_bytes", _l),
         ("rowsum", _p),
         ("zout_mode", _i),
+        ("tile_m", _i), ("tile_n", _i), ("ksub", _i),
     ]
 
 
@@ -105,9 +106,6 @@ SIGNATURES = {
     "lasr_counter_add": [_p, _u, _p],
     "lasr_gemm": [C.POINTER(GemmArgs), _p],
     "lasr_gemm_plan": [C.POINTER(GemmArgs), _p, _p, _p, _p],
-    "lasr_gemm_force_tile": [C.c_int, C.c_int],
-    "lasr_gemm_force_split": [C.c_int, C.c_int],
-    "lasr_gemm_force_ksub": [C.c_int],
     "lasr_gemm_dw_group": [C.POINTER(GemmArgs), _i, _p],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_attn_fwd": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],

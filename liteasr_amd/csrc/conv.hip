@@ -731,11 +731,7 @@ extern "C" int lasr_conv1_fwd(const float* x, int B, int T, int F, int C, const 
   const size_t shm = (size_t)(3 * F + 10 * C) * sizeof(float);
   LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_conv1_fwd: too much LDS");
   hipStream_t st = (hipStream_t)stream;
-  static const int rpb = [] {  // rows per block (LASR_C1F_ROWS: A/B)
-    const char* e = getenv("LASR_C1F_ROWS");
-    const int v = e && e[0] ? atoi(e) : C1F_ROWS;
-    return v >= 1 && v <= 32 ? v : C1F_ROWS;
-  }();
+  constexpr int rpb = C1F_ROWS;  // rows per block
   if (C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)y1 & 15) == 0 &&
       (size_t)rpb * 3 * F * sizeof(float) <= 64 * 1024) {
     const size_t shv = (size_t)rpb * 3 * F * sizeof(float);
@@ -755,9 +751,8 @@ extern "C" int lasr_conv1_bwd(const float* x, int B, int T, int F, int C, const 
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const int nrows = B * T1;
   // rows per block: 16 (998 blocks at config 2, four per CU: twice the loads in flight of
-  // 32-row blocks, 143 -> 108 us standalone, tools/conv1_bench.py); LASR_C1B_ROWS=32 for A/B
-  static const int rpb_env = [] { const char* e = getenv("LASR_C1B_ROWS"); return e && e[0] ? atoi(e) : C1B_ROWS; }();
-  const int rpb = rpb_env >= 8 && rpb_env <= C1V_ROWS ? rpb_env : C1B_ROWS;
+  // 32-row blocks, 143 -> 108 us standalone, tools/conv1_bench.py)
+  constexpr int rpb = C1B_ROWS;
   const bool vec = C % 8 == 0 && 256 % (C / 8) == 0 && ((uintptr_t)dy1 & 15) == 0 &&
                    (size_t)(rpb * 3 * F + 8 * 256) * sizeof(float) <= 64 * 1024;
   const int nparts = (int)cdiv(nrows, vec ? rpb : C1B_ROWS);

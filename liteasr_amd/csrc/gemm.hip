@@ -17,14 +17,8 @@
 #include "gemm_kernel.h"
 
 // ================================ host launcher ==================================
-int g_stages = 0;  // lasr_gemm_force_split (tuning hook)
-// Ring depth of the 64 x 64 tiles with 64-deep stages (LASR_KS2_STAGES, read once at load;
-// 3 or 4): S - 1 stages in flight per workgroup.
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && v[0] ? atoi(v) : dflt;
-}
-int g_ks2_stages = env_int("LASR_KS2_STAGES", 3);
+// The launcher keeps no process-wide state: tile / stage-depth overrides are per-call fields of
+// lasr_gemm_args (tile_m, tile_n, ksub; 0 = the planner's choice).
 
 // bf16 launch table: gemm_launch.h, instantiated per operand layout in gemm_l{0..3}.hip
 template <bool AKC, bool BKC, typename TC>
@@ -52,45 +46,6 @@ static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int
     else if (bkc) gemm_f32_kernel<false, true, TC><<<grid, 256, 0, st>>>(p);
     else gemm_f32_kernel<false, false, TC><<<grid, 256, 0, st>>>(p);
   }
-}
-
-static bool getenv_flag(const char* name) {
-  static int cached = -1;  // read once (A/B switch for benchmarking the register-staged path)
-  if (cached < 0) {
-    const char* v = getenv(name);
-    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
-  }
-  return cached == 1;
-}
-
-// Tuning hook (tools/gemm_graph_bench.py): force the LDS-DMA tile of every later call;
-// 0 = the planner's choice.  Process-wide, not for product use.
-int g_tile_m = 0, g_tile_n = 0, g_split = 0, g_ksub = 0;
-extern "C" int lasr_gemm_force_tile(int tile_m, int tile_n) {
-  const bool ok = (tile_m == 0 && tile_n == 0) ||
-                  ((tile_m == 64 || tile_m == 128 || tile_m == 256) &&
-                   (tile_n == 64 || tile_n == 128 || tile_n == 256) && (tile_m < 256 || tile_n >= 128) &&
-                   (tile_n < 256 || tile_m >= 128));
-  LASR_CHECK_ARG(ok, "lasr_gemm_force_tile: unsupported tile");
-  g_tile_m = tile_m;
-  g_tile_n = tile_n;
-  return LASR_OK;
-}
-
-// Tuning hook: force the split-K factor of autosplit calls and the ring depth of split-K
-// LDS-DMA launches (0 = planner).  Benchmarks only.
-extern "C" int lasr_gemm_force_split(int split_k, int stages) {
-  LASR_CHECK_ARG(split_k >= 0 && split_k <= 64 && (stages == 0 || (stages >= 3 && stages <= 6)),
-                 "lasr_gemm_force_split: bad arguments");
-  g_split = split_k;
-  g_stages = stages;
-  return LASR_OK;
-}
-
-extern "C" int lasr_gemm_force_ksub(int ksub) {
-  LASR_CHECK_ARG(ksub >= 0 && ksub <= 2, "lasr_gemm_force_ksub: ksub must be 0, 1 or 2");
-  g_ksub = ksub;
-  return LASR_OK;
 }
 
 // Tile and split-K choice for one call (shared by lasr_gemm and lasr_gemm_plan).  nwo: 8 for
@@ -155,12 +110,11 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)batch;
     while (nb * split < 512 && split * 2 <= 32 && kt / (split * 2) >= 4) split *= 2;
   }
-  if (bf && g_tile_m) {
-    BM = g_tile_m;
-    BN = g_tile_n;
+  if (bf && a->tile_m) {  // per-call override (A/B tools, bit-identity tests)
+    BM = a->tile_m;
+    BN = a->tile_n;
     nw = 4;
   }
-  if (autosplit && g_split) split = g_split;
   if (a->split_k <= -2 && plain && a->workspace) split = -a->split_k;  // explicit partials-only
   const int64_t rs_floats = a->rowsum ? (int64_t)split * a->M : 0;
   if (split > 1 && ((!plain && !autosplit) || !a->workspace ||
@@ -174,7 +128,7 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
     const bool small = BM * BN <= 64 * 128;
     *kso = (bf && BM < 256 && BN < 256 && ((BM == 64 && BN == 64) || kc >= 1024 || (kc >= 512 && small))) ? 2 : 1;
     if (nw == 8) *kso = 2;
-    else if (g_ksub) *kso = g_ksub;
+    else if (a->ksub) *kso = a->ksub;
   }
   if (nwo) *nwo = nw;
   *BMo = BM;
@@ -185,7 +139,6 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
 // LDS-DMA eligibility: bf16, 16-B aligned rows/columns; for a non-K-contiguous operand the
 // row stride covers the extent rounded up to 8 (a 16-B chunk never leaves its row; the
 // padding columns only feed discarded outputs).
-static bool getenv_flag(const char* name);
 static bool gemm_uses_glds(const lasr_gemm_args* a) {
   if (a->in_dtype != LASR_BF16) return false;
   const bool akc = (a->lda_k == 1), bkc = (a->ldb_k == 1);
@@ -194,7 +147,12 @@ static bool gemm_uses_glds(const lasr_gemm_args* a) {
   const bool a_vec = aligned16(a->A) && s_a % 8 == 0 && a->sa1 % 8 == 0 && a->sa2 % 8 == 0;
   const bool b_vec = aligned16(a->B) && s_b % 8 == 0 && a->sb1 % 8 == 0 && a->sb2 % 8 == 0;
   const int64_t M8 = cdiv(a->M, 8) * 8, N8 = cdiv(a->N, 8) * 8;
-  return a_vec && b_vec && (akc || a->lda_k >= M8) && (bkc || a->ldb_k >= N8) && !getenv_flag("LASR_GEMM_NO_GLDS");
+  return a_vec && b_vec && (akc || a->lda_k >= M8) && (bkc || a->ldb_k >= N8);
+}
+
+static bool tile_ok(int tm, int tn) {
+  return (tm == 0 && tn == 0) || ((tm == 64 || tm == 128 || tm == 256) && (tn == 64 || tn == 128 || tn == 256) &&
+                                  (tm < 256 || tn >= 128) && (tn < 256 || tm >= 128));
 }
 
 extern "C" int lasr_gemm_plan(const lasr_gemm_args* a, int* tile_m, int* tile_n, int* split_k, int* flags) {
@@ -226,6 +184,9 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   LASR_CHECK_ARG(a->zout_mode == 0 || a->zout_mode == 1, "lasr_gemm: zout_mode must be 0 or 1");
   LASR_CHECK_ARG(a->act != LASR_ACT_GATE && (!a->aux || a->aux_act != LASR_ACT_NONE),
                  "lasr_gemm: act GATE is only an aux_act; aux needs an aux_act");
+  LASR_CHECK_ARG(tile_ok(a->tile_m, a->tile_n) && a->ksub >= 0 && a->ksub <= 2,
+                 "lasr_gemm: tile override must be 64/128/256 x 64/128/256 (256 only beside >= 128) or 0 x 0, "
+                 "ksub 0, 1 or 2");
   if (a->M == 0 || a->N == 0 || a->batch == 0) return LASR_OK;
   const int batch = a->batch > 0 ? a->batch : 1;
   const int bdiv = a->batch_div > 0 ? a->batch_div : 1;
@@ -328,15 +289,6 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
 
 
 // ---------------------------------------------------------------------------------------
-static int dw_wide() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("LASR_DW_WIDE");
-    v = e && e[0] ? atoi(e) : 1;
-  }
-  return v;
-}
-
 // Grouped split-K weight gradients (partials only): the deferred dW GEMMs of one backward
 // node in one launch.  Every problem must be what lasr_gemm would run as a partials-only
 // (split_k = -1) LDS-DMA launch with 64-deep stages, A M-contiguous and B N-contiguous
@@ -374,8 +326,8 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
       // 256 x 128 tiles on 8 waves, one workgroup per CU, the same K slices (one tile for
       // the whole group): 0.25 fewer LDS-DMA bytes per MFMA than the 4-wave 128 x 128 tile;
       // 11.84 -> 11.63-11.70 ms/step on two boxes (profiles/r03/dw_group_ab.json; 256 x 256
-      // with twice the slices, and a 2-stage ring, measured no better).  LASR_DW_WIDE=0: A/B.
-      if (dw_wide() && a->M >= 256 && a->N >= 256) {
+      // with twice the slices, and a 2-stage ring, measured no better).
+      if (a->M >= 256 && a->N >= 256) {
         BM = 256;
         BN = 128;
       }
@@ -397,7 +349,7 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     blocks += (int)cdiv(nb, 8) * 8;
   }
   g.start[n] = blocks;
-  static const int slice_xcd = env_int("LASR_DW_SLICE_XCD", 1);
+  static const int slice_xcd = [] { const char* e = getenv("LASR_DW_SLICE_XCD"); return e && e[0] ? atoi(e) : 1; }();
   g.slice_xcd = slice_xcd;
   LASR_CHECK_ARG(launch_dw_group(g, BM0, BN0, blocks, (hipStream_t)stream) == 0,
                  "lasr_gemm_dw_group: no grouped instance for tile %dx%d", BM0, BN0);

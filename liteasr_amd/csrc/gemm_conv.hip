@@ -33,13 +33,13 @@ static GemmP conv_params(const lasr_conv2_args* a) {
 // (tools/conv2_bench.py, profiles/r03).  Forward and data gradient stay on the 4-wave
 // 128 x 256 tiles: their 8-wave variants (256 x 256 with 64- or 32-deep stages, 256 x 128)
 // took 265-299 / 523-529 us against 262 / 468 (their 592-tile grids run 2.3 rounds of one
-// workgroup per CU).  LASR_CONV_WIDE=0 keeps the 4-wave weight gradient (A/B).
+// workgroup per CU).
 // The data gradient's four output parity classes in ONE launch: class i owns the blocks
 // [start[i], start[i+1]) (starts multiples of 8: the XCD remap stays exact inside a class),
 // heaviest class (4 taps) first.  One launch of ~4.9k workgroups instead of four of ~1.2k
 // (each 2.3-2.4 rounds of the 512 resident workgroups, so every class paid its own
-// partially filled last round).  Same tiles, same k order per output: bit-identical to the
-// per-class launches.  LASR_DX_MERGED=0 launches per class (A/B).
+// partially filled last round).  Same tiles, same k order per output as the per-class
+// launches it replaced (profiles/r03/conv2_dx_ab.json: hashes equal).
 struct DxClasses {
   int start[5];
   int M[4], K[4];
@@ -63,20 +63,6 @@ __global__ __launch_bounds__(256, 2) void conv2_dx_kernel(GemmP p, DxClasses c) 
   gemm_glds_tile<128, BN, true, false, bf16_t, 3, G_DX, 1, 4, EPI>(q, wg % ntx, wg / ntx, 0);
 }
 
-static int env_flag_dflt(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && e[0] ? atoi(e) : dflt;
-}
-
-static int conv_wide() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("LASR_CONV_WIDE");
-    v = e && e[0] ? atoi(e) : 1;
-  }
-  return v;
-}
-
 extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   LASR_CHECK_ARG(a != nullptr, "lasr_conv2_gemm: null args");
   LASR_CHECK_ARG(a->mode == LASR_CONV2_FWD || a->mode == LASR_CONV2_DW || a->mode == LASR_CONV2_DX,
@@ -97,7 +83,7 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     LASR_CHECK_ARG(a->w2p && aligned16(a->w2p), "lasr_conv2_gemm: w2p");
   hipStream_t st = (hipStream_t)stream;
   const int BN = C % 256 == 0 ? 256 : 128;
-  const bool wide = BN == 256 && conv_wide() > 0;
+  const bool wide = BN == 256;
   p.c_vec = 1;
   if (a->mode == LASR_CONV2_FWD) {
     LASR_CHECK_ARG(a->bias && aligned16(a->bias), "lasr_conv2_gemm: bias");
@@ -122,13 +108,11 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     p.B = a->y1; p.ldb_n = 1; p.ldb_k = 9 * C;
     p.C = a->out; p.ldc = 9 * C;
     p.epi_mode = 0; p.ws_vec = 1; p.v4 = 1;
-    const bool big = (g_tile_m == 256 || wide) && C % 256 == 0;
-    const int TM = big ? 256 : 128, TN = big ? 256 : 128;
+    const int TM = wide ? 256 : 128, TN = wide ? 256 : 128;
     const int64_t tiles = (int64_t)(C / TM) * (9 * C / TN);
     int split = 1;
     const int kt = (int)(kpad / 32);
-    if (g_split > 0) split = g_split;
-    else if (wide)  // one 512-thread workgroup per CU: fill the 256 CUs once, no second round
+    if (wide)  // one 512-thread workgroup per CU: fill the 256 CUs once, no second round
       split = (int)std::max<int64_t>(1, std::min<int64_t>(256 / tiles, kt / 16));
     else while (tiles * split < 512 && kt / (split * 2) >= 16 && split * 2 <= 64) split *= 2;
     // fewer K slices when the workspace holds fewer partial slabs (never silently one slice)
@@ -144,8 +128,6 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     if (a->rowsum && split > 1) p.rs_ws = p.ws + (int64_t)split * C * 9 * C;
     dim3 grid((unsigned)(9 * C / TN), (unsigned)(C / TM), (unsigned)split);
     if (wide) gemm_bf16_glds_kernel<256, 256, false, false, float, 2, 1, G_DW, 2, 8><<<grid, 512, 0, st>>>(p);
-    else if (big) gemm_bf16_glds_kernel<256, 256, false, false, float, 3, 1, G_DW><<<grid, 256, 0, st>>>(p);
-    else if (g_stages >= 4) gemm_bf16_glds_kernel<128, 128, false, false, float, 4, 2, G_DW><<<grid, 256, 0, st>>>(p);
     else gemm_bf16_glds_kernel<128, 128, false, false, float, 3, 3, G_DW><<<grid, 256, 0, st>>>(p);
     int rc = lasr_check_launch("lasr_conv2_gemm/dw");
     if (!rc && split > 1) {
@@ -156,7 +138,7 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
     }
     return rc;
   }
-  // LASR_CONV2_DX: one launch per output parity class, heaviest (4 taps) first
+  // LASR_CONV2_DX: the four output parity classes in one launch, heaviest (4 taps) first
   p.N = C;
   p.A = a->dy2; p.lda_m = C; p.lda_k = 1;
   p.B = a->w2p; p.ldb_n = 1; p.ldb_k = 9 * C;
@@ -164,38 +146,19 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   p.aux = a->y1; p.aux_dtype = LASR_BF16; p.ldaux = C; p.aux_act = LASR_ACT_RELU; p.aux_vec = 1;
   p.epi_mode = 1;
   p.cv.zero = (const bf16_t*)a->dy2 + (int64_t)g.M2 * C;
-  static const int rowtab = env_flag_dflt("LASR_DX_ROWTAB", 1), merged = env_flag_dflt("LASR_DX_MERGED", 1);
-  p.cv.rowtab = rowtab;
-  if (merged) {
-    DxClasses dc = {};
-    int nb = 0;
-    for (int cls = 0; cls < 4; ++cls) {
-      const int pt = cls >> 1, pf = cls & 1;
-      const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
-      dc.M[cls] = g.B * nI * nJ;
-      dc.K[cls] = (pt ? 1 : 2) * (pf ? 1 : 2) * C;
-      dc.start[cls] = nb;
-      nb += (int)(cdiv(cdiv(dc.M[cls], 128) * (C / BN), 8) * 8);
-    }
-    dc.start[4] = nb;
-    if (BN == 256 && epi_code(p) == EPI_AUX_RELU) conv2_dx_kernel<256, EPI_AUX_RELU><<<nb, 256, 0, st>>>(p, dc);
-    else if (BN == 256) conv2_dx_kernel<256><<<nb, 256, 0, st>>>(p, dc);
-    else conv2_dx_kernel<128><<<nb, 256, 0, st>>>(p, dc);
-    return lasr_check_launch("lasr_conv2_gemm/dx");
-  }
+  DxClasses dc = {};
+  int nb = 0;
   for (int cls = 0; cls < 4; ++cls) {
     const int pt = cls >> 1, pf = cls & 1;
     const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
-    p.cv.cls = cls;
-    p.M = g.B * nI * nJ;
-    p.K = (pt ? 1 : 2) * (pf ? 1 : 2) * C;
-    p.kchunk = p.K;
-    dim3 grid((unsigned)(C / BN), (unsigned)cdiv(p.M, 128), 1);
-    LASR_CHECK_ARG(grid.y <= 65535, "lasr_conv2_gemm: grid too large");
-    if (BN == 256) gemm_bf16_glds_kernel<128, 256, true, false, bf16_t, 3, 2, G_DX><<<grid, 256, 0, st>>>(p);
-    else gemm_bf16_glds_kernel<128, 128, true, false, bf16_t, 3, 3, G_DX><<<grid, 256, 0, st>>>(p);
-    const int rc = lasr_check_launch("lasr_conv2_gemm/dx");
-    if (rc) return rc;
+    dc.M[cls] = g.B * nI * nJ;
+    dc.K[cls] = (pt ? 1 : 2) * (pf ? 1 : 2) * C;
+    dc.start[cls] = nb;
+    nb += (int)(cdiv(cdiv(dc.M[cls], 128) * (C / BN), 8) * 8);
   }
-  return LASR_OK;
+  dc.start[4] = nb;
+  if (BN == 256 && epi_code(p) == EPI_AUX_RELU) conv2_dx_kernel<256, EPI_AUX_RELU><<<nb, 256, 0, st>>>(p, dc);
+  else if (BN == 256) conv2_dx_kernel<256><<<nb, 256, 0, st>>>(p, dc);
+  else conv2_dx_kernel<128><<<nb, 256, 0, st>>>(p, dc);
+  return lasr_check_launch("lasr_conv2_gemm/dx");
 }

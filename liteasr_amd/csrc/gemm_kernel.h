@@ -23,7 +23,6 @@ struct ConvG {
   int cls;              // G_DX: output parity class (t1 & 1) * 2 + (f1 & 1)
   int q32, r32;         // G_DW: 32 = q32 * F2 + r32 (row-walk increments)
   const bf16_t* zero;   // G_DX: >= 32 zero bf16 (taps that fall outside dy2)
-  int rowtab;           // G_DX: epilogue rows from the per-tile table (A/B switch)
 };
 typedef ConvG ConvGeom;
 enum { G_LIN = 0, G_FWD = 1, G_DW = 2, G_DX = 3 };
@@ -332,7 +331,7 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)]
   // output-row offsets: linear (ldc, ld of the aux/res source), or the transposed-conv scatter
   // of a G_DX launch (aux = y1 shares dy1's layout)
   auto crow = [&](int m) -> int64_t {
-    if constexpr (G == G_DX) return p.cv.rowtab ? dxrow[m - m0] : dx_row(p.cv, m);
+    if constexpr (G == G_DX) return dxrow[m - m0];
     else return (int64_t)z1 * p.sc1 + (int64_t)z2 * p.sc2 + (int64_t)m * p.ldc;
   };
   // NW waves as 2 (rows) x NW/2 (columns); NT threads finish the staged rows
@@ -379,14 +378,14 @@ LASR_DEV void gemm_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)]
 #pragma unroll
         for (int it = 0; it < PF; ++it) {
           const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          const int64_t ro = G == G_DX ? (p.cv.rowtab ? dxrow[m - m0] : dx_row(p.cv, m)) : (int64_t)m * src_ld;
+          const int64_t ro = G == G_DX ? dxrow[m - m0] : (int64_t)m * src_ld;
           ld8((const float*)src + ro + nc, sv[it]);
         }
       } else {
 #pragma unroll
         for (int it = 0; it < PF; ++it) {
           const int m = min(m0 + h * WM + er0 + (b + it) * RPI, mlast);
-          const int64_t ro = G == G_DX ? (p.cv.rowtab ? dxrow[m - m0] : dx_row(p.cv, m)) : (int64_t)m * src_ld;
+          const int64_t ro = G == G_DX ? dxrow[m - m0] : (int64_t)m * src_ld;
           ld8((const bf16_t*)src + ro + nc, sv[it]);
         }
       }
@@ -1170,6 +1169,4 @@ static inline int epi_code(const GemmP& p) {
   return EPI_RT;
 }
 
-// host-side tuning state shared by the two launch units (gemm.hip defines it)
-extern int g_stages, g_tile_m, g_tile_n, g_split, g_ks2_stages;
 static inline bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }

@@ -7,18 +7,6 @@
 template <bool AKC, bool BKC, typename TC>
 void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3 grid, hipStream_t st) {
   (void)nw;  // no 8-wave generic instance is planned (gemm.hip gemm_plan)
-  if constexpr (!AKC && !BKC && std::is_same<TC, float>::value) {
-    // split-K weight-gradient GEMMs: one block per CU, so a deeper ring hides the latency
-    const int S = g_stages;
-    if (glds && p.split_k > 1 && S >= 4) {
-#define DWL(bm, bn, s, mb) gemm_bf16_glds_kernel<bm, bn, false, false, float, s, mb><<<grid, 256, 0, st>>>(p)
-      if (BM == 128 && BN == 128) { if (S == 4) DWL(128, 128, 4, 2); else if (S == 5) DWL(128, 128, 5, 1); else DWL(128, 128, 6, 1); return; }
-      if (BM == 64 && BN == 128) { if (S == 4) DWL(64, 128, 4, 3); else if (S == 5) DWL(64, 128, 5, 2); else DWL(64, 128, 6, 2); return; }
-      if (BM == 128 && BN == 64) { if (S == 4) DWL(128, 64, 4, 3); else if (S == 5) DWL(128, 64, 5, 2); else DWL(128, 64, 6, 2); return; }
-      if (BM == 64 && BN == 64) { if (S == 4) DWL(64, 64, 4, 4); else if (S == 5) DWL(64, 64, 5, 3); else DWL(64, 64, 6, 3); return; }
-#undef DWL
-    }
-  }
   if (glds && ks == 2 && BM < 256) {
     // 64-deep ring stages (two 32-deep sub-tiles per wait + barrier); shallower rings keep
     // the LDS footprint at the KS = 1 instances' occupancy where it fits
@@ -26,7 +14,6 @@ void launch_bf16(const GemmP& p, int BM, int BN, int ks, int nw, bool glds, dim3
     else if (BM == 128 && BN == 128) gemm_bf16_glds_kernel<128, 128, AKC, BKC, TC, 2, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else if (BM == 128) gemm_bf16_glds_kernel<128, 64, AKC, BKC, TC, 3, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else if (BN == 128) gemm_bf16_glds_kernel<64, 128, AKC, BKC, TC, 3, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
-    else if (g_ks2_stages == 4) gemm_bf16_glds_kernel<64, 64, AKC, BKC, TC, 4, 2, G_LIN, 2><<<grid, 256, 0, st>>>(p);
     else {
       // the 64 x 64 launches of the N = d family: input gradients (B N-contiguous, bf16 out) and
       // the residual projections (fp32 out)

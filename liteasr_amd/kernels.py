@@ -98,26 +98,20 @@ def _defer(part, P, Ncols, out0, out1=None, split=None, accumulate=True):
 
 # Grouped weight gradients: dW GEMMs marked group=True inside a deferred_reductions block are
 # queued and launched at its end, one lasr_gemm_dw_group launch per planned tile (<= 8
-# problems each), before the reductions.  LASR_DW_GROUP=0 launches them one by one instead.
-DW_GROUP = os.environ.get("LASR_DW_GROUP", "1") != "0"
+# problems each), before the reductions (tests set DW_GROUP = False to compare with lone launches).
+DW_GROUP = True
 # plan tile -> group (lasr_gemm_dw_group runs the 64 x 128 / 128 x 64 plans, the FFN-sized
 # weights, on 128 x 128 tiles)
 _GROUP_TILES = {(64, 64): (64, 64), (64, 128): (128, 128), (128, 64): (128, 128)}
 # grouped problems fill the chip together: each takes 1/div of the K slices the planner gives
 # a lone launch (fewer fp32 partial slabs to write and reduce); 128 x 128 groups keep half
-# (tools: LASR_DW_GROUP_SPLIT_DIV overrides both)
-_DIV_ENV = os.environ.get("LASR_DW_GROUP_SPLIT_DIV")
-if _DIV_ENV is None:
-    DW_GROUP_SPLIT_DIV = {(64, 64): 4, (128, 128): 2}
-elif "," in _DIV_ENV:  # "d64,d128": one divisor per group tile
-    DW_GROUP_SPLIT_DIV = dict(zip([(64, 64), (128, 128)], map(int, _DIV_ENV.split(","))))
-else:
-    DW_GROUP_SPLIT_DIV = int(_DIV_ENV)
+# (the other divisors measured slower)
+DW_GROUP_SPLIT_DIV = {(64, 64): 4, (128, 128): 2}
 
 
 # GEMMs whose 64 x 64 grid cannot fill half the chip and whose K is long are split over K
-# (lasr_gemm autosplit; the split-K reduction applies the epilogue).  LASR_SMALL_GRID_SPLIT=0: off.
-SMALL_GRID_SPLIT = os.environ.get("LASR_SMALL_GRID_SPLIT", "1") != "0"
+# (lasr_gemm autosplit; the split-K reduction applies the epilogue).
+SMALL_GRID_SPLIT = True
 
 
 def _group_div(key):
@@ -195,11 +189,16 @@ def gemm(
     plan_only: bool = False,
     zout_mode: int = 0,
     group: bool = False,
+    tile: Optional[tuple] = None,
+    ksub: int = 0,
 ):
     """c = epilogue(alpha * a @ b) for logical views a (..,M,K), b (..,K,N), c (..,M,N).
 
     Views may be arbitrarily strided as long as each operand has one unit stride
     (the kernel handles K-contiguous and M/N-contiguous operands).
+
+    tile=(tile_m, tile_n) / ksub: per-call plan overrides of the LDS-DMA tile and ring-stage depth
+    (A/B tools, bit-identity tests); None / 0 = the planner.
 
     group=True (a split-K weight gradient inside deferred_reductions): the launch itself may
     be deferred to the end of the block and grouped with the block's other dW GEMMs, so
@@ -238,6 +237,9 @@ def gemm(
     if aux is not None:
         args.aux, args.aux_dtype, args.ldaux, args.aux_act = ptr(aux), dt(aux), aux.stride(0), aux_act
     args.drop_p, args.drop_seed = drop_p, drop_seed
+    if tile is not None:
+        args.tile_m, args.tile_n = int(tile[0]), int(tile[1])
+    args.ksub = int(ksub)
     if res is not None:
         args.res, args.res_dtype, args.ldres, args.res_scale = ptr(res), dt(res), res.stride(0), res_scale
     auto_split = (split_k == 1 and SMALL_GRID_SPLIT and rowsum is None and zout is None and not group
@@ -365,7 +367,7 @@ def _al16(t):
 # The row kernel's main loop ingests the whole weight per 32-row workgroup, one workgroup per CU:
 # measured faster than GEMM + norm up to K = 768 (tools/row_ln_bench.py, profiles/r03), slower at
 # K = 2048, where the 64 x 64 GEMM's 2-3 workgroups per CU keep more of the LDS-DMA in flight.
-ROW_LN_MAX_K = int(os.environ.get("LASR_ROW_LN_MAX_K", "1024"))
+ROW_LN_MAX_K = 1024
 
 
 def row_ln_ok(a, w, D, max_k=None):

@@ -169,7 +169,7 @@ def _slot(t, B, T, nslot, k, H, dk):
 
 
 # ============================================================ rel-pos MHSA ======
-FUSED_RELATTN = os.environ.get("LASR_FUSED_RELATTN", "1") != "0"
+FUSED_RELATTN = True
 
 
 def fused_relattn(adt, dk, p_att):

@@ -117,3 +117,21 @@ def test_comm_header_symbols_exported():
     assert set(NR._SIGS) == declared
     L = NR.load()
     assert L.lasr_reducer_uid_bytes() == 128  # NCCL_UNIQUE_ID_BYTES
+
+
+def test_switch_names_are_every_product_switch():
+    """The getenv switches in csrc/ and the LASR_* environment reads in liteasr_amd/ are exactly
+    the ones tested here (plus LASR_ROCTX, the tracing flag, and the decoder attention switch
+    held to the materialised path in test_kernels_gpu.py)."""
+    import re
+
+    from test_switches_gpu import SWITCHES
+
+    found = set()
+    for base, _, files in os.walk(os.path.join(ROOT, "liteasr_amd")):
+        for f in files:
+            if f.endswith((".hip", ".h", ".cpp", ".py")):
+                src = open(os.path.join(base, f)).read()
+                found |= set(re.findall(r'getenv\("(LASR_[A-Z0-9_]+)"', src))
+                found |= set(re.findall(r'environ\.get\("(LASR_[A-Z0-9_]+)"', src))
+    assert found == set(SWITCHES) | {"LASR_ROCTX", "LASR_FUSED_DEC_ATTN"}, found

@@ -226,7 +226,7 @@ def test_gemm_fused_rowsum(dtype, R, M, N, split):
                                          (1000, 256, 100, (128, 64)), (999, 384, 160, (64, 128)),
                                          (700, 512, 224, (128, 128)), (700, 512, 2048, (128, 256))])
 def test_gemm_ksub2_bit_identical(ta, tb, M, N, Kd, tile):
-    """64-deep ring stages (two 32-deep sub-tiles per wait + barrier, lasr_gemm_force_ksub(2))
+    """64-deep ring stages (two 32-deep sub-tiles per wait + barrier, per-call ksub = 2)
     accumulate in the same k order as 32-deep stages: outputs bit-identical, including a
     leftover 32-deep sub-tile (K % 64 = 32), a ragged tail (K % 32 != 0), epilogues, and
     split-K weight gradients with the fused bias rowsum."""
@@ -243,23 +243,18 @@ def test_gemm_ksub2_bit_identical(ta, tb, M, N, Kd, tile):
     dy = torch.randn(3001, M, generator=g).to(DEV, torch.bfloat16)
     x = torch.randn(3001, N, generator=g).to(DEV, torch.bfloat16)
     outs = []
-    try:
-        Nn.call("lasr_gemm_force_tile", *tile)
-        for ks in (1, 2):
-            Nn.call("lasr_gemm_force_ksub", ks)
-            c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-            z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-            kn.gemm(a, b, c, bias=bias, act=Nn.ACT_SWISH, zout=z)
-            o32 = torch.empty(M, N, device=DEV)
-            kn.gemm(a, b, o32, bias=bias, res=res, res_scale=0.5)
-            dw = torch.ones(M, N, device=DEV)
-            db = torch.ones(M, device=DEV)
-            kn.gemm(dy.t(), x, dw, beta=1.0, split_k=0, rowsum=db)
-            torch.cuda.synchronize()
-            outs.append((c, z, o32, dw, db))
-    finally:
-        Nn.call("lasr_gemm_force_ksub", 0)
-        Nn.call("lasr_gemm_force_tile", 0, 0)
+    tl = tile if tile != (0, 0) else None
+    for ks in (1, 2):
+        c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        kn.gemm(a, b, c, bias=bias, act=Nn.ACT_SWISH, zout=z, tile=tl, ksub=ks)
+        o32 = torch.empty(M, N, device=DEV)
+        kn.gemm(a, b, o32, bias=bias, res=res, res_scale=0.5, tile=tl, ksub=ks)
+        dw = torch.ones(M, N, device=DEV)
+        db = torch.ones(M, device=DEV)
+        kn.gemm(dy.t(), x, dw, beta=1.0, split_k=0, rowsum=db, tile=tl, ksub=ks)
+        torch.cuda.synchronize()
+        outs.append((c, z, o32, dw, db))
     for name, u, v in zip(("out", "zout", "res", "dW", "db"), outs[0], outs[1]):
         assert torch.equal(u, v), f"ksub 2 differs from ksub 1: {name}"
     ref = (a.double() @ b.double()).cpu() + bias.double().cpu()

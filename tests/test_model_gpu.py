@@ -302,6 +302,28 @@ def test_parity_config2_full_model_bf16_emulated():
     _check_emulated(run_case(CONFIG2, 2, 1000, 40, "bf16", emulate=True))
 
 
+# BASELINE config 4's per-rank workload at its real size: U2-Conformer-large, 12 encoder / 6
+# decoder layers, d 512, 16 heads (d_k 32), ff 2048, V 4233, dynamic-chunk streaming mask at
+# chunk 16, T 1000 (T' 249), two utterances
+CONFIG4 = O.default_cfg(enc_dim=512, enc_heads=16, enc_ff=2048, enc_layers=12, dec_dim=512, dec_heads=16,
+                        dec_ff=2048, dec_layers=6, vocab_size=4233)
+
+
+def test_parity_config4_full_model_fp32():
+    """liteasr/nets/transformer_encoder.py:107-127 with the chunk mask of liteasr/utils/mask.py:
+    30-90 and the 16-head relative attention of liteasr/nets/attention.py:120-154, full depth
+    and length, fp32 build vs the fp64 oracle: loss 1e-5 relative, logits and every gradient
+    1e-3 of max (the subsampling convs' ReLU-kink bar as in test_parity_fp32)."""
+    _check_fp32(run_case(CONFIG4, 2, 1000, 40, "fp32", chunk=16), 1e-3)
+
+
+def test_parity_config4_full_model_bf16_emulated():
+    """Config 4's full model in the default bf16 build (fused d_k 32 attention with the staged
+    chunk-mask tiles, the full-row LayerNorm GEMMs at d 512) against the bf16-emulating
+    oracle at the whole-model bars."""
+    _check_emulated(run_case(CONFIG4, 2, 1000, 40, "bf16", chunk=16, emulate=True))
+
+
 def test_parity_config5_long_bf16_emulated():
     """BASELINE config 5's shape: T 4000 (T' 999), CTC-only (w 1.0: the decoder runs and gets
     zero gradient), label length 150, full depth, one utterance pair."""

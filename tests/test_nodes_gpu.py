@@ -41,14 +41,14 @@ NOISE = ("linear_k.bias", "depthwise_conv.bias")
 B, TX, L = 32, 1000, 40
 
 
-def _model(cfg, seed):
+def _model(cfg, seed, chunk=0):
     from liteasr_amd.models.u2 import U2, U2Config
     from liteasr_amd.utils.cfg import resolve_self
 
     c = U2Config(input_dim=80, vocab_size=cfg["vocab_size"], enc_dim=cfg["enc_dim"], enc_ff_dim=cfg["enc_ff"],
                  enc_attn_heads=cfg["enc_heads"], enc_layers=cfg["enc_layers"], dec_dim=cfg["dec_dim"],
                  dec_ff_dim=cfg["dec_ff"], dec_attn_heads=cfg["dec_heads"], dec_layers=cfg["dec_layers"],
-                 dropout_rate=0.0, compute_dtype="bf16")
+                 dropout_rate=0.0, compute_dtype="bf16", chunk_size=chunk)
     resolve_self(c)
     params = {k: (v.bfloat16().float() if v.is_floating_point() else v)
               for k, v in O.init_params(cfg, seed=seed).items()}
@@ -90,14 +90,27 @@ def _leaf(params, prefix):
 
 def test_conformer_layer_node_config2():
     """RelativeEncoderLayer (liteasr/nets/conformer_layer.py:130-147) at B 32 x T' 249."""
+    _conformer_node(O.default_cfg(enc_layers=1, dec_layers=1), chunk=0, seed=31)
+
+
+def test_conformer_layer_node_config4():
+    """The same node at BASELINE config 4's layer shape: d 512, 16 heads (d_k 32), ff 2048, the
+    dynamic-chunk streaming mask at chunk 16 (liteasr/utils/mask.py:30-90 triangle_mask with
+    stage 16, OR the key padding), B 32 x T' 249 (liteasr/nets/attention.py:120-154 with the
+    query-dependent mask staged per block pair in attn_fused.hip)."""
+    cfg = O.default_cfg(enc_dim=512, enc_heads=16, enc_ff=2048, enc_layers=1, dec_dim=512, dec_heads=16,
+                        dec_ff=2048, dec_layers=1)
+    _conformer_node(cfg, chunk=16, seed=61)
+
+
+def _conformer_node(cfg, chunk, seed):
     from liteasr_amd import kernels as K
     from liteasr_amd.nets import functional as FN
 
-    cfg = O.default_cfg(enc_layers=1, dec_layers=1)
-    model, params = _model(cfg, seed=31)
-    env, prep, _ = _env(model, seed=32)
+    model, params = _model(cfg, seed=seed, chunk=chunk)
+    env, prep, _ = _env(model, seed=seed + 1)
     T, d = prep.T, cfg["enc_dim"]
-    g = torch.Generator().manual_seed(33)
+    g = torch.Generator().manual_seed(seed + 2)
     x = torch.randn(B * T, d, generator=g)
     dy = torch.randn(B * T, d, generator=g)
     enc = model.encoder
@@ -115,6 +128,9 @@ def test_conformer_layer_node_config2():
     leaf = _leaf(params, pre + ".")
     x64 = x.double().requires_grad_()
     mask = prep.enc_mask.bool().cpu()[:, None, :]
+    if chunk > 0:
+        assert prep.chunk_mask is not None
+        mask = mask | O.triangle_mask(T, stage=chunk)[None]
     bn = {k: v.double() if v.is_floating_point() else v.clone() for k, v in O.init_buffers(cfg).items()}
     y64 = E.conformer_layer(x64.view(B, T, d), pos.double().cpu(), mask, leaf, pre, cfg["enc_heads"], bn, True)
     y64.backward(dy.double().view(B, T, d))

@@ -1,0 +1,50 @@
+#!/bin/bash
+# Round-4 GPU pass.  Usage: tools/gpu_r04.sh TAG STEP...; output under gpurun_out/TAG/.
+# Every step has its own time limit; the script stops at the first failure.
+set -u
+TAG=${1:-r04}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+run() { echo "=== $*" >&2; "$@"; rc=$?; echo "=== rc=$rc" >&2; [ $rc -eq 0 ] || exit $rc; }
+for s in "$@"; do
+  cd "$R"
+  case $s in
+    tests) run timeout -k 10 900 $PYT tests > "$OUT/tests.log" 2>&1 ;;
+    new) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py tests/test_switches_gpu.py tests/test_nodes_gpu.py \
+           "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" "tests/test_model_gpu.py::test_parity_config4_full_model_bf16_emulated" \
+           "tests/test_kernels_gpu.py::test_gemm_ksub2_bit_identical" -s > "$OUT/new.log" 2>&1 ;;
+    kgpu) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py tests/test_row_ln_gpu.py > "$OUT/kgpu.log" 2>&1 ;;
+    model) run timeout -k 10 900 $PYT tests/test_model_gpu.py tests/test_nodes_gpu.py -s > "$OUT/model.log" 2>&1 ;;
+    smoke) run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    bench) run timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    benchq) run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/benchq.json" 2> "$OUT/benchq.err" ;;
+    long) run timeout -k 10 300 python3 bench.py --config long --no-cpu-baseline > "$OUT/bench_long.json" 2> "$OUT/bench_long.err" ;;
+    large) run timeout -k 10 400 python3 bench.py --config large --no-cpu-baseline > "$OUT/bench_large.json" 2> "$OUT/bench_large.err" ;;
+    ddp1) run timeout -k 10 300 python3 bench.py --force-ddp --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1.json" 2> "$OUT/bench_ddp1.err" ;;
+    ddp1n) run timeout -k 10 300 python3 bench.py --force-ddp --comm native --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1_native.json" 2> "$OUT/bench_ddp1_native.err" ;;
+    blaslt) run timeout -k 10 120 python3 tools/blaslt_ref.py > "$OUT/blaslt.jsonl" 2> "$OUT/blaslt.err" ;;
+    trace) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace.log" 2>&1
+           db=$(find "$OUT/trace" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary.txt" 2>&1
+           python3 "$R/tools/step_summary.py" "$db" 5 --grid > "$OUT/step_summary_grid.txt" 2>&1; rm -f "$db" ;;
+    tracelong) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_long" -o run -- python3 "$R/bench.py" --config long --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace_long.log" 2>&1
+           db=$(find "$OUT/trace_long" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_long.txt" 2>&1; rm -f "$db" ;;
+    tracelarge) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_large" -o run -- python3 "$R/bench.py" --config large --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace_large.log" 2>&1
+           db=$(find "$OUT/trace_large" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_large.txt" 2>&1; rm -f "$db" ;;
+    profile) cd /tmp && run timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d "$OUT/prof_markers" -o run -- python3 "$R/bench.py" --profile --no-cpu-baseline --no-roofline --steps 3 --warmup 1 > "$OUT/profile.log" 2>&1 ;;
+    pmc) for c in ${PMC_CASES:-family dw hot}; do
+           cd /tmp && run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$c" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 20 --roofline-case $c > "$OUT/pmc_fetch_$c.log" 2>&1
+           run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$c" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 20 --roofline-case $c > "$OUT/pmc_write_$c.log" 2>&1
+           grep "^{" "$OUT/pmc_fetch_$c.log" | tail -1 > "$OUT/roofline_meta_$c.json"
+           run python3 "$R/tools/pmc_traffic.py" "$(find "$OUT/pmc_fetch_$c" -name '*.db' | head -1)" "$(find "$OUT/pmc_write_$c" -name '*.db' | head -1)" "$OUT/roofline_meta_$c.json" "$OUT/roofline_pmc_$c.json"
+           rm -rf "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c"
+         done ;;
+    mfma) cd /tmp && run timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --graph off --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > "$OUT/pmc_mfma.log" 2>&1
+          run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mfma" -name '*counter_collection.csv' | head -1)" ${PMC_CONFIG:-small} > "$OUT/pmc_mfma_summary_${PMC_CONFIG:-small}.json"
+          rm -rf "$OUT/pmc_mfma" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done
