@@ -1,0 +1,497 @@
+// Fused relative-position / plain attention, transposed-score formulation (gfx950), bf16
+// operands, d_k 64 or 32.  Reference: liteasr/nets/attention.py RelativeMultiHeadAttention
+// .forward :120-154 (ac = (q+u) k^T, bd = rel_shift((q+v) p^T), (ac+bd)/sqrt(d_k),
+// masked_fill(-1e38), softmax, attn @ v), legacy rel_shift :99-118; MultiHeadedAttention
+// :24-73 for the plain (decoder) case.
+//
+// Layout of the work.  A workgroup of NW waves owns 16*NW queries of one (b, h); wave w owns
+// the 16 queries iw = i0 + 16w ..  Key blocks of 64 stream through a 2-stage LDS ring filled by
+// LDS-DMA (global_load_lds_dwordx4, no register staging): K, V, the relative-position window
+// and (query-dependent masks) the mask tile of the block pair.  Scores are formed TRANSPOSED,
+// S^T[key][query] = K . Qu^T on v_mfma_f32_16x16x32_bf16, so a lane owns ONE query (its
+// column) and 4 consecutive keys per 16-key tile:
+//   * the online softmax is per lane: a block max needs two cross-lane steps (the 4 lane
+//     groups of a query), the running sum none until the end;
+//   * P^T never leaves the registers: it is the B operand of O^T = V^T P^T as it stands, with
+//     the k slots of a 32-key sub-block ordered {4g..4g+3 of tile 2ks, 4g..4g+3 of tile
+//     2ks+1} and the V^T operand read in that same key order by ds_read_b64_tr_b16.
+// rel_shift as a relative-position lookup (the closed form of attn.hip): with m = j - i + T - 1
+//   j <= i   : bd = (q_i + v) . p[m]        j == i+1 : bd = 0
+//   j >= i+2 : bd = (q_{i+1} + v) . p[m - T - 1]
+// i.e. bd = G1[i][m] (m <= T-1) or G2[i][m] (m >= T) over the window table W[m] = p[m]
+// (0 <= m < T), 0 (m = T), p[m-T-1] (T < m <= 2T); G1/G2 = (qv_i / qv_{i+1}) . W[m].  A wave's
+// 16 queries x 64 keys span an 80-row window of W: G'[m][query] for it is 5 MFMA tiles, parked
+// in the wave's LDS scratch as [query][m] (one 16-B write per tile and lane) and read back
+// along the diagonal m = (j - j0) - (i - iw) + 15.
+#include "common.h"
+#include "tile.h"
+
+namespace {
+
+constexpr int KB = 64;   // keys per block
+constexpr int GLD = 84;  // fp32 row stride of a wave's G' scratch ([16 queries][80 m] + pad)
+
+struct FlashP {
+  const bf16_t *qu, *qv, *k, *v, *pos;  // qu/qv [B*T, ldq]; k/v [B*Tk, ldkv]; pos [T, ldp]
+  int64_t ldq, ldkv, ldp;
+  const uint8_t* mask;                  // mask[b*msb + i*msq + j] != 0 -> masked
+  int64_t msb, msq;
+  int B, H, T, Tk;
+  float scale;
+  float* stats;                         // [B*H*T][2]: row max (scaled-score units), 1/row sum
+  bf16_t* ctx;
+  int64_t ldc;
+};
+
+// bf16 zero row: the relative-position window's rows outside the table (m == T, past 2T)
+__device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];
+
+// One image layout serves both MFMA operand orientations: row r of DK bf16, its 16-column
+// (32-B) slots XOR-swizzled by hq(r).  A row fragment (8 consecutive columns of one row,
+// ds_read_b128) and the transposed read (4 consecutive rows of one column,
+// ds_read_b64_tr_b16) are both bank-conflict free on it.
+template <int DK>
+LASR_DEV int hq(int r) {
+  if constexpr (DK == 64) return ((r >> 1) & 1) | ((r >> 2) & 2);
+  else return (r >> 2) & 1;
+}
+template <int DK>
+LASR_DEV int toff(int r, int c) {
+  return r * DK + ((((c >> 4) ^ hq<DK>(r))) << 4) + (c & 15);
+}
+// image chunk P (16 B) of a row-major [rows][DK] image -> (row, logical first column)
+template <int DK>
+LASR_DEV void chunk_rc(int P, int& r, int& col) {
+  constexpr int CPR = DK / 8;
+  r = P / CPR;
+  const int ps = P % CPR;
+  col = (((ps >> 1) ^ hq<DK>(r)) << 4) | ((ps & 1) << 3);
+}
+
+LASR_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+LASR_DEV f32x4 zero4() { return (f32x4){0.f, 0.f, 0.f, 0.f}; }
+
+// LDS reads in inline asm: invisible to hipcc's waitcnt pass, which would otherwise drain the
+// LDS-DMA ring (vmcnt(0)) before every read it cannot prove disjoint from the DMA.  Callers
+// wait with lgkm_wait<>() before using the results.
+LASR_DEV v4i lds_b128(uint32_t addr) {
+  v4i r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+LASR_DEV v2i lds_tr(uint32_t addr) {
+  v2i r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+LASR_DEV void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// After lgkm0(): route every asm-read register through an empty asm so its consumers depend on
+// a statement ordered after the wait (volatile asm statements keep their relative order).
+template <typename T>
+LASR_DEV void keep(T& x) { asm volatile("" : "+v"(x)); }
+
+LASR_DEV uint32_t ldsa(const void* p) { return (uint32_t)(uintptr_t)(lptr_t)p; }
+
+// row fragment (A or B operand with k along the image columns): rows rbase + lane%16,
+// columns kb + 8*(lane/16) .. +8
+template <int DK>
+LASR_DEV uint32_t frag_row_addr(uint32_t img, int rbase, int kb, int lane) {
+  return img + 2u * (uint32_t)toff<DK>(rbase + (lane & 15), kb + 8 * (lane >> 4));
+}
+// transposed fragment half: image rows k0 .. k0+3 of column cbase + lane%16 (the lane's own
+// address is row k0 + (lane>>2)&3, columns cbase + 4*(lane&3) .. +3)
+template <int DK>
+LASR_DEV uint32_t frag_tr_addr(uint32_t img, int k0, int cbase, int lane) {
+  return img + 2u * (uint32_t)toff<DK>(k0 + ((lane >> 2) & 3), cbase + (lane & 3) * 4);
+}
+LASR_DEV bf16x8 as_frag(v4i r) { return __builtin_bit_cast(bf16x8, r); }
+LASR_DEV bf16x8 as_frag(v2i lo, v2i hi) {
+  const v4i v = {lo[0], lo[1], hi[0], hi[1]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+LASR_DEV bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  const v4i v = {(int)pk_bf16(a[0], a[1]), (int)pk_bf16(a[2], a[3]), (int)pk_bf16(b[0], b[1]),
+                 (int)pk_bf16(b[2], b[3])};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+LASR_DEV float xmax16_32(float v) {  // max over the 4 lane groups of a column (lanes l, l^16, l^32, l^48)
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+LASR_DEV float xsum16_32(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// ---- stage geometry -------------------------------------------------------------------
+// A ring stage is [K image | V image | W window | mask tile], contiguous, filled by one
+// linear LDS-DMA sweep: every thread issues GL 16-B pieces; region boundaries are multiples
+// of 64 pieces so a wave instruction never straddles two regions.
+template <int DK, int NW, bool RP, bool RM>
+struct Geo {
+  static constexpr int NT = NW * 64, QB = 16 * NW, CPR = DK / 8;
+  static constexpr int K_CH = KB * CPR, V_CH = KB * CPR;
+  static constexpr int W_ROWS0 = RP ? KB + QB : 0;  // >= 64 + 16 NW - 1 rows of the window
+  static constexpr int M_CH = RM ? QB * (KB / 16) : 0;
+  static constexpr int BASE = K_CH + V_CH + M_CH;
+  // pad the window so the stage is a whole number of sweeps
+  static constexpr int W_CH0 = W_ROWS0 * CPR;
+  static constexpr int TOT = ((BASE + W_CH0 + NT - 1) / NT) * NT;
+  static constexpr int W_CH = TOT - BASE;
+  static constexpr int W_ROWS = W_CH / CPR;
+  static constexpr int GL = TOT / NT;
+  static constexpr int STAGE_BYTES = TOT * 16;
+  // region starts (pieces)
+  static constexpr int K0 = 0, V0 = K_CH, W0 = K_CH + V_CH, M0 = W0 + W_CH;
+  static_assert(K_CH % 64 == 0 && V_CH % 64 == 0 && M_CH % 64 == 0 && W_CH % 64 == 0, "wave-aligned regions");
+  static_assert(!RP || W_ROWS >= KB + QB - 1, "window rows");
+  static_assert(RP || W_CH == 0, "no window without the positional term");
+};
+
+// One block pair's LDS-DMA sweep into stage `st` (shared by the forward and the query-side
+// backward).
+template <int DK, int NW, bool RP, bool RM>
+LASR_DEV void issue_stage(const FlashP& a, int b, int h, int i0, int j0, char* st, int tid) {
+  using Gm = Geo<DK, NW, RP, RM>;
+  const int wid = tid >> 6;
+  const int T = a.T, Tk = a.Tk;
+  const int64_t kb = (int64_t)b * Tk;
+  const bf16_t* kh = a.k + kb * a.ldkv + h * DK;
+  const bf16_t* vh = a.v + kb * a.ldkv + h * DK;
+#pragma unroll
+  for (int i = 0; i < Gm::GL; ++i) {
+    const int P = i * Gm::NT + tid;
+    const void* src;
+    if (P < Gm::V0) {
+      int r, c;
+      chunk_rc<DK>(P, r, c);
+      src = kh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c;
+    } else if (P < Gm::W0) {
+      int r, c;
+      chunk_rc<DK>(P - Gm::V0, r, c);
+      src = vh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c;
+    } else if (RP && P < Gm::M0) {
+      int r, c;
+      chunk_rc<DK>(P - Gm::W0, r, c);
+      const int m = j0 - i0 + T - Gm::QB + r;  // window row r <-> m
+      const int src_row = m >= 0 && m <= T - 1 ? m : (m >= T + 1 && m <= 2 * T ? m - T - 1 : -1);
+      src = src_row >= 0 ? (const void*)(a.pos + (int64_t)src_row * a.ldp + h * DK + c) : (const void*)(g_zero_row + c);
+    } else {
+      // mask tile [query r][64 keys] bytes (RM): rows 16-B aligned (host-checked); a piece
+      // starting past the row stride holds only keys >= Tk (masked anyway): clamped
+      const int q = P - Gm::M0, r = q >> 2, c16 = (q & 3) * 16;
+      const int64_t col = min<int64_t>(j0 + c16, a.msq - 16);
+      src = a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + r, T - 1) * a.msq + col;
+    }
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(st + (size_t)(i * Gm::NT + wid * 64) * 16), 16, 0, 0);
+  }
+}
+
+// Query-side fragments of the lane's query (B operands: n = lane%16, k = 8*(lane/16) ..).
+template <int DK>
+LASR_DEV void load_q(const bf16_t* base, int64_t ld, int row, int h, int lane, bf16x8 (&f)[DK / 32]) {
+  const bf16_t* p = base + (int64_t)row * ld + h * DK + 8 * (lane >> 4);
+#pragma unroll
+  for (int ks = 0; ks < DK / 32; ++ks) f[ks] = *(const bf16x8*)(p + 32 * ks);
+}
+
+// Scaled + masked transposed scores of the lane's query against the 64 keys of block j0,
+// in log2 units (c2 = scale * log2 e): s[c][e] for key j0 + 16c + 4*(lane/16) + e.
+template <int DK, int NW, bool RP, bool RM>
+LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t* km, const bf16x8 (&qu)[DK / 32],
+                       const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int w, int i0, int j0, float c2,
+                       int lane, f32x4 (&s)[4]) {
+  using Gm = Geo<DK, NW, RP, RM>;
+  constexpr int KS = DK / 32;
+  const int g = lane >> 4, col = lane & 15;
+  const uint32_t kimg = ldsa(st), wimg = ldsa(st + Gm::W0 * 16);
+  // S^T = K . Qu^T
+  {
+    v4i r[4][KS];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) r[c][ks] = lds_b128(frag_row_addr<DK>(kimg, 16 * c, 32 * ks, lane));
+    lgkm0();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) keep(r[c][ks]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(r[c][ks]), qu[ks], acc);
+      s[c] = acc;
+    }
+  }
+  float bd[4][4];
+  if constexpr (RP) {
+    const int T = a.T;
+    const int wb = 16 * (NW - 1 - w);                   // the wave's first window row
+    const int mlo = j0 - i0 + T - Gm::QB + wb;          // m of that row
+    const uint32_t gq = ldsa(gw);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int lo = mlo + 16 * t;
+      const bool n1 = lo <= T - 1 && lo + 15 >= 0;      // rows with m in [0, T-1]
+      const bool n2 = lo + 15 >= T + 1 && lo <= 2 * T;  // rows with m in [T+1, 2T]
+      v4i r[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) r[ks] = lds_b128(frag_row_addr<DK>(wimg, wb + 16 * t, 32 * ks, lane));
+      lgkm0();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) keep(r[ks]);
+      f32x4 g1 = zero4(), g2 = zero4();
+      if (n1) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(r[ks]), qv[ks], g1);
+      }
+      if (n2) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(r[ks]), qv1[ks], g2);
+      }
+      f32x4 gsel;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gsel[e] = lo + 4 * g + e <= T - 1 ? g1[e] : g2[e];
+      // G'[query col][m - mlo = 16t + 4g + e]
+      asm volatile("ds_write_b128 %0, %1" ::"v"(gq + 4u * (uint32_t)(col * GLD + 16 * t + 4 * g)), "v"(gsel) : "memory");
+    }
+    lgkm0();
+    // diagonal: bd(query col, key 16c + 4g + e) = G'[col][16c + 4g + e - col + 15]
+    const uint32_t base = gq + 4u * (uint32_t)(col * (GLD - 1) + 4 * g + 15);
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x;
+        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(x) : "v"(base), "i"(4 * (16 * c + e)));
+        v[4 * c + e] = x;
+      }
+    lgkm0();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        keep(v[4 * c + e]);
+        bd[c][e] = v[4 * c + e];
+      }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bd[c][e] = 0.f;
+  }
+  // masks: key padding bytes (staged per utterance) or the query-dependent tile
+  uint32_t mw[4] = {0u, 0u, 0u, 0u};
+  if (RM || km) {
+    const uint32_t mimg = RM ? ldsa(st + Gm::M0 * 16) + (uint32_t)((16 * w + col) * KB + 4 * g)
+                             : ldsa(km) + (uint32_t)(j0 + 4 * g);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(mw[c]) : "v"(mimg), "i"(16 * c));
+    lgkm0();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) keep(mw[c]);
+  }
+  const bool tail = j0 + KB > a.Tk;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = (s[c][e] + bd[c][e]) * c2;
+      if ((mw[c] >> (8 * e)) & 0xffu) x = -1e38f;
+      if (tail && j0 + 16 * c + 4 * g + e >= a.Tk) x = -INFINITY;
+      s[c][e] = x;
+    }
+}
+
+// LDS of the forward: 2 ring stages, the waves' G' scratch (RP), the key-padding bytes (!RM)
+constexpr int KMASK_BYTES = 8192;  // Tk <= 8192 (host-checked)
+template <int DK, int NW, bool RP, bool RM>
+constexpr int fwd_lds() {
+  return 2 * Geo<DK, NW, RP, RM>::STAGE_BYTES + (RP ? NW * 16 * GLD * 4 : 0) + (RM ? 0 : KMASK_BYTES);
+}
+
+template <int DK, int NW, bool RP, bool RM>
+__global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
+  using Gm = Geo<DK, NW, RP, RM>;
+  constexpr int KS = DK / 32, NT = Gm::NT;
+  __shared__ __attribute__((aligned(16))) char smem[fwd_lds<DK, NW, RP, RM>()];
+  char* ring = smem;                                   // 2 stages
+  float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);   // RP: NW x [16][GLD]
+  uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * 16 * GLD : 0));  // !RM: key padding bytes
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, col = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
+  const int i0 = blockIdx.x * Gm::QB, iw = i0 + 16 * w, iq = iw + col;
+  const int nb = (Tk + KB - 1) / KB;
+  const float c2 = a.scale * 1.4426950408889634f;
+
+  issue_stage<DK, NW, RP, RM>(a, b, h, i0, 0, ring, tid);
+  const uint8_t* km = nullptr;
+  if constexpr (!RM) {
+    if (a.mask) {  // key padding: this utterance's row, bytes past Tk read as unmasked (keys >= Tk are -inf anyway)
+      const uint8_t* mr = a.mask + (int64_t)b * a.msb;
+      const int kpad = nb * KB;
+      for (int j = tid; j < kpad; j += NT) kmask[j] = j < Tk ? mr[j] : 0;
+      km = kmask;
+    }
+  }
+  bf16x8 qu[KS], qv[KS], qv1[KS];
+  load_q<DK>(a.qu, a.ldq, b * T + min(iq, T - 1), h, lane, qu);
+  if constexpr (RP) {
+    load_q<DK>(a.qv, a.ldq, b * T + min(iq, T - 1), h, lane, qv);
+    load_q<DK>(a.qv, a.ldq, b * T + min(iq + 1, T - 1), h, lane, qv1);
+  }
+  float* gw = gsh + w * 16 * GLD;
+  float mrun = -INFINITY, lrun = 0.f;
+  f32x4 o[DK / 16];
+#pragma unroll
+  for (int t = 0; t < DK / 16; ++t) o[t] = zero4();
+
+  for (int jb = 0; jb < nb; ++jb) {
+    const int j0 = jb * KB;
+    char* st = ring + (jb & 1) * Gm::STAGE_BYTES;
+    wait_vmcnt<0>();  // this block's pieces (issued one block ago) and the Q loads
+    lds_barrier();    // ... of every wave; every wave is done with block jb-1's stage
+    if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
+    f32x4 s[4];
+    scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
+    // online softmax (one query per lane; the 4 lane groups of a query share its max)
+    float bm = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                     fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+    bm = fmaxf(bm, fmaxf(fmaxf(fmaxf(s[2][0], s[2][1]), fmaxf(s[2][2], s[2][3])),
+                         fmaxf(fmaxf(s[3][0], s[3][1]), fmaxf(s[3][2], s[3][3]))));
+    bm = xmax16_32(bm);
+    const float mn = fmaxf(mrun, bm);
+    const float al = __builtin_amdgcn_exp2f(mrun - mn);
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float p = __builtin_amdgcn_exp2f(s[c][e] - mn);
+        s[c][e] = p;
+        sum += p;
+      }
+    lrun = lrun * al + sum;
+    mrun = mn;
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) o[t] *= al;
+    // O^T += V^T P^T (k slots of sub-block ks: keys 32ks + 4g + e, then 32ks + 16 + 4g + e)
+    const uint32_t vimg = ldsa(st + Gm::V0 * 16);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pb = pack8(s[2 * ks], s[2 * ks + 1]);
+      v2i lo[DK / 16], hi[DK / 16];
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        lo[t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 4 * g, 16 * t, lane));
+        hi[t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
+      }
+      lgkm0();
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        keep(lo[t]);
+        keep(hi[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) o[t] = mfma(as_frag(lo[t], hi[t]), pb, o[t]);
+    }
+  }
+  // statistics in scaled-score units (max * ln 2), 1/sum: P = exp(S - max) / sum
+  const float l = xsum16_32(lrun);
+  const float il = 1.f / l;
+  if (iq < T) {
+    if (g == 0) {  // a fully masked row keeps the masked score itself as its max (uniform P)
+      float* sp = a.stats + 2 * (((int64_t)b * a.H + h) * T + iq);
+      sp[0] = mrun <= -1e38f ? -1e38f : mrun * 0.6931471805599453f;
+      sp[1] = il;
+    }
+    bf16_t* dst = a.ctx + ((int64_t)b * T + iq) * a.ldc + h * DK + 4 * g;
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) {
+      const uint2 pk = make_uint2(pk_bf16(o[t][0] * il, o[t][1] * il), pk_bf16(o[t][2] * il, o[t][3] * il));
+      *(uint2*)(dst + 16 * t) = pk;
+    }
+  }
+}
+
+template <int DK, int NW, bool RP, bool RM>
+void launch_fwd_t(const FlashP& a, hipStream_t st) {
+  const dim3 grid((unsigned)cdiv(a.T, 16 * NW), (unsigned)a.H, (unsigned)a.B);
+  flash_fwd_kernel<DK, NW, RP, RM><<<grid, NW * 64, 0, st>>>(a);
+}
+
+// RP: the encoder's relative-position attention (8 waves, 128 queries per workgroup); plain:
+// the decoder's (4 waves, 64 queries: Tq = L + 1 is short)
+void launch_flash_fwd(const FlashP& a, int dk, bool rp, bool rm, hipStream_t st) {
+  if (rp) {
+    if (dk == 64) rm ? launch_fwd_t<64, 8, true, true>(a, st) : launch_fwd_t<64, 8, true, false>(a, st);
+    else rm ? launch_fwd_t<32, 8, true, true>(a, st) : launch_fwd_t<32, 8, true, false>(a, st);
+    return;
+  }
+  if (dk == 64) rm ? launch_fwd_t<64, 4, false, true>(a, st) : launch_fwd_t<64, 4, false, false>(a, st);
+  else rm ? launch_fwd_t<32, 4, false, true>(a, st) : launch_fwd_t<32, 4, false, false>(a, st);
+}
+
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// query-dependent masks are staged by LDS-DMA: 16-B aligned rows
+int check_mask(const uint8_t* mask, int64_t msb, int64_t msq, int Tk, const char* who) {
+  if (mask && msq != 0)
+    LASR_CHECK_ARG(al16(mask) && msq % 16 == 0 && msb % 16 == 0 && msq >= Tk,
+                   "%s: a query-dependent mask needs 16-B aligned rows (row stride %% 16 == 0, >= Tk)", who);
+  else
+    LASR_CHECK_ARG(Tk <= KMASK_BYTES, "%s: Tk=%d above %d keys", who, Tk, KMASK_BYTES);
+  return LASR_OK;
+}
+
+}  // namespace
+
+extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, const void* k,
+                                const void* v, int64_t ldkv, const void* pos, int64_t ldp, int B,
+                                int H, int T, int dk, const uint8_t* mask, int64_t mask_sb,
+                                int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc,
+                                void* stream) {
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_fwd: d_k=%d (32 or 64)", dk);
+  LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_fwd: bad B/H/T");
+  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
+                 "lasr_relattn_fwd: row strides must be multiples of 8");
+  LASR_CHECK_ARG(al16(qu) && al16(qv) && al16(k) && al16(v) && al16(pos) && al16(ctx), "lasr_relattn_fwd: 16-B alignment");
+  if (B == 0 || T == 0) return LASR_OK;
+  if (int rc = check_mask(mask, mask_sb, mask_sq, T, "lasr_relattn_fwd")) return rc;
+  FlashP a = {};
+  a.qu = (const bf16_t*)qu; a.qv = (const bf16_t*)qv; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.pos = (const bf16_t*)pos;
+  a.ldq = ldq; a.ldkv = ldkv; a.ldp = ldp;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
+  a.B = B; a.H = H; a.T = T; a.Tk = T; a.scale = scale;
+  a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
+  launch_flash_fwd(a, dk, true, mask && mask_sq != 0, (hipStream_t)stream);
+  return lasr_check_launch("relattn_fwd");
+}
+
+// Plain scaled dot-product attention (no positional term) with Tk keys per utterance: the
+// decoder's self attention (Tk = Tq, causal + padding mask) and source attention over the
+// encoder output (Tk = T', key padding).
+extern "C" int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                             int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc, void* stream) {
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_fwd: d_k=%d (32 or 64)", dk);
+  LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_fwd: bad B/H/T");
+  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
+                 "lasr_attn_fwd: row strides must be multiples of 8");
+  LASR_CHECK_ARG(al16(q) && al16(k) && al16(v) && al16(ctx), "lasr_attn_fwd: 16-B alignment");
+  if (B == 0 || Tq == 0) return LASR_OK;
+  if (int rc = check_mask(mask, mask_sb, mask_sq, Tk, "lasr_attn_fwd")) return rc;
+  FlashP a = {};
+  a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.ldq = ldq; a.ldkv = ldkv;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
+  a.B = B; a.H = H; a.T = Tq; a.Tk = Tk; a.scale = scale;
+  a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
+  launch_flash_fwd(a, dk, false, mask && mask_sq != 0, (hipStream_t)stream);
+  return lasr_check_launch("attn_fwd");
+}

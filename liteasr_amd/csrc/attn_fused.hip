@@ -286,103 +286,6 @@ LASR_DEV void load_qfrags(const RelAttnP& a, int b, int h, int iw, int lane, bf1
   }
 }
 
-// Forward, one pass with the online softmax: per key block, stage K / V / the position
-// window (the next block's global loads in flight while this one computes), S on MFMA,
-// running max / sum, O = O * exp(m_old - m_new) + P V.
-template <int DK, bool RM, bool RP>
-__global__ __launch_bounds__(256, 2) void relattn_fwd_kernel(RelAttnP a) {
-  constexpr int KS = DK / 32;
-  __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
-  __shared__ __attribute__((aligned(16))) bf16_t psh[4][16 * PLD];
-  __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t vsh[64 * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t pesh[PE_ROWS * PELD];
-  __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
-  const int h = blockIdx.y, b = blockIdx.z, T = a.T;
-  const int i0 = blockIdx.x * 64, iw = i0 + 16 * w, Tk = a.Tk;
-  const int64_t base = (int64_t)b * T, kbase = (int64_t)b * Tk;
-  const bf16_t* kh = a.k + kbase * a.ldkv + h * DK;
-  const bf16_t* vh = a.v + kbase * a.ldkv + h * DK;
-  const bf16_t* ph = a.pos + h * DK;
-  float* gw = gsh[w];
-  bf16_t* pw = psh[w];
-
-  bf16x8 qu[KS], qv[KS], qv1[KS];
-  load_qfrags<DK>(a, b, h, iw, lane, qu, qv, qv1);
-    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, Tk, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, Tk, tid);
-  PeWin rp{};
-  if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
-  KeyMask km;
-  keymask_fetch(a, b, 0, lane, km);
-  MaskBlk mk{};
-  if constexpr (RM) mk = mask_fetch(a, b, i0, 0, tid);
-
-  float mrun[4], lrun[4];
-  f32x4 o[DK / 16], s[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) { mrun[q] = -INFINITY; lrun[q] = 0.f; }
-#pragma unroll
-  for (int t = 0; t < DK / 16; ++t) o[t] = zero4();
-  for (int j0 = 0; j0 < Tk; j0 += 64) {
-    __syncthreads();  // previous block's images consumed
-    blk_store<DK>(ksh, rk, tid);
-    blk_store<DK>(vsh, rv, tid);
-    if constexpr (RP) pe_store<DK>(pesh, rp, tid);
-    const uint32_t mb_cur = keymask_bits(km);
-    if constexpr (RM) mask_store(msh, mk, tid);
-    __syncthreads();
-    // prefetch the next key block (unconditional: clamped rows keep the last one in
-    // bounds, and no branch merge forces a wait on the loads)
-    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, Tk, tid);
-    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, Tk, tid);
-    if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
-    keymask_fetch(a, b, j0 + 64, lane, km);
-    if constexpr (RM) mk = mask_fetch(a, b, i0, j0 + 64, tid);
-    score_tile<DK, RM, RP>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float bm = rmax16(fmaxf(fmaxf(s[0][q], s[1][q]), fmaxf(s[2][q], s[3][q])));
-      const float mn = fmaxf(mrun[q], bm);
-      const float al = __expf(mrun[q] - mn);
-      float e = 0.f;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float pv = __expf(s[c][q] - mn);
-        e += pv;
-        pw[(4 * g + q) * PLD + 16 * c + col] = f2bf(pv);
-      }
-      lrun[q] = lrun[q] * al + rsum16(e);
-      mrun[q] = mn;
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) o[t][q] *= al;
-    }
-    lds_fence();
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pa = *(const bf16x8*)(pw + col * PLD + 8 * g + 32 * ks);
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) o[t] = mfma(pa, frag_tr(vsh + ks * 2048, 16 * t, lane), o[t]);
-    }
-  }
-  // row statistics (max, 1/sum): P = exp(S - max) / sum stays exact for a fully masked
-  // row (every score -1e38), where max + log(sum) would round back to -1e38
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float il = 1.f / lrun[q];
-    const int i = iw + 4 * g + q;
-    if (i >= T) continue;
-    if (col == 0) {
-      float* st = a.stats + 2 * (((int64_t)b * a.H + h) * T + i);
-      st[0] = mrun[q];
-      st[1] = il;
-    }
-    bf16_t* dst = a.ctx + (base + i) * a.ldc + h * DK + col;
-#pragma unroll
-    for (int t = 0; t < DK / 16; ++t) dst[16 * t] = f2bf(o[t][q] * il);
-  }
-}
-
 // P and dS of one (16 x 64) tile: P as the forward normalised it (a fully masked row is
 // uniform, attention.py:54-55), dS = P (dP - D), zero where masked (masked_fill backward),
 // past T or past the rows.  dP = dO V^T with V from its staged image.
@@ -634,15 +537,6 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 template <bool RP>
-void launch_fwd(const RelAttnP& a, int dk, bool rm, hipStream_t st) {
-  const dim3 grid((unsigned)cdiv(a.T, 64), (unsigned)a.H, (unsigned)a.B);
-  if (dk == 64 && rm) relattn_fwd_kernel<64, true, RP><<<grid, 256, 0, st>>>(a);
-  else if (dk == 64) relattn_fwd_kernel<64, false, RP><<<grid, 256, 0, st>>>(a);
-  else if (rm) relattn_fwd_kernel<32, true, RP><<<grid, 256, 0, st>>>(a);
-  else relattn_fwd_kernel<32, false, RP><<<grid, 256, 0, st>>>(a);
-}
-
-template <bool RP>
 int launch_bwd(const RelAttnP& a, int dk, bool rm, hipStream_t st) {
   const dim3 gq((unsigned)cdiv(a.T, 64), (unsigned)a.H, (unsigned)a.B);
   if (dk == 64 && rm) relattn_bwd_q_kernel<64, true, RP><<<gq, 256, 0, st>>>(a);
@@ -660,28 +554,6 @@ int launch_bwd(const RelAttnP& a, int dk, bool rm, hipStream_t st) {
 }
 
 }  // namespace
-
-extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, const void* k,
-                                const void* v, int64_t ldkv, const void* pos, int64_t ldp, int B,
-                                int H, int T, int dk, const uint8_t* mask, int64_t mask_sb,
-                                int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc,
-                                void* stream) {
-  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_fwd: d_k=%d (32 or 64)", dk);
-  LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_fwd: bad B/H/T");
-  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc >= H * dk,
-                 "lasr_relattn_fwd: row strides must be multiples of 8");
-  LASR_CHECK_ARG(al16(qu) && al16(qv) && al16(k) && al16(v) && al16(pos), "lasr_relattn_fwd: 16-B alignment");
-  if (B == 0 || T == 0) return LASR_OK;
-  RelAttnP a = {};
-  a.qu = (const bf16_t*)qu; a.qv = (const bf16_t*)qv; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
-  a.pos = (const bf16_t*)pos;
-  a.ldq = ldq; a.ldkv = ldkv; a.ldp = ldp;
-  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
-  a.B = B; a.H = H; a.T = T; a.Tk = T; a.scale = scale;
-  a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
-  launch_fwd<true>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
-  return lasr_check_launch("relattn_fwd");
-}
 
 extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, const void* k,
                                 const void* v, int64_t ldkv, const void* pos, int64_t ldp, int B,
@@ -709,27 +581,6 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   a.dqu = (bf16_t*)dqu; a.dbd = (bf16_t*)dbd; a.ldS = ldS; a.dbd_hb = dbd_head_major;
   a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
   return launch_bwd<true>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
-}
-
-// Plain scaled dot-product attention (no positional term) on the same kernels, with Tk keys
-// per utterance: the decoder's self attention (Tk = Tq, causal + padding mask) and source
-// attention over the encoder output (Tk = T', key padding).
-extern "C" int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
-                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
-                             int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc, void* stream) {
-  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_fwd: d_k=%d (32 or 64)", dk);
-  LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_fwd: bad B/H/T");
-  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc >= H * dk, "lasr_attn_fwd: row strides must be multiples of 8");
-  LASR_CHECK_ARG(al16(q) && al16(k) && al16(v), "lasr_attn_fwd: 16-B alignment");
-  if (B == 0 || Tq == 0) return LASR_OK;
-  RelAttnP a = {};
-  a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
-  a.ldq = ldq; a.ldkv = ldkv;
-  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
-  a.B = B; a.H = H; a.T = Tq; a.Tk = Tk; a.scale = scale;
-  a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
-  launch_fwd<false>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
-  return lasr_check_launch("attn_fwd");
 }
 
 extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,

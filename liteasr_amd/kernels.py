@@ -519,9 +519,34 @@ def relshift_bwd(dS, Z, T, ldS, dBD):
     N.call("lasr_relshift_bwd", ptr(dS), dt(dS), Z, T, ldS, ptr(dBD), stream())
 
 
+def pad_mask16(mask, B, Tq, Tk):
+    """A query-dependent mask [B, Tq, Tk] (u8, any layout) as a view of a buffer whose rows are
+    16-B aligned (the forward kernels stage its tiles by LDS-DMA): (view, msb, msq).  Padding
+    columns are 1 (masked); the view is the same tensor when already aligned."""
+    if mask.stride(-1) == 1 and mask.stride(-2) % 16 == 0 and mask.stride(0) % 16 == 0 and mask.data_ptr() % 16 == 0:
+        return mask, mask.stride(0), mask.stride(-2)
+    P = (Tk + 15) // 16 * 16
+    buf = torch.ones(B, Tq, P, dtype=torch.uint8, device=mask.device)
+    buf[:, :, :Tk] = mask
+    v = buf[:, :, :Tk]
+    return v, v.stride(0), v.stride(1)
+
+
+def _fwd_mask(mask, msb, msq, B, Tq, Tk):
+    """(mask, msb, msq) for the forward kernels: query-dependent masks re-laid out with 16-B
+    aligned rows when they are not (callers that build masks per step pre-align them)."""
+    if mask is None or msq == 0:
+        return mask, msb, msq
+    if msq % 16 == 0 and msb % 16 == 0 and mask.data_ptr() % 16 == 0:
+        return mask, msb, msq
+    m = mask.reshape(-1).as_strided((B, Tq, Tk), (msb, msq, 1))
+    return pad_mask16(m, B, Tq, Tk)
+
+
 def relattn_fwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx):
     """Fused rel-pos self-attention (bf16, d_k 32 or 64); 2-D row-major operands (row
     strides read from the tensors), stats [B*H*T*2] fp32 out, ctx [B*T, H*d_k] out."""
+    mask, msb, msq = _fwd_mask(mask, msb, msq, B, T, T)
     N.call("lasr_relattn_fwd", ptr(qu), ptr(qv), qu.stride(0), ptr(k), ptr(v), k.stride(0), ptr(pos),
            pos.stride(0), B, H, T, qu.shape[1] // H, ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx),
            ctx.stride(0), stream())
@@ -541,6 +566,7 @@ def attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx):
     """Plain attention on the fused kernels (lasr_attn_fwd): q [B*Tq, H*d_k], k / v
     [B*Tk, H*d_k] row-major views (k and v share a row stride), stats [B*H*Tq*2] fp32."""
     assert v.stride(0) == k.stride(0)
+    mask, msb, msq = _fwd_mask(mask, msb, msq, B, Tq, Tk)
     N.call("lasr_attn_fwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, q.shape[1] // H,
            ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ctx.stride(0), stream())
 

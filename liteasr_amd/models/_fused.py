@@ -139,12 +139,15 @@ class FusedEncoderModel(LiteasrModel):
         yy = ys.to(device=dev, dtype=torch.int64).contiguous()
         yl = ylens.to(device=dev, dtype=torch.int64)
         K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, 0, out)
+        # query-dependent masks as views with 16-B aligned rows (the attention kernels stage
+        # their tiles by LDS-DMA); kernels read them through (msb, msq) = the view's strides
+        out["dec_mask"] = K.pad_mask16(out["dec_mask"], B, L + 1, L + 1)[0]
         chunk = None
         if self.chunk_size > 0:
             tmp = dict(out)
             tmp["enc_mask"] = torch.empty(B, Tsub, Tsub, dtype=u8, device=dev)
             K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, self.chunk_size, tmp)
-            chunk = tmp["enc_mask"]
+            chunk = K.pad_mask16(tmp["enc_mask"], B, Tsub, Tsub)[0]
         p = SimpleNamespace(B=B, Tx=Tx, T=Tsub, L=L, chunk_mask=chunk, **out)
         return p
 
@@ -167,7 +170,7 @@ class FusedEncoderModel(LiteasrModel):
             p_dec_pos=getattr(dr, "pos", 0.0), ys_in=prep.ys_in, dec_mask=prep.dec_mask, mask_k=prep.enc_mask,
             seed=self._seed_base)
         if prep.chunk_mask is not None:
-            env.mask, env.msb, env.msq = prep.chunk_mask, T * T, T
+            env.mask, env.msb, env.msq = prep.chunk_mask, prep.chunk_mask.stride(0), prep.chunk_mask.stride(1)
         else:
             env.mask, env.msb, env.msq = prep.enc_mask, T, 0
         K.set_dropout_counter(self._drop_ctr)

@@ -912,7 +912,7 @@ class HeadsFn(torch.autograd.Function):
         y = _e((R, d), F32, dev)
         K.embed_pe_fwd(env.ys_in, L1, wd.E, wd.pe, math.sqrt(d), y, env.p_dec_pos if tr else 0.0,
                        env.seed + 3)
-        masks = (env.dec_mask, L1 * L1, L1, env.mask_k)
+        masks = (env.dec_mask, env.dec_mask.stride(0), env.dec_mask.stride(1), env.mask_k)
         h_attn, dsv = decoder_layers_fwd(dec, wd, y, h, B, L1, T, masks, p, adt)
         ctx.sv = SimpleNamespace(x=x, h=h, hd=hd, me=me, re=re, dec=dsv)
         ctx.model, ctx.env = model, env
@@ -1405,7 +1405,8 @@ def decoder_logits(model, h, ys_in, dec_mask, mem_mask, B, L1, T):
     K.embed_pe_fwd(ys_in, L1, wd.E, wd.pe, math.sqrt(d), y, 0.0, 0)
     for lw in wd.layers:
         l1, _, _, _ = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
-        y1, _ = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, dec_mask, L1 * L1, L1, y, 0.0, 0, 0.0, 0)
+        y1, _ = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, dec_mask, dec_mask.stride(0), dec_mask.stride(1), y,
+                            0.0, 0, 0.0, 0)
         l2, _, _, _ = ln_forward(y1, lw.ln2.g, lw.ln2.b, adt)
         y2, _ = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, mem_mask, T, 0, y1, 0.0, 0, 0.0, 0)
         l3, _, _, _ = ln_forward(y2, lw.ln3.g, lw.ln3.b, adt)

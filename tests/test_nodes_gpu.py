@@ -186,7 +186,7 @@ def test_decoder_layer_node_config2():
     dec = model.decoder
     model.store.ensure_grad().zero_()
     wd, gd = dec.weights(), dec.grads()
-    masks = (prep.dec_mask, L1 * L1, L1, prep.enc_mask)
+    masks = (prep.dec_mask, prep.dec_mask.stride(0), prep.dec_mask.stride(1), prep.enc_mask)
     memd = mem.cuda()
     h_attn, sv = FN.decoder_layers_fwd(dec, wd, y_in.cuda(), memd, B, L1, T, masks, (0.0, 0.0, 0.0, 0.0),
                                        torch.bfloat16)

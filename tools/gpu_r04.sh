@@ -16,6 +16,8 @@ for s in "$@"; do
     new) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py tests/test_switches_gpu.py tests/test_nodes_gpu.py \
            "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" "tests/test_model_gpu.py::test_parity_config4_full_model_bf16_emulated" \
            "tests/test_kernels_gpu.py::test_gemm_ksub2_bit_identical" -s > "$OUT/new.log" 2>&1 ;;
+    attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
+    attnbench) run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_bench.jsonl" 2> "$OUT/attn_bench.err" ;;
     kgpu) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py tests/test_row_ln_gpu.py > "$OUT/kgpu.log" 2>&1 ;;
     model) run timeout -k 10 900 $PYT tests/test_model_gpu.py tests/test_nodes_gpu.py -s > "$OUT/model.log" 2>&1 ;;
     smoke) run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
