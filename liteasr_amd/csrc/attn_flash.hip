@@ -41,6 +41,13 @@ struct FlashP {
   float* stats;                         // [B*H*T][2]: row max (scaled-score units), 1/row sum
   bf16_t* ctx;
   int64_t ldc;
+  // backward (query side)
+  const bf16_t* dctx;                   // [B*T, ldc]
+  const bf16_t* ctx_in;                 // forward output (for D = rowsum(dO * O))
+  float* Dbuf;                          // [B*H*T]
+  bf16_t* dqu;                          // [B*T, ldq]
+  bf16_t* dbd;                          // [B][H] (or [H][B] if dbd_hb) x [T, ldS]
+  int ldS, dbd_hb;
 };
 
 // bf16 zero row: the relative-position window's rows outside the table (m == T, past 2T)
@@ -418,6 +425,173 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
   }
 }
 
+// ---- backward, query side ----------------------------------------------------------------
+// Per (b, h, 16*NW queries), over the key blocks (the forward's ring, stages and transposed
+// scores): P = exp(S - max) / sum from the forward's statistics, dP^T = V . dO^T, dS = P (dP - D)
+// (zero where masked), dQu^T += K^T dS^T (dS^T kept in registers as the forward keeps P^T), and
+// dS scattered through the inverse rel_shift into dBD, the G-space gradient the positional
+// GEMMs consume (exactly relshift_bwd's output).  D_i = rowsum(dO * O) is formed here and
+// stored for the key-side kernel.
+template <int DK, int NW, bool RP, bool RM>
+__global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
+  using Gm = Geo<DK, NW, RP, RM>;
+  constexpr int KS = DK / 32, NT = Gm::NT;
+  __shared__ __attribute__((aligned(16))) char smem[fwd_lds<DK, NW, RP, RM>()];
+  char* ring = smem;
+  float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);
+  uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * 16 * GLD : 0));
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, col = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
+  const int i0 = blockIdx.x * Gm::QB, iw = i0 + 16 * w, iq = iw + col, ic = min(iq, T - 1);
+  const int nb = (Tk + KB - 1) / KB;
+  const float c2 = a.scale * 1.4426950408889634f;
+  const int64_t zrow = ((int64_t)b * a.H + h) * T;
+
+  issue_stage<DK, NW, RP, RM>(a, b, h, i0, 0, ring, tid);
+  const uint8_t* km = nullptr;
+  if constexpr (!RM) {
+    if (a.mask) {
+      const uint8_t* mr = a.mask + (int64_t)b * a.msb;
+      const int kpad = nb * KB;
+      for (int j = tid; j < kpad; j += NT) kmask[j] = j < Tk ? mr[j] : 0;
+      km = kmask;
+    }
+  }
+  bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
+  load_q<DK>(a.qu, a.ldq, b * T + ic, h, lane, qu);
+  load_q<DK>(a.dctx, a.ldc, b * T + ic, h, lane, dof);
+  if constexpr (RP) {
+    load_q<DK>(a.qv, a.ldq, b * T + ic, h, lane, qv);
+    load_q<DK>(a.qv, a.ldq, b * T + min(iq + 1, T - 1), h, lane, qv1);
+  }
+  // the forward's statistics in log2 units (a fully masked row keeps the masked value)
+  const float mx = a.stats[2 * (zrow + ic)], il = a.stats[2 * (zrow + ic) + 1];
+  const float m2 = mx <= -1e38f ? -1e38f : mx * 1.4426950408889634f;
+  // D_i = sum_c dO[i,c] O[i,c]: the 4 lane groups of a query take DK/4 columns each
+  float D;
+  {
+    const bf16_t* pd = a.dctx + ((int64_t)b * T + ic) * a.ldc + h * DK + g * (DK / 4);
+    const bf16_t* po = a.ctx_in + ((int64_t)b * T + ic) * a.ldc + h * DK + g * (DK / 4);
+    float vd[DK / 4], vo[DK / 4];
+    ldv<DK / 4>(pd, vd);
+    ldv<DK / 4>(po, vo);
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < DK / 4; ++e) acc += vd[e] * vo[e];
+    D = xsum16_32(acc);
+    if (g == 0 && iq < T) a.Dbuf[zrow + iq] = D;
+  }
+  bf16_t* dbd = RP ? a.dbd + (a.dbd_hb ? ((int64_t)h * a.B + b) * T : zrow) * a.ldS : nullptr;
+  float* gw = gsh + w * 16 * GLD;
+  f32x4 dq[DK / 16];
+#pragma unroll
+  for (int t = 0; t < DK / 16; ++t) dq[t] = zero4();
+
+  for (int jb = 0; jb < nb; ++jb) {
+    const int j0 = jb * KB;
+    char* st = ring + (jb & 1) * Gm::STAGE_BYTES;
+    wait_vmcnt<0>();
+    lds_barrier();
+    if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
+    f32x4 s[4];
+    scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
+    // dP^T = V . dO^T (V rows = keys as the A operand)
+    const uint32_t vimg = ldsa(st + Gm::V0 * 16);
+    f32x4 dp[4];
+    {
+      v4i r[4][KS];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) r[c][ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * c, 32 * ks, lane));
+      lgkm0();
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) keep(r[c][ks]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(r[c][ks]), dof[ks], acc);
+        dp[c] = acc;
+      }
+    }
+    // dS = P (dP - D), zero where masked or past Tk (the forward's masked_fill backward)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = s[c][e];
+        const float p = __builtin_amdgcn_exp2f(v - m2) * il;
+        s[c][e] = v > -1e38f ? p * (dp[c][e] - D) : 0.f;
+      }
+    // dQu^T += K^T dS^T (bf16 dS, the key order of the forward's P^T)
+    const uint32_t kimg = ldsa(st);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 db = pack8(s[2 * ks], s[2 * ks + 1]);
+      v2i lo[DK / 16], hi[DK / 16];
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        lo[t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 4 * g, 16 * t, lane));
+        hi[t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
+      }
+      lgkm0();
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        keep(lo[t]);
+        keep(hi[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(as_frag(lo[t], hi[t]), db, dq[t]);
+    }
+    if constexpr (RP) {
+      // inverse rel_shift: the bd entry each score read (none for j == i + 1)
+      if (iq < T) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int j = j0 + 16 * c + 4 * g + e;
+            if (j < T && j != iq + 1) {
+              const int64_t off = j <= iq ? (int64_t)iq * a.ldS + (T - 1 - iq + j) : (int64_t)(iq + 1) * a.ldS + (j - iq - 2);
+              dbd[off] = f2bf(s[c][e]);
+            }
+          }
+      }
+    }
+  }
+  if (iq < T) {
+    bf16_t* dst = a.dqu + ((int64_t)b * T + iq) * a.ldq + h * DK + 4 * g;
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) {
+      const uint2 pk = make_uint2(pk_bf16(dq[t][0] * a.scale, dq[t][1] * a.scale),
+                                  pk_bf16(dq[t][2] * a.scale, dq[t][3] * a.scale));
+      *(uint2*)(dst + 16 * t) = pk;
+    }
+  }
+  // bd row 0, columns 0..T-2 are read by no score (rel_shift pads them): zero gradient
+  if (RP && blockIdx.x == 0)
+    for (int c = tid; c < T - 1; c += NT) dbd[c] = f2bf(0.f);
+}
+
+template <int DK, int NW, bool RP, bool RM>
+void launch_bwd_q_t(const FlashP& a, hipStream_t st) {
+  const dim3 grid((unsigned)cdiv(a.T, 16 * NW), (unsigned)a.H, (unsigned)a.B);
+  flash_bwd_q_kernel<DK, NW, RP, RM><<<grid, NW * 64, 0, st>>>(a);
+}
+
+void launch_flash_bwd_q(const FlashP& a, int dk, bool rp, bool rm, hipStream_t st) {
+  if (rp) {
+    if (dk == 64) rm ? launch_bwd_q_t<64, 8, true, true>(a, st) : launch_bwd_q_t<64, 8, true, false>(a, st);
+    else rm ? launch_bwd_q_t<32, 8, true, true>(a, st) : launch_bwd_q_t<32, 8, true, false>(a, st);
+    return;
+  }
+  if (dk == 64) rm ? launch_bwd_q_t<64, 4, false, true>(a, st) : launch_bwd_q_t<64, 4, false, false>(a, st);
+  else rm ? launch_bwd_q_t<32, 4, false, true>(a, st) : launch_bwd_q_t<32, 4, false, false>(a, st);
+}
+
 template <int DK, int NW, bool RP, bool RM>
 void launch_fwd_t(const FlashP& a, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(a.T, 16 * NW), (unsigned)a.H, (unsigned)a.B);
@@ -449,6 +623,12 @@ int check_mask(const uint8_t* mask, int64_t msb, int64_t msq, int Tk, const char
 }
 
 }  // namespace
+
+int lasr_attn_bwd_kv_launch(const void* qu, const void* qv, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                            const void* pos, int64_t ldp, int B, int H, int T, int Tk, int dk, const uint8_t* mask,
+                            int64_t mask_sb, int64_t mask_sq, float scale, const float* stats, const void* dctx,
+                            int64_t ldc, const float* Dbuf, void* dk_out, void* dv_out, int64_t lddkv, bool rp,
+                            void* stream);
 
 extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, const void* k,
                                 const void* v, int64_t ldkv, const void* pos, int64_t ldp, int B,
@@ -494,4 +674,61 @@ extern "C" int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const vo
   a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
   launch_flash_fwd(a, dk, false, mask && mask_sq != 0, (hipStream_t)stream);
   return lasr_check_launch("attn_fwd");
+}
+
+extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, const void* k,
+                                const void* v, int64_t ldkv, const void* pos, int64_t ldp, int B,
+                                int H, int T, int dk, const uint8_t* mask, int64_t mask_sb,
+                                int64_t mask_sq, float scale, const float* stats, const void* ctx,
+                                const void* dctx, int64_t ldc, float* Dbuf, void* dqu, void* dbd,
+                                int ldS, int dbd_head_major, void* dk_out, void* dv_out, int64_t lddkv,
+                                void* stream) {
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_bwd: d_k=%d (32 or 64)", dk);
+  LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_bwd: bad B/H/T");
+  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
+                 "lasr_relattn_bwd: row strides must be multiples of 8");
+  LASR_CHECK_ARG(ldS >= T, "lasr_relattn_bwd: ldS < T");
+  LASR_CHECK_ARG(al16(qu) && al16(qv) && al16(k) && al16(v) && al16(pos) && al16(dctx) && al16(ctx) && al16(dqu),
+                 "lasr_relattn_bwd: 16-B alignment");
+  if (B == 0 || T == 0) return LASR_OK;
+  if (int rc = check_mask(mask, mask_sb, mask_sq, T, "lasr_relattn_bwd")) return rc;
+  FlashP a = {};
+  a.qu = (const bf16_t*)qu; a.qv = (const bf16_t*)qv; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.pos = (const bf16_t*)pos;
+  a.ldq = ldq; a.ldkv = ldkv; a.ldp = ldp;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
+  a.B = B; a.H = H; a.T = T; a.Tk = T; a.scale = scale;
+  a.stats = (float*)stats; a.ldc = ldc;
+  a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
+  a.dqu = (bf16_t*)dqu; a.dbd = (bf16_t*)dbd; a.ldS = ldS; a.dbd_hb = dbd_head_major;
+  launch_flash_bwd_q(a, dk, true, mask && mask_sq != 0, (hipStream_t)stream);
+  if (int rc = lasr_check_launch("relattn_bwd_q")) return rc;
+  return lasr_attn_bwd_kv_launch(qu, qv, ldq, k, v, ldkv, pos, ldp, B, H, T, T, dk, mask, mask_sb, mask_sq, scale,
+                                 stats, dctx, ldc, Dbuf, dk_out, dv_out, lddkv, true, stream);
+}
+
+extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                             int64_t mask_sq, float scale, const float* stats, const void* ctx, const void* dctx,
+                             int64_t ldc, float* Dbuf, void* dq, void* dk_out, void* dv_out, int64_t lddkv,
+                             void* stream) {
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_bwd: d_k=%d (32 or 64)", dk);
+  LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_bwd: bad B/H/T");
+  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk && lddkv % 8 == 0,
+                 "lasr_attn_bwd: row strides must be multiples of 8");
+  LASR_CHECK_ARG(al16(q) && al16(k) && al16(v) && al16(dctx) && al16(ctx) && al16(dq), "lasr_attn_bwd: 16-B alignment");
+  if (B == 0 || Tq == 0) return LASR_OK;
+  if (int rc = check_mask(mask, mask_sb, mask_sq, Tk, "lasr_attn_bwd")) return rc;
+  FlashP a = {};
+  a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.ldq = ldq; a.ldkv = ldkv;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
+  a.B = B; a.H = H; a.T = Tq; a.Tk = Tk; a.scale = scale;
+  a.stats = (float*)stats; a.ldc = ldc;
+  a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
+  a.dqu = (bf16_t*)dq;
+  launch_flash_bwd_q(a, dk, false, mask && mask_sq != 0, (hipStream_t)stream);
+  if (int rc = lasr_check_launch("attn_bwd_q")) return rc;
+  return lasr_attn_bwd_kv_launch(q, q, ldq, k, v, ldkv, nullptr, 0, B, H, Tq, Tk, dk, mask, mask_sb, mask_sq, scale,
+                                 stats, dctx, ldc, Dbuf, dk_out, dv_out, lddkv, false, stream);
 }

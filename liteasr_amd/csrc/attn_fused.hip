@@ -310,112 +310,6 @@ LASR_DEV void dscore_tile(const RelAttnP& a, const bf16_t* vimg, const bf16x8 (&
   }
 }
 
-template <int DK, bool RM, bool RP>
-__global__ __launch_bounds__(256, 2) void relattn_bwd_q_kernel(RelAttnP a) {
-  constexpr int KS = DK / 32;
-  __shared__ __attribute__((aligned(16))) float gsh[4][16 * GLD];
-  __shared__ __attribute__((aligned(16))) bf16_t psh[4][16 * PLD];
-  __shared__ __attribute__((aligned(16))) bf16_t ksh[64 * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t vsh[64 * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t pesh[PE_ROWS * PELD];
-  __shared__ __attribute__((aligned(16))) uint8_t msh[RM ? 64 * MLD : 16];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, g = lane >> 4;
-  const int h = blockIdx.y, b = blockIdx.z, T = a.T;
-  const int i0 = blockIdx.x * 64, iw = i0 + 16 * w, Tk = a.Tk;
-  const int64_t base = (int64_t)b * T, kbase = (int64_t)b * Tk, zrow = ((int64_t)b * a.H + h) * T;
-  const bf16_t* kh = a.k + kbase * a.ldkv + h * DK;
-  const bf16_t* vh = a.v + kbase * a.ldkv + h * DK;
-  const bf16_t* ph = a.pos + h * DK;
-  float* gw = gsh[w];
-  bf16_t* pw = psh[w];
-
-    Blk rk = blk_fetch<DK>(kh, a.ldkv, 0, Tk, tid), rv = blk_fetch<DK>(vh, a.ldkv, 0, Tk, tid);
-  PeWin rp{};
-  if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, -i0 + T - 64, tid);
-  KeyMask km;
-  keymask_fetch(a, b, 0, lane, km);
-  MaskBlk mk{};
-  if constexpr (RM) mk = mask_fetch(a, b, i0, 0, tid);
-  bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
-  load_qfrags<DK>(a, b, h, iw, lane, qu, qv, qv1);
-  {
-    const bf16_t* pd = a.dctx + (base + min(iw + col, T - 1)) * a.ldc + h * DK + 8 * g;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) dof[ks] = ldg8(pd + 32 * ks);
-  }
-  float mx[4], il[4], D[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int i = min(iw + 4 * g + q, T - 1);
-    mx[q] = a.stats[2 * (zrow + i)];
-    il[q] = a.stats[2 * (zrow + i) + 1];
-    // D_i = sum_c dO[i,c] O[i,c]: the 16 lanes of the row group take DK/16 columns each
-    const bf16_t* pd = a.dctx + (base + i) * a.ldc + h * DK + (DK / 16) * col;
-    const bf16_t* po = a.ctx_in + (base + i) * a.ldc + h * DK + (DK / 16) * col;
-    float vd[DK / 16], vo[DK / 16];
-    ldv<DK / 16>(pd, vd);
-    ldv<DK / 16>(po, vo);
-    float acc = 0.f;
-#pragma unroll
-    for (int e = 0; e < DK / 16; ++e) acc += vd[e] * vo[e];
-    D[q] = rsum16(acc);
-    if (col == 0 && iw + 4 * g + q < T) a.Dbuf[zrow + iw + 4 * g + q] = D[q];
-  }
-
-  f32x4 dq[DK / 16];
-#pragma unroll
-  for (int t = 0; t < DK / 16; ++t) dq[t] = zero4();
-  bf16_t* dbd = a.dbd + (a.dbd_hb ? ((int64_t)h * a.B + b) * T : zrow) * a.ldS;
-  f32x4 s[4], p[4], ds[4];
-  for (int j0 = 0; j0 < Tk; j0 += 64) {
-    __syncthreads();
-    blk_store<DK>(ksh, rk, tid);
-    blk_store<DK>(vsh, rv, tid);
-    if constexpr (RP) pe_store<DK>(pesh, rp, tid);
-    const uint32_t mb_cur = keymask_bits(km);
-    if constexpr (RM) mask_store(msh, mk, tid);
-    __syncthreads();
-    rk = blk_fetch<DK>(kh, a.ldkv, j0 + 64, Tk, tid);  // next block (unconditional, clamped)
-    rv = blk_fetch<DK>(vh, a.ldkv, j0 + 64, Tk, tid);
-    if constexpr (RP) rp = pe_fetch<DK>(ph, a.ldp, T, j0 + 64 - i0 + T - 64, tid);
-    keymask_fetch(a, b, j0 + 64, lane, km);
-    if constexpr (RM) mk = mask_fetch(a, b, i0, j0 + 64, tid);
-    score_tile<DK, RM, RP>(a, ksh, pesh, qu, qv, qv1, b, w, iw, j0, mb_cur, msh, gw, s, lane);
-    dscore_tile<DK>(a, vsh, dof, s, mx, il, D, iw, lane, p, ds);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 4 * g + q, i = iw + r, j = j0 + 16 * c + col;
-        const bf16_t v = f2bf(ds[c][q]);
-        pw[r * PLD + 16 * c + col] = v;
-        // inverse rel_shift: the bd entry this score read (none for j == i+1)
-        if (RP && i < T && j < T && j != i + 1) {
-          const int64_t off = j <= i ? (int64_t)i * a.ldS + (T - 1 - i + j) : (int64_t)(i + 1) * a.ldS + (j - i - 2);
-          dbd[off] = v;
-        }
-      }
-    lds_fence();
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 da = *(const bf16x8*)(pw + col * PLD + 8 * g + 32 * ks);
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(da, frag_tr(ksh + ks * 2048, 16 * t, lane), dq[t]);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int i = iw + 4 * g + q;
-    if (i >= T) continue;
-    bf16_t* dst = a.dqu + (base + i) * a.ldq + h * DK + col;
-#pragma unroll
-    for (int t = 0; t < DK / 16; ++t) dst[16 * t] = f2bf(dq[t][q] * a.scale);
-  }
-  // bd row 0, columns 0..T-2 are read by no score (rel_shift pads them): zero gradient
-  if (RP && blockIdx.x == 0)
-    for (int c = tid; c < T - 1; c += 256) dbd[c] = f2bf(0.f);
-}
-
 // dK, dV of one key block: loops over the query blocks; per block the Qu / dO images (A of
 // the scores, B of dK / dV), query stats and the position window are staged (next block
 // prefetched), the K / V fragments of the block stay in registers.
@@ -537,70 +431,35 @@ __global__ __launch_bounds__(256, (DK == 64 && RM) ? 1 : 2) void relattn_bwd_kv_
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 template <bool RP>
-int launch_bwd(const RelAttnP& a, int dk, bool rm, hipStream_t st) {
-  const dim3 gq((unsigned)cdiv(a.T, 64), (unsigned)a.H, (unsigned)a.B);
-  if (dk == 64 && rm) relattn_bwd_q_kernel<64, true, RP><<<gq, 256, 0, st>>>(a);
-  else if (dk == 64) relattn_bwd_q_kernel<64, false, RP><<<gq, 256, 0, st>>>(a);
-  else if (rm) relattn_bwd_q_kernel<32, true, RP><<<gq, 256, 0, st>>>(a);
-  else relattn_bwd_q_kernel<32, false, RP><<<gq, 256, 0, st>>>(a);
-  int rc = lasr_check_launch("relattn_bwd_q");
-  if (rc) return rc;
+void launch_bwd_kv(const RelAttnP& a, int dk, bool rm, hipStream_t st) {
   const dim3 gk((unsigned)cdiv(a.Tk, 64), (unsigned)a.H, (unsigned)a.B);
   if (dk == 64 && rm) relattn_bwd_kv_kernel<64, true, RP><<<gk, 256, 0, st>>>(a);
   else if (dk == 64) relattn_bwd_kv_kernel<64, false, RP><<<gk, 256, 0, st>>>(a);
   else if (rm) relattn_bwd_kv_kernel<32, true, RP><<<gk, 256, 0, st>>>(a);
   else relattn_bwd_kv_kernel<32, false, RP><<<gk, 256, 0, st>>>(a);
-  return lasr_check_launch("relattn_bwd_kv");
 }
 
 }  // namespace
 
-extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, const void* k,
-                                const void* v, int64_t ldkv, const void* pos, int64_t ldp, int B,
-                                int H, int T, int dk, const uint8_t* mask, int64_t mask_sb,
-                                int64_t mask_sq, float scale, const float* stats, const void* ctx,
-                                const void* dctx, int64_t ldc, float* Dbuf, void* dqu, void* dbd,
-                                int ldS, int dbd_head_major, void* dk_out, void* dv_out, int64_t lddkv,
-                                void* stream) {
-  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_bwd: d_k=%d (32 or 64)", dk);
-  LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_bwd: bad B/H/T");
-  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
-                 "lasr_relattn_bwd: row strides must be multiples of 8");
-  LASR_CHECK_ARG(ldS >= T, "lasr_relattn_bwd: ldS < T");
-  LASR_CHECK_ARG(al16(qu) && al16(qv) && al16(k) && al16(v) && al16(pos) && al16(dctx) && al16(ctx),
-                 "lasr_relattn_bwd: 16-B alignment");
-  if (B == 0 || T == 0) return LASR_OK;
+// Key-side backward (dK, dV over all query blocks), after the query-side kernel of
+// attn_flash.hip has written D = rowsum(dO * O) to Dbuf.  Argument checks: the callers
+// (lasr_relattn_bwd / lasr_attn_bwd).
+int lasr_attn_bwd_kv_launch(const void* qu, const void* qv, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                            const void* pos, int64_t ldp, int B, int H, int T, int Tk, int dk, const uint8_t* mask,
+                            int64_t mask_sb, int64_t mask_sq, float scale, const float* stats, const void* dctx,
+                            int64_t ldc, const float* Dbuf, void* dk_out, void* dv_out, int64_t lddkv, bool rp,
+                            void* stream) {
   RelAttnP a = {};
   a.qu = (const bf16_t*)qu; a.qv = (const bf16_t*)qv; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
   a.pos = (const bf16_t*)pos;
   a.ldq = ldq; a.ldkv = ldkv; a.ldp = ldp;
   a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
-  a.B = B; a.H = H; a.T = T; a.Tk = T; a.scale = scale;
+  a.B = B; a.H = H; a.T = T; a.Tk = Tk; a.scale = scale;
   a.stats = (float*)stats; a.ldc = ldc;
-  a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
-  a.dqu = (bf16_t*)dqu; a.dbd = (bf16_t*)dbd; a.ldS = ldS; a.dbd_hb = dbd_head_major;
+  a.dctx = (const bf16_t*)dctx; a.Dbuf = (float*)Dbuf;
   a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
-  return launch_bwd<true>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
-}
-
-extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
-                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
-                             int64_t mask_sq, float scale, const float* stats, const void* ctx, const void* dctx,
-                             int64_t ldc, float* Dbuf, void* dq, void* dk_out, void* dv_out, int64_t lddkv,
-                             void* stream) {
-  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_bwd: d_k=%d (32 or 64)", dk);
-  LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_bwd: bad B/H/T");
-  LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk && lddkv % 8 == 0,
-                 "lasr_attn_bwd: row strides must be multiples of 8");
-  LASR_CHECK_ARG(al16(q) && al16(k) && al16(v) && al16(dctx) && al16(ctx), "lasr_attn_bwd: 16-B alignment");
-  if (B == 0 || Tq == 0) return LASR_OK;
-  RelAttnP a = {};
-  a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
-  a.ldq = ldq; a.ldkv = ldkv;
-  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
-  a.B = B; a.H = H; a.T = Tq; a.Tk = Tk; a.scale = scale;
-  a.stats = (float*)stats; a.ldc = ldc;
-  a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
-  a.dqu = (bf16_t*)dq; a.dk = (bf16_t*)dk_out; a.dv = (bf16_t*)dv_out; a.lddkv = lddkv;
-  return launch_bwd<false>(a, dk, a.mask && a.msq != 0, (hipStream_t)stream);
+  const bool rm = mask && mask_sq != 0;
+  if (rp) launch_bwd_kv<true>(a, dk, rm, (hipStream_t)stream);
+  else launch_bwd_kv<false>(a, dk, rm, (hipStream_t)stream);
+  return lasr_check_launch("attn_bwd_kv");
 }

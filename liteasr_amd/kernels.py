@@ -556,6 +556,7 @@ def relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, d
                 dbd, ldS, dk, dv, dbd_head_major=False):
     assert qv.stride(0) == qu.stride(0) and dqu.stride(0) == qu.stride(0)
     assert v.stride(0) == k.stride(0) and dv.stride(0) == dk.stride(0) and dctx.stride(0) == ctx.stride(0)
+    mask, msb, msq = _fwd_mask(mask, msb, msq, B, T, T)
     N.call("lasr_relattn_bwd", ptr(qu), ptr(qv), qu.stride(0), ptr(k), ptr(v), k.stride(0), ptr(pos),
            pos.stride(0), B, H, T, qu.shape[1] // H, ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx),
            ctx.stride(0), ptr(Dbuf), ptr(dqu), ptr(dbd), ldS, int(dbd_head_major), ptr(dk), ptr(dv), dk.stride(0),
@@ -574,6 +575,7 @@ def attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx):
 def attn_bwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dq, dk, dv):
     assert dq.stride(0) == q.stride(0) and v.stride(0) == k.stride(0) and dv.stride(0) == dk.stride(0)
     assert dctx.stride(0) == ctx.stride(0)
+    mask, msb, msq = _fwd_mask(mask, msb, msq, B, Tq, Tk)
     N.call("lasr_attn_bwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, q.shape[1] // H,
            ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx), ctx.stride(0), ptr(Dbuf), ptr(dq),
            ptr(dk), ptr(dv), dk.stride(0), stream())
