@@ -467,18 +467,20 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
   // the forward's statistics in log2 units (a fully masked row keeps the masked value)
   const float mx = a.stats[2 * (zrow + ic)], il = a.stats[2 * (zrow + ic) + 1];
   const float m2 = mx <= -1e38f ? -1e38f : mx * 1.4426950408889634f;
-  // D_i = sum_c dO[i,c] O[i,c]: the 4 lane groups of a query take DK/4 columns each
+  // D_i = sum_c dO[i,c] O[i,c] on the MFMA that forms dP (the diagonal of O . dO^T over the
+  // wave's 16 queries): the same products summed in the same order as dP, so dP - D cancels
+  // exactly where it should (one key: P = 1, O = V)
   float D;
   {
-    const bf16_t* pd = a.dctx + ((int64_t)b * T + ic) * a.ldc + h * DK + g * (DK / 4);
-    const bf16_t* po = a.ctx_in + ((int64_t)b * T + ic) * a.ldc + h * DK + g * (DK / 4);
-    float vd[DK / 4], vo[DK / 4];
-    ldv<DK / 4>(pd, vd);
-    ldv<DK / 4>(po, vo);
-    float acc = 0.f;
+    bf16x8 oq[KS];
+    load_q<DK>(a.ctx_in, a.ldc, b * T + ic, h, lane, oq);
+    f32x4 dt = zero4();
 #pragma unroll
-    for (int e = 0; e < DK / 4; ++e) acc += vd[e] * vo[e];
-    D = xsum16_32(acc);
+    for (int ks = 0; ks < KS; ++ks) dt = mfma(oq[ks], dof[ks], dt);
+    // lane (g, col) holds rows 4g .. 4g+3 of column col: the diagonal sits in lane group col / 4
+    const int e = col & 3;
+    const float x = e == 0 ? dt[0] : e == 1 ? dt[1] : e == 2 ? dt[2] : dt[3];
+    D = __shfl(x, ((col >> 2) << 4) | col, 64);
     if (g == 0 && iq < T) a.Dbuf[zrow + iq] = D;
   }
   bf16_t* dbd = RP ? a.dbd + (a.dbd_hb ? ((int64_t)h * a.B + b) * T : zrow) * a.ldS : nullptr;
@@ -592,6 +594,273 @@ void launch_flash_bwd_q(const FlashP& a, int dk, bool rp, bool rm, hipStream_t s
   else rm ? launch_bwd_q_t<32, 4, false, true>(a, st) : launch_bwd_q_t<32, 4, false, false>(a, st);
 }
 
+// ---- backward, key side --------------------------------------------------------------------
+// Per (b, h, 16*NW keys): wave w owns 16 keys (its lanes' columns: the lane's K and V rows live in
+// registers) and loops over query blocks of 64 staged by LDS-DMA (Qu, dO, Qv + one row, the
+// position window, the mask tile), with the forward statistics and D of the block in a small
+// double-buffered LDS slot.  Scores in the forward's orientation, S[query][key] = Qu . K^T, so
+// the products with the queries as k are register-fed again: dV^T += dO^T P and dK^T += Qu^T dS,
+// with P / dS of two 16-query tiles as the B operand and dO / Qu read transposed in that order.
+// The positional term: a wave's 16 keys x 16 queries span 31 window rows: two MFMA tiles of
+// G[query][m], parked [m][query] in the wave's scratch and read along the diagonal.
+constexpr int QBK = 64;   // queries per block of the key-side kernel
+constexpr int KLD = 20;   // fp32 row stride of its G scratch ([32 m][16 queries] + pad)
+
+template <int DK, int NW, bool RP, bool RM>
+struct GeoKV {
+  static constexpr int NT = NW * 64, KBW = 16 * NW, CPR = DK / 8;
+  static constexpr int Q_CH = QBK * CPR, O_CH = QBK * CPR;
+  static constexpr int QV_CH = RP ? ((QBK + 1) * CPR + 63) / 64 * 64 : 0;
+  static constexpr int QV_ROWS = QV_CH / CPR;
+  static constexpr int M_CH = RM ? QBK * KBW / 16 : 0;
+  static constexpr int BASE = Q_CH + O_CH + QV_CH + M_CH;
+  static constexpr int W_CH0 = RP ? (QBK + KBW) * CPR : 0;
+  static constexpr int TOT = ((BASE + W_CH0 + NT - 1) / NT) * NT;
+  static constexpr int W_CH = TOT - BASE, W_ROWS = W_CH / CPR;
+  static constexpr int GL = TOT / NT, STAGE_BYTES = TOT * 16;
+  static constexpr int O0 = Q_CH, QV0 = Q_CH + O_CH, M0 = QV0 + QV_CH, W0 = M0 + M_CH;
+  static_assert(Q_CH % 64 == 0 && QV_CH % 64 == 0 && M_CH % 64 == 0 && W_CH % 64 == 0, "wave-aligned regions");
+  static_assert(!RP || W_ROWS >= QBK + KBW - 1, "window rows");
+  static_assert(RP || W_CH == 0, "no window without the positional term");
+  static constexpr int LDS = 2 * STAGE_BYTES + (RP ? NW * 32 * KLD * 4 : 0) + 2 * 3 * QBK * 4;
+};
+
+template <int DK, int NW, bool RP, bool RM>
+LASR_DEV void issue_stage_kv(const FlashP& a, int b, int h, int i0, int j0, char* st, int tid) {
+  using Gm = GeoKV<DK, NW, RP, RM>;
+  const int wid = tid >> 6, T = a.T;
+  const int64_t qb = (int64_t)b * T;
+#pragma unroll
+  for (int i = 0; i < Gm::GL; ++i) {
+    const int P = i * Gm::NT + tid;
+    const void* src;
+    int r, c;
+    if (P < Gm::O0) {
+      chunk_rc<DK>(P, r, c);
+      src = a.qu + (qb + min(i0 + r, T - 1)) * a.ldq + h * DK + c;
+    } else if (P < Gm::QV0) {
+      chunk_rc<DK>(P - Gm::O0, r, c);
+      src = a.dctx + (qb + min(i0 + r, T - 1)) * a.ldc + h * DK + c;
+    } else if (RP && P < Gm::M0) {
+      chunk_rc<DK>(P - Gm::QV0, r, c);
+      src = a.qv + (qb + min(i0 + r, T - 1)) * a.ldq + h * DK + c;
+    } else if (RM && P < Gm::W0) {
+      const int q = P - Gm::M0, rr = q / (Gm::KBW / 16), c16 = (q % (Gm::KBW / 16)) * 16;
+      const int64_t col = min<int64_t>(j0 + c16, a.msq - 16);
+      src = a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + rr, T - 1) * a.msq + col;
+    } else {
+      chunk_rc<DK>(P - Gm::W0, r, c);
+      const int m = j0 - (i0 + QBK - 1) + T - 1 + r;  // window row r <-> m
+      const int src_row = m >= 0 && m <= T - 1 ? m : (m >= T + 1 && m <= 2 * T ? m - T - 1 : -1);
+      src = src_row >= 0 ? (const void*)(a.pos + (int64_t)src_row * a.ldp + h * DK + c) : (const void*)(g_zero_row + c);
+    }
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(st + (size_t)(i * Gm::NT + wid * 64) * 16), 16, 0, 0);
+  }
+}
+
+template <int DK, int NW, bool RP, bool RM>
+__global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16_t* dk_out, bf16_t* dv_out,
+                                                                  int64_t lddkv) {
+  using Gm = GeoKV<DK, NW, RP, RM>;
+  constexpr int KS = DK / 32;
+  __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
+  char* ring = smem;
+  float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);
+  float* sst = gsh + (RP ? NW * 32 * KLD : 0);  // [2][3][QBK]: m (log2 units), 1/sum, D
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, col = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
+  const int j0 = blockIdx.x * Gm::KBW, jw = j0 + 16 * w, jq = jw + col;
+  const int nq = (T + QBK - 1) / QBK;
+  const float c2 = a.scale * 1.4426950408889634f;
+  const int64_t zrow = ((int64_t)b * a.H + h) * T;
+
+  issue_stage_kv<DK, NW, RP, RM>(a, b, h, 0, j0, ring, tid);
+  // the lane's key: K and V rows (B operands), its padding byte
+  bf16x8 kf[KS], vf[KS];
+  load_q<DK>(a.k, a.ldkv, b * Tk + min(jq, Tk - 1), h, lane, kf);
+  load_q<DK>(a.v, a.ldkv, b * Tk + min(jq, Tk - 1), h, lane, vf);
+  bool kmasked = false;
+  if (!RM && a.mask) kmasked = a.mask[(int64_t)b * a.msb + min(jq, Tk - 1)] != 0;
+  // the block's statistics, loaded by wave 0 one block ahead
+  float st_m = 0.f, st_l = 0.f, st_d = 0.f;
+  auto load_stats = [&](int i0) {
+    const int i = i0 + lane, ic = min(i, T - 1);
+    st_m = a.stats[2 * (zrow + ic)];
+    st_l = i < T ? a.stats[2 * (zrow + ic) + 1] : 0.f;  // queries past T: P = 0
+    st_d = a.Dbuf[zrow + ic];
+  };
+  if (w == 0) load_stats(0);
+  float* gk = gsh + w * 32 * KLD;
+  f32x4 dkt[DK / 16], dvt[DK / 16];
+#pragma unroll
+  for (int t = 0; t < DK / 16; ++t) { dkt[t] = zero4(); dvt[t] = zero4(); }
+
+  for (int qb = 0; qb < nq; ++qb) {
+    const int i0 = qb * QBK;
+    char* st = ring + (qb & 1) * Gm::STAGE_BYTES;
+    float* ss = sst + (qb & 1) * 3 * QBK;
+    wait_vmcnt<0>();
+    if (w == 0) {  // this block's statistics into its slot (the other slot may still be read)
+      const float m2 = st_m <= -1e38f ? -1e38f : st_m * 1.4426950408889634f;
+      const uint32_t sa = ldsa(ss + lane);
+      asm volatile("ds_write_b32 %0, %1" ::"v"(sa), "v"(m2) : "memory");
+      asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(sa), "v"(st_l), "i"(4 * QBK) : "memory");
+      asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(sa), "v"(st_d), "i"(8 * QBK) : "memory");
+    }
+    lds_barrier();
+    if (qb + 1 < nq) {
+      issue_stage_kv<DK, NW, RP, RM>(a, b, h, i0 + QBK, j0, ring + ((qb + 1) & 1) * Gm::STAGE_BYTES, tid);
+      if (w == 0) load_stats(i0 + QBK);
+    }
+    const uint32_t qimg = ldsa(st), oimg = ldsa(st + Gm::O0 * 16), vimg = ldsa(st + Gm::QV0 * 16);
+    const uint32_t wimg = ldsa(st + Gm::W0 * 16), mimg = ldsa(st + Gm::M0 * 16);
+#pragma unroll
+    for (int rs = 0; rs < 2; ++rs) {  // query tile pairs (2rs, 2rs + 1)
+      f32x4 p2[2], ds2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = 2 * rs + u;  // queries i0 + 16r ..; lane rows 4g + e
+        // S = Qu . K^T and dP = dO . V^T (query rows as the A operand)
+        v4i aq[KS], ao[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          aq[ks] = lds_b128(frag_row_addr<DK>(qimg, 16 * r, 32 * ks, lane));
+          ao[ks] = lds_b128(frag_row_addr<DK>(oimg, 16 * r, 32 * ks, lane));
+        }
+        v4i smv, slv, sdv;  // m, 1/sum, D of the lane's 4 query rows
+        asm volatile("ds_read_b128 %0, %1" : "=v"(smv) : "v"(ldsa(ss + 16 * r + 4 * g)));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(slv) : "v"(ldsa(ss + 16 * r + 4 * g)), "i"(4 * QBK));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(sdv) : "v"(ldsa(ss + 16 * r + 4 * g)), "i"(8 * QBK));
+        uint32_t mb[4] = {0u, 0u, 0u, 0u};
+        if constexpr (RM) {
+          const uint32_t ma = mimg + (uint32_t)((16 * r + 4 * g) * Gm::KBW + 16 * w + col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(mb[e]) : "v"(ma), "i"(e * Gm::KBW));
+        }
+        lgkm0();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) { keep(aq[ks]); keep(ao[ks]); }
+        keep(smv); keep(slv); keep(sdv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) keep(mb[e]);
+        f32x4 sc = zero4(), dp = zero4();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          sc = mfma(as_frag(aq[ks]), kf[ks], sc);
+          dp = mfma(as_frag(ao[ks]), vf[ks], dp);
+        }
+        float bd[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (RP) {
+          // window rows of this (query tile, key tile): m0 = jw - (i0 + 16r + 15) + T - 1 at image
+          // row 16w - 16r + 48; G1 uses qv rows i, G2 rows i + 1
+          const int wr0 = 16 * w - 16 * r + QBK - 16;
+          const int mlo = jw - (i0 + 16 * r + 15) + T - 1;
+          const uint32_t gka = ldsa(gk);
+#pragma unroll
+          for (int uu = 0; uu < 2; ++uu) {
+            const int lo = mlo + 16 * uu;
+            const bool n1 = lo <= T - 1 && lo + 15 >= 0;
+            const bool n2 = lo + 15 >= T + 1 && lo <= 2 * T;
+            v4i av[KS], av1[KS], bw[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              av[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r, 32 * ks, lane));
+              av1[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r + 1, 32 * ks, lane));
+              bw[ks] = lds_b128(frag_row_addr<DK>(wimg, wr0 + 16 * uu, 32 * ks, lane));
+            }
+            lgkm0();
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bw[ks]); }
+            f32x4 g1 = zero4(), g2 = zero4();
+            if (n1) {
+#pragma unroll
+              for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(av[ks]), as_frag(bw[ks]), g1);
+            }
+            if (n2) {
+#pragma unroll
+              for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(av1[ks]), as_frag(bw[ks]), g2);
+            }
+            // lane (g, col) holds G[query 4g + e][m = lo + col]: select by m <= T - 1, park as [m][query]
+            const bool v1 = lo + col <= T - 1;
+            const f32x4 gs = v1 ? g1 : g2;
+            asm volatile("ds_write_b128 %0, %1" ::"v"(gka + 4u * (uint32_t)((16 * uu + col) * KLD + 4 * g)), "v"(gs)
+                         : "memory");
+          }
+          lgkm0();
+          // bd(query 4g + e, key col) = G[4g + e][m - mlo = col - 4g - e + 15]
+          const uint32_t ba = gka + 4u * (uint32_t)((col - 4 * g + 12) * KLD + 4 * g + 3);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[e]) : "v"(ba), "i"(4 * ((3 - e) * KLD - (3 - e))));
+          lgkm0();
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            keep(v[e]);
+            bd[e] = v[e];
+          }
+        }
+        const f32x4 sm = __builtin_bit_cast(f32x4, smv), sl = __builtin_bit_cast(f32x4, slv),
+                    sd = __builtin_bit_cast(f32x4, sdv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = (sc[e] + bd[e]) * c2;
+          if (RM ? mb[e] != 0u : kmasked) x = -1e38f;
+          const float p = __builtin_amdgcn_exp2f(x - sm[e]) * sl[e];
+          p2[u][e] = p;
+          ds2[u][e] = x > -1e38f ? p * (dp[e] - sd[e]) : 0.f;
+        }
+      }
+      // dV^T += dO^T P, dK^T += Qu^T dS (queries of the pair as k: 32rs + 4g + e, then + 16)
+      const bf16x8 pb = pack8(p2[0], p2[1]), sb = pack8(ds2[0], ds2[1]);
+      v2i olo[DK / 16], ohi[DK / 16], qlo[DK / 16], qhi[DK / 16];
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        olo[t] = lds_tr(frag_tr_addr<DK>(oimg, 32 * rs + 4 * g, 16 * t, lane));
+        ohi[t] = lds_tr(frag_tr_addr<DK>(oimg, 32 * rs + 16 + 4 * g, 16 * t, lane));
+        qlo[t] = lds_tr(frag_tr_addr<DK>(qimg, 32 * rs + 4 * g, 16 * t, lane));
+        qhi[t] = lds_tr(frag_tr_addr<DK>(qimg, 32 * rs + 16 + 4 * g, 16 * t, lane));
+      }
+      lgkm0();
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) { keep(olo[t]); keep(ohi[t]); keep(qlo[t]); keep(qhi[t]); }
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        dvt[t] = mfma(as_frag(olo[t], ohi[t]), pb, dvt[t]);
+        dkt[t] = mfma(as_frag(qlo[t], qhi[t]), sb, dkt[t]);
+      }
+    }
+  }
+  if (jq < Tk) {
+    bf16_t* pk = dk_out + ((int64_t)b * Tk + jq) * lddkv + h * DK + 4 * g;
+    bf16_t* pv = dv_out + ((int64_t)b * Tk + jq) * lddkv + h * DK + 4 * g;
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) {
+      *(uint2*)(pk + 16 * t) = make_uint2(pk_bf16(dkt[t][0] * a.scale, dkt[t][1] * a.scale),
+                                          pk_bf16(dkt[t][2] * a.scale, dkt[t][3] * a.scale));
+      *(uint2*)(pv + 16 * t) = make_uint2(pk_bf16(dvt[t][0], dvt[t][1]), pk_bf16(dvt[t][2], dvt[t][3]));
+    }
+  }
+}
+
+template <int DK, int NW, bool RP, bool RM>
+void launch_bwd_kv_t(const FlashP& a, bf16_t* dk, bf16_t* dv, int64_t lddkv, hipStream_t st) {
+  const dim3 grid((unsigned)cdiv(a.Tk, 16 * NW), (unsigned)a.H, (unsigned)a.B);
+  flash_bwd_kv_kernel<DK, NW, RP, RM><<<grid, NW * 64, 0, st>>>(a, dk, dv, lddkv);
+}
+
+void launch_flash_bwd_kv(const FlashP& a, int dk, bool rp, bool rm, bf16_t* dko, bf16_t* dvo, int64_t ld,
+                         hipStream_t st) {
+  if (rp) {
+    if (dk == 64) rm ? launch_bwd_kv_t<64, 8, true, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<64, 8, true, false>(a, dko, dvo, ld, st);
+    else rm ? launch_bwd_kv_t<32, 8, true, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<32, 8, true, false>(a, dko, dvo, ld, st);
+    return;
+  }
+  if (dk == 64) rm ? launch_bwd_kv_t<64, 4, false, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<64, 4, false, false>(a, dko, dvo, ld, st);
+  else rm ? launch_bwd_kv_t<32, 4, false, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<32, 4, false, false>(a, dko, dvo, ld, st);
+}
+
 template <int DK, int NW, bool RP, bool RM>
 void launch_fwd_t(const FlashP& a, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(a.T, 16 * NW), (unsigned)a.H, (unsigned)a.B);
@@ -623,12 +892,6 @@ int check_mask(const uint8_t* mask, int64_t msb, int64_t msq, int Tk, const char
 }
 
 }  // namespace
-
-int lasr_attn_bwd_kv_launch(const void* qu, const void* qv, int64_t ldq, const void* k, const void* v, int64_t ldkv,
-                            const void* pos, int64_t ldp, int B, int H, int T, int Tk, int dk, const uint8_t* mask,
-                            int64_t mask_sb, int64_t mask_sq, float scale, const float* stats, const void* dctx,
-                            int64_t ldc, const float* Dbuf, void* dk_out, void* dv_out, int64_t lddkv, bool rp,
-                            void* stream);
 
 extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, const void* k,
                                 const void* v, int64_t ldkv, const void* pos, int64_t ldp, int B,
@@ -701,10 +964,12 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   a.stats = (float*)stats; a.ldc = ldc;
   a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
   a.dqu = (bf16_t*)dqu; a.dbd = (bf16_t*)dbd; a.ldS = ldS; a.dbd_hb = dbd_head_major;
-  launch_flash_bwd_q(a, dk, true, mask && mask_sq != 0, (hipStream_t)stream);
+  LASR_CHECK_ARG(lddkv % 8 == 0 && al16(dk_out) && al16(dv_out), "lasr_relattn_bwd: dk/dv rows 16-B aligned");
+  const bool rm = mask && mask_sq != 0;
+  launch_flash_bwd_q(a, dk, true, rm, (hipStream_t)stream);
   if (int rc = lasr_check_launch("relattn_bwd_q")) return rc;
-  return lasr_attn_bwd_kv_launch(qu, qv, ldq, k, v, ldkv, pos, ldp, B, H, T, T, dk, mask, mask_sb, mask_sq, scale,
-                                 stats, dctx, ldc, Dbuf, dk_out, dv_out, lddkv, true, stream);
+  launch_flash_bwd_kv(a, dk, true, rm, (bf16_t*)dk_out, (bf16_t*)dv_out, lddkv, (hipStream_t)stream);
+  return lasr_check_launch("relattn_bwd_kv");
 }
 
 extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
@@ -727,8 +992,10 @@ extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const vo
   a.stats = (float*)stats; a.ldc = ldc;
   a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
   a.dqu = (bf16_t*)dq;
-  launch_flash_bwd_q(a, dk, false, mask && mask_sq != 0, (hipStream_t)stream);
+  LASR_CHECK_ARG(al16(dk_out) && al16(dv_out), "lasr_attn_bwd: dk/dv 16-B alignment");
+  const bool rm = mask && mask_sq != 0;
+  launch_flash_bwd_q(a, dk, false, rm, (hipStream_t)stream);
   if (int rc = lasr_check_launch("attn_bwd_q")) return rc;
-  return lasr_attn_bwd_kv_launch(q, q, ldq, k, v, ldkv, nullptr, 0, B, H, Tq, Tk, dk, mask, mask_sb, mask_sq, scale,
-                                 stats, dctx, ldc, Dbuf, dk_out, dv_out, lddkv, false, stream);
+  launch_flash_bwd_kv(a, dk, false, rm, (bf16_t*)dk_out, (bf16_t*)dv_out, lddkv, (hipStream_t)stream);
+  return lasr_check_launch("attn_bwd_kv");
 }
