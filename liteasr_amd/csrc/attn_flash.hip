@@ -92,6 +92,12 @@ LASR_DEV v2i lds_tr(uint32_t addr) {
   return r;
 }
 LASR_DEV void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// wait until at most N of the wave's LDS operations are outstanding (they retire in order)
+template <int N>
+LASR_DEV void lgkm() {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt is 4 bits");
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
 // After lgkm0(): route every asm-read register through an empty asm so its consumers depend on
 // a statement ordered after the wait (volatile asm statements keep their relative order).
 template <typename T>
@@ -156,43 +162,60 @@ struct Geo {
   static_assert(RP || W_CH == 0, "no window without the positional term");
 };
 
+// LDS-DMA of one region of a stage: CH pieces (a multiple of 64), piece p of the region from
+// src(p); thread tid issues pieces tid, tid + NT, ... (wave-uniform: a wave instruction covers
+// 64 consecutive pieces).  The ring waits use vmcnt(0), so waves may issue different counts.
+template <int CH, int NT, typename Src>
+LASR_DEV void dma_region(char* st, int base, int tid, Src src) {
+  const int wid = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < (CH + NT - 1) / NT; ++k) {
+    const int p = k * NT + tid;
+    if (CH % NT == 0 || k * NT + wid * 64 < CH)
+      __builtin_amdgcn_global_load_lds((gptr_t)src(p), (lptr_t)(st + (size_t)(base + k * NT + wid * 64) * 16), 16, 0, 0);
+  }
+}
+
+// relative-position window row r of a block pair whose row 0 is m = mlo (zero rows outside the table)
+LASR_DEV const void* wrow(const FlashP& a, int h, int DK, int m, int c) {
+  const int T = a.T;
+  const int src_row = m >= 0 && m <= T - 1 ? m : (m >= T + 1 && m <= 2 * T ? m - T - 1 : -1);
+  return src_row >= 0 ? (const void*)(a.pos + (int64_t)src_row * a.ldp + h * DK + c) : (const void*)(g_zero_row + c);
+}
+
 // One block pair's LDS-DMA sweep into stage `st` (shared by the forward and the query-side
 // backward).
 template <int DK, int NW, bool RP, bool RM>
 LASR_DEV void issue_stage(const FlashP& a, int b, int h, int i0, int j0, char* st, int tid) {
   using Gm = Geo<DK, NW, RP, RM>;
-  const int wid = tid >> 6;
   const int T = a.T, Tk = a.Tk;
   const int64_t kb = (int64_t)b * Tk;
   const bf16_t* kh = a.k + kb * a.ldkv + h * DK;
   const bf16_t* vh = a.v + kb * a.ldkv + h * DK;
-#pragma unroll
-  for (int i = 0; i < Gm::GL; ++i) {
-    const int P = i * Gm::NT + tid;
-    const void* src;
-    if (P < Gm::V0) {
+  dma_region<Gm::K_CH, Gm::NT>(st, Gm::K0, tid, [&](int p) {
+    int r, c;
+    chunk_rc<DK>(p, r, c);
+    return (const void*)(kh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c);
+  });
+  dma_region<Gm::V_CH, Gm::NT>(st, Gm::V0, tid, [&](int p) {
+    int r, c;
+    chunk_rc<DK>(p, r, c);
+    return (const void*)(vh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c);
+  });
+  if constexpr (RP)
+    dma_region<Gm::W_CH, Gm::NT>(st, Gm::W0, tid, [&](int p) {
       int r, c;
-      chunk_rc<DK>(P, r, c);
-      src = kh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c;
-    } else if (P < Gm::W0) {
-      int r, c;
-      chunk_rc<DK>(P - Gm::V0, r, c);
-      src = vh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c;
-    } else if (RP && P < Gm::M0) {
-      int r, c;
-      chunk_rc<DK>(P - Gm::W0, r, c);
-      const int m = j0 - i0 + T - Gm::QB + r;  // window row r <-> m
-      const int src_row = m >= 0 && m <= T - 1 ? m : (m >= T + 1 && m <= 2 * T ? m - T - 1 : -1);
-      src = src_row >= 0 ? (const void*)(a.pos + (int64_t)src_row * a.ldp + h * DK + c) : (const void*)(g_zero_row + c);
-    } else {
-      // mask tile [query r][64 keys] bytes (RM): rows 16-B aligned (host-checked); a piece
-      // starting past the row stride holds only keys >= Tk (masked anyway): clamped
-      const int q = P - Gm::M0, r = q >> 2, c16 = (q & 3) * 16;
-      const int64_t col = min<int64_t>(j0 + c16, a.msq - 16);
-      src = a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + r, T - 1) * a.msq + col;
-    }
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(st + (size_t)(i * Gm::NT + wid * 64) * 16), 16, 0, 0);
-  }
+      chunk_rc<DK>(p, r, c);
+      return wrow(a, h, DK, j0 - i0 + T - Gm::QB + r, c);
+    });
+  if constexpr (RM)
+    // mask tile [query r][64 keys] bytes: rows 16-B aligned (host-checked); a piece starting
+    // past the row stride holds only keys >= Tk (masked anyway): clamped
+    dma_region<Gm::M_CH, Gm::NT>(st, Gm::M0, tid, [&](int p) {
+      const int r = p >> 2;
+      const int64_t col = min<int64_t>(j0 + (p & 3) * 16, a.msq - 16);
+      return (const void*)(a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + r, T - 1) * a.msq + col);
+    });
 }
 
 // Query-side fragments of the lane's query (B operands: n = lane%16, k = 8*(lane/16) ..).
@@ -204,60 +227,73 @@ LASR_DEV void load_q(const bf16_t* base, int64_t ld, int row, int h, int lane, b
 }
 
 // Scaled + masked transposed scores of the lane's query against the 64 keys of block j0,
-// in log2 units (c2 = scale * log2 e): s[c][e] for key j0 + 16c + 4*(lane/16) + e.
+// in log2 units (c2 = scale * log2 e): s[c][e] for key j0 + 16c + 4*(lane/16) + e.  Every LDS
+// read of the block (K and window fragments, mask words) is issued up front; counted waits
+// release the S products while the window reads are still landing.
 template <int DK, int NW, bool RP, bool RM>
 LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t* km, const bf16x8 (&qu)[DK / 32],
                        const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int w, int i0, int j0, float c2,
                        int lane, f32x4 (&s)[4]) {
   using Gm = Geo<DK, NW, RP, RM>;
-  constexpr int KS = DK / 32;
+  constexpr int KS = DK / 32, NWT = RP ? 5 : 0;
   const int g = lane >> 4, col = lane & 15;
   const uint32_t kimg = ldsa(st), wimg = ldsa(st + Gm::W0 * 16);
-  // S^T = K . Qu^T
+  const int wb = 16 * (NW - 1 - w);  // the wave's first window row
+  v4i rk[4][KS], rw[RP ? 5 : 1][KS];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) rk[c][ks] = lds_b128(frag_row_addr<DK>(kimg, 16 * c, 32 * ks, lane));
+  if constexpr (RP)
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) rw[t][ks] = lds_b128(frag_row_addr<DK>(wimg, wb + 16 * t, 32 * ks, lane));
+  // mask words: the query-dependent tile, or the key-padding bytes (read unconditionally;
+  // ignored without a mask)
+  uint32_t mw[4];
   {
-    v4i r[4][KS];
+    const uint32_t mimg = RM ? ldsa(st + Gm::M0 * 16) + (uint32_t)((16 * w + col) * KB + 4 * g)
+                             : ldsa(km) + (uint32_t)(j0 + 4 * g);
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < 4; ++c) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(mw[c]) : "v"(mimg), "i"(16 * c));
+  }
+  lgkm<NWT * KS + 4>();  // the K fragments
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) r[c][ks] = lds_b128(frag_row_addr<DK>(kimg, 16 * c, 32 * ks, lane));
-    lgkm0();
+  for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int ks = 0; ks < KS; ++ks) keep(rk[c][ks]);
+  // S^T = K . Qu^T
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) keep(r[c][ks]);
+  for (int c = 0; c < 4; ++c) {
+    f32x4 acc = zero4();
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      f32x4 acc = zero4();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(r[c][ks]), qu[ks], acc);
-      s[c] = acc;
-    }
+    for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(rk[c][ks]), qu[ks], acc);
+    s[c] = acc;
   }
   float bd[4][4];
   if constexpr (RP) {
     const int T = a.T;
-    const int wb = 16 * (NW - 1 - w);                   // the wave's first window row
-    const int mlo = j0 - i0 + T - Gm::QB + wb;          // m of that row
+    const int mlo = j0 - i0 + T - Gm::QB + wb;  // m of the wave's first window row
     const uint32_t gq = ldsa(gw);
+    lgkm<4>();  // the window fragments
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) keep(rw[t][ks]);
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
       const int lo = mlo + 16 * t;
       const bool n1 = lo <= T - 1 && lo + 15 >= 0;      // rows with m in [0, T-1]
       const bool n2 = lo + 15 >= T + 1 && lo <= 2 * T;  // rows with m in [T+1, 2T]
-      v4i r[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) r[ks] = lds_b128(frag_row_addr<DK>(wimg, wb + 16 * t, 32 * ks, lane));
-      lgkm0();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) keep(r[ks]);
       f32x4 g1 = zero4(), g2 = zero4();
       if (n1) {
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(r[ks]), qv[ks], g1);
+        for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(rw[t][ks]), qv[ks], g1);
       }
       if (n2) {
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(r[ks]), qv1[ks], g2);
+        for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(rw[t][ks]), qv1[ks], g2);
       }
       f32x4 gsel;
 #pragma unroll
@@ -265,18 +301,15 @@ LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t
       // G'[query col][m - mlo = 16t + 4g + e]
       asm volatile("ds_write_b128 %0, %1" ::"v"(gq + 4u * (uint32_t)(col * GLD + 16 * t + 4 * g)), "v"(gsel) : "memory");
     }
-    lgkm0();
-    // diagonal: bd(query col, key 16c + 4g + e) = G'[col][16c + 4g + e - col + 15]
+    // diagonal: bd(query col, key 16c + 4g + e) = G'[col][16c + 4g + e - col + 15] (the wave's
+    // own writes above retire first: LDS operations of a wave complete in order)
     const uint32_t base = gq + 4u * (uint32_t)(col * (GLD - 1) + 4 * g + 15);
     float v[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x;
-        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(x) : "v"(base), "i"(4 * (16 * c + e)));
-        v[4 * c + e] = x;
-      }
+      for (int e = 0; e < 4; ++e)
+        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[4 * c + e]) : "v"(base), "i"(4 * (16 * c + e)));
     lgkm0();
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -286,22 +319,14 @@ LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t
         bd[c][e] = v[4 * c + e];
       }
   } else {
+    lgkm0();
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int e = 0; e < 4; ++e) bd[c][e] = 0.f;
   }
-  // masks: key padding bytes (staged per utterance) or the query-dependent tile
-  uint32_t mw[4] = {0u, 0u, 0u, 0u};
-  if (RM || km) {
-    const uint32_t mimg = RM ? ldsa(st + Gm::M0 * 16) + (uint32_t)((16 * w + col) * KB + 4 * g)
-                             : ldsa(km) + (uint32_t)(j0 + 4 * g);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(mw[c]) : "v"(mimg), "i"(16 * c));
-    lgkm0();
-#pragma unroll
-    for (int c = 0; c < 4; ++c) keep(mw[c]);
-  }
+  for (int c = 0; c < 4; ++c) keep(mw[c]);
   const bool tail = j0 + KB > a.Tk;
 #pragma unroll
   for (int c = 0; c < 4; ++c)
@@ -336,14 +361,11 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
   const float c2 = a.scale * 1.4426950408889634f;
 
   issue_stage<DK, NW, RP, RM>(a, b, h, i0, 0, ring, tid);
-  const uint8_t* km = nullptr;
-  if constexpr (!RM) {
-    if (a.mask) {  // key padding: this utterance's row, bytes past Tk read as unmasked (keys >= Tk are -inf anyway)
-      const uint8_t* mr = a.mask + (int64_t)b * a.msb;
-      const int kpad = nb * KB;
-      for (int j = tid; j < kpad; j += NT) kmask[j] = j < Tk ? mr[j] : 0;
-      km = kmask;
-    }
+  const uint8_t* km = kmask;
+  if constexpr (!RM) {  // key padding bytes of this utterance (zeros without a mask; keys >= Tk are -inf anyway)
+    const uint8_t* mr = a.mask ? a.mask + (int64_t)b * a.msb : nullptr;
+    const int kpad = nb * KB;
+    for (int j = tid; j < kpad; j += NT) kmask[j] = mr && j < Tk ? mr[j] : 0;
   }
   bf16x8 qu[KS], qv[KS], qv1[KS];
   load_q<DK>(a.qu, a.ldq, b * T + min(iq, T - 1), h, lane, qu);
@@ -365,6 +387,17 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
     if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
     f32x4 s[4];
     scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
+    // V^T fragments for O^T += V^T P^T, in flight during the softmax (k slots of sub-block ks:
+    // keys 32ks + 4g + e, then 32ks + 16 + 4g + e)
+    const uint32_t vimg = ldsa(st + Gm::V0 * 16);
+    v2i lo[2][DK / 16], hi[2][DK / 16];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        lo[ks][t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 4 * g, 16 * t, lane));
+        hi[ks][t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
+      }
     // online softmax (one query per lane; the 4 lane groups of a query share its max)
     float bm = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
                      fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
@@ -386,25 +419,19 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
     mrun = mn;
 #pragma unroll
     for (int t = 0; t < DK / 16; ++t) o[t] *= al;
-    // O^T += V^T P^T (k slots of sub-block ks: keys 32ks + 4g + e, then 32ks + 16 + 4g + e)
-    const uint32_t vimg = ldsa(st + Gm::V0 * 16);
+    lgkm0();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        keep(lo[ks][t]);
+        keep(hi[ks][t]);
+      }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 pb = pack8(s[2 * ks], s[2 * ks + 1]);
-      v2i lo[DK / 16], hi[DK / 16];
 #pragma unroll
-      for (int t = 0; t < DK / 16; ++t) {
-        lo[t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 4 * g, 16 * t, lane));
-        hi[t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
-      }
-      lgkm0();
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) {
-        keep(lo[t]);
-        keep(hi[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) o[t] = mfma(as_frag(lo[t], hi[t]), pb, o[t]);
+      for (int t = 0; t < DK / 16; ++t) o[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), pb, o[t]);
     }
   }
   // statistics in scaled-score units (max * ln 2), 1/sum: P = exp(S - max) / sum
@@ -448,14 +475,11 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
   const int64_t zrow = ((int64_t)b * a.H + h) * T;
 
   issue_stage<DK, NW, RP, RM>(a, b, h, i0, 0, ring, tid);
-  const uint8_t* km = nullptr;
-  if constexpr (!RM) {
-    if (a.mask) {
-      const uint8_t* mr = a.mask + (int64_t)b * a.msb;
-      const int kpad = nb * KB;
-      for (int j = tid; j < kpad; j += NT) kmask[j] = j < Tk ? mr[j] : 0;
-      km = kmask;
-    }
+  const uint8_t* km = kmask;
+  if constexpr (!RM) {  // key padding bytes of this utterance (zeros without a mask; keys >= Tk are -inf anyway)
+    const uint8_t* mr = a.mask ? a.mask + (int64_t)b * a.msb : nullptr;
+    const int kpad = nb * KB;
+    for (int j = tid; j < kpad; j += NT) kmask[j] = mr && j < Tk ? mr[j] : 0;
   }
   bf16x8 qu[KS], qv[KS], qv1[KS], dof[KS];
   load_q<DK>(a.qu, a.ldq, b * T + ic, h, lane, qu);
@@ -497,27 +521,34 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
     if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
     f32x4 s[4];
     scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
-    // dP^T = V . dO^T (V rows = keys as the A operand)
-    const uint32_t vimg = ldsa(st + Gm::V0 * 16);
-    f32x4 dp[4];
-    {
-      v4i r[4][KS];
+    // V fragments for dP^T = V . dO^T (V rows = keys as the A operand), then the K^T
+    // fragments for dQu^T += K^T dS^T, in flight during dP and dS
+    const uint32_t vimg = ldsa(st + Gm::V0 * 16), kimg = ldsa(st);
+    v4i rv[4][KS];
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) r[c][ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * c, 32 * ks, lane));
-      lgkm0();
+      for (int ks = 0; ks < KS; ++ks) rv[c][ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * c, 32 * ks, lane));
+    v2i lo[2][DK / 16], hi[2][DK / 16];
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) keep(r[c][ks]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        f32x4 acc = zero4();
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(r[c][ks]), dof[ks], acc);
-        dp[c] = acc;
+      for (int t = 0; t < DK / 16; ++t) {
+        lo[ks][t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 4 * g, 16 * t, lane));
+        hi[ks][t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
       }
+    lgkm<(4 * DK / 16 > 15 ? 15 : 4 * DK / 16)>();  // the V fragments (older than the K^T reads)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) keep(rv[c][ks]);
+    f32x4 dp[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(rv[c][ks]), dof[ks], acc);
+      dp[c] = acc;
     }
     // dS = P (dP - D), zero where masked or past Tk (the forward's masked_fill backward)
 #pragma unroll
@@ -528,25 +559,19 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
         const float p = __builtin_amdgcn_exp2f(v - m2) * il;
         s[c][e] = v > -1e38f ? p * (dp[c][e] - D) : 0.f;
       }
-    // dQu^T += K^T dS^T (bf16 dS, the key order of the forward's P^T)
-    const uint32_t kimg = ldsa(st);
+    lgkm0();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) {
+        keep(lo[ks][t]);
+        keep(hi[ks][t]);
+      }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 db = pack8(s[2 * ks], s[2 * ks + 1]);
-      v2i lo[DK / 16], hi[DK / 16];
 #pragma unroll
-      for (int t = 0; t < DK / 16; ++t) {
-        lo[t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 4 * g, 16 * t, lane));
-        hi[t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
-      }
-      lgkm0();
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) {
-        keep(lo[t]);
-        keep(hi[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(as_frag(lo[t], hi[t]), db, dq[t]);
+      for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), db, dq[t]);
     }
     if constexpr (RP) {
       // inverse rel_shift: the bd entry each score read (none for j == i + 1)

@@ -18,6 +18,13 @@ for s in "$@"; do
            "tests/test_kernels_gpu.py::test_gemm_ksub2_bit_identical" -s > "$OUT/new.log" 2>&1 ;;
     attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
     attnbench) run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_bench.jsonl" 2> "$OUT/attn_bench.err" ;;
+    attnprof) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/attn_trace" -o run -- python3 "$R/tools/attn_bench.py" > "$OUT/attn_trace.log" 2>&1
+           cp "$(find "$OUT/attn_trace" -name '*kernel_stats.csv' | head -1)" "$OUT/attn_kernel_stats.csv"; rm -rf "$OUT/attn_trace"
+           S1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_INSTS_VALU"
+           S2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_SCA"
+           i=0; for set in "$S1" "$S2"; do i=$((i+1))
+             run timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/ap$i" -o run -- python3 "$R/tools/attn_bench.py" > "$OUT/ap$i.log" 2>&1
+             run python3 "$R/tools/pmc_kernels.py" "$(find "$OUT/ap$i" -name '*.db' | head -1)" flash_ > "$OUT/attn_pmc_$i.json"; rm -rf "$OUT/ap$i"; done ;;
     kgpu) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py tests/test_row_ln_gpu.py > "$OUT/kgpu.log" 2>&1 ;;
     model) run timeout -k 10 900 $PYT tests/test_model_gpu.py tests/test_nodes_gpu.py -s > "$OUT/model.log" 2>&1 ;;
     smoke) run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
