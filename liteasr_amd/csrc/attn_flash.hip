@@ -739,13 +739,14 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
     }
     const uint32_t qimg = ldsa(st), oimg = ldsa(st + Gm::O0 * 16), vimg = ldsa(st + Gm::QV0 * 16);
     const uint32_t wimg = ldsa(st + Gm::W0 * 16), mimg = ldsa(st + Gm::M0 * 16);
-#pragma unroll
+#pragma unroll 1
     for (int rs = 0; rs < 2; ++rs) {  // query tile pairs (2rs, 2rs + 1)
       f32x4 p2[2], ds2[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = 2 * rs + u;  // queries i0 + 16r ..; lane rows 4g + e
-        // S = Qu . K^T and dP = dO . V^T (query rows as the A operand)
+        // every LDS read of the tile up front: S = Qu . K^T and dP = dO . V^T (query rows as the A
+        // operand), the rows' statistics and mask bytes, then the window products' fragments
         v4i aq[KS], ao[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -763,7 +764,22 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
           for (int e = 0; e < 4; ++e)
             asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(mb[e]) : "v"(ma), "i"(e * Gm::KBW));
         }
-        lgkm0();
+        // window rows of this (query tile, key tile): m0 = jw - (i0 + 16r + 15) + T - 1 at image
+        // row 16w - 16r + 48; G1 uses qv rows i, G2 rows i + 1
+        const int wr0 = 16 * w - 16 * r + QBK - 16;
+        v4i av[RP ? KS : 1], av1[RP ? KS : 1], bw[RP ? 2 : 1][RP ? KS : 1];
+        if constexpr (RP) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            av[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r, 32 * ks, lane));
+            av1[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r + 1, 32 * ks, lane));
+            bw[0][ks] = lds_b128(frag_row_addr<DK>(wimg, wr0, 32 * ks, lane));
+            bw[1][ks] = lds_b128(frag_row_addr<DK>(wimg, wr0 + 16, 32 * ks, lane));
+          }
+          lgkm<4 * KS>();  // all but the window fragments
+        } else {
+          lgkm0();
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) { keep(aq[ks]); keep(ao[ks]); }
         keep(smv); keep(slv); keep(sdv);
@@ -777,34 +793,24 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
         }
         float bd[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr (RP) {
-          // window rows of this (query tile, key tile): m0 = jw - (i0 + 16r + 15) + T - 1 at image
-          // row 16w - 16r + 48; G1 uses qv rows i, G2 rows i + 1
-          const int wr0 = 16 * w - 16 * r + QBK - 16;
           const int mlo = jw - (i0 + 16 * r + 15) + T - 1;
           const uint32_t gka = ldsa(gk);
+          lgkm0();
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bw[0][ks]); keep(bw[1][ks]); }
 #pragma unroll
           for (int uu = 0; uu < 2; ++uu) {
             const int lo = mlo + 16 * uu;
             const bool n1 = lo <= T - 1 && lo + 15 >= 0;
             const bool n2 = lo + 15 >= T + 1 && lo <= 2 * T;
-            v4i av[KS], av1[KS], bw[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-              av[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r, 32 * ks, lane));
-              av1[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r + 1, 32 * ks, lane));
-              bw[ks] = lds_b128(frag_row_addr<DK>(wimg, wr0 + 16 * uu, 32 * ks, lane));
-            }
-            lgkm0();
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bw[ks]); }
             f32x4 g1 = zero4(), g2 = zero4();
             if (n1) {
 #pragma unroll
-              for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(av[ks]), as_frag(bw[ks]), g1);
+              for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(av[ks]), as_frag(bw[uu][ks]), g1);
             }
             if (n2) {
 #pragma unroll
-              for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(av1[ks]), as_frag(bw[ks]), g2);
+              for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(av1[ks]), as_frag(bw[uu][ks]), g2);
             }
             // lane (g, col) holds G[query 4g + e][m = lo + col]: select by m <= T - 1, park as [m][query]
             const bool v1 = lo + col <= T - 1;
@@ -812,8 +818,8 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
             asm volatile("ds_write_b128 %0, %1" ::"v"(gka + 4u * (uint32_t)((16 * uu + col) * KLD + 4 * g)), "v"(gs)
                          : "memory");
           }
-          lgkm0();
-          // bd(query 4g + e, key col) = G[4g + e][m - mlo = col - 4g - e + 15]
+          // bd(query 4g + e, key col) = G[4g + e][m - mlo = col - 4g - e + 15] (the wave's writes
+          // above retire first)
           const uint32_t ba = gka + 4u * (uint32_t)((col - 4 * g + 12) * KLD + 4 * g + 3);
           float v[4];
 #pragma unroll
