@@ -574,18 +574,37 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
       for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), db, dq[t]);
     }
     if constexpr (RP) {
-      // inverse rel_shift: the bd entry each score read (none for j == i + 1)
+      // inverse rel_shift: the bd entry each score read (none for j == i + 1).  A lane's 4 keys
+      // of a tile land on 4 consecutive columns of one dBD row unless they straddle the
+      // diagonal or T: 2 or 3 stores (by column parity; ldS is even) instead of 4.
       if (iq < T) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < 4; ++c) {
+          const int ja = j0 + 16 * c + 4 * g;  // first of the 4 keys
+          const uint32_t w01 = pk_bf16(s[c][0], s[c][1]), w23 = pk_bf16(s[c][2], s[c][3]);
+          const bool lowr = ja + 3 <= iq, highr = ja >= iq + 2;
+          if ((lowr || highr) && ja + 3 < T) {
+            const int64_t off = lowr ? (int64_t)iq * a.ldS + (T - 1 - iq + ja) : (int64_t)(iq + 1) * a.ldS + (ja - iq - 2);
+            bf16_t* d = dbd + off;
+            if ((off & 1) == 0) {
+              *(uint32_t*)d = w01;
+              *(uint32_t*)(d + 2) = w23;
+            } else {
+              *(uint16_t*)d = (uint16_t)w01;
+              *(uint32_t*)(d + 1) = (w01 >> 16) | (w23 << 16);
+              *(uint16_t*)(d + 3) = (uint16_t)(w23 >> 16);
+            }
+          } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int j = j0 + 16 * c + 4 * g + e;
-            if (j < T && j != iq + 1) {
-              const int64_t off = j <= iq ? (int64_t)iq * a.ldS + (T - 1 - iq + j) : (int64_t)(iq + 1) * a.ldS + (j - iq - 2);
-              dbd[off] = f2bf(s[c][e]);
+            for (int e = 0; e < 4; ++e) {
+              const int j = ja + e;
+              if (j < T && j != iq + 1) {
+                const int64_t off = j <= iq ? (int64_t)iq * a.ldS + (T - 1 - iq + j) : (int64_t)(iq + 1) * a.ldS + (j - iq - 2);
+                dbd[off] = f2bf(s[c][e]);
+              }
             }
           }
+        }
       }
     }
   }
@@ -981,7 +1000,8 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_bwd: bad B/H/T");
   LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
                  "lasr_relattn_bwd: row strides must be multiples of 8");
-  LASR_CHECK_ARG(ldS >= T, "lasr_relattn_bwd: ldS < T");
+  LASR_CHECK_ARG(ldS >= T && ldS % 2 == 0 && ((uintptr_t)dbd & 3) == 0,
+                 "lasr_relattn_bwd: dBD rows need ldS >= T, ldS even and a 4-B aligned base");
   LASR_CHECK_ARG(al16(qu) && al16(qv) && al16(k) && al16(v) && al16(pos) && al16(dctx) && al16(ctx) && al16(dqu),
                  "lasr_relattn_bwd: 16-B alignment");
   if (B == 0 || T == 0) return LASR_OK;
