@@ -287,6 +287,95 @@ def hottest_case(cfgd, dev):
     return launch, flops, bytes_, meta
 
 
+def attention_case(cfgd, dev):
+    """The encoder's fused relative-position attention of one layer at the config's shape
+    (liteasr/nets/attention.py:120-154): lasr_relattn_fwd + lasr_relattn_bwd (query-side and
+    key-side flash kernels, csrc/attn_flash.hip) exactly as ConformerLayerFn issues them (bf16,
+    key padding from the synthetic lengths, the chunk mask of the config).  Algorithmic flops
+    per layer = 9 x 2*B*H*T'^2*d_k: forward 3 (QK^T, the positional product Qv P^T over the
+    needed diagonal band, PV), backward 6 (S recomputed once: 2; dP, dQu, dK, dV: 4); the
+    kernels execute 12 (the backward's two kernels each recompute S) -- the MFMA fraction is
+    quoted on the algorithmic count.  Bytes: Qu, Qv, K, V, the position table, ctx and dctx
+    read, ctx, dQu, dK, dV and the dBD G-space gradient written once (bound: mfma)."""
+    import torch
+
+    from liteasr_amd import kernels as K
+    from liteasr_amd.utils.synthetic import synthetic_batch
+
+    B, H, d = cfgd["B"], cfgd["H"], cfgd["d"]
+    dk = d // H
+    T = _rows(cfgd) // B
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(5)
+    rn = lambda *sh: (torch.randn(*sh, device=dev, generator=g) * 0.5).to(bf)  # noqa: E731
+    qkv, qu, qv, pos, dctx = rn(B * T, 3 * d), rn(B * T, d), rn(B * T, d), rn(T, d), rn(B * T, d)
+    _, xlens, _, _ = synthetic_batch(B, cfgd["T"], cfgd["L"], V, seed=99)
+    tl = (((xlens - 1) // 2 - 1) // 2).to(dev)
+    pad = torch.arange(T, device=dev)[None, :] >= tl[:, None]
+    if cfgd["chunk"]:
+        ch = cfgd["chunk"]
+        tri = (torch.arange(T, device=dev)[None, :] // ch) > (torch.arange(T, device=dev)[:, None] // ch)
+        mask, msb, msq = K.pad_mask16((pad[:, None, :] | tri[None]).to(torch.uint8), B, T, T)
+    else:
+        mask, msb, msq = pad.to(torch.uint8).contiguous(), T, 0
+    scale = dk ** -0.5
+    stats = torch.empty(B * H * T * 2, device=dev)
+    ctx = torch.empty(B * T, d, dtype=bf, device=dev)
+    ldS = (T + 7) // 8 * 8
+    Dbuf = torch.empty(B * H * T, device=dev)
+    dqu = torch.empty(B * T, d, dtype=bf, device=dev)
+    dbd = torch.empty(H, B, T, ldS, dtype=bf, device=dev)
+    dqkv = torch.zeros(B * T, 3 * d, dtype=bf, device=dev)
+    k, v = qkv[:, d:2 * d], qkv[:, 2 * d:]
+
+    def launch():
+        K.relattn_fwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx)
+        K.relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dqu, dbd, ldS,
+                      dqkv[:, d:2 * d], dqkv[:, 2 * d:], dbd_head_major=True)
+
+    unit = 2.0 * B * H * T * T * dk
+    flops = 9 * unit
+    bytes_ = 2.0 * (6 * B * T * d + T * d) + 2.0 * (4 * B * T * d + H * B * T * ldS)
+    rm = "true" if cfgd["chunk"] else "false"
+    meta = {"kernel": f"flash_fwd_kernel + flash_bwd_q_kernel + flash_bwd_kv_kernel<{dk}, 8, true, {rm}>",
+            "match": ["flash_fwd_kernel", "flash_bwd_q_kernel", "flash_bwd_kv_kernel"],
+            "shape": f"B={B} H={H} T'={T} d_k={dk}" + (f" chunk {cfgd['chunk']}" if cfgd["chunk"] else " key padding"),
+            "build": build_key(), "units": {"fwd": 3, "bwd": 6, "executed": 12}}
+    return launch, flops, bytes_, meta
+
+
+def attention_roofline(cfgd, dev, iters=20):
+    """Live HIP-event time of one layer's attention set (attention_case) and its fraction of the
+    bf16 MFMA peak; the MFMA-busy counter of the same build from a committed PMC pass."""
+    launch, flops, bytes_, meta = attention_case(cfgd, dev)
+    sec = _time_case(launch, iters)
+    out = {"kernel": meta["kernel"], "shape": meta["shape"], "bound": "mfma",
+           "achieved": round(flops / sec / 1e12, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(flops / sec / 1e12 / PEAK_BF16_TFLOPS, 4), "traffic": None,
+           "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_,
+           "layer_set_us": round(sec * 1e6, 2), "flop_units": meta["units"],
+           "per": "one encoder layer's attention (forward + backward launches)"}
+    busy = pmc_mfma_case(meta)
+    out["mfma_busy_counter"] = busy
+    return out
+
+
+def pmc_mfma_case(meta):
+    """SQ_VALU_MFMA_BUSY_CYCLES fraction of a roofline case from a committed pass of the same build
+    (profiles/*/pmc_mfma_case*.json, written by tools/pmc_mfma.py --case)."""
+    import glob
+
+    key = build_key()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_mfma_case*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("build") == key and d.get("shape") == meta["shape"]:
+            return {"mfma_busy_frac": d["mfma_util"], "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def _time_case(launch, iters):
     """Average device time of one launch(): `iters` launches captured into one hipGraph (as the
     step runs them) and replayed between two HIP events on the launch stream.  Timing eager
@@ -582,7 +671,7 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", type=int, default=0, metavar="N",
                     help="only launch the roofline kernel N times (for rocprofv3 --pmc passes)")
-    ap.add_argument("--roofline-case", default="family", choices=["family", "dw", "hot"],
+    ap.add_argument("--roofline-case", default="family", choices=["family", "dw", "hot", "attn"],
                     help="--roofline-only: the dominant kernel family (one layer's set), the grouped "
                          "weight-gradient launch (dw) or the hottest instance (hot)")
     args = ap.parse_args()
@@ -610,7 +699,7 @@ def main():
                     for _ in range(it["count"]):
                         it["launch"]()
         else:
-            case = roofline_case if args.roofline_case == "dw" else hottest_case
+            case = {"dw": roofline_case, "hot": hottest_case, "attn": attention_case}[args.roofline_case]
             launch, flops, bytes_, meta = case(CONFIGS[args.config], torch.device("cuda", 0))
         for _ in range(args.roofline_only):
             launch()
@@ -734,7 +823,16 @@ def main():
             out["config"]["profile"] = "roctx ranges per fused node (eager)"
         out["mfma_counter"] = pmc_mfma(args.config)
         if not args.no_roofline:
-            out["roofline"] = dominant_kernel_roofline(cfgd, dev)
+            fam = dominant_kernel_roofline(cfgd, dev)
+            att = attention_roofline(cfgd, dev)
+            # `roofline` = the config's dominant family by time per step (12 encoder layers each:
+            # the family's layer set vs the layer's attention); the other one rides along
+            if att["layer_set_us"] > fam["layer_set_us"]:
+                out["roofline"] = att
+                out["roofline"]["gemm_family"] = fam
+            else:
+                out["roofline"] = fam
+                out["roofline"]["attention"] = att
             out["ctc"] = ctc_roofline(cfgd, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.config)

@@ -53,6 +53,10 @@ for s in "$@"; do
     mfma) cd /tmp && run timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --graph off --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > "$OUT/pmc_mfma.log" 2>&1
           run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mfma" -name '*counter_collection.csv' | head -1)" ${PMC_CONFIG:-small} > "$OUT/pmc_mfma_summary_${PMC_CONFIG:-small}.json"
           rm -rf "$OUT/pmc_mfma" ;;
+    mfmacase) cd /tmp && run timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mc" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 10 --roofline-case attn > "$OUT/pmc_mc.log" 2>&1
+          grep "^{" "$OUT/pmc_mc.log" | tail -1 > "$OUT/mc_meta.json"
+          run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mc" -name '*counter_collection.csv' | head -1)" --case "$OUT/mc_meta.json" > "$OUT/pmc_mfma_case_attn_${PMC_CONFIG:-small}.json"
+          rm -rf "$OUT/pmc_mc" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

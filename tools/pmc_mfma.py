@@ -20,6 +20,33 @@ from collections import defaultdict
 SIMDS = 256 * 4
 
 
+def case_summary(path, meta_path):
+    """MFMA utilisation over the dispatches of one roofline case (bench.py --roofline-only N
+    --roofline-case C under the counter pass): kernels whose names contain one of meta["match"]."""
+    meta = json.load(open(meta_path))
+    busy = el = 0.0
+    n = 0
+    rows = defaultdict(lambda: defaultdict(float))
+    name = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d = r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id")
+            name[d] = r.get("Kernel_Name", "?")
+            rows[d][r["Counter_Name"]] += float(r["Counter_Value"])
+    for d, c in rows.items():
+        if any(m in name[d] for m in meta["match"]) and "GRBM_GUI_ACTIVE" in c:
+            busy += c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+            el += c["GRBM_GUI_ACTIVE"] / 8.0
+            n += 1
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import build_key
+
+    print(json.dumps({"build": build_key(), "kernel": meta["kernel"], "shape": meta["shape"], "dispatches": n,
+                      "mfma_util": busy / (el * SIMDS) if el else None,
+                      "note": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs) over the case's "
+                              "dispatches (counter mode serialises dispatches)"}, indent=1))
+
+
 def main(path, config="small"):
     rows = defaultdict(lambda: defaultdict(float))  # dispatch id -> counter -> value
     name = {}
@@ -54,4 +81,7 @@ def main(path, config="small"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], *(sys.argv[2:3]))
+    if len(sys.argv) > 3 and sys.argv[2] == "--case":
+        case_summary(sys.argv[1], sys.argv[3])
+    else:
+        main(sys.argv[1], *(sys.argv[2:3]))
