@@ -295,9 +295,11 @@ LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(rw[t][ks]), qv1[ks], g2);
       }
-      f32x4 gsel;
+      f32x4 gsel = n2 ? g2 : g1;  // a tile on one side of m = T (zeros elsewhere)
+      if (n1 && n2) {             // the straddle tile (wave-uniform branch)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) gsel[e] = lo + 4 * g + e <= T - 1 ? g1[e] : g2[e];
+        for (int e = 0; e < 4; ++e) gsel[e] = lo + 4 * g + e <= T - 1 ? g1[e] : g2[e];
+      }
       // G'[query col][m - mlo = 16t + 4g + e]
       asm volatile("ds_write_b128 %0, %1" ::"v"(gq + 4u * (uint32_t)(col * GLD + 16 * t + 4 * g)), "v"(gsel) : "memory");
     }
@@ -327,16 +329,20 @@ LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) keep(mw[c]);
-  const bool tail = j0 + KB > a.Tk;
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float x = (s[c][e] + bd[c][e]) * c2;
-      if ((mw[c] >> (8 * e)) & 0xffu) x = -1e38f;
-      if (tail && j0 + 16 * c + 4 * g + e >= a.Tk) x = -INFINITY;
-      s[c][e] = x;
+      const float x = (s[c][e] + bd[c][e]) * c2;
+      s[c][e] = (mw[c] >> (8 * e)) & 0xffu ? -1e38f : x;
     }
+  if (j0 + KB > a.Tk) {  // the last block: keys past Tk (wave-uniform branch)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j0 + 16 * c + 4 * g + e >= a.Tk) s[c][e] = -INFINITY;
+  }
 }
 
 // LDS of the forward: 2 ring stages, the waves' G' scratch (RP), the key-padding bytes (!RM)
@@ -354,7 +360,10 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
   char* ring = smem;                                   // 2 stages
   float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);   // RP: NW x [16][GLD]
   uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * 16 * GLD : 0));  // !RM: key padding bytes
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, col = lane & 15;
+  // the wave index through readfirstlane: wave-uniform values derived from it stay in SGPRs
+  // (uniform branches and scalar address arithmetic instead of exec-masked vector code)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            col = lane & 15;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
   const int i0 = blockIdx.x * Gm::QB, iw = i0 + 16 * w, iq = iw + col;
   const int nb = (Tk + KB - 1) / KB;
@@ -467,7 +476,10 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
   char* ring = smem;
   float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);
   uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * 16 * GLD : 0));
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, col = lane & 15;
+  // the wave index through readfirstlane: wave-uniform values derived from it stay in SGPRs
+  // (uniform branches and scalar address arithmetic instead of exec-masked vector code)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            col = lane & 15;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
   const int i0 = blockIdx.x * Gm::QB, iw = i0 + 16 * w, iq = iw + col, ic = min(iq, T - 1);
   const int nb = (Tk + KB - 1) / KB;
@@ -711,7 +723,10 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
   char* ring = smem;
   float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);
   float* sst = gsh + (RP ? NW * 32 * KLD : 0);  // [2][3][QBK]: m (log2 units), 1/sum, D
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, col = lane & 15;
+  // the wave index through readfirstlane: wave-uniform values derived from it stay in SGPRs
+  // (uniform branches and scalar address arithmetic instead of exec-masked vector code)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            col = lane & 15;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
   const int j0 = blockIdx.x * Gm::KBW, jw = j0 + 16 * w, jq = jw + col;
   const int nq = (T + QBK - 1) / QBK;
@@ -832,8 +847,8 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
               for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(av1[ks]), as_frag(bw[uu][ks]), g2);
             }
             // lane (g, col) holds G[query 4g + e][m = lo + col]: select by m <= T - 1, park as [m][query]
-            const bool v1 = lo + col <= T - 1;
-            const f32x4 gs = v1 ? g1 : g2;
+            f32x4 gs = n2 ? g2 : g1;
+            if (n1 && n2) gs = lo + col <= T - 1 ? g1 : g2;
             asm volatile("ds_write_b128 %0, %1" ::"v"(gka + 4u * (uint32_t)((16 * uu + col) * KLD + 4 * g)), "v"(gs)
                          : "memory");
           }

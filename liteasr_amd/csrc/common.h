@@ -238,6 +238,21 @@ LASR_DEV uint32_t drop_keep_mask(const DropCfg& d, uint32_t key, uint64_t idx0) 
   }
   return km;
 }
+// The same for an even idx0 (the specialised vector epilogues: N % 8 == 0 host-checked, so a
+// row's 8-column vector starts on an even element): no per-element fallback code.
+template <int N>
+LASR_DEV uint32_t drop_keep_mask_even(const DropCfg& d, uint32_t key, uint64_t idx0) {
+  static_assert(N % 2 == 0, "pairs");
+  uint32_t km = 0u;
+  const uint64_t pair0 = idx0 >> 1;
+#pragma unroll
+  for (int q = 0; q < N; q += 2) {
+    const uint32_t b = drop_bits(key, pair0 + (q >> 1));
+    km |= ((b & 0xFFFFu) >= d.thr ? 1u : 0u) << q;
+    km |= ((b >> 16) >= d.thr ? 1u : 0u) << (q + 1);
+  }
+  return km;
+}
 template <int N>
 LASR_DEV void drop_mul_n(const DropCfg& d, uint32_t key, uint64_t idx0, float* m) {
   drop_keep_n<N>(d, key, idx0, m);

@@ -94,7 +94,7 @@ LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)
                        bool has_aux, const float (&resv)[N], bool has_res, ZST zst) {
   if constexpr (EPI == EPI_SWISH_GATE_DROP) {
     // zout_mode 1, Swish, dropout on; no aux, residual or beta (FFN fc1 forward)
-    const uint32_t km = drop_keep_mask<N>(p.drop, dkey, dbase);
+    const uint32_t km = drop_keep_mask_even<N>(p.drop, dkey, dbase);
     float g[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) {
@@ -115,7 +115,7 @@ LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)
     return;
   } else if constexpr (EPI == EPI_RELU_GATE_DROP) {
     // zout_mode 1, ReLU, dropout on; no aux, residual or beta (the decoder's FFN fc1 forward)
-    const uint32_t km = drop_keep_mask<N>(p.drop, dkey, dbase);
+    const uint32_t km = drop_keep_mask_even<N>(p.drop, dkey, dbase);
     float g[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) g[q] = v[q] > 0.f ? 1.f : 0.f;
@@ -139,7 +139,7 @@ LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)
     return;  // alpha * acc + bias only (input-gradient GEMMs)
   } else if constexpr (EPI == EPI_RES_DROP) {
     // res + res_scale * dropout(v), dropout on; no activation, zout or aux (residual projections)
-    const uint32_t km = drop_keep_mask<N>(p.drop, dkey, dbase);
+    const uint32_t km = drop_keep_mask_even<N>(p.drop, dkey, dbase);
 #pragma unroll
     for (int q = 0; q < N; ++q) v[q] *= (km >> q) & 1u ? p.drop.scale : 0.f;
 #pragma unroll
@@ -1152,7 +1152,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
 // against exactly the parameters the specialised path assumes; LASR_EPI_SPEC=0 disables it.
 static inline int epi_code(const GemmP& p) {
   static const int on = [] { const char* e = getenv("LASR_EPI_SPEC"); return e && e[0] ? atoi(e) : 1; }();
-  if (!on || p.split_k > 1 || p.beta != 0.f || p.alpha_dev) return EPI_RT;
+  // (N % 8 == 0: every 8-column vector of the specialised epilogues starts on an even element,
+  // so their dropout draws take the pair-aligned path only)
+  if (!on || p.split_k > 1 || p.beta != 0.f || p.alpha_dev || p.N % 8 != 0) return EPI_RT;
   if (p.res) {
     return !p.zout && p.act == LASR_ACT_NONE && !p.aux && p.drop.p > 0.f && p.epi_mode == 1 ? EPI_RES_DROP : EPI_RT;
   }
