@@ -57,6 +57,9 @@ for s in "$@"; do
           grep "^{" "$OUT/pmc_mc.log" | tail -1 > "$OUT/mc_meta.json"
           run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mc" -name '*counter_collection.csv' | head -1)" --case "$OUT/mc_meta.json" > "$OUT/pmc_mfma_case_attn_${PMC_CONFIG:-small}.json"
           rm -rf "$OUT/pmc_mc" ;;
+    libab) for v in ${AB_ORDER:-base new base new}; do lib=liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=liteasr_amd/lib/ab/${AB_BASE:-libliteasr_hip_r03.so}
+             LITEASR_HIP_LIB=$R/$lib run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/ab_$v.json" 2> "$OUT/ab_$v.err"
+             grep "^{" "$OUT/ab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'ms': d['ms_per_step'], 'median': d['ms_per_step_median'], 'utt_s': d['value']}))" >> "$OUT/libab.jsonl"; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
