@@ -34,6 +34,8 @@ for s in "$@"; do
     large) run timeout -k 10 400 python3 bench.py --config large --no-cpu-baseline > "$OUT/bench_large.json" 2> "$OUT/bench_large.err" ;;
     ddp1) run timeout -k 10 300 python3 bench.py --force-ddp --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1.json" 2> "$OUT/bench_ddp1.err" ;;
     ddp1n) run timeout -k 10 300 python3 bench.py --force-ddp --comm native --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1_native.json" 2> "$OUT/bench_ddp1_native.err" ;;
+    kg) run timeout -k 10 300 $PYT tests/test_kernels_gpu.py -k "kgroups or ksub2" > "$OUT/kg.log" 2>&1 ;;
+    tileab) run timeout -k 10 200 python3 tools/tile_ab.py > "$OUT/tile_ab.jsonl" 2> "$OUT/tile_ab.err" ;;
     blaslt) run timeout -k 10 120 python3 tools/blaslt_ref.py > "$OUT/blaslt.jsonl" 2> "$OUT/blaslt.err" ;;
     trace) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace.log" 2>&1
            db=$(find "$OUT/trace" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary.txt" 2>&1
@@ -57,9 +59,11 @@ for s in "$@"; do
           grep "^{" "$OUT/pmc_mc.log" | tail -1 > "$OUT/mc_meta.json"
           run python3 "$R/tools/pmc_mfma.py" "$(find "$OUT/pmc_mc" -name '*counter_collection.csv' | head -1)" --case "$OUT/mc_meta.json" > "$OUT/pmc_mfma_case_attn_${PMC_CONFIG:-small}.json"
           rm -rf "$OUT/pmc_mc" ;;
-    libab) for v in ${AB_ORDER:-base new base new}; do lib=liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=liteasr_amd/lib/ab/${AB_BASE:-libliteasr_hip_r03.so}
-             LITEASR_HIP_LIB=$R/$lib run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/ab_$v.json" 2> "$OUT/ab_$v.err"
-             grep "^{" "$OUT/ab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'ms': d['ms_per_step'], 'median': d['ms_per_step_median'], 'utt_s': d['value']}))" >> "$OUT/libab.jsonl"; done ;;
+    libab) # whole-step A/B against the round-3 tree (ab_r03/: `git archive 42f6a8d` + its built
+           # library; the Python layer changed ABI this round, so the base runs its own tree)
+           for v in ${AB_ORDER:-base new base new}; do d=$R; [ $v = base ] && d=$R/ab_r03
+             (cd $d && run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-}) > "$OUT/ab_$v.json" 2> "$OUT/ab_$v.err"
+             grep "^{" "$OUT/ab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'tree': '$v', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'utt_s': d['value']}))" >> "$OUT/libab.jsonl"; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
