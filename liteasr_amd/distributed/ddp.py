@@ -135,7 +135,7 @@ class FlatReducer:
         it (between steps) instead of silently averaging the old buffer."""
         g = self.store.grad
         if self.native.grad_ptr() != g.data_ptr():
-            if self.native.launched() or any(self.ready):
+            if self.native.launched():  # buckets of this step already went out from the old buffer
                 raise RuntimeError("FlatReducer: the flat gradient buffer was replaced inside a step")
             self.native.rebind(g)
 

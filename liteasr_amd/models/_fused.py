@@ -139,15 +139,17 @@ class FusedEncoderModel(LiteasrModel):
         yy = ys.to(device=dev, dtype=torch.int64).contiguous()
         yl = ylens.to(device=dev, dtype=torch.int64)
         K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, 0, out)
-        # query-dependent masks as views with 16-B aligned rows (the attention kernels stage
-        # their tiles by LDS-DMA); kernels read them through (msb, msq) = the view's strides
-        out["dec_mask"] = K.pad_mask16(out["dec_mask"], B, L + 1, L + 1)[0]
         chunk = None
         if self.chunk_size > 0:
-            tmp = dict(out)
+            # (u2_prep writes every output: the chunk-mask call gets scratch for the others, so
+            # nothing it writes lands in a buffer laid out differently from what it assumes)
+            tmp = {k: torch.empty_like(v) for k, v in out.items()}
             tmp["enc_mask"] = torch.empty(B, Tsub, Tsub, dtype=u8, device=dev)
             K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, self.chunk_size, tmp)
             chunk = K.pad_mask16(tmp["enc_mask"], B, Tsub, Tsub)[0]
+        # query-dependent masks as views with 16-B aligned rows (the attention kernels stage
+        # their tiles by LDS-DMA); kernels read them through (msb, msq) = the view's strides
+        out["dec_mask"] = K.pad_mask16(out["dec_mask"], B, L + 1, L + 1)[0]
         p = SimpleNamespace(B=B, Tx=Tx, T=Tsub, L=L, chunk_mask=chunk, **out)
         return p
 

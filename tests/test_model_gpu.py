@@ -251,14 +251,21 @@ DEEP = O.default_cfg(enc_dim=128, enc_heads=4, enc_ff=256, enc_layers=12, dec_di
                      dec_layers=6, vocab_size=64)
 
 
-def _check_fp32(r, tol):
+def _check_fp32(r, tol, loss_tol=1e-5, dec_ffn_kink=False):
+    """dec_ffn_kink: the decoder FFN's ReLU-gated parameters (fc1, and the FFN norm in front of
+    it) get the kink bar of the subsampling convs: there fp32 rounding itself can flip a ReLU
+    pre-activation that lies within rounding of 0 (see test_parity_config4_full_model_fp32)."""
     lg, lo = r["loss"]
-    assert abs(lg - lo) <= 1e-5 * abs(lo), r["loss"]
-    assert rel(*r["h_attn"]) < tol and rel(*r["h_ctc"]) < tol
     g, go = r["grads"]
     errs, _ = grad_errs(g, go)
-    kink = {k for k in errs if k.startswith("encoder.embed.conv.")}  # see test_parity_fp32
+    kink = {k for k in errs if k.startswith("encoder.embed.conv.")  # see test_parity_fp32
+            or (dec_ffn_kink and k.startswith("decoder.dec_layers.") and (".feed_forward.fc1." in k or
+                                                                          ".feed_forward_norm." in k))}
     worst = max((v, k) for k, v in errs.items() if k not in kink)
+    print(f"fp32 parity: loss rel {abs(lg - lo) / abs(lo):.2e}, logits {rel(*r['h_attn']):.2e} / "
+          f"{rel(*r['h_ctc']):.2e}, worst grad {worst[0]:.2e} ({worst[1]})")
+    assert abs(lg - lo) <= loss_tol * abs(lo), r["loss"]
+    assert rel(*r["h_attn"]) < tol and rel(*r["h_ctc"]) < tol
     assert worst[0] < tol, worst
     assert max(errs[k] for k in kink) < 2e-2, {k: errs[k] for k in kink}
 
@@ -309,12 +316,38 @@ CONFIG4 = O.default_cfg(enc_dim=512, enc_heads=16, enc_ff=2048, enc_layers=12, d
                         dec_ff=2048, dec_layers=6, vocab_size=4233)
 
 
+@pytest.mark.parametrize("L", [10, 40])
+def test_prep_with_chunk_mask_keeps_every_other_output(L):
+    """The streaming chunk mask is a second bookkeeping pass: every other output (decoder mask
+    with its 16-B padded rows, targets, lengths, key mask) must be what the chunk-free pass
+    gives (round 4: the chunk pass wrote the decoder mask in the unpadded layout over the
+    padded view)."""
+    B, T = 3, 400
+    xs, xlens, ys, ylens = O.synthetic_batch(B, T, L, TINY["vocab_size"], seed=5)
+    preps = []
+    for chunk in (0, 16):
+        m = build(TINY, "bf16", chunk).cuda()
+        preps.append(m._prep(xs.cuda(), xlens.cuda(), ys.cuda(), ylens.cuda()))
+    a, b = preps
+    for k in ("ys_in", "tgt", "tgt_ctc", "dec_mask", "enc_mask", "pred_len", "ylen"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert a.dec_mask.stride(1) % 16 == 0
+    assert a.chunk_mask is None and b.chunk_mask is not None and b.chunk_mask.stride(1) % 16 == 0
+
+
 def test_parity_config4_full_model_fp32():
     """liteasr/nets/transformer_encoder.py:107-127 with the chunk mask of liteasr/utils/mask.py:
     30-90 and the 16-head relative attention of liteasr/nets/attention.py:120-154, full depth
     and length, fp32 build vs the fp64 oracle: loss 1e-5 relative, logits and every gradient
-    1e-3 of max (the subsampling convs' ReLU-kink bar as in test_parity_fp32)."""
-    _check_fp32(run_case(CONFIG4, 2, 1000, 40, "fp32", chunk=16), 1e-3)
+    1e-3 of max; the ReLU-kink bar (2e-2) for the subsampling convs as in test_parity_fp32 and
+    for the decoder FFNs' ReLU-gated parameters: decoder layer 4's fc1 weight gradient is off by
+    1.32e-2 of max in the HIP fp32 build, and by the same 1.32e-2 when the oracle itself runs in
+    fp32 against its fp64 run on this container's CPU (one pre-activation within fp32 rounding
+    of 0 flips; a decoder fc1 row sums only B*(L+1) = 82 rows) -- on the GPU box's CPU the fp32
+    oracle happened not to flip it, so the bar is the kink bar, not a measured multiple.  This
+    case caught the round-4 padded decoder mask being overwritten by the chunk-mask preparation
+    (decoder logits 9.9e-2 of max)."""
+    _check_fp32(run_case(CONFIG4, 2, 1000, 40, "fp32", chunk=16), 1e-3, dec_ffn_kink=True)
 
 
 def test_parity_config4_full_model_bf16_emulated():
