@@ -224,11 +224,16 @@ def roofline_case(cfgd, dev):
         for a, b, c, r in probs:
             K.gemm(a.t(), b, c, beta=1.0, split_k=0, rowsum=r, group=True)
         q = list(K._DEFER.gemms)
+        # the fp32 partial buffers the queued args write into are owned by the deferred
+        # reductions (segs): keep them alive with the launch, or the args point at freed memory
+        parts = [sg[0] for sg in K._DEFER.segs]
         K._DEFER.gemms.clear()
         K._DEFER.segs.clear()
     assert q and all(k == q[0][0] for k, _, _ in q), "FFN weight gradients did not group"
     arr = (Nn.GemmArgs * len(q))(*[x[1] for x in q])
-    keep = [x[2] for x in q] + [probs]  # the partial buffers are referenced by the args
+    wsp = {int(x[1].workspace) for x in q}
+    assert wsp <= {pt.data_ptr() for pt in parts}, "a queued dW launch writes outside the kept partial buffers"
+    keep = [x[2] for x in q] + [probs, parts]
 
     def launch():
         Nn.call("lasr_gemm_dw_group", arr, len(q), K.stream())
