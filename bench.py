@@ -342,7 +342,8 @@ def attention_case(cfgd, dev):
     flops = 9 * unit
     bytes_ = 2.0 * (6 * B * T * d + T * d) + 2.0 * (4 * B * T * d + H * B * T * ldS)
     rm = "true" if cfgd["chunk"] else "false"
-    meta = {"kernel": f"flash_fwd_kernel + flash_bwd_q_kernel + flash_bwd_kv_kernel<{dk}, 8, true, {rm}>",
+    nw = "8" if dk == 64 else "4 (fwd) / 8"
+    meta = {"kernel": f"flash_fwd_kernel + flash_bwd_q_kernel + flash_bwd_kv_kernel<{dk}, {nw}, true, {rm}>",
             "match": ["flash_fwd_kernel", "flash_bwd_q_kernel", "flash_bwd_kv_kernel"],
             "shape": f"B={B} H={H} T'={T} d_k={dk}" + (f" chunk {cfgd['chunk']}" if cfgd["chunk"] else " key padding"),
             "build": build_key(), "units": {"fwd": 3, "bwd": 6, "executed": 12}}

@@ -192,22 +192,53 @@ LASR_DEV void issue_stage(const FlashP& a, int b, int h, int i0, int j0, char* s
   const int64_t kb = (int64_t)b * Tk;
   const bf16_t* kh = a.k + kb * a.ldkv + h * DK;
   const bf16_t* vh = a.v + kb * a.ldkv + h * DK;
-  dma_region<Gm::K_CH, Gm::NT>(st, Gm::K0, tid, [&](int p) {
-    int r, c;
-    chunk_rc<DK>(p, r, c);
-    return (const void*)(kh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c);
-  });
-  dma_region<Gm::V_CH, Gm::NT>(st, Gm::V0, tid, [&](int p) {
-    int r, c;
-    chunk_rc<DK>(p, r, c);
-    return (const void*)(vh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c);
-  });
-  if constexpr (RP)
-    dma_region<Gm::W_CH, Gm::NT>(st, Gm::W0, tid, [&](int p) {
+  // (uniform branches) a block whose 64 key rows all exist, and a window that lies on one side
+  // of m = T, take a uniform base plus the thread's loop-invariant 32-bit offset per piece;
+  // only the last key block and the window straddling m = T clamp / select per piece
+  if (j0 + KB <= Tk) {
+    const bf16_t* kj = kh + (int64_t)j0 * a.ldkv;
+    const bf16_t* vj = vh + (int64_t)j0 * a.ldkv;
+    dma_region<Gm::K_CH, Gm::NT>(st, Gm::K0, tid, [&](int p) {
       int r, c;
       chunk_rc<DK>(p, r, c);
-      return wrow(a, h, DK, j0 - i0 + T - Gm::QB + r, c);
+      return (const void*)(kj + (uint32_t)(r * a.ldkv + c));
     });
+    dma_region<Gm::V_CH, Gm::NT>(st, Gm::V0, tid, [&](int p) {
+      int r, c;
+      chunk_rc<DK>(p, r, c);
+      return (const void*)(vj + (uint32_t)(r * a.ldkv + c));
+    });
+  } else {
+    dma_region<Gm::K_CH, Gm::NT>(st, Gm::K0, tid, [&](int p) {
+      int r, c;
+      chunk_rc<DK>(p, r, c);
+      return (const void*)(kh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c);
+    });
+    dma_region<Gm::V_CH, Gm::NT>(st, Gm::V0, tid, [&](int p) {
+      int r, c;
+      chunk_rc<DK>(p, r, c);
+      return (const void*)(vh + (int64_t)min(j0 + r, Tk - 1) * a.ldkv + c);
+    });
+  }
+  if constexpr (RP) {
+    const int mb = j0 - i0 + T - Gm::QB;  // m of window row 0
+    const bool lo_side = mb >= 0 && mb + Gm::W_ROWS <= T;              // rows p[m]
+    const bool hi_side = mb >= T + 1 && mb + Gm::W_ROWS <= 2 * T + 1;  // rows p[m - T - 1]
+    if (lo_side || hi_side) {
+      const bf16_t* wb = a.pos + (int64_t)(lo_side ? mb : mb - T - 1) * a.ldp + h * DK;
+      dma_region<Gm::W_CH, Gm::NT>(st, Gm::W0, tid, [&](int p) {
+        int r, c;
+        chunk_rc<DK>(p, r, c);
+        return (const void*)(wb + (uint32_t)(r * a.ldp + c));
+      });
+    } else {
+      dma_region<Gm::W_CH, Gm::NT>(st, Gm::W0, tid, [&](int p) {
+        int r, c;
+        chunk_rc<DK>(p, r, c);
+        return wrow(a, h, DK, mb + r, c);
+      });
+    }
+  }
   if constexpr (RM)
     // mask tile [query r][64 keys] bytes: rows 16-B aligned (host-checked); a piece starting
     // past the row stride holds only keys >= Tk (masked anyway): clamped
@@ -231,7 +262,7 @@ LASR_DEV void load_q(const bf16_t* base, int64_t ld, int row, int h, int lane, b
 // read of the block (K and window fragments, mask words) is issued up front; counted waits
 // release the S products while the window reads are still landing.
 template <int DK, int NW, bool RP, bool RM>
-LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t* km, const bf16x8 (&qu)[DK / 32],
+LASR_DEV bool scores_t(const FlashP& a, const char* st, float* gw, const uint8_t* km, const bf16x8 (&qu)[DK / 32],
                        const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int w, int i0, int j0, float c2,
                        int lane, f32x4 (&s)[4]) {
   using Gm = Geo<DK, NW, RP, RM>;
@@ -329,20 +360,59 @@ LASR_DEV void scores_t(const FlashP& a, const char* st, float* gw, const uint8_t
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) keep(mw[c]);
+  // (s + bd) * c2 on packed fp32 pairs (the same two roundings per element)
+  const lasr_f2 c2v = {c2, c2};
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float x = (s[c][e] + bd[c][e]) * c2;
-      s[c][e] = (mw[c] >> (8 * e)) & 0xffu ? -1e38f : x;
+    for (int e = 0; e < 4; e += 2) {
+      lasr_f2 x = {s[c][e], s[c][e + 1]};
+      const lasr_f2 y = {bd[c][e], bd[c][e + 1]};
+      x = (x + y) * c2v;
+      s[c][e] = x[0];
+      s[c][e + 1] = x[1];
     }
-  if (j0 + KB > a.Tk) {  // the last block: keys past Tk (wave-uniform branch)
+  // the per-element mask select only where the wave's block has a masked key (uniform: most
+  // blocks of a key-padding mask have none)
+  const bool anym = __builtin_amdgcn_ballot_w64((mw[0] | mw[1] | mw[2] | mw[3]) != 0u) != 0;
+  if (anym) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[c][e] = (mw[c] >> (8 * e)) & 0xffu ? -1e38f : s[c][e];
+  }
+  const bool tail = j0 + KB > a.Tk;
+  if (tail) {  // the last block: keys past Tk (wave-uniform branch)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (j0 + 16 * c + 4 * g + e >= a.Tk) s[c][e] = -INFINITY;
   }
+  return anym || tail;
+}
+
+// Query-dependent mask (RM): is every score of the wave's block (its 16 queries x the 64 keys)
+// masked?  (wave-uniform; every mask byte nonzero.)  A block fully masked for rows that do have an
+// unmasked key elsewhere contributes exactly nothing (P = 0 after the rescale, dS = 0): callers
+// skip its arithmetic when every row of the wave is known to have one, which keeps a fully
+// masked row's uniform-P semantics intact.
+template <int DK, int NW, bool RP, bool RM>
+LASR_DEV bool block_all_masked(const char* st, int w, int lane) {
+  using Gm = Geo<DK, NW, RP, RM>;
+  const int g = lane >> 4, col = lane & 15;
+  const uint32_t mimg = ldsa(st + Gm::M0 * 16) + (uint32_t)((16 * w + col) * KB + 4 * g);
+  uint32_t mw[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(mw[c]) : "v"(mimg), "i"(16 * c));
+  lgkm0();
+  bool zero_byte = false;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    keep(mw[c]);
+    zero_byte |= ((mw[c] - 0x01010101u) & ~mw[c] & 0x80808080u) != 0u;
+  }
+  return __builtin_amdgcn_ballot_w64(zero_byte) == 0;
 }
 
 // LDS of the forward: 2 ring stages, the waves' G' scratch (RP), the key-padding bytes (!RM)
@@ -353,7 +423,7 @@ constexpr int fwd_lds() {
 }
 
 template <int DK, int NW, bool RP, bool RM>
-__global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
+__global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
   using Gm = Geo<DK, NW, RP, RM>;
   constexpr int KS = DK / 32, NT = Gm::NT;
   __shared__ __attribute__((aligned(16))) char smem[fwd_lds<DK, NW, RP, RM>()];
@@ -394,8 +464,11 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
     wait_vmcnt<0>();  // this block's pieces (issued one block ago) and the Q loads
     lds_barrier();    // ... of every wave; every wave is done with block jb-1's stage
     if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
+    if constexpr (RM) {  // (the streaming chunk mask: the blocks of future chunks)
+      if (__builtin_amdgcn_ballot_w64(mrun <= -1e38f) == 0 && block_all_masked<DK, NW, RP, RM>(st, w, lane)) continue;
+    }
     f32x4 s[4];
-    scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
+    (void)scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
     // V^T fragments for O^T += V^T P^T, in flight during the softmax (k slots of sub-block ks:
     // keys 32ks + 4g + e, then 32ks + 16 + 4g + e)
     const uint32_t vimg = ldsa(st + Gm::V0 * 16);
@@ -415,16 +488,21 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
     bm = xmax16_32(bm);
     const float mn = fmaxf(mrun, bm);
     const float al = __builtin_amdgcn_exp2f(mrun - mn);
-    float sum = 0.f;
+    const lasr_f2 mnv = {mn, mn};
+    lasr_f2 sum2 = {0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float p = __builtin_amdgcn_exp2f(s[c][e] - mn);
-        s[c][e] = p;
-        sum += p;
+      for (int e = 0; e < 4; e += 2) {
+        lasr_f2 x = {s[c][e], s[c][e + 1]};
+        x -= mnv;
+        x[0] = __builtin_amdgcn_exp2f(x[0]);
+        x[1] = __builtin_amdgcn_exp2f(x[1]);
+        s[c][e] = x[0];
+        s[c][e + 1] = x[1];
+        sum2 += x;
       }
-    lrun = lrun * al + sum;
+    lrun = lrun * al + (sum2[0] + sum2[1]);
     mrun = mn;
 #pragma unroll
     for (int t = 0; t < DK / 16; ++t) o[t] *= al;
@@ -469,7 +547,7 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_fwd_kernel(FlashP a) {
 // GEMMs consume (exactly relshift_bwd's output).  D_i = rowsum(dO * O) is formed here and
 // stored for the key-side kernel.
 template <int DK, int NW, bool RP, bool RM>
-__global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
+__global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) {
   using Gm = Geo<DK, NW, RP, RM>;
   constexpr int KS = DK / 32, NT = Gm::NT;
   __shared__ __attribute__((aligned(16))) char smem[fwd_lds<DK, NW, RP, RM>()];
@@ -503,6 +581,8 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
   // the forward's statistics in log2 units (a fully masked row keeps the masked value)
   const float mx = a.stats[2 * (zrow + ic)], il = a.stats[2 * (zrow + ic) + 1];
   const float m2 = mx <= -1e38f ? -1e38f : mx * 1.4426950408889634f;
+  // every row of the wave has an unmasked key (none fully masked): fully masked blocks may be skipped
+  [[maybe_unused]] const bool rows_live = __builtin_amdgcn_ballot_w64(m2 <= -1e38f) == 0;
   // D_i = sum_c dO[i,c] O[i,c] on the MFMA that forms dP (the diagonal of O . dO^T over the
   // wave's 16 queries): the same products summed in the same order as dP, so dP - D cancels
   // exactly where it should (one key: P = 1, O = V)
@@ -532,7 +612,13 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
     lds_barrier();
     if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
     f32x4 s[4];
-    scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
+    bool skip = false;
+    if constexpr (RM) skip = rows_live && block_all_masked<DK, NW, RP, RM>(st, w, lane);
+    if (skip) {  // dS = 0 over the block: only its (zero) dBD entries are written
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[c] = zero4();
+    } else {
+    const bool msk = scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
     // V fragments for dP^T = V . dO^T (V rows = keys as the A operand), then the K^T
     // fragments for dQu^T += K^T dS^T, in flight during dP and dS
     const uint32_t vimg = ldsa(st + Gm::V0 * 16), kimg = ldsa(st);
@@ -562,15 +648,28 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
       for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(rv[c][ks]), dof[ks], acc);
       dp[c] = acc;
     }
-    // dS = P (dP - D), zero where masked or past Tk (the forward's masked_fill backward)
+    // dS = P (dP - D), zero where masked or past Tk (the forward's masked_fill backward), on
+    // packed fp32 pairs (the same roundings per element); the select only in masked blocks
+    {
+      const lasr_f2 m2v = {m2, m2}, ilv = {il, il}, Dv = {D, D};
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = s[c][e];
-        const float p = __builtin_amdgcn_exp2f(v - m2) * il;
-        s[c][e] = v > -1e38f ? p * (dp[c][e] - D) : 0.f;
-      }
+        for (int e = 0; e < 4; e += 2) {
+          const lasr_f2 v = {s[c][e], s[c][e + 1]};
+          lasr_f2 x = v - m2v;
+          x[0] = __builtin_amdgcn_exp2f(x[0]);
+          x[1] = __builtin_amdgcn_exp2f(x[1]);
+          const lasr_f2 d = {dp[c][e], dp[c][e + 1]};
+          x = (x * ilv) * (d - Dv);
+          s[c][e] = x[0];
+          s[c][e + 1] = x[1];
+          if (msk) {
+            s[c][e] = v[0] > -1e38f ? s[c][e] : 0.f;
+            s[c][e + 1] = v[1] > -1e38f ? s[c][e + 1] : 0.f;
+          }
+        }
+    }
     lgkm0();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -585,6 +684,7 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_q_kernel(FlashP a) {
 #pragma unroll
       for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), db, dq[t]);
     }
+    }  // !skip
     if constexpr (RP) {
       // inverse rel_shift: the bd entry each score read (none for j == i + 1).  A lane's 4 keys
       // of a tile land on 4 consecutive columns of one dBD row unless they straddle the
@@ -684,38 +784,70 @@ struct GeoKV {
 template <int DK, int NW, bool RP, bool RM>
 LASR_DEV void issue_stage_kv(const FlashP& a, int b, int h, int i0, int j0, char* st, int tid) {
   using Gm = GeoKV<DK, NW, RP, RM>;
-  const int wid = tid >> 6, T = a.T;
+  const int T = a.T;
   const int64_t qb = (int64_t)b * T;
-#pragma unroll
-  for (int i = 0; i < Gm::GL; ++i) {
-    const int P = i * Gm::NT + tid;
-    const void* src;
-    int r, c;
-    if (P < Gm::O0) {
-      chunk_rc<DK>(P, r, c);
-      src = a.qu + (qb + min(i0 + r, T - 1)) * a.ldq + h * DK + c;
-    } else if (P < Gm::QV0) {
-      chunk_rc<DK>(P - Gm::O0, r, c);
-      src = a.dctx + (qb + min(i0 + r, T - 1)) * a.ldc + h * DK + c;
-    } else if (RP && P < Gm::M0) {
-      chunk_rc<DK>(P - Gm::QV0, r, c);
-      src = a.qv + (qb + min(i0 + r, T - 1)) * a.ldq + h * DK + c;
-    } else if (RM && P < Gm::W0) {
-      const int q = P - Gm::M0, rr = q / (Gm::KBW / 16), c16 = (q % (Gm::KBW / 16)) * 16;
-      const int64_t col = min<int64_t>(j0 + c16, a.msq - 16);
-      src = a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + rr, T - 1) * a.msq + col;
+  // one region at a time (uniform region bounds); a query block whose rows all exist, and a
+  // window on one side of m = T, take a uniform base plus the thread's loop-invariant offset
+  auto rows3 = [&](int nrows, auto&& emit) {
+    if (i0 + nrows <= T) {
+      emit([&](const bf16_t* base, int64_t ld, int r, int c) {
+        return (const void*)(base + (qb + i0) * ld + (uint32_t)(r * ld + c));
+      });
     } else {
-      chunk_rc<DK>(P - Gm::W0, r, c);
-      const int m = j0 - (i0 + QBK - 1) + T - 1 + r;  // window row r <-> m
-      const int src_row = m >= 0 && m <= T - 1 ? m : (m >= T + 1 && m <= 2 * T ? m - T - 1 : -1);
-      src = src_row >= 0 ? (const void*)(a.pos + (int64_t)src_row * a.ldp + h * DK + c) : (const void*)(g_zero_row + c);
+      emit([&](const bf16_t* base, int64_t ld, int r, int c) {
+        return (const void*)(base + (qb + min(i0 + r, T - 1)) * ld + c);
+      });
     }
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(st + (size_t)(i * Gm::NT + wid * 64) * 16), 16, 0, 0);
+  };
+  rows3(QBK, [&](auto addr) {
+    dma_region<Gm::Q_CH, Gm::NT>(st, 0, tid, [&](int p) {
+      int r, c;
+      chunk_rc<DK>(p, r, c);
+      return addr(a.qu + h * DK, a.ldq, r, c);
+    });
+    dma_region<Gm::O_CH, Gm::NT>(st, Gm::O0, tid, [&](int p) {
+      int r, c;
+      chunk_rc<DK>(p, r, c);
+      return addr(a.dctx + h * DK, a.ldc, r, c);
+    });
+  });
+  if constexpr (RP)
+    rows3(Gm::QV_ROWS, [&](auto addr) {
+      dma_region<Gm::QV_CH, Gm::NT>(st, Gm::QV0, tid, [&](int p) {
+        int r, c;
+        chunk_rc<DK>(p, r, c);
+        return addr(a.qv + h * DK, a.ldq, r, c);
+      });
+    });
+  if constexpr (RM)
+    dma_region<Gm::M_CH, Gm::NT>(st, Gm::M0, tid, [&](int q) {
+      const int rr = q / (Gm::KBW / 16), c16 = (q % (Gm::KBW / 16)) * 16;
+      const int64_t col = min<int64_t>(j0 + c16, a.msq - 16);
+      return (const void*)(a.mask + (int64_t)b * a.msb + (int64_t)min(i0 + rr, T - 1) * a.msq + col);
+    });
+  if constexpr (RP) {
+    const int mb = j0 - (i0 + QBK - 1) + T - 1;  // m of window row 0
+    const bool lo_side = mb >= 0 && mb + Gm::W_ROWS <= T;
+    const bool hi_side = mb >= T + 1 && mb + Gm::W_ROWS <= 2 * T + 1;
+    if (lo_side || hi_side) {
+      const bf16_t* wb = a.pos + (int64_t)(lo_side ? mb : mb - T - 1) * a.ldp + h * DK;
+      dma_region<Gm::W_CH, Gm::NT>(st, Gm::W0, tid, [&](int p) {
+        int r, c;
+        chunk_rc<DK>(p, r, c);
+        return (const void*)(wb + (uint32_t)(r * a.ldp + c));
+      });
+    } else {
+      dma_region<Gm::W_CH, Gm::NT>(st, Gm::W0, tid, [&](int p) {
+        int r, c;
+        chunk_rc<DK>(p, r, c);
+        return wrow(a, h, DK, mb + r, c);
+      });
+    }
   }
 }
 
 template <int DK, int NW, bool RP, bool RM>
-__global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16_t* dk_out, bf16_t* dv_out,
+__global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a, bf16_t* dk_out, bf16_t* dv_out,
                                                                   int64_t lddkv) {
   using Gm = GeoKV<DK, NW, RP, RM>;
   constexpr int KS = DK / 32;
@@ -740,6 +872,8 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
   load_q<DK>(a.v, a.ldkv, b * Tk + min(jq, Tk - 1), h, lane, vf);
   bool kmasked = false;
   if (!RM && a.mask) kmasked = a.mask[(int64_t)b * a.msb + min(jq, Tk - 1)] != 0;
+  // (key padding) any masked key among the wave's 16: the per-element selects are needed
+  const bool kany = __builtin_amdgcn_ballot_w64(kmasked) != 0;
   // the block's statistics, loaded by wave 0 one block ahead
   float st_m = 0.f, st_l = 0.f, st_d = 0.f;
   auto load_stats = [&](int i0) {
@@ -819,6 +953,25 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
         keep(smv); keep(slv); keep(sdv);
 #pragma unroll
         for (int e = 0; e < 4; ++e) keep(mb[e]);
+        const f32x4 sm = __builtin_bit_cast(f32x4, smv), sl = __builtin_bit_cast(f32x4, slv),
+                    sd = __builtin_bit_cast(f32x4, sdv);
+        bool anym = kany;
+        if constexpr (RM) {
+          // the tile's 16 queries x the wave's 16 keys all masked, for rows that each have an
+          // unmasked key elsewhere: P = dS = 0 exactly (the streaming chunk mask's future chunks)
+          const bool any_zero = mb[0] == 0u || mb[1] == 0u || mb[2] == 0u || mb[3] == 0u;
+          const bool dead_row = sm[0] <= -1e38f || sm[1] <= -1e38f || sm[2] <= -1e38f || sm[3] <= -1e38f;
+          if (__builtin_amdgcn_ballot_w64(any_zero || dead_row) == 0) {
+            lgkm0();  // the window reads issued above land before their registers are reused
+            if constexpr (RP)
+#pragma unroll
+              for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bw[0][ks]); keep(bw[1][ks]); }
+            p2[u] = zero4();
+            ds2[u] = zero4();
+            continue;
+          }
+          anym = __builtin_amdgcn_ballot_w64((mb[0] | mb[1] | mb[2] | mb[3]) != 0u) != 0;
+        }
         f32x4 sc = zero4(), dp = zero4();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -866,15 +1019,30 @@ __global__ __launch_bounds__(NW * 64, 1) void flash_bwd_kv_kernel(FlashP a, bf16
             bd[e] = v[e];
           }
         }
-        const f32x4 sm = __builtin_bit_cast(f32x4, smv), sl = __builtin_bit_cast(f32x4, slv),
-                    sd = __builtin_bit_cast(f32x4, sdv);
+        // packed fp32 pairs (the same roundings per element); masking only where the wave's
+        // tile has a masked score (uniform)
+        const lasr_f2 c2v = {c2, c2};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = (sc[e] + bd[e]) * c2;
-          if (RM ? mb[e] != 0u : kmasked) x = -1e38f;
-          const float p = __builtin_amdgcn_exp2f(x - sm[e]) * sl[e];
-          p2[u][e] = p;
-          ds2[u][e] = x > -1e38f ? p * (dp[e] - sd[e]) : 0.f;
+        for (int e = 0; e < 4; e += 2) {
+          lasr_f2 x = {sc[e], sc[e + 1]};
+          x = (x + (lasr_f2){bd[e], bd[e + 1]}) * c2v;
+          if (anym) {
+            if (RM ? mb[e] != 0u : kmasked) x[0] = -1e38f;
+            if (RM ? mb[e + 1] != 0u : kmasked) x[1] = -1e38f;
+          }
+          lasr_f2 pv = x - (lasr_f2){sm[e], sm[e + 1]};
+          pv[0] = __builtin_amdgcn_exp2f(pv[0]);
+          pv[1] = __builtin_amdgcn_exp2f(pv[1]);
+          pv *= (lasr_f2){sl[e], sl[e + 1]};
+          const lasr_f2 dsv = pv * ((lasr_f2){dp[e], dp[e + 1]} - (lasr_f2){sd[e], sd[e + 1]});
+          p2[u][e] = pv[0];
+          p2[u][e + 1] = pv[1];
+          ds2[u][e] = dsv[0];
+          ds2[u][e + 1] = dsv[1];
+          if (anym) {
+            if (!(x[0] > -1e38f)) ds2[u][e] = 0.f;
+            if (!(x[1] > -1e38f)) ds2[u][e + 1] = 0.f;
+          }
         }
       }
       // dV^T += dO^T P, dK^T += Qu^T dS (queries of the pair as k: 32rs + 4g + e, then + 16)
@@ -932,12 +1100,15 @@ void launch_fwd_t(const FlashP& a, hipStream_t st) {
   flash_fwd_kernel<DK, NW, RP, RM><<<grid, NW * 64, 0, st>>>(a);
 }
 
-// RP: the encoder's relative-position attention (8 waves, 128 queries per workgroup); plain:
+// RP: the encoder's relative-position attention (8 waves, 128 queries per workgroup; 4 waves at d_k 32); plain:
 // the decoder's (4 waves, 64 queries: Tq = L + 1 is short)
 void launch_flash_fwd(const FlashP& a, int dk, bool rp, bool rm, hipStream_t st) {
   if (rp) {
+    // d_k 32: 4-wave workgroups (62 KB of LDS: two per CU, whose block loops and prologues
+    // interleave; 47 -> 43.6 us at config 4's shape, profiles/r04/attn_nw.jsonl); d_k 64 keeps 8
+    // waves (its 4-wave workgroup needs 95 KB: one per CU, 15 -> 25 us at config 2's)
     if (dk == 64) rm ? launch_fwd_t<64, 8, true, true>(a, st) : launch_fwd_t<64, 8, true, false>(a, st);
-    else rm ? launch_fwd_t<32, 8, true, true>(a, st) : launch_fwd_t<32, 8, true, false>(a, st);
+    else rm ? launch_fwd_t<32, 4, true, true>(a, st) : launch_fwd_t<32, 4, true, false>(a, st);
     return;
   }
   if (dk == 64) rm ? launch_fwd_t<64, 4, false, true>(a, st) : launch_fwd_t<64, 4, false, false>(a, st);

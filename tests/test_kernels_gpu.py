@@ -615,10 +615,13 @@ def test_attn_softmax(relpos):
 @pytest.mark.parametrize("B,H,T,masking,dk", [(2, 2, 37, "pad", 64), (3, 4, 130, "pad", 64), (2, 4, 249, "pad", 64),
                                                (2, 2, 100, "chunk", 64), (2, 1, 64, "none", 64), (1, 1, 1, "none", 64),
                                                (2, 16, 249, "chunk", 32), (3, 3, 70, "pad", 32),
-                                               (2, 4, 999, "pad", 64), (2, 16, 500, "chunk", 32)])
+                                               (2, 4, 999, "pad", 64), (2, 16, 500, "chunk", 32),
+                                               (3, 4, 200, "chunk", 32), (3, 2, 300, "chunk", 64)])
 def test_relattn_fused(B, H, T, masking, dk):
-    """attn_fused.hip fwd + bwd vs the literal reference chain (attention.py:120-154) in fp64 on
-    the same bf16-rounded operands; one utterance fully masked when masking == "pad"."""
+    """attn_flash.hip fwd + bwd vs the literal reference chain (attention.py:120-154) in fp64 on
+    the same bf16-rounded operands; one utterance fully masked when masking == "pad" or (B = 3)
+    "chunk" (the kernels skip the chunk mask's fully masked blocks only for rows that have an
+    unmasked key: a fully masked row keeps its uniform attention)."""
     kn = K()
     torch.manual_seed(T)
     d = dk * H
@@ -634,7 +637,7 @@ def test_relattn_fused(B, H, T, masking, dk):
         mask = (torch.arange(T)[None, :] >= xl[:, None]).to(torch.uint8).contiguous()  # (B, T)
         msb, msq, m4 = T, 0, mask.bool()[:, None, None, :]
     elif masking == "chunk":
-        xl = torch.tensor([T, T - 17][:B])
+        xl = torch.tensor([T, T - 17, 0][:B])
         pad = torch.arange(T)[None, :] >= xl[:, None]
         tri = (torch.arange(T)[None, :] // 16) > (torch.arange(T)[:, None] // 16)
         mask = (pad[:, None, :] | tri[None]).to(torch.uint8).contiguous()  # (B, T, T)

@@ -18,6 +18,14 @@ for s in "$@"; do
            "tests/test_kernels_gpu.py::test_gemm_ksub2_bit_identical" -s > "$OUT/new.log" 2>&1 ;;
     attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
     attnbench) run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_bench.jsonl" 2> "$OUT/attn_bench.err" ;;
+    attnab) # attention kernels: the library in ab/ (same ABI) vs the tree's, alternating
+           for v in base new base new; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=$R/ab/libliteasr_hip_base.so
+             LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
+             sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_ab_$v.tmp" >> "$OUT/attn_ab.jsonl"; rm -f "$OUT/attn_ab_$v.tmp"; done ;;
+    stepab) # whole step: the library in ab/ (same ABI) vs the tree's, alternating (AB_ARGS: e.g. --config large)
+           for v in base new base new; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=$R/ab/libliteasr_hip_base.so
+             LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/step_ab_$v.json" 2> "$OUT/step_ab_$v.err"
+             grep "^{" "$OUT/step_ab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'utt_s': d['value']}))" >> "$OUT/step_ab.jsonl"; done ;;
     attnprof) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/attn_trace" -o run -- python3 "$R/tools/attn_bench.py" > "$OUT/attn_trace.log" 2>&1
            cp "$(find "$OUT/attn_trace" -name '*kernel_stats.csv' | head -1)" "$OUT/attn_kernel_stats.csv"; rm -rf "$OUT/attn_trace"
            S1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_INSTS_VALU"
