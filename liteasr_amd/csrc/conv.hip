@@ -435,11 +435,30 @@ __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const T* __restrict
   st[2 * C + cc] = M2;
 }
 
+// the dy window: 8 values per access, stored as channel pairs (dw_window's pairing)
+template <typename TD>
+struct DyWin {
+  LASR_DEV void load8(const TD* row, int ce, float* v, float* u) const {
+    ldv<8>(row + ce, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = 0.f;
+  }
+  LASR_DEV void load2(const TD* row, int ce, float* v, float* u) const {
+    ldv<2>(row + ce, v);
+    u[0] = u[1] = 0.f;
+  }
+  LASR_DEV float2 pair(const float* v, const float*) const { return make_float2(v[0], v[1]); }
+};
+
+// Backward of y = dwconv(GLU(z1)) over the block's DW_TT rows x 128 channels: dW / db partials
+// (dy x the GLU window), dg = the transposed conv of dy, dz1 = GLU'(z1) dg.  The two windows
+// (GLU recomputed, dy) come in with 8-channel loads (dw_window); dg is staged through LDS so
+// the z1 re-read and the dz1 stores are 16-B row vectors (8 channels of a and of the gate).
 template <typename T, typename TD>
 __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict__ z1,
                                                              const TD* __restrict__ dy, int T_,
                                                              int C, const float* w, T* dz1,
-                                                             float* part) {
+                                                             float* part, int vec) {
   __shared__ float sp[DW_G][DW_K + 1][2 * DW_CP];
   const int cp = threadIdx.x % DW_CP, grp = threadIdx.x / DW_CP;
   const int c = (blockIdx.y * DW_CP + cp) * 2;
@@ -449,19 +468,8 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
   // the block's GLU and dy windows (DW_TT + halo rows x 128 channels), loaded once
   __shared__ float2 wg[DW_WIN][DW_CP], wd[DW_WIN][DW_CP];
   const int tb = t0 - grp * DW_R;
-  for (int e = threadIdx.x; e < DW_WIN * DW_CP; e += 256) {
-    const int rr = e / DW_CP, cq = e % DW_CP, t = tb - DW_P + rr, ce = (blockIdx.y * DW_CP + cq) * 2;
-    float2 gv = make_float2(0.f, 0.f), dv2 = make_float2(0.f, 0.f);
-    if (ce < C && t >= 0 && t < T_) {
-      const int64_t r = (int64_t)b * T_ + t;
-      gv = glu2(z1 + r * 2 * C, C, ce);
-      float dv[2];
-      ldv<2>(dy + r * C + ce, dv);
-      dv2 = make_float2(dv[0], dv[1]);
-    }
-    wg[rr][cq] = gv;
-    wd[rr][cq] = dv2;
-  }
+  dw_window<DW_CP>(z1, 2 * (int64_t)C, 0, b, T_, C, tb, vec != 0, wg, GluWin<T>{C});
+  dw_window<DW_CP>(dy, (int64_t)C, 0, b, T_, C, tb, vec != 0, wd, DyWin<TD>{});
   __syncthreads();
   float2 g[DW_RW], d[DW_RW];
 #pragma unroll
@@ -469,6 +477,8 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
     g[i] = wg[grp * DW_R + i][cp];
     d[i] = wd[grp * DW_R + i][cp];
   }
+  __syncthreads();  // wd is reused below as the dg tile
+  float* dgs = reinterpret_cast<float*>(&wd[0][0]);  // [DW_TT][2 * DW_CP] fp32
   float dw0[DW_K], dw1[DW_K], db0 = 0.f, db1 = 0.f;
 #pragma unroll
   for (int k = 0; k < DW_K; ++k) { dw0[k] = 0.f; dw1[k] = 0.f; }
@@ -492,15 +502,42 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
           dg0 += w0[k] * d[i + 2 * DW_P - k].x;
           dg1 += w1[k] * d[i + 2 * DW_P - k].y;
         }
-        const int64_t r = (int64_t)b * T_ + t;
-        float a[2], gt[2];
-        ldv<2>(z1 + r * 2 * C + c, a);
-        ldv<2>(z1 + r * 2 * C + C + c, gt);
-        const float s0 = sigmoidf_(gt[0]), s1 = sigmoidf_(gt[1]);
-        const float da[2] = {dg0 * s0, dg1 * s1};
-        const float dgt[2] = {dg0 * a[0] * s0 * (1.f - s0), dg1 * a[1] * s1 * (1.f - s1)};
-        stv<2>(dz1 + r * 2 * C + c, da);
-        stv<2>(dz1 + r * 2 * C + C + c, dgt);
+        *(float2*)(dgs + (grp * DW_R + i) * 2 * DW_CP + 2 * cp) = make_float2(dg0, dg1);
+      }
+    }
+  }
+  __syncthreads();
+  // dz1 = [dg * s | dg * a * s * (1 - s)], 8 channels per item: DW_TT rows x 16 channel octets
+  {
+    constexpr int OCT = 2 * DW_CP / 8;
+    for (int e = threadIdx.x; e < DW_TT * OCT; e += 256) {
+      const int rr = e / OCT, q = e % OCT, t = tb + rr, ce = blockIdx.y * 2 * DW_CP + q * 8;
+      if (t >= T_ || ce >= C) continue;
+      const int64_t r = (int64_t)b * T_ + t;
+      const float* dgr = dgs + rr * 2 * DW_CP + q * 8;
+      if (vec) {
+        float a[8], gt[8], da[8], dgt[8];
+        ldv<8>(z1 + r * 2 * C + ce, a);
+        ldv<8>(z1 + r * 2 * C + C + ce, gt);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float s = sigmoidf_(gt[k]), dg = dgr[k];
+          da[k] = dg * s;
+          dgt[k] = dg * a[k] * s * (1.f - s);
+        }
+        stv<8>(dz1 + r * 2 * C + ce, da);
+        stv<8>(dz1 + r * 2 * C + C + ce, dgt);
+      } else {
+        for (int k = 0; k < 8 && ce + k < C; k += 2) {
+          float a[2], gt[2];
+          ldv<2>(z1 + r * 2 * C + ce + k, a);
+          ldv<2>(z1 + r * 2 * C + C + ce + k, gt);
+          const float s0 = sigmoidf_(gt[0]), s1 = sigmoidf_(gt[1]);
+          const float da[2] = {dgr[k] * s0, dgr[k + 1] * s1};
+          const float dgt[2] = {dgr[k] * a[0] * s0 * (1.f - s0), dgr[k + 1] * a[1] * s1 * (1.f - s1)};
+          stv<2>(dz1 + r * 2 * C + ce + k, da);
+          stv<2>(dz1 + r * 2 * C + C + ce + k, dgt);
+        }
       }
     }
   }
@@ -929,7 +966,8 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
   LASR_CHECK_ARG(C % 2 == 0, "lasr_glu_dwconv_bwd: C must be even");
   dim3 g((unsigned)nparts, (unsigned)cdiv(C, 2 * DW_CP));
   hipStream_t st = (hipStream_t)stream;
-#define GB(TT, TD) glu_dwconv_bwd_kernel<TT, TD><<<g, 256, 0, st>>>((const TT*)z1, (const TD*)dy, T, C, w, (TT*)dz1, ws)
+  const int vec = C % 8 == 0 && ((uintptr_t)z1 & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dz1 & 15) == 0;
+#define GB(TT, TD) glu_dwconv_bwd_kernel<TT, TD><<<g, 256, 0, st>>>((const TT*)z1, (const TD*)dy, T, C, w, (TT*)dz1, ws, vec)
   if (dt == LASR_F32 && dydt == LASR_F32) GB(float, float);
   else if (dt == LASR_F32) GB(float, bf16_t);
   else if (dydt == LASR_F32) GB(bf16_t, float);

@@ -898,6 +898,36 @@ def test_conformer_conv_module_pieces(dtype, Cc, T):
     close(db, gb2, 1e-5, "dwconv db")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Cc,T,offset", [(66, 50, 0), (64, 41, 2)])
+def test_glu_dwconv_unvectorised(dtype, Cc, T, offset):
+    """The GLU + depthwise kernels' 2-channel path: C not a multiple of 8, or rows not 16-B
+    aligned (a view starting 2 elements into its buffer), against fp64."""
+    kn = K()
+    B, Kk = 2, 15
+    z1 = torch.randn(B * T * 2 * Cc + offset, device=DEV).to(dtype)[offset:].view(B, T, 2 * Cc)
+    w = torch.randn(Cc, Kk, device=DEV) * 0.2
+    bias = torch.randn(Cc, device=DEV) * 0.1
+    y = torch.empty(B, T, Cc, device=DEV, dtype=dtype)
+    stats = torch.empty(kn.dwconv_nparts(B, T) * 3 * Cc, device=DEV)
+    kn.glu_dwconv_fwd(z1, B, T, Cc, Kk, w, bias, y, stats)
+    zr = z1.double().requires_grad_()
+    wr = w.double().requires_grad_()
+    br = bias.double().requires_grad_()
+    yr = F.conv1d(F.glu(zr.transpose(1, 2), dim=1), wr.unsqueeze(1), br, padding=(Kk - 1) // 2, groups=Cc)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    close(y, yr.transpose(1, 2), tol, "dwconv fwd")
+    dy = torch.randn(B, T, Cc, device=DEV)
+    dz1 = torch.empty(B * T * 2 * Cc + offset, device=DEV, dtype=dtype)[offset:].view(B, T, 2 * Cc)
+    dw = torch.zeros(Cc, Kk, device=DEV)
+    db = torch.zeros(Cc, device=DEV)
+    kn.glu_dwconv_bwd(z1, dy, B, T, Cc, Kk, w, dz1, dw, db)
+    gz, gw2, gb2 = torch.autograd.grad(yr, (zr, wr, br), dy.double().transpose(1, 2))
+    close(dz1, gz, tol, "dwconv dz1")
+    close(dw, gw2, 1e-5 if dtype == torch.float32 else 1e-2, "dwconv dw")
+    close(db, gb2, 1e-5, "dwconv db")
+
+
 # ------------------------------------------------------------------ elementwise
 def test_embed_pe_and_prep():
     kn = K()
