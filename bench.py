@@ -243,8 +243,8 @@ def roofline_case(cfgd, dev):
     bytes_ = sum(2.0 * (a.numel() + b.numel()) + 4.0 * c.numel() for a, b, c, _ in probs)
     tm, tn = q[0][0]
     # the group key is the planner's family; lasr_gemm_dw_group (gemm.hip) runs the FFN-sized
-    # family on 8-wave 256 x 128 tiles unless LASR_DW_WIDE=0
-    if (tm, tn) == (128, 128) and os.environ.get("LASR_DW_WIDE", "1") != "0":
+    # family on 8-wave 256 x 128 tiles
+    if (tm, tn) == (128, 128):
         kname = "gemm_dw_group_kernel<256, 128, 3, 1, 8>"
     else:
         S, minb = {(64, 64): (3, 3), (128, 128): (2, 2)}[(tm, tn)]

@@ -173,7 +173,7 @@ FUSED_RELATTN = True
 
 
 def fused_relattn(adt, dk, p_att):
-    """The fused kernels (attn_fused.hip) cover bf16, d_k 32 or 64, no attention dropout
+    """The fused kernels (attn_flash.hip) cover bf16, d_k 32 or 64, no attention dropout
     (the my_U2 preset); other shapes take the materialised-score kernels."""
     return FUSED_RELATTN and adt == torch.bfloat16 and dk in (32, 64) and p_att == 0.0
 
@@ -222,7 +222,7 @@ def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None, po
     qv = _e((M, d), adt, dev)
     K.qbias_fwd(qkv, B, T, H, dk, w.u, w.v, qu, qv)
     if fused_relattn(adt, dk, p_att):
-        # scores never materialised (attn_fused.hip); row stats kept for the backward
+        # scores never materialised (attn_flash.hip); row stats kept for the backward
         stats = _e((B * H * T * 2,), F32, dev)
         ctx = _e((M, d), adt, dev)
         K.relattn_fwd(qu, qv, qkv[:, d:2 * d], qkv[:, 2 * d:], p, B, H, T, env.mask, env.msb, env.msq,
@@ -307,7 +307,7 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att, lnb=None):
 
 
 # ============================================================ plain MHA =========
-# Decoder attention on the fused kernels (attn_fused.hip, lasr_attn_fwd/bwd: the relative-
+# Decoder attention on the fused kernels (attn_flash.hip, lasr_attn_fwd/bwd: the relative-
 # position kernels without the positional term, Tq queries x Tk keys): scores / softmax /
 # P.V (3 launches forward, 5 backward) become 1 + 2 launches, for the self attention (causal +
 # padding mask) and the source attention over the encoder output (key padding).

@@ -18,7 +18,7 @@ accumulation and the rare element whose fp32 value straddles a bf16 rounding bou
         tensor handed to the next kernel);
   ActGate  Swish / ReLU whose backward multiplies by the STORED bf16 gate act'(u) and
         rounds the product (nets/functional.py ffn_forward / ffn_backward);
-  FlashAttn  the fused attention kernels (csrc/attn_fused.hip): 64-key blocks with the
+  FlashAttn  the fused attention kernels (csrc/attn_flash.hip): 64-key blocks with the
         online softmax, P rounded to bf16 before P.V, ctx rounded; backward recomputes P
         from the forward's row statistics, D = rowsum(dctx * ctx) on the rounded tensors,
         dS rounded before the dQ / dK / dBD products, P rounded before dV.
@@ -124,7 +124,7 @@ def _relshift_index(T):
 
 
 class FlashAttn(torch.autograd.Function):
-    """Scaled dot-product attention as csrc/attn_fused.hip computes it (relative-position
+    """Scaled dot-product attention as csrc/attn_flash.hip computes it (relative-position
     term when p is given: liteasr/nets/attention.py:120-154; plain: :61-71).
     qu, qv (B,H,T,dk), k, v (B,H,Tk,dk), p (H,T,dk) or None, mask bool (B,1|T,Tk) True =
     masked (-1e38, attention.py:54).  Returns ctx (B,H,T,dk), bf16-rounded."""

@@ -97,7 +97,7 @@ def test_conformer_layer_node_config4():
     """The same node at BASELINE config 4's layer shape: d 512, 16 heads (d_k 32), ff 2048, the
     dynamic-chunk streaming mask at chunk 16 (liteasr/utils/mask.py:30-90 triangle_mask with
     stage 16, OR the key padding), B 32 x T' 249 (liteasr/nets/attention.py:120-154 with the
-    query-dependent mask staged per block pair in attn_fused.hip)."""
+    query-dependent mask staged per block pair in attn_flash.hip)."""
     cfg = O.default_cfg(enc_dim=512, enc_heads=16, enc_ff=2048, enc_layers=1, dec_dim=512, dec_heads=16,
                         dec_ff=2048, dec_layers=1)
     _conformer_node(cfg, chunk=16, seed=61)

@@ -1,7 +1,7 @@
 """Time lasr_conv2_gemm (fwd / dW / dX) at a config's subsampling size and print hashes of
-the outputs, so two processes with different LASR_CONV_WIDE settings can be compared bit for
+the outputs, so two processes (e.g. two library builds via LITEASR_HIP_LIB) can be compared bit for
 bit (forward and data gradient: same k order per output, so equal hashes are expected).
-Usage: LASR_CONV_WIDE=0|1 python tools/conv2_bench.py [B T F C]"""
+Usage: python tools/conv2_bench.py [B T F C]"""
 import hashlib
 import json
 import os
@@ -47,7 +47,7 @@ def h(t):
     return hashlib.sha256(t.contiguous().view(torch.uint8).cpu().numpy().tobytes()).hexdigest()[:16]
 
 
-out = {"wide": os.environ.get("LASR_CONV_WIDE", "1"), "shape": [B, T1, F1, C], "gflop": round(flop / 1e9, 1)}
+out = {"lib": os.environ.get("LITEASR_HIP_LIB", "tree"), "shape": [B, T1, F1, C], "gflop": round(flop / 1e9, 1)}
 out["fwd_us"] = timeit(lambda: K.conv2_fwd(y1, w2p, b2, y2))
 out["dx_us"] = timeit(lambda: K.conv2_dx(dy2, w2p, y1, dy1))
 

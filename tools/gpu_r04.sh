@@ -19,12 +19,13 @@ for s in "$@"; do
     attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
     attnbench) run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_bench.jsonl" 2> "$OUT/attn_bench.err" ;;
     attnab) # attention kernels: the library in ab/ (same ABI) vs the tree's, alternating
-           for v in base new base new; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=$R/ab/libliteasr_hip_base.so
+           for v in base new base new; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=$R/ab_prev/liteasr_amd/lib/libliteasr_hip.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_ab_$v.tmp" >> "$OUT/attn_ab.jsonl"; rm -f "$OUT/attn_ab_$v.tmp"; done ;;
-    stepab) # whole step: the library in ab/ (same ABI) vs the tree's, alternating (AB_ARGS: e.g. --config large)
-           for v in base new base new; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=$R/ab/libliteasr_hip_base.so
-             LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/step_ab_$v.json" 2> "$OUT/step_ab_$v.err"
+    stepab) # whole step: the previous commit's tree (ab_prev/: `git archive` + its built library) vs this
+           # tree, alternating (AB_ARGS: e.g. --config large)
+           for v in base new base new; do d=$R; [ $v = base ] && d=$R/ab_prev
+             (cd $d && run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-}) > "$OUT/step_ab_$v.json" 2> "$OUT/step_ab_$v.err" || exit 1
              grep "^{" "$OUT/step_ab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'utt_s': d['value']}))" >> "$OUT/step_ab.jsonl"; done ;;
     attnprof) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/attn_trace" -o run -- python3 "$R/tools/attn_bench.py" > "$OUT/attn_trace.log" 2>&1
            cp "$(find "$OUT/attn_trace" -name '*kernel_stats.csv' | head -1)" "$OUT/attn_kernel_stats.csv"; rm -rf "$OUT/attn_trace"
@@ -42,7 +43,9 @@ for s in "$@"; do
     large) run timeout -k 10 400 python3 bench.py --config large --no-cpu-baseline > "$OUT/bench_large.json" 2> "$OUT/bench_large.err" ;;
     ddp1) run timeout -k 10 300 python3 bench.py --force-ddp --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1.json" 2> "$OUT/bench_ddp1.err" ;;
     ddp1n) run timeout -k 10 300 python3 bench.py --force-ddp --comm native --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1_native.json" 2> "$OUT/bench_ddp1_native.err" ;;
-    kg) run timeout -k 10 300 $PYT tests/test_kernels_gpu.py -k "kgroups or ksub2" > "$OUT/kg.log" 2>&1 ;;
+    tracefam) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_family" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 50 --roofline-case family > "$OUT/trace_family.log" 2>&1
+           grep "^{" "$OUT/trace_family.log" | tail -1 > "$OUT/trace_family_meta.json"
+           run python3 "$R/tools/family_trace.py" "$(find "$OUT/trace_family" -name '*.db' | head -1)" "$OUT/trace_family_meta.json" > "$OUT/family_trace_summary_${PMC_CONFIG:-small}.json"; rm -rf "$OUT/trace_family" ;;
     tileab) run timeout -k 10 200 python3 tools/tile_ab.py > "$OUT/tile_ab.jsonl" 2> "$OUT/tile_ab.err" ;;
     blaslt) run timeout -k 10 120 python3 tools/blaslt_ref.py > "$OUT/blaslt.jsonl" 2> "$OUT/blaslt.err" ;;
     trace) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace.log" 2>&1
