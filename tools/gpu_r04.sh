@@ -60,7 +60,7 @@ for s in "$@"; do
            cd /tmp && run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$c" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 20 --roofline-case $c > "$OUT/pmc_fetch_$c.log" 2>&1
            run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$c" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 20 --roofline-case $c > "$OUT/pmc_write_$c.log" 2>&1
            grep "^{" "$OUT/pmc_fetch_$c.log" | tail -1 > "$OUT/roofline_meta_$c.json"
-           run python3 "$R/tools/pmc_traffic.py" "$(find "$OUT/pmc_fetch_$c" -name '*.db' | head -1)" "$(find "$OUT/pmc_write_$c" -name '*.db' | head -1)" "$OUT/roofline_meta_$c.json" "$OUT/roofline_pmc_$c.json"
+           run python3 "$R/tools/pmc_traffic.py" "$(find "$OUT/pmc_fetch_$c" -name '*.db' | head -1)" "$(find "$OUT/pmc_write_$c" -name '*.db' | head -1)" "$OUT/roofline_meta_$c.json" "$OUT/roofline_pmc_${c}_${PMC_CONFIG:-small}.json"
            rm -rf "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c"
          done ;;
     mfma) cd /tmp && run timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --graph off --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > "$OUT/pmc_mfma.log" 2>&1
