@@ -689,7 +689,26 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
       // inverse rel_shift: the bd entry each score read (none for j == i + 1).  A lane's 4 keys
       // of a tile land on 4 consecutive columns of one dBD row unless they straddle the
       // diagonal or T: 2 or 3 stores (by column parity; ldS is even) instead of 4.
-      if (iq < T) {
+      // A block entirely below the wave's diagonal band (or above it) and inside T -- every
+      // block but the one or two around the diagonal -- takes one uniform path: 4 16-bit
+      // stores per tile and lane, no per-lane parity or straddle branches.
+      bf16_t* const rowL = dbd + (int64_t)iq * a.ldS + (T - 1 - iq);  // + j for j <= iq
+      bf16_t* const rowU = dbd + (int64_t)(iq + 1) * a.ldS - (iq + 2);  // + j for j >= iq + 2
+      const bool below = j0 + KB - 1 <= iw, above = j0 >= iw + 17;
+      if (j0 + KB <= T && (below || above)) {
+        if (iq < T) {
+          bf16_t* const row = above ? rowU : rowL;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const uint32_t w01 = pk_bf16(s[c][0], s[c][1]), w23 = pk_bf16(s[c][2], s[c][3]);
+            bf16_t* d = row + (j0 + 16 * c + 4 * g);
+            d[0] = (bf16_t)w01;
+            d[1] = (bf16_t)(w01 >> 16);
+            d[2] = (bf16_t)w23;
+            d[3] = (bf16_t)(w23 >> 16);
+          }
+        }
+      } else if (iq < T) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int ja = j0 + 16 * c + 4 * g;  // first of the 4 keys
