@@ -303,6 +303,133 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
     g[c] = from_f<TG>(gs * (__expf(to_f(x[c]) - l) - gamma_of(c)));
 }
 
+// ---- the lattice with its emissions staged in LDS ---------------------------------------
+// The block kernel above syncs each time step with __syncthreads(), a workgroup release fence
+// that waits for every outstanding global access of the thread -- the step's alpha/beta store
+// and the emission prefetch of the step CTC_PF ahead -- so each of the T' serial steps pays a
+// memory round trip.  Here the emissions of CTC_CH steps are copied into LDS once per chunk
+// (registers loaded at the chunk's start, written to LDS at its end, off the step chain), a
+// step reads its emission from LDS, and the step barrier waits for LDS only; the alpha/beta
+// stores drain in the background.  Per state the arithmetic is the block kernel's, in the same
+// order: alpha, beta and nll are unchanged.
+constexpr int CTC_CH = 32;   // time steps per emission chunk
+constexpr int CTC_CHR = 17;  // chunk registers per thread: CTC_CH * ld / blockDim <= 17 (blockDim >= 2 ld - 1)
+
+LASR_DEV void lds_step_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// dir = +1: alpha (t = 0 .. Tb-1), -1: beta (t = Tb-1 .. 0)
+template <int DIR>
+LASR_DEV void ctc_lattice_chunked(int b, int T_, int Lmax, const int32_t* __restrict__ targets, const int32_t* ilen,
+                                  const int32_t* tlen, const float* lp, float* out, float* nll) {
+  extern __shared__ float sh[];
+  const int Tb = ilen[b], Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
+  if (Tb <= 0) {
+    if (DIR > 0 && threadIdx.x == 0) nll[b] = (Lb == 0) ? 0.f : INFINITY;
+    return;
+  }
+  const int32_t* tg = targets + (int64_t)b * Lmax;
+  const int s = threadIdx.x, nt = blockDim.x;
+  const bool act = s < S;
+  const bool skip = DIR > 0 ? act && s >= 2 && (s & 1) && ext_label(tg, s) != ext_label(tg, s - 2)
+                            : act && s + 2 < S && (s & 1) && ext_label(tg, s) != ext_label(tg, s + 2);
+  const int eix = (s & 1) ? 1 + (s >> 1) : 0;
+  const int ld = Lmax + 1;
+  const float* lpu = lp + (int64_t)b * T_ * ld;  // the utterance's [T_][ld] emissions
+  const int64_t last = (int64_t)T_ * ld - 1;
+  float* o = out + (int64_t)b * T_ * Smax;
+  float* buf0 = sh;
+  float* buf1 = sh + Smax;
+  float* chunk = sh + 2 * Smax;  // [CTC_CH][ld]: rows r0 .. r0 + CTC_CH - 1
+  const int CHN = CTC_CH * ld;
+  const int t_first = DIR > 0 ? 0 : Tb - 1;
+  if (act) {
+    const float e = lpu[(int64_t)t_first * ld + eix];
+    const float v = DIR > 0 ? (s <= 1 ? e : -INFINITY) : (s >= S - 2 ? e : -INFINITY);
+    buf0[s] = v;
+    o[(int64_t)t_first * Smax + s] = v;
+  }
+  // chunk c holds the emissions of steps i = 1 + c CTC_CH .. (step i: t = t_first + DIR i);
+  // its first row r0 = the lowest t of the chunk
+  const int nsteps = Tb - 1;
+  auto row0 = [&](int c) {
+    const int i_lo = 1 + c * CTC_CH, i_hi = min(i_lo + CTC_CH - 1, nsteps);
+    return DIR > 0 ? t_first + i_lo : t_first - i_hi;
+  };
+  float pre[CTC_CHR];
+  auto load_regs = [&](int c) {
+    const int64_t base = (int64_t)row0(c) * ld;
+#pragma unroll
+    for (int r = 0; r < CTC_CHR; ++r) {
+      const int idx = r * nt + s;
+      pre[r] = idx < CHN ? lpu[min(base + idx, last)] : 0.f;
+    }
+  };
+  auto store_regs = [&]() {
+#pragma unroll
+    for (int r = 0; r < CTC_CHR; ++r) {
+      const int idx = r * nt + s;
+      if (idx < CHN) chunk[idx] = pre[r];
+    }
+  };
+  const int nchunks = (nsteps + CTC_CH - 1) / CTC_CH;
+  if (nchunks > 0) {
+    load_regs(0);
+    store_regs();
+  }
+  __syncthreads();
+  float* prev = buf0;
+  float* cur = buf1;
+  for (int c = 0; c < nchunks; ++c) {
+    if (c + 1 < nchunks) load_regs(c + 1);  // lands during this chunk's steps
+    const int r0 = row0(c), i_lo = 1 + c * CTC_CH, i_hi = min(i_lo + CTC_CH - 1, nsteps);
+    for (int i = i_lo; i <= i_hi; ++i) {
+      const int t = t_first + DIR * i;
+      if (act) {
+        const float e = chunk[(t - r0) * ld + eix];
+        float v;
+        if (DIR > 0) {
+          const float a0 = prev[s];
+          const float a1 = s >= 1 ? prev[s - 1] : -INFINITY;
+          const float a2 = skip ? prev[s - 2] : -INFINITY;
+          v = lse3(a0, a1, a2) + e;
+        } else {
+          const float b0 = prev[s];
+          const float b1 = (s + 1 < S) ? prev[s + 1] : -INFINITY;
+          const float b2 = skip ? prev[s + 2] : -INFINITY;
+          v = lse3(b0, b1, b2) + e;
+        }
+        cur[s] = v;
+        o[(int64_t)t * Smax + s] = v;
+      }
+      lds_step_sync();
+      float* tmp = prev; prev = cur; cur = tmp;
+    }
+    if (c + 1 < nchunks) {  // every wave is past its last read of this chunk (the step barrier)
+      store_regs();
+      lds_step_sync();
+    }
+  }
+  if (DIR > 0 && threadIdx.x == 0) {
+    const float ll = (S >= 2) ? lse2(prev[S - 1], prev[S - 2]) : prev[0];
+    nll[b] = -ll;
+  }
+}
+
+__global__ void ctc_lattice_chunked_kernel(int B, int T_, int Lmax, const int32_t* __restrict__ targets,
+                                           const int32_t* ilen, const int32_t* tlen, const float* lp, float* alpha,
+                                           float* nll, float* beta, int beta_only) {
+  if (!beta_only && (int)blockIdx.x < B)
+    ctc_lattice_chunked<1>(blockIdx.x, T_, Lmax, targets, ilen, tlen, lp, alpha, nll);
+  else
+    ctc_lattice_chunked<-1>(beta_only ? blockIdx.x : blockIdx.x - B, T_, Lmax, targets, ilen, tlen, lp, beta, nullptr);
+}
+
+static size_t ctc_chunk_lds(int Lmax) { return ((size_t)2 * (2 * Lmax + 1) + (size_t)CTC_CH * (Lmax + 1)) * sizeof(float); }
+
 static int ctc_block(int S) {
   int nt = ((S + 63) / 64) * 64;
   return nt < 64 ? 64 : (nt > 1024 ? 1024 : nt);
@@ -331,6 +458,11 @@ extern "C" int lasr_ctc_lattice(int B, int T, int Lmax, const int32_t* targets, 
   LASR_CHECK_ARG(B > 0 && T > 0 && Lmax >= 0 && 2 * Lmax + 1 <= 1024, "lasr_ctc_lattice: bad sizes");
   LASR_CHECK_ARG(lp && alpha && nll, "lasr_ctc_lattice: lp / alpha / nll");
   const int Smax = 2 * Lmax + 1;
+  if (ctc_chunk_lds(Lmax) <= 64 * 1024) {
+    ctc_lattice_chunked_kernel<<<beta ? 2 * B : B, ctc_block(Smax), ctc_chunk_lds(Lmax), (hipStream_t)stream>>>(
+        B, T, Lmax, targets, ilen, tlen, lp, alpha, nll, beta, 0);
+    return lasr_check_launch("ctc_lattice");
+  }
   ctc_alpha_beta_kernel<<<beta ? 2 * B : B, ctc_block(Smax), 2 * Smax * sizeof(float), (hipStream_t)stream>>>(
       B, T, Lmax, targets, ilen, tlen, lp, alpha, nll, beta);
   return lasr_check_launch("ctc_alpha_beta");
@@ -345,7 +477,12 @@ extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, in
   LASR_CHECK_ARG(2 * Lmax + 1 <= 1024, "lasr_ctc_bwd: Lmax=%d too large", Lmax);
   hipStream_t st = (hipStream_t)stream;
   const int Smax = 2 * Lmax + 1;
-  if (!beta_ready) {
+  if (!beta_ready && ctc_chunk_lds(Lmax) <= 64 * 1024) {
+    ctc_lattice_chunked_kernel<<<B, ctc_block(Smax), ctc_chunk_lds(Lmax), st>>>(B, T, Lmax, targets, ilen, tlen, lp,
+                                                                                nullptr, nullptr, beta, 1);
+    const int rc = lasr_check_launch("ctc_beta");
+    if (rc) return rc;
+  } else if (!beta_ready) {
     ctc_beta_kernel<<<B, ctc_block(Smax), 2 * Smax * sizeof(float), st>>>(T, Lmax, targets, ilen, tlen, lp, beta);
     const int rc = lasr_check_launch("ctc_beta");
     if (rc) return rc;
