@@ -99,6 +99,35 @@ def dec_case(name, B, H, L1, dk):
                           "tflops": round(units * unit / sec / 1e12, 1)}), flush=True)
 
 
+def src_case(name, B, H, Tq, Tk, dk):
+    """The decoder's source attention: Tq = L + 1 queries over the encoder output's Tk keys
+    (key padding), plain scaled dot-product (no positional term)."""
+    dev = "cuda"
+    d = H * dk
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(3)
+    rn = lambda *s: (torch.randn(*s, device=dev, generator=g) * 0.5).to(bf)  # noqa: E731
+    q, kv, dctx = rn(B * Tq, d), rn(B * Tk, 2 * d), rn(B * Tq, d)
+    xl = torch.full((B,), Tk, device=dev)
+    xl[1::2] = Tk - 17
+    mask = (torch.arange(Tk, device=dev)[None, :] >= xl[:, None]).to(torch.uint8).contiguous()
+    scale = dk ** -0.5
+    stats = torch.empty(B * H * Tq * 2, device=dev)
+    ctx = torch.empty(B * Tq, d, dtype=bf, device=dev)
+    k, v = kv[:, :d], kv[:, d:]
+    fwd = lambda: K.attn_fwd(q, k, v, B, H, Tq, Tk, mask, Tk, 0, scale, stats, ctx)  # noqa: E731
+    Dbuf = torch.empty(B * H * Tq, device=dev)
+    dq = torch.empty(B * Tq, d, dtype=bf, device=dev)
+    dkv = torch.zeros(B * Tk, 2 * d, dtype=bf, device=dev)
+    bwd = lambda: K.attn_bwd(q, k, v, B, H, Tq, Tk, mask, Tk, 0, scale, stats, ctx, dctx, Dbuf,  # noqa: E731
+                             dq, dkv[:, :d], dkv[:, d:])
+    unit = 2.0 * B * H * Tq * Tk * dk
+    for dirn, fn, units in (("fwd", fwd, 2), ("bwd", bwd, 5)):
+        sec = graph_time(fn)
+        print(json.dumps({"case": name, "dir": dirn, "B": B, "H": H, "Tq": Tq, "Tk": Tk, "dk": dk,
+                          "us": round(sec * 1e6, 2), "tflops": round(units * unit / sec / 1e12, 1)}), flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
     sel = sys.argv[1:]
@@ -108,6 +137,10 @@ def main():
             rel_case(*c)
     if not sel or "dec" in sel:
         dec_case("dec", 32, 4, 41, 64)
+    if not sel or "src" in sel:
+        src_case("src", 32, 4, 41, 249, 64)
+    if not sel or "srclong" in sel:
+        src_case("srclong", 8, 4, 151, 999, 64)
 
 
 if __name__ == "__main__":
