@@ -348,10 +348,17 @@ int lasr_col2im3x3s2(const void* dcol, int dt, int B, int T1, int F1, int C,
  * max(roundup32(M2), M2 + 1) and rows M2.. zero (the weight-gradient k padding and the taps
  * that fall outside dy2).  C % 128 == 0, every pointer 16-B aligned.  DW splits K over
  * workgroups when the workspace holds split*(9C*C + C) floats (summed in fixed order).
- * Replaces nn.Conv2d(C, C, 3, 2)'s forward and backward at liteasr/nets/subsampling.py:42. */
+ *  LASR_CONV2_DX_W1: the data gradient of DX consumed in place by the conv1 weight gradient
+ *                  (lasr_conv1_bwd's dW1 / db1), dy1 never stored: dw1 [C, 9] += sum over
+ *                  dy1 positions of dy1 (x) the 3x3 stride-2 patch of x [B, T, F] fp32 (k = kh*3
+ *                  + kw), db1 [C] += sum of dy1.  Needs C % 256 == 0 and a workspace of
+ *                  lasr_conv2_dx_w1_workspace(B, T1, F1, C) bytes; out unused.
+ * Replaces nn.Conv2d(C, C, 3, 2)'s forward and backward at liteasr/nets/subsampling.py:42
+ * (DX_W1: also the weight gradient of the first nn.Conv2d(1, C, 3, 2) there). */
 #define LASR_CONV2_FWD 0
 #define LASR_CONV2_DW 1
 #define LASR_CONV2_DX 2
+#define LASR_CONV2_DX_W1 3
 typedef struct lasr_conv2_args {
   int mode;
   int B, T1, F1, C;
@@ -362,8 +369,13 @@ typedef struct lasr_conv2_args {
   void* out;
   float* rowsum;
   void* workspace; int64_t workspace_bytes;
+  /* LASR_CONV2_DX_W1 only */
+  const float* x; int T, F;
+  float* dw1; float* db1;
 } lasr_conv2_args;
 int lasr_conv2_gemm(const lasr_conv2_args* args, void* stream);
+/* Workspace bytes of a LASR_CONV2_DX_W1 call (per-tile partials of dw1 / db1). */
+int64_t lasr_conv2_dx_w1_workspace(int B, int T1, int F1, int C);
 /* ---- Paraformer CIF predictor (liteasr/nets/paraformer/predictor.py:24-118) ----------
  * fwd: alpha[b,t] = t < plen[b] ? sigmoid(z[b,t]) : 0; sum_alpha[b] = sum_t alpha;
  *      beta = sum_alpha / ylen - 1e-4; integrate-and-fire over t (the reference's update

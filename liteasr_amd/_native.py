@@ -59,10 +59,12 @@ class Conv2Args(C.Structure):
         ("dy2", _p), ("dy2_rows", _l),
         ("out", _p), ("rowsum", _p),
         ("workspace", _p), ("workspace_bytes", _l),
+        ("x", _p), ("T", _i), ("F", _i),
+        ("dw1", _p), ("db1", _p),
     ]
 
 
-CONV2_FWD, CONV2_DW, CONV2_DX = 0, 1, 2
+CONV2_FWD, CONV2_DW, CONV2_DX, CONV2_DX_W1 = 0, 1, 2, 3
 
 
 class CifArgs(C.Structure):
@@ -144,6 +146,7 @@ SIGNATURES = {
     "lasr_conv1_fwd": [_p, _i, _i, _i, _i, _p, _p, _p, _i, _p],
     "lasr_conv1_bwd": [_p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _l, _p],
     "lasr_conv2_gemm": [C.POINTER(Conv2Args), _p],
+    "lasr_conv2_dx_w1_workspace": [_i, _i, _i, _i],
     "lasr_cif_fwd": [C.POINTER(CifArgs), _p],
     "lasr_cif_bwd": [C.POINTER(CifArgs), _p],
     "lasr_glancing_mix": [_l, _i, _p, _p, _p, _p, _p, _i, _p],
@@ -172,6 +175,7 @@ SIGNATURES = {
     "lasr_logsoftmax_topk": [_p, _i, _l, _i, _l, _i, _p, _p, _p, _p, _p],
 }
 _RESTYPES = {"lasr_last_error": C.c_char_p, "lasr_spec_augment_ws_bytes": C.c_int64,
+             "lasr_conv2_dx_w1_workspace": C.c_int64,
              "lasr_dropout_scale": C.c_float}
 
 

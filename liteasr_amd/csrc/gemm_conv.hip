@@ -43,6 +43,7 @@ static GemmP conv_params(const lasr_conv2_args* a) {
 struct DxClasses {
   int start[5];
   int M[4], K[4];
+  int rb[4];  // DX_W1: first conv1 partial row of each class (its 128-row tiles in order)
 };
 
 template <int BN, int EPI = EPI_RT>
@@ -56,6 +57,7 @@ __global__ __launch_bounds__(256, 2) void conv2_dx_kernel(GemmP p, DxClasses c) 
   q.M = c.M[i];
   q.K = c.K[i];
   q.kchunk = c.K[i];
+  q.cv.w1rb = c.rb[i];
   const int ntx = p.N / BN, nty = (q.M + 127) / 128, ntile = ntx * nty;
   const int local = blk - c.start[i];
   if (local >= ntile) return;  // alignment padding
@@ -63,15 +65,54 @@ __global__ __launch_bounds__(256, 2) void conv2_dx_kernel(GemmP p, DxClasses c) 
   gemm_glds_tile<128, BN, true, false, bf16_t, 3, G_DX, 1, 4, EPI>(q, wg % ntx, wg / ntx, 0);
 }
 
+// The conv1 weight-gradient partials of LASR_CONV2_DX_W1 ([rows][10][C], one row per 128-row
+// tile of the four classes) summed in fixed order: groups of W1_GROUP rows here (coalesced
+// 1-KB row reads, ~800 workgroups), then the group sums by lasr_reduce_cols.
+constexpr int W1_GROUP = 64;
+__global__ __launch_bounds__(256) void w1_group_sum_kernel(const float* __restrict__ part, int P, int N,
+                                                           float* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+  if (n >= N) return;
+  const int p0 = g * W1_GROUP, p1 = min(P, p0 + W1_GROUP);
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+  for (int p = p0; p < p1; p += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p + k < p1 ? part[(int64_t)(p + k) * N + n] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] += v[k];
+  }
+  out[(int64_t)g * N + n] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+static int64_t dx_tile_rows(int B, int T1, int F1) {
+  int64_t rows = 0;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int pt = cls >> 1, pf = cls & 1;
+    rows += cdiv((int64_t)B * ((T1 - pt + 1) >> 1) * ((F1 - pf + 1) >> 1), 128);
+  }
+  return rows;
+}
+
+// partials [P][10C], group sums [cdiv(P, W1_GROUP)][10C], total [10C]
+extern "C" int64_t lasr_conv2_dx_w1_workspace(int B, int T1, int F1, int C) {
+  if (B <= 0 || T1 < 3 || F1 < 3 || C <= 0) return 0;
+  const int64_t P = dx_tile_rows(B, T1, F1);
+  return (P + cdiv(P, W1_GROUP) + 1) * 10 * (int64_t)C * 4;
+}
+
 extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   LASR_CHECK_ARG(a != nullptr, "lasr_conv2_gemm: null args");
-  LASR_CHECK_ARG(a->mode == LASR_CONV2_FWD || a->mode == LASR_CONV2_DW || a->mode == LASR_CONV2_DX,
-                 "lasr_conv2_gemm: bad mode");
+  LASR_CHECK_ARG(a->mode == LASR_CONV2_FWD || a->mode == LASR_CONV2_DW || a->mode == LASR_CONV2_DX ||
+                 a->mode == LASR_CONV2_DX_W1, "lasr_conv2_gemm: bad mode");
   LASR_CHECK_ARG(a->B > 0 && a->T1 >= 3 && a->F1 >= 3 && a->C > 0 && a->C % 128 == 0,
                  "lasr_conv2_gemm: needs B > 0, T1, F1 >= 3 and C % 128 == 0");
   LASR_CHECK_ARG((int64_t)a->B * a->T1 * a->F1 * a->C < (1LL << 31) && 9LL * a->C * a->C < (1LL << 31),
                  "lasr_conv2_gemm: tensors past 2^31 elements");
-  LASR_CHECK_ARG(a->y1 && a->out && aligned16(a->y1) && aligned16(a->out), "lasr_conv2_gemm: y1/out");
+  const bool w1 = a->mode == LASR_CONV2_DX_W1;
+  LASR_CHECK_ARG(a->y1 && aligned16(a->y1) && (w1 || (a->out && aligned16(a->out))), "lasr_conv2_gemm: y1/out");
   GemmP p = conv_params(a);
   const ConvG& g = p.cv;
   const int C = a->C;
@@ -147,16 +188,39 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   p.epi_mode = 1;
   p.cv.zero = (const bf16_t*)a->dy2 + (int64_t)g.M2 * C;
   DxClasses dc = {};
-  int nb = 0;
+  int nb = 0, rows = 0;
   for (int cls = 0; cls < 4; ++cls) {
     const int pt = cls >> 1, pf = cls & 1;
     const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
     dc.M[cls] = g.B * nI * nJ;
     dc.K[cls] = (pt ? 1 : 2) * (pf ? 1 : 2) * C;
     dc.start[cls] = nb;
+    dc.rb[cls] = rows;
+    rows += (int)cdiv(dc.M[cls], 128);
     nb += (int)(cdiv(cdiv(dc.M[cls], 128) * (C / BN), 8) * 8);
   }
   dc.start[4] = nb;
+  if (w1) {
+    // the conv1 weight gradient in the epilogue (conv1: x [B, T, F] -> y1, 3x3 stride 2)
+    LASR_CHECK_ARG(BN == 256 && epi_code(p) == EPI_AUX_RELU, "lasr_conv2_gemm/dx_w1: needs C %% 256 == 0");
+    LASR_CHECK_ARG(a->x && a->dw1 && a->db1 && a->T >= 3 && a->F >= 3 && (a->T - 3) / 2 + 1 == g.T1 &&
+                   (a->F - 3) / 2 + 1 == g.F1, "lasr_conv2_gemm/dx_w1: x [B, T, F] must give y1's T1 / F1");
+    LASR_CHECK_ARG((int64_t)g.B * a->T * a->F < (1LL << 31), "lasr_conv2_gemm/dx_w1: x past 2^31 elements");
+    const int64_t need = lasr_conv2_dx_w1_workspace(g.B, g.T1, g.F1, C);
+    LASR_CHECK_ARG(a->workspace && aligned16(a->workspace) && a->workspace_bytes >= need,
+                   "lasr_conv2_gemm/dx_w1: workspace needs %lld bytes", (long long)need);
+    p.cv.x = a->x; p.cv.T0 = a->T; p.cv.F0 = a->F;
+    p.cv.w1part = (float*)a->workspace;
+    conv2_dx_kernel<256, EPI_AUX_RELU_W1><<<nb, 256, 0, st>>>(p, dc);
+    if (int rc = lasr_check_launch("lasr_conv2_gemm/dx_w1")) return rc;
+    const int N10 = 10 * C, ng = (int)cdiv(rows, W1_GROUP);
+    float* grp = p.cv.w1part + (int64_t)rows * N10;
+    float* tot = grp + (int64_t)ng * N10;
+    w1_group_sum_kernel<<<dim3((unsigned)cdiv(N10, 256), (unsigned)ng), 256, 0, st>>>(p.cv.w1part, rows, N10, grp);
+    if (int rc = lasr_check_launch("lasr_conv2_gemm/dx_w1_groups")) return rc;
+    if (int rc = lasr_reduce_cols(grp, ng, N10, tot, nullptr, N10, 0, st)) return rc;
+    return lasr_scatter_kc(tot, 9, C, 9, a->dw1, a->db1, st);
+  }
   if (BN == 256 && epi_code(p) == EPI_AUX_RELU) conv2_dx_kernel<256, EPI_AUX_RELU><<<nb, 256, 0, st>>>(p, dc);
   else if (BN == 256) conv2_dx_kernel<256><<<nb, 256, 0, st>>>(p, dc);
   else conv2_dx_kernel<128><<<nb, 256, 0, st>>>(p, dc);

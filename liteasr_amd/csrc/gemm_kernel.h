@@ -23,6 +23,12 @@ struct ConvG {
   int cls;              // G_DX: output parity class (t1 & 1) * 2 + (f1 & 1)
   int q32, r32;         // G_DW: 32 = q32 * F2 + r32 (row-walk increments)
   const bf16_t* zero;   // G_DX: >= 32 zero bf16 (taps that fall outside dy2)
+  // G_DX with EPI_AUX_RELU_W1 (the conv1 weight gradient in the epilogue): conv1's input
+  // x [B, T0, F0] fp32, the per-tile partials [rows][10][C] and this class's first row
+  const float* x;
+  int T0, F0;
+  float* w1part;
+  int w1rb;
 };
 typedef ConvG ConvGeom;
 enum { G_LIN = 0, G_FWD = 1, G_DW = 2, G_DX = 3 };
@@ -86,7 +92,10 @@ LASR_DEV float load_any(const void* p, int dt, int64_t i) {
 // the uniform values they keep live, cost SGPR spills and ~2x the VALU of the arithmetic).
 enum {
   EPI_RT = 0, EPI_SWISH_GATE_DROP = 1, EPI_AUX_GATE = 2, EPI_PLAIN = 3, EPI_RES_DROP = 4, EPI_RELU_GATE_DROP = 5,
-  EPI_RELU = 6, EPI_AUX_RELU = 7
+  EPI_RELU = 6, EPI_AUX_RELU = 7,
+  // G_DX only: EPI_AUX_RELU's values are not stored but reduced into the conv1 weight-gradient
+  // partials of the tile (dx_w1_epilogue)
+  EPI_AUX_RELU_W1 = 8
 };
 
 template <int N, int EPI = EPI_RT, typename ZST>
@@ -131,7 +140,7 @@ LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)
 #pragma unroll
     for (int q = 0; q < N; ++q) v[q] = fmaxf(v[q], 0.f);
     return;
-  } else if constexpr (EPI == EPI_AUX_RELU) {  // * relu'(aux) (subsampling conv2 data gradient)
+  } else if constexpr (EPI == EPI_AUX_RELU || EPI == EPI_AUX_RELU_W1) {  // * relu'(aux) (conv2 data gradient)
 #pragma unroll
     for (int q = 0; q < N; ++q) v[q] *= auxv[q] > 0.f ? 1.f : 0.f;
     return;
@@ -618,6 +627,101 @@ LASR_DEV void gemm_epilogue_direct(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8
   }
 }
 
+// Epilogue of the conv2 data gradient fused with conv1's weight gradient (EPI_AUX_RELU_W1,
+// BM x 256 tiles, 4 waves): dy1 = bf16(acc) * relu'(y1) -- exactly the values the plain G_DX
+// epilogue stores -- is never written; the tile's partial of dW1 [C][9] / db1 [C] is formed
+// instead.  (1) every wave parks its accumulators as bf16 in LDS (the whole tile at once:
+// 128 x 264 bf16 + the rows' conv1 patches xr -> [BM][12] fp32, 73.7 KB, inside the ring's
+// space); (2) wave w takes rows w, w + NW, ..., lane l columns 4l..4l+3: per row one 8-B LDS
+// read of v, the row's y1 (8 B per lane, coalesced 512-B rows, all loads issued before the
+// staging), three broadcast 16-B reads of its patch, 20 packed FMAs into 40 accumulators;
+// (3) the NW waves' sums combined in fixed order through LDS into one [10][C] partial row.
+// The per-element work is ~20 VALU per 4 outputs; LDS traffic stays below it (the first,
+// LDS-bound form -- fp32 staging and a column-per-thread sum with 9 patch reads per 4 rows --
+// cost 53 us over the 343 us launch).
+template <int BM, int BN, int NW>
+LASR_DEV void dx_w1_epilogue(const GemmP& p, f32x4 (&acc)[BM / 32][BN / (8 * NW)], char* smem, int m0, int n0,
+                             const int64_t* dxrow, const float (&xr)[(9 * BM + NW * 64 - 1) / (NW * 64)]) {
+  static_assert(BN == 256 && NW == 4, "conv1 weight gradient: 4 columns per lane over a 256-column tile");
+  constexpr int NT = NW * 64, WCOLS = NW / 2;
+  constexpr int WM = BM / 2, WN = BN / WCOLS, FM = WM / 16, FN = WN / 16;
+  constexpr int LDB = BN + 8;        // bf16 row stride of the parked tile (528 B: rows 4 banks apart)
+  constexpr int RPW = BM / NW;       // rows per wave
+  constexpr int XN = (9 * BM + NT - 1) / NT;
+  static_assert(BM * LDB * 2 + BM * 12 * 4 <= 73728 && NW * 10 * BN * 4 <= BM * LDB * 2, "LDS budget");
+  bf16_t* tb = reinterpret_cast<bf16_t*>(smem);
+  float* xs = reinterpret_cast<float*>(smem + BM * LDB * 2);  // [BM][12]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WCOLS, wc = wid % WCOLS;
+  // this wave's rows of y1 (the relu' factor), in flight during the staging
+  const bf16_t* y1 = (const bf16_t*)p.aux;
+  uint2 ya[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int r = wid + NW * i;
+    ya[i] = m0 + r < p.M ? *(const uint2*)(y1 + dxrow[r] + n0 + 4 * lane) : make_uint2(0u, 0u);
+  }
+  // (the tile has passed a barrier after its last ring read; the epilogue's barriers are
+  // LDS-only, so the y1 loads stay in flight across them)
+  {
+    const int rq = (lane >> 4) * 4, cl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wr * WM + i * 16 + cl, c = wc * WN + j * 16 + rq;
+        *(uint2*)(tb + r * LDB + c) = make_uint2(pk_bf16(acc[i][j][0], acc[i][j][1]), pk_bf16(acc[i][j][2], acc[i][j][3]));
+      }
+#pragma unroll
+    for (int i = 0; i < XN; ++i) {
+      const int e = i * NT + tid;
+      if (e < 9 * BM) xs[(e / 9) * 12 + e % 9] = xr[i];
+    }
+  }
+  lds_barrier();
+  lasr_f2 w[10][2];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) w[k][0] = w[k][1] = (lasr_f2){0.f, 0.f};
+#pragma unroll  // (fully: ya[] stays in registers)
+  for (int i = 0; i < RPW; ++i) {
+    const int r = wid + NW * i;
+    const uint2 vb = *(const uint2*)(tb + r * LDB + 4 * lane);
+    const uint2 ab = ya[i];
+    // bf16 -> fp32 is exact; times relu'(y1) in {0, 1} as the store path (which rounds after
+    // the product: the same value)
+    const lasr_f2 g0 = {__uint_as_float(ab.x << 16) > 0.f ? 1.f : 0.f, __uint_as_float(ab.x & 0xffff0000u) > 0.f ? 1.f : 0.f};
+    const lasr_f2 g1 = {__uint_as_float(ab.y << 16) > 0.f ? 1.f : 0.f, __uint_as_float(ab.y & 0xffff0000u) > 0.f ? 1.f : 0.f};
+    const lasr_f2 v0 = (lasr_f2){__uint_as_float(vb.x << 16), __uint_as_float(vb.x & 0xffff0000u)} * g0;
+    const lasr_f2 v1 = (lasr_f2){__uint_as_float(vb.y << 16), __uint_as_float(vb.y & 0xffff0000u)} * g1;
+    const f32x4 xa = *(const f32x4*)(xs + r * 12), xb = *(const f32x4*)(xs + r * 12 + 4),
+                xc = *(const f32x4*)(xs + r * 12 + 8);
+    const float xv[9] = {xa[0], xa[1], xa[2], xa[3], xb[0], xb[1], xb[2], xb[3], xc[0]};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const lasr_f2 xx = {xv[k], xv[k]};
+      w[k][0] += v0 * xx;
+      w[k][1] += v1 * xx;
+    }
+    w[9][0] += v0;
+    w[9][1] += v1;
+  }
+  lds_barrier();  // the parked tile is no longer read: its space takes the wave sums
+  float* red = reinterpret_cast<float*>(smem);  // [NW][10][BN]
+#pragma unroll
+  for (int k = 0; k < 10; ++k)
+    *(f32x4*)(red + (wid * 10 + k) * BN + 4 * lane) = (f32x4){w[k][0][0], w[k][0][1], w[k][1][0], w[k][1][1]};
+  lds_barrier();
+  float* dst = p.cv.w1part + (int64_t)(p.cv.w1rb + m0 / BM) * 10 * p.N + n0 + tid;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) t += red[(q * 10 + k) * BN + tid];
+    dst[(int64_t)k * p.N] = t;
+  }
+}
+
 // ---------------- bf16 kernel, LDS-DMA pipeline (16-B aligned operands) ----------------
 // Same tiles, LDS images, fragment reads and epilogue as gemm_bf16_kernel, but every full
 // 32-deep k tile is copied HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging) into an
@@ -781,6 +885,28 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
   [[maybe_unused]] __shared__ int64_t dxrow[G == G_DX ? BM : 1];
   if constexpr (G == G_DX)
     for (int r = tid; r < BM; r += NT) dxrow[r] = dx_row(p.cv, min(m0 + r, p.M - 1));
+  // EPI_AUX_RELU_W1: the conv1 patch x[b, 2 t1 + kh, 2 f1 + kw] of every tile row (dy1 position
+  // (b, t1, f1)), loaded into registers here (in flight under the main loop) and staged for
+  // dx_w1_epilogue
+  constexpr bool W1 = G == G_DX && EPI == EPI_AUX_RELU_W1;
+  constexpr int XN = W1 ? (9 * BM + NT - 1) / NT : 1;
+  [[maybe_unused]] float xr[XN];
+  if constexpr (W1) {
+    const ConvG& g = p.cv;
+    const int pt = g.cls >> 1, pf = g.cls & 1;
+    const int nI = (g.T1 - pt + 1) >> 1, nJ = (g.F1 - pf + 1) >> 1;
+#pragma unroll
+    for (int i = 0; i < XN; ++i) {
+      const int e = i * NT + tid, r = e / 9, k = e - 9 * r;
+      xr[i] = 0.f;
+      if (e < 9 * BM) {
+        const int m = min(m0 + r, p.M - 1);
+        const int j = m % nJ, t = m / nJ, ii = t % nI, b = t / nI;
+        const int kh = k / 3, kw = k - 3 * kh;
+        xr[i] = g.x[((int64_t)b * g.T0 + 2 * (2 * ii + pt) + kh) * g.F0 + 2 * (2 * j + pf) + kw];
+      }
+    }
+  }
   if constexpr (G == G_DW) gb.init(p.cv, n0, p.N, kbeg, tid);
   // one 32-deep sub-tile at k0 into dst (the conv walkers keep per-position state: sub-tiles
   // are issued in k order)
@@ -927,6 +1053,10 @@ LASR_DEV void gemm_glds_tile(const GemmP& p, const int tx, const int ty, const i
       }
       __syncthreads();
     }
+  }
+  if constexpr (W1) {
+    dx_w1_epilogue<BM, BN, NW>(p, acc, smem_epi, m0, n0, dxrow, xr);
+    return;
   }
   // split-K partials: fp32, 16-B per lane straight from the accumulators; final outputs:
   // staged through LDS (full 256-B rows per wave store)

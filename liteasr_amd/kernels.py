@@ -617,9 +617,9 @@ def conv2_dy2_rows(M2):
     return ((M2 + 1 + 31) // 32) * 32
 
 
-def _conv2(mode, y1, out, w2p=None, bias=None, dy2=None, rowsum=None):
+def _conv2(mode, y1, out, w2p=None, bias=None, dy2=None, rowsum=None, x=None, dw1=None, db1=None):
     B, T1, F1, Cc = y1.shape
-    assert y1.dtype == torch.bfloat16 and y1.is_contiguous() and out.is_contiguous()
+    assert y1.dtype == torch.bfloat16 and y1.is_contiguous() and (out is None or out.is_contiguous())
     a = N.Conv2Args()
     a.mode, a.B, a.T1, a.F1, a.C = mode, B, T1, F1, Cc
     a.y1, a.out = ptr(y1), ptr(out)
@@ -637,6 +637,15 @@ def _conv2(mode, y1, out, w2p=None, bias=None, dy2=None, rowsum=None):
     if mode == N.CONV2_DW:
         ws = WS.get(32 * (9 * Cc * Cc + Cc), y1.device)  # K slices: <= 32 (gemm_conv.hip caps to fit)
         a.workspace, a.workspace_bytes = ptr(ws), ws.numel() * 4
+    if mode == N.CONV2_DX_W1:
+        assert x.dtype == torch.float32 and x.is_contiguous() and x.shape[0] == B
+        assert dw1.dtype == torch.float32 and dw1.is_contiguous() and tuple(dw1.shape) == (Cc, 9)
+        assert db1.dtype == torch.float32 and db1.is_contiguous() and db1.numel() == Cc
+        nbytes = N.load().lasr_conv2_dx_w1_workspace(B, T1, F1, Cc)
+        ws = WS.get((nbytes + 3) // 4, y1.device)
+        a.workspace, a.workspace_bytes = ptr(ws), ws.numel() * 4
+        a.x, a.T, a.F = ptr(x), x.shape[1], x.shape[2]
+        a.dw1, a.db1 = ptr(dw1), ptr(db1)
     N.call("lasr_conv2_gemm", C.byref(a), stream())
 
 
@@ -653,6 +662,17 @@ def conv2_dw(dy2, y1, dw, rowsum=None):
 def conv2_dx(dy2, w2p, y1, dy1):
     """dy1 [B, T1, F1, C] bf16 = col2im(dy2 w2p) * relu'(y1)."""
     _conv2(N.CONV2_DX, y1, dy1, w2p=w2p, dy2=dy2)
+
+
+def conv2_dx_w1_ok(Cc):
+    """lasr_conv2_gemm's LASR_CONV2_DX_W1 mode serves this channel count."""
+    return Cc % 256 == 0
+
+
+def conv2_dx_w1(dy2, w2p, y1, x, dw1, db1):
+    """conv2_dx's dy1 consumed in place by conv1's weight gradient (dy1 never stored):
+    dw1 [C, 9] += sum dy1 (x) patch3x3s2(x), db1 [C] += sum dy1; x [B, T, F] fp32."""
+    _conv2(N.CONV2_DX_W1, y1, None, w2p=w2p, dy2=dy2, x=x, dw1=dw1, db1=db1)
 
 
 def permute_last2(src, Nn, A, Bd, dst, reverse=False, accumulate=False):

@@ -543,6 +543,18 @@ class EmbedFn(torch.autograd.Function):
         K.permute_last2(dWo, d, C, F2, g.out_w, reverse=True, accumulate=True)
         M2 = M * F2
         dW2 = _e((C, 9 * C), F32, dev)
+        if sv.implicit and K.conv2_dx_w1_ok(C):
+            # as below, with dy1 consumed inside the data-gradient GEMM's epilogue by conv1's
+            # weight gradient (the 2-byte-per-element dy1 is never written or re-read)
+            dy2_full = _e((K.conv2_dy2_rows(M2), C), adt, dev)
+            dy2_full[M2:].zero_()
+            dy2 = dy2_full[:M2].view(M, F2 * C)
+            K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
+            K.conv2_dw(dy2_full, sv.y1, dW2, rowsum=g.b2)
+            K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
+            K.conv2_dx_w1(dy2_full, w.W2p, sv.y1, sv.xs, g.W1, g.b1)
+            mod.on_grads_ready()
+            return None, None, None, None
         dy1 = torch.empty_like(sv.y1)
         if sv.implicit:
             # dy2 with the zero tail rows the implicit backward GEMMs read (k padding, taps

@@ -838,6 +838,65 @@ def test_conv2_implicit_gemm(B, T, Fd, Cc, ref64):
     assert torch.equal(dy1[y1 <= 0].float(), torch.zeros_like(dy1[y1 <= 0].float()))
 
 
+@pytest.mark.parametrize("B,T,Fd,Cc,ref64", [(2, 42, 81, 256, True), (3, 67, 40, 256, True), (2, 41, 80, 512, True),
+                                             (32, 1000, 80, 256, False)])
+def test_conv2_dx_w1(B, T, Fd, Cc, ref64):
+    """LASR_CONV2_DX_W1: the conv2 data gradient reduced in its epilogue into conv1's weight
+    and bias gradients (dy1 never stored) against conv2_dx + conv1_bwd -- the same bf16 dy1
+    values, summed in another fp32 order -- and, at small sizes, fp64 autograd of
+    conv1(x) . conv2 (within dy1's bf16 rounding); odd and even T1/F1 (every parity class
+    and both edges, rows past each class's last tile), C 256 and 512 (two column tiles), and
+    the full config-2 size.  Accumulates into dw1 / db1; deterministic."""
+    kn = K()
+    g = torch.Generator(device="cpu").manual_seed(B * 7 + T + Cc)
+    T1, F1 = (T - 3) // 2 + 1, (Fd - 3) // 2 + 1
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    M2 = B * T2 * F2
+    bf = torch.bfloat16
+    x = torch.randn(B, T, Fd, generator=g).to(DEV)
+    y1 = torch.relu(torch.randn(B, T1, F1, Cc, generator=g)).to(bf).to(DEV)
+    w2 = (torch.randn(Cc, Cc, 3, 3, generator=g) / (3 * Cc ** 0.5)).to(DEV)
+    w2p = torch.empty(Cc, 9 * Cc, device=DEV, dtype=bf)
+    kn.permute_last2(w2.reshape(Cc, Cc, 9), Cc, Cc, 9, w2p)
+    dy2f = torch.zeros(kn.conv2_dy2_rows(M2), Cc, device=DEV, dtype=bf)
+    dy2f[:M2] = torch.randn(M2, Cc, generator=g).to(bf).to(DEV)
+    assert kn.conv2_dx_w1_ok(Cc)
+    dw1 = torch.full((Cc, 9), 0.25, device=DEV)
+    db1 = torch.full((Cc,), -0.5, device=DEV)
+    kn.conv2_dx_w1(dy2f, w2p, y1, x, dw1, db1)
+    dy1 = torch.empty_like(y1)
+    kn.conv2_dx(dy2f, w2p, y1, dy1)
+    dw1e = torch.zeros(Cc, 9, device=DEV)
+    db1e = torch.zeros(Cc, device=DEV)
+    kn.conv1_bwd(x, dy1, dw1e, db1e)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dw1).all() and torch.isfinite(db1).all()
+    close(dw1 - 0.25, dw1e, 1e-4, "conv1 dW1 fused vs conv2_dx + conv1_bwd")
+    close(db1 + 0.5, db1e, 1e-4, "conv1 db1 fused vs conv2_dx + conv1_bwd")
+    # deterministic: a second call adds exactly the same values
+    dw2 = torch.zeros(Cc, 9, device=DEV)
+    db2 = torch.zeros(Cc, device=DEV)
+    kn.conv2_dx_w1(dy2f, w2p, y1, x, dw2, db2)
+    dw3 = torch.zeros(Cc, 9, device=DEV)
+    db3 = torch.zeros(Cc, device=DEV)
+    kn.conv2_dx_w1(dy2f, w2p, y1, x, dw3, db3)
+    torch.cuda.synchronize()
+    assert torch.equal(dw2, dw3) and torch.equal(db2, db3)
+    if not ref64:
+        return
+    y1r = y1.double().permute(0, 3, 1, 2).requires_grad_()
+    w2r = w2p.double().view(Cc, 3, 3, Cc).permute(0, 3, 1, 2).contiguous()
+    pre = F.conv2d(y1r, w2r, None, stride=2)
+    (gy1,) = torch.autograd.grad(pre, (y1r,), dy2f[:M2].double().view(B, T2, F2, Cc).permute(0, 3, 1, 2))
+    dy1r = gy1 * (y1r.detach() > 0)
+    w1r = torch.zeros(Cc, 1, 3, 3, dtype=torch.float64, device=DEV, requires_grad=True)
+    b1r = torch.zeros(Cc, dtype=torch.float64, device=DEV, requires_grad=True)
+    y1pre = F.conv2d(x.double().unsqueeze(1), w1r, b1r, stride=2)
+    gw, gb = torch.autograd.grad(y1pre, (w1r, b1r), dy1r)
+    close(dw2, gw.view(Cc, 9), 1e-2, "conv1 dW1 fused vs fp64")
+    close(db2, gb, 1e-2, "conv1 db1 fused vs fp64")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("Cc,T", [(64, 70), (200, 133)])
 def test_conformer_conv_module_pieces(dtype, Cc, T):
