@@ -202,7 +202,9 @@ extern "C" int lasr_conv2_gemm(const lasr_conv2_args* a, void* stream) {
   dc.start[4] = nb;
   if (w1) {
     // the conv1 weight gradient in the epilogue (conv1: x [B, T, F] -> y1, 3x3 stride 2)
-    LASR_CHECK_ARG(BN == 256 && epi_code(p) == EPI_AUX_RELU, "lasr_conv2_gemm/dx_w1: needs C %% 256 == 0");
+    // (its own epilogue: the LASR_EPI_SPEC switch, which only selects between equal-result
+    // store epilogues, does not apply)
+    LASR_CHECK_ARG(BN == 256, "lasr_conv2_gemm/dx_w1: needs C %% 256 == 0");
     LASR_CHECK_ARG(a->x && a->dw1 && a->db1 && a->T >= 3 && a->F >= 3 && (a->T - 3) / 2 + 1 == g.T1 &&
                    (a->F - 3) / 2 + 1 == g.F1, "lasr_conv2_gemm/dx_w1: x [B, T, F] must give y1's T1 / F1");
     LASR_CHECK_ARG((int64_t)g.B * a->T * a->F < (1LL << 31), "lasr_conv2_gemm/dx_w1: x past 2^31 elements");
