@@ -62,6 +62,12 @@ def test_host_entries_without_gpu(lib):
         thr = int(p * 65536 + 0.5)
         assert abs(L.lasr_dropout_scale(p) - 65536 / (65536 - thr)) <= 1e-6
     assert L.lasr_dropout_scale(0.0) == 1.0 and L.lasr_dropout_scale(1.0) == 0.0
+    # conv2 DX_W1 workspace: one [10][C] fp32 partial row per 128-row tile of the four output
+    # parity classes, their 64-row group sums and the total
+    for B, T1, F1, C in ((32, 499, 39, 256), (2, 20, 39, 512), (3, 32, 18, 256)):
+        P = sum(-(-(B * ((T1 - pt + 1) >> 1) * ((F1 - pf + 1) >> 1)) // 128) for pt in (0, 1) for pf in (0, 1))
+        assert L.lasr_conv2_dx_w1_workspace(B, T1, F1, C) == (P + -(-P // 64) + 1) * 10 * C * 4
+    assert L.lasr_conv2_dx_w1_workspace(0, 20, 39, 256) == 0
 
 
 def test_extern_c_no_mangling(lib):
