@@ -49,15 +49,19 @@ __global__ void embed_pe_fwd_kernel(const int32_t* ids, int R, int L, int D, con
 
 // Deterministic embedding backward: the workgroup of the first row holding an id sums
 // every row with that id and adds it to dE[id].  The rows holding the id are found in
-// parallel (ballot compaction, row order kept); the sum runs over 4 row groups x 8
-// accumulators per column and is combined in a fixed order (run-to-run identical).
-constexpr int EMB_EC = 4;  // 64-column chunks per pass of embed_bwd_kernel
+// parallel (ballot compaction, row order kept); the sum runs over EMB_NW row groups (one per
+// wave) x 8 accumulators per column and is combined in a fixed order (run-to-run identical).
+// 16 waves: a frequent id (the eos padding of the decoder input: hundreds of rows) is one
+// chain of dependent load rounds per row group, so its workgroup's time scales with
+// rows / (8 x EMB_NW).
+constexpr int EMB_EC = 4;   // 64-column chunks per pass of embed_bwd_kernel
+constexpr int EMB_NW = 16;  // waves (row groups) per workgroup
 
 template <typename TD>
-__global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int R, int D, const TD* dy,
-                                                        float xscale, DropCfg d, float* dE) {
-  extern __shared__ int sid[];  // R ids, up to R matching rows, 4 x EMB_EC x 64 partial sums
-  __shared__ int wcnt[4];
+__global__ __launch_bounds__(EMB_NW * 64) void embed_bwd_kernel(const int32_t* ids, int R, int D, const TD* dy,
+                                                                float xscale, DropCfg d, float* dE) {
+  extern __shared__ int sid[];  // R ids, up to R matching rows, EMB_NW x EMB_EC x 64 partial sums
+  __shared__ int wcnt[EMB_NW];
   int* rows = sid + R;
   for (int i = threadIdx.x; i < R; i += blockDim.x) sid[i] = ids[i];
   __syncthreads();
@@ -68,16 +72,19 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
   if (__syncthreads_or(earlier)) return;  // not the first occurrence (uniform)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int n = 0;
-  for (int base = r; base < R; base += 256) {
+  for (int base = r; base < R; base += EMB_NW * 64) {
     const int k = base + threadIdx.x;
     const bool m = k < R && sid[k] == id;
     const uint64_t bal = __ballot(m);
     if (lane == 0) wcnt[w] = __popcll(bal);
     __syncthreads();
-    int off = n;
-    for (int q = 0; q < w; ++q) off += wcnt[q];
+    int off = n, tot = 0;
+    for (int q = 0; q < EMB_NW; ++q) {
+      off += q < w ? wcnt[q] : 0;
+      tot += wcnt[q];
+    }
     if (m) rows[off + __popcll(bal & ((1ull << lane) - 1))] = k;
-    n += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    n += tot;
     __syncthreads();
   }
   // 4 row groups x 64 columns per chunk, EC chunks (EC * 64 columns) per pass so a frequent
@@ -85,7 +92,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
   // frequent id, e.g. the eos padding, has hundreds of rows: the latency chain, not
   // bandwidth, bounds this block); per column the same summation order as one chunk a pass
   const uint32_t key = d.p > 0.f ? drop_key(d) : 0u;
-  float* part = reinterpret_cast<float*>(rows + R);  // [4][EC * 64]
+  float* part = reinterpret_cast<float*>(rows + R);  // [EMB_NW][EC * 64]
   if ((D & 1) == 0) {
     // even D: a lane takes a column PAIR (one 4/8-B load, one dropout draw for both halves,
     // as the forward drew them); per column the same order as below, so the same bits
@@ -96,10 +103,10 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
       for (int pc = 0; pc < PC; ++pc)
 #pragma unroll
         for (int u = 0; u < 8; ++u) a[pc][0][u] = a[pc][1][u] = 0.f;
-      for (int q0 = w; q0 < n; q0 += 32) {
+      for (int q0 = w; q0 < n; q0 += 8 * EMB_NW) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int q = q0 + 4 * u;
+          const int q = q0 + EMB_NW * u;
           if (q < n) {
             const int64_t rb = (int64_t)rows[q] * D;
 #pragma unroll
@@ -129,8 +136,10 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int o = 128 * pc + 2 * lane + j, c = c0 + o;
-            if (c < D)
-              dE[(int64_t)id * D + c] += (((part[o] + part[S + o]) + part[2 * S + o]) + part[3 * S + o]) * xscale;
+            float t = 0.f;
+#pragma unroll
+            for (int g = 0; g < EMB_NW; ++g) t += part[g * S + o];
+            if (c < D) dE[(int64_t)id * D + c] += t * xscale;
           }
       }
       __syncthreads();
@@ -143,10 +152,10 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
     for (int cc = 0; cc < EMB_EC; ++cc)
 #pragma unroll
       for (int u = 0; u < 8; ++u) a[cc][u] = 0.f;
-    for (int q0 = w; q0 < n; q0 += 32) {
+    for (int q0 = w; q0 < n; q0 += 8 * EMB_NW) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int q = q0 + 4 * u;
+        const int q = q0 + EMB_NW * u;
         if (q < n) {
           const int64_t rb = (int64_t)rows[q] * D;
 #pragma unroll
@@ -166,8 +175,10 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, int 
 #pragma unroll
       for (int cc = 0; cc < EMB_EC; ++cc) {
         const int c = c0 + 64 * cc + lane, o = 64 * cc + lane, S = 64 * EMB_EC;
-        if (c < D)
-          dE[(int64_t)id * D + c] += (((part[o] + part[S + o]) + part[2 * S + o]) + part[3 * S + o]) * xscale;
+        float t = 0.f;
+#pragma unroll
+        for (int g = 0; g < EMB_NW; ++g) t += part[g * S + o];
+        if (c < D) dE[(int64_t)id * D + c] += t * xscale;
       }
     }
     __syncthreads();
@@ -239,12 +250,12 @@ extern "C" int lasr_embed_pe_fwd(const int32_t* ids, int R, int L, int D, const 
 extern "C" int lasr_embed_bwd(const int32_t* ids, int R, int D, const void* dy, int dydt,
                               float xscale, float p, uint64_t seed, float* dE, void* stream) {
   if (R <= 0) return LASR_OK;
-  LASR_CHECK_ARG(R <= 16384, "lasr_embed_bwd: R=%d > 16384", R);  // 2 R ints of LDS
+  LASR_CHECK_ARG(R <= 16384, "lasr_embed_bwd: R=%d > 16384", R);  // 2 R ints + 16 KB of LDS
   DropCfg d = mkdrop(p, seed);
   hipStream_t st = (hipStream_t)stream;
-  const size_t shm = ((size_t)2 * R + 256 * EMB_EC) * sizeof(int);
-  if (dydt == LASR_F32) embed_bwd_kernel<float><<<R, 256, shm, st>>>(ids, R, D, (const float*)dy, xscale, d, dE);
-  else embed_bwd_kernel<bf16_t><<<R, 256, shm, st>>>(ids, R, D, (const bf16_t*)dy, xscale, d, dE);
+  const size_t shm = ((size_t)2 * R + EMB_NW * 64 * EMB_EC) * sizeof(int);
+  if (dydt == LASR_F32) embed_bwd_kernel<float><<<R, EMB_NW * 64, shm, st>>>(ids, R, D, (const float*)dy, xscale, d, dE);
+  else embed_bwd_kernel<bf16_t><<<R, EMB_NW * 64, shm, st>>>(ids, R, D, (const bf16_t*)dy, xscale, d, dE);
   return lasr_check_launch("embed_bwd");
 }
 
