@@ -319,6 +319,22 @@ int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int6
                   int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
                   const float* stats, const void* ctx, const void* dctx, int64_t ldc, float* Dbuf, void* dq,
                   void* dk_out, void* dv_out, int64_t lddkv, void* stream);
+/* The same two with the key blocks split over nsplit workgroups per query block (1 <=
+ * nsplit <= ceil(Tk / 64)) and combined in a second launch, for few query blocks over long
+ * key runs (the decoder's source attention).  The results are those of the one-pass entries
+ * up to fp32 summation order.  work: 16-B aligned fp32 scratch of lasr_attn_split_work floats.
+ * lasr_attn_split_count suggests nsplit (1 = no split) for a shape. */
+int lasr_attn_fwd_split(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B, int H,
+                        int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                        float* stats, void* ctx, int64_t ldc, int nsplit, float* work, int64_t work_floats,
+                        void* stream);
+int lasr_attn_bwd_split(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B, int H,
+                        int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                        const float* stats, const void* ctx, const void* dctx, int64_t ldc, float* Dbuf, void* dq,
+                        void* dk_out, void* dv_out, int64_t lddkv, int nsplit, float* work, int64_t work_floats,
+                        void* stream);
+int64_t lasr_attn_split_work(int B, int H, int Tq, int dk, int nsplit);
+int lasr_attn_split_count(int B, int H, int Tq, int Tk);
 /* dst[t, h*dk + c] = sum_b src[b,h,t,c]  (pos-projection grad reduced over batch). */
 int lasr_reduce_batch(const float* src, int B, int H, int T, int dk, void* dst, int dt,
                       void* stream);

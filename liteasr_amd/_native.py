@@ -113,6 +113,11 @@ SIGNATURES = {
     "lasr_attn_fwd": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_attn_bwd": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l, _p, _p, _p, _p,
                       _l, _p],
+    "lasr_attn_fwd_split": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _i, _p, _l, _p],
+    "lasr_attn_bwd_split": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l, _p, _p, _p,
+                            _p, _l, _i, _p, _l, _p],
+    "lasr_attn_split_work": [_i, _i, _i, _i, _i],
+    "lasr_attn_split_count": [_i, _i, _i, _i],
     "lasr_relattn_bwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l,
                          _p, _p, _p, _i, _i, _p, _p, _l, _p],
     "lasr_reduce_multi": [C.POINTER(ReduceSeg), _i, _p],
@@ -175,7 +180,7 @@ SIGNATURES = {
     "lasr_logsoftmax_topk": [_p, _i, _l, _i, _l, _i, _p, _p, _p, _p, _p],
 }
 _RESTYPES = {"lasr_last_error": C.c_char_p, "lasr_spec_augment_ws_bytes": C.c_int64,
-             "lasr_conv2_dx_w1_workspace": C.c_int64,
+             "lasr_conv2_dx_w1_workspace": C.c_int64, "lasr_attn_split_work": C.c_int64,
              "lasr_dropout_scale": C.c_float}
 
 

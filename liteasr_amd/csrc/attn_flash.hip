@@ -48,6 +48,12 @@ struct FlashP {
   bf16_t* dqu;                          // [B*T, ldq]
   bf16_t* dbd;                          // [B][H] (or [H][B] if dbd_hb) x [T, ldS]
   int ldS, dbd_hb;
+  // plain attention only: the key blocks split over nsplit workgroups per query block (few
+  // query blocks, long key runs: the decoder's source attention); each writes its partial
+  // O (forward; dQ in the backward) to opart [nsplit][B*H*T][DK] fp32 and its (max, sum) to
+  // mpart [nsplit][B*H*T][2], combined in split order by a second launch
+  int nsplit;
+  float *opart, *mpart;
 };
 
 // bf16 zero row: the relative-position window's rows outside the table (m == T, past 2T)
@@ -435,11 +441,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             col = lane & 15;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
-  const int i0 = blockIdx.x * Gm::QB, iw = i0 + 16 * w, iq = iw + col;
+  const int ns = RP ? 1 : max(a.nsplit, 1), qblk = blockIdx.x / ns, sp = blockIdx.x - qblk * ns;
+  const int i0 = qblk * Gm::QB, iw = i0 + 16 * w, iq = iw + col;
   const int nb = (Tk + KB - 1) / KB;
+  const int jb0 = sp * nb / ns, jb1 = (sp + 1) * nb / ns;  // this workgroup's key blocks
   const float c2 = a.scale * 1.4426950408889634f;
 
-  issue_stage<DK, NW, RP, RM>(a, b, h, i0, 0, ring, tid);
+  issue_stage<DK, NW, RP, RM>(a, b, h, i0, jb0 * KB, ring, tid);
   const uint8_t* km = kmask;
   if constexpr (!RM) {  // key padding bytes of this utterance (zeros without a mask; keys >= Tk are -inf anyway)
     const uint8_t* mr = a.mask ? a.mask + (int64_t)b * a.msb : nullptr;
@@ -458,12 +466,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) o[t] = zero4();
 
-  for (int jb = 0; jb < nb; ++jb) {
+  for (int jb = jb0; jb < jb1; ++jb) {
     const int j0 = jb * KB;
-    char* st = ring + (jb & 1) * Gm::STAGE_BYTES;
+    char* st = ring + ((jb - jb0) & 1) * Gm::STAGE_BYTES;
     wait_vmcnt<0>();  // this block's pieces (issued one block ago) and the Q loads
     lds_barrier();    // ... of every wave; every wave is done with block jb-1's stage
-    if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
+    if (jb + 1 < jb1)
+      issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb - jb0 + 1) & 1) * Gm::STAGE_BYTES, tid);
     if constexpr (RM) {  // (the streaming chunk mask: the blocks of future chunks)
       if (__builtin_amdgcn_ballot_w64(mrun <= -1e38f) == 0 && block_all_masked<DK, NW, RP, RM>(st, w, lane)) continue;
     }
@@ -523,6 +532,16 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
   }
   // statistics in scaled-score units (max * ln 2), 1/sum: P = exp(S - max) / sum
   const float l = xsum16_32(lrun);
+  if (ns > 1) {  // a key split: unnormalised O, running max (log2 units) and sum, for the combine
+    if (iq < T) {
+      const int64_t row = (int64_t)sp * a.B * a.H * T + ((int64_t)b * a.H + h) * T + iq;
+      if (g == 0) *(float2*)(a.mpart + 2 * row) = make_float2(mrun, l);
+      float* op = a.opart + row * DK + 4 * g;
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) *(f32x4*)(op + 16 * t) = o[t];
+    }
+    return;
+  }
   const float il = 1.f / l;
   if (iq < T) {
     if (g == 0) {  // a fully masked row keeps the masked score itself as its max (uniform P)
@@ -559,12 +578,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             col = lane & 15;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
-  const int i0 = blockIdx.x * Gm::QB, iw = i0 + 16 * w, iq = iw + col, ic = min(iq, T - 1);
+  const int ns = RP ? 1 : max(a.nsplit, 1), qblk = blockIdx.x / ns, sp = blockIdx.x - qblk * ns;
+  const int i0 = qblk * Gm::QB, iw = i0 + 16 * w, iq = iw + col, ic = min(iq, T - 1);
   const int nb = (Tk + KB - 1) / KB;
+  const int jb0 = sp * nb / ns, jb1 = (sp + 1) * nb / ns;  // this workgroup's key blocks
   const float c2 = a.scale * 1.4426950408889634f;
   const int64_t zrow = ((int64_t)b * a.H + h) * T;
 
-  issue_stage<DK, NW, RP, RM>(a, b, h, i0, 0, ring, tid);
+  issue_stage<DK, NW, RP, RM>(a, b, h, i0, jb0 * KB, ring, tid);
   const uint8_t* km = kmask;
   if constexpr (!RM) {  // key padding bytes of this utterance (zeros without a mask; keys >= Tk are -inf anyway)
     const uint8_t* mr = a.mask ? a.mask + (int64_t)b * a.msb : nullptr;
@@ -597,7 +618,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
     const int e = col & 3;
     const float x = e == 0 ? dt[0] : e == 1 ? dt[1] : e == 2 ? dt[2] : dt[3];
     D = __shfl(x, ((col >> 2) << 4) | col, 64);
-    if (g == 0 && iq < T) a.Dbuf[zrow + iq] = D;
+    if (g == 0 && iq < T && sp == 0) a.Dbuf[zrow + iq] = D;
   }
   bf16_t* dbd = RP ? a.dbd + (a.dbd_hb ? ((int64_t)h * a.B + b) * T : zrow) * a.ldS : nullptr;
   float* gw = gsh + w * 16 * GLD;
@@ -605,12 +626,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) dq[t] = zero4();
 
-  for (int jb = 0; jb < nb; ++jb) {
+  for (int jb = jb0; jb < jb1; ++jb) {
     const int j0 = jb * KB;
-    char* st = ring + (jb & 1) * Gm::STAGE_BYTES;
+    char* st = ring + ((jb - jb0) & 1) * Gm::STAGE_BYTES;
     wait_vmcnt<0>();
     lds_barrier();
-    if (jb + 1 < nb) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb + 1) & 1) * Gm::STAGE_BYTES, tid);
+    if (jb + 1 < jb1)
+      issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb - jb0 + 1) & 1) * Gm::STAGE_BYTES, tid);
     f32x4 s[4];
     bool skip = false;
     if constexpr (RM) skip = rows_live && block_all_masked<DK, NW, RP, RM>(st, w, lane);
@@ -739,6 +761,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
       }
     }
   }
+  if (ns > 1) {  // a key split: the unscaled partial dQ, summed by flash_dq_combine_kernel
+    if (iq < T) {
+      float* dp = a.opart + ((int64_t)sp * a.B * a.H * T + zrow + iq) * DK + 4 * g;
+#pragma unroll
+      for (int t = 0; t < DK / 16; ++t) *(f32x4*)(dp + 16 * t) = dq[t];
+    }
+    return;
+  }
   if (iq < T) {
     bf16_t* dst = a.dqu + ((int64_t)b * T + iq) * a.ldq + h * DK + 4 * g;
 #pragma unroll
@@ -755,7 +785,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
 
 template <int DK, int NW, bool RP, bool RM>
 void launch_bwd_q_t(const FlashP& a, hipStream_t st) {
-  const dim3 grid((unsigned)cdiv(a.T, 16 * NW), (unsigned)a.H, (unsigned)a.B);
+  const dim3 grid((unsigned)(cdiv(a.T, 16 * NW) * (RP || a.nsplit < 1 ? 1 : a.nsplit)), (unsigned)a.H, (unsigned)a.B);
   flash_bwd_q_kernel<DK, NW, RP, RM><<<grid, NW * 64, 0, st>>>(a);
 }
 
@@ -1115,9 +1145,52 @@ void launch_flash_bwd_kv(const FlashP& a, int dk, bool rp, bool rm, bf16_t* dko,
 
 template <int DK, int NW, bool RP, bool RM>
 void launch_fwd_t(const FlashP& a, hipStream_t st) {
-  const dim3 grid((unsigned)cdiv(a.T, 16 * NW), (unsigned)a.H, (unsigned)a.B);
+  const dim3 grid((unsigned)(cdiv(a.T, 16 * NW) * (RP || a.nsplit < 1 ? 1 : a.nsplit)), (unsigned)a.H, (unsigned)a.B);
   flash_fwd_kernel<DK, NW, RP, RM><<<grid, NW * 64, 0, st>>>(a);
 }
+
+// The key-split combines (plain attention, nsplit > 1), one thread per (row, 4 columns), the
+// splits in order.  Forward: M = max_s m_s, L = sum_s l_s 2^(m_s - M), O = sum_s 2^(m_s - M) O_s,
+// ctx = O / L and the statistics the backward reads (as the one-pass epilogue writes them).
+template <int DK>
+__global__ __launch_bounds__(256) void flash_fwd_combine_kernel(FlashP a) {
+  const int64_t BHT = (int64_t)a.B * a.H * a.T;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= BHT * (DK / 4)) return;
+  const int64_t row = e / (DK / 4);
+  const int cg = (int)(e - row * (DK / 4));
+  const int iq = (int)(row % a.T), h = (int)((row / a.T) % a.H), b = (int)(row / ((int64_t)a.T * a.H));
+  float M = -INFINITY;
+  for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.mpart[2 * (s * BHT + row)]);
+  float L = 0.f;
+  f32x4 O = zero4();
+  for (int s = 0; s < a.nsplit; ++s) {
+    const float2 ml = *(const float2*)(a.mpart + 2 * (s * BHT + row));
+    const float wgt = __builtin_amdgcn_exp2f(ml.x - M);
+    L += ml.y * wgt;
+    O += *(const f32x4*)(a.opart + (s * BHT + row) * DK + 4 * cg) * wgt;
+  }
+  const float il = 1.f / L;
+  bf16_t* dst = a.ctx + ((int64_t)b * a.T + iq) * a.ldc + h * DK + 4 * cg;
+  *(uint2*)dst = make_uint2(pk_bf16(O[0] * il, O[1] * il), pk_bf16(O[2] * il, O[3] * il));
+  if (cg == 0) *(float2*)(a.stats + 2 * row) = make_float2(M <= -1e38f ? -1e38f : M * 0.6931471805599453f, il);
+}
+// Backward: dQ = scale * sum_s dQ_s.
+template <int DK>
+__global__ __launch_bounds__(256) void flash_dq_combine_kernel(FlashP a) {
+  const int64_t BHT = (int64_t)a.B * a.H * a.T;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= BHT * (DK / 4)) return;
+  const int64_t row = e / (DK / 4);
+  const int cg = (int)(e - row * (DK / 4));
+  const int iq = (int)(row % a.T), h = (int)((row / a.T) % a.H), b = (int)(row / ((int64_t)a.T * a.H));
+  f32x4 q = zero4();
+  for (int s = 0; s < a.nsplit; ++s) q += *(const f32x4*)(a.opart + (s * BHT + row) * DK + 4 * cg);
+  bf16_t* dst = a.dqu + ((int64_t)b * a.T + iq) * a.ldq + h * DK + 4 * cg;
+  *(uint2*)dst = make_uint2(pk_bf16(q[0] * a.scale, q[1] * a.scale), pk_bf16(q[2] * a.scale, q[3] * a.scale));
+}
+
+unsigned combine_blocks(const FlashP& a, int dk) { return (unsigned)cdiv((int64_t)a.B * a.H * a.T * (dk / 4), 256); }
 
 // RP: the encoder's relative-position attention (8 waves, 128 queries per workgroup; 4 waves at d_k 32); plain:
 // the decoder's (4 waves, 64 queries: Tq = L + 1 is short)
@@ -1173,10 +1246,12 @@ extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, con
 
 // Plain scaled dot-product attention (no positional term) with Tk keys per utterance: the
 // decoder's self attention (Tk = Tq, causal + padding mask) and source attention over the
-// encoder output (Tk = T', key padding).
-extern "C" int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
-                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
-                             int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc, void* stream) {
+// encoder output (Tk = T', key padding).  nsplit > 1 splits the key blocks over that many
+// workgroups per query block (work: lasr_attn_split_work floats), combined in a second launch.
+static int attn_fwd_impl(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B, int H,
+                         int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                         float* stats, void* ctx, int64_t ldc, int nsplit, float* work, int64_t work_floats,
+                         void* stream) {
   LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_fwd: d_k=%d (32 or 64)", dk);
   LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_fwd: bad B/H/T");
   LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk,
@@ -1184,14 +1259,60 @@ extern "C" int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const vo
   LASR_CHECK_ARG(al16(q) && al16(k) && al16(v) && al16(ctx), "lasr_attn_fwd: 16-B alignment");
   if (B == 0 || Tq == 0) return LASR_OK;
   if (int rc = check_mask(mask, mask_sb, mask_sq, Tk, "lasr_attn_fwd")) return rc;
+  const int nb = (Tk + KB - 1) / KB;
+  LASR_CHECK_ARG(nsplit >= 1 && nsplit <= nb, "lasr_attn_fwd: nsplit=%d outside [1, %d key blocks]", nsplit, nb);
+  if (nsplit > 1)
+    LASR_CHECK_ARG(work && al16(work) && work_floats >= lasr_attn_split_work(B, H, Tq, dk, nsplit) &&
+                   ((uintptr_t)stats & 7) == 0, "lasr_attn_fwd: split workspace");
   FlashP a = {};
   a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
   a.ldq = ldq; a.ldkv = ldkv;
   a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
   a.B = B; a.H = H; a.T = Tq; a.Tk = Tk; a.scale = scale;
   a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
+  a.nsplit = nsplit;
+  if (nsplit > 1) {
+    a.opart = work;
+    a.mpart = work + (int64_t)nsplit * B * H * Tq * dk;
+  }
   launch_flash_fwd(a, dk, false, mask && mask_sq != 0, (hipStream_t)stream);
-  return lasr_check_launch("attn_fwd");
+  if (int rc = lasr_check_launch("attn_fwd")) return rc;
+  if (nsplit > 1) {
+    if (dk == 64) flash_fwd_combine_kernel<64><<<combine_blocks(a, dk), 256, 0, (hipStream_t)stream>>>(a);
+    else flash_fwd_combine_kernel<32><<<combine_blocks(a, dk), 256, 0, (hipStream_t)stream>>>(a);
+    return lasr_check_launch("attn_fwd_combine");
+  }
+  return LASR_OK;
+}
+
+extern "C" int64_t lasr_attn_split_work(int B, int H, int Tq, int dk, int nsplit) {
+  return nsplit > 1 ? (int64_t)nsplit * B * H * Tq * (dk + 2) : 0;
+}
+
+// Key blocks per workgroup >= 4 and about 512 workgroups: only long key runs over few query
+// blocks split (the decoder's source attention at T' 999: 96 query blocks x 16 key blocks -> 4)
+extern "C" int lasr_attn_split_count(int B, int H, int Tq, int Tk) {
+  if (B <= 0 || H <= 0 || Tq <= 0 || Tk <= 0) return 1;
+  const int64_t qblocks = cdiv(Tq, 64) * (int64_t)B * H;
+  const int nb = (Tk + KB - 1) / KB;
+  int ns = 1;
+  while (ns * 2 <= nb / 4 && qblocks * ns * 2 <= 512) ns *= 2;
+  return ns;
+}
+
+extern "C" int lasr_attn_fwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                             int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc, void* stream) {
+  return attn_fwd_impl(q, ldq, k, v, ldkv, B, H, Tq, Tk, dk, mask, mask_sb, mask_sq, scale, stats, ctx, ldc, 1,
+                       nullptr, 0, stream);
+}
+
+extern "C" int lasr_attn_fwd_split(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                                   int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                                   int64_t mask_sq, float scale, float* stats, void* ctx, int64_t ldc, int nsplit,
+                                   float* work, int64_t work_floats, void* stream) {
+  return attn_fwd_impl(q, ldq, k, v, ldkv, B, H, Tq, Tk, dk, mask, mask_sb, mask_sq, scale, stats, ctx, ldc,
+                       nsplit, work, work_floats, stream);
 }
 
 extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, const void* k,
@@ -1228,11 +1349,11 @@ extern "C" int lasr_relattn_bwd(const void* qu, const void* qv, int64_t ldq, con
   return lasr_check_launch("relattn_bwd_kv");
 }
 
-extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
-                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
-                             int64_t mask_sq, float scale, const float* stats, const void* ctx, const void* dctx,
-                             int64_t ldc, float* Dbuf, void* dq, void* dk_out, void* dv_out, int64_t lddkv,
-                             void* stream) {
+static int attn_bwd_impl(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B, int H,
+                         int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
+                         const float* stats, const void* ctx, const void* dctx, int64_t ldc, float* Dbuf, void* dq,
+                         void* dk_out, void* dv_out, int64_t lddkv, int nsplit, float* work, int64_t work_floats,
+                         void* stream) {
   LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_attn_bwd: d_k=%d (32 or 64)", dk);
   LASR_CHECK_ARG(B >= 0 && H > 0 && Tq >= 0 && Tk > 0 && B <= 65535 && H <= 65535, "lasr_attn_bwd: bad B/H/T");
   LASR_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk && lddkv % 8 == 0,
@@ -1240,6 +1361,11 @@ extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const vo
   LASR_CHECK_ARG(al16(q) && al16(k) && al16(v) && al16(dctx) && al16(ctx) && al16(dq), "lasr_attn_bwd: 16-B alignment");
   if (B == 0 || Tq == 0) return LASR_OK;
   if (int rc = check_mask(mask, mask_sb, mask_sq, Tk, "lasr_attn_bwd")) return rc;
+  const int nb = (Tk + KB - 1) / KB;
+  LASR_CHECK_ARG(nsplit >= 1 && nsplit <= nb, "lasr_attn_bwd: nsplit=%d outside [1, %d key blocks]", nsplit, nb);
+  if (nsplit > 1)
+    LASR_CHECK_ARG(work && al16(work) && work_floats >= lasr_attn_split_work(B, H, Tq, dk, nsplit),
+                   "lasr_attn_bwd: split workspace");
   FlashP a = {};
   a.qu = a.qv = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
   a.ldq = ldq; a.ldkv = ldkv;
@@ -1248,10 +1374,35 @@ extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const vo
   a.stats = (float*)stats; a.ldc = ldc;
   a.dctx = (const bf16_t*)dctx; a.ctx_in = (const bf16_t*)ctx; a.Dbuf = Dbuf;
   a.dqu = (bf16_t*)dq;
+  a.nsplit = nsplit;
+  a.opart = nsplit > 1 ? work : nullptr;
   LASR_CHECK_ARG(al16(dk_out) && al16(dv_out), "lasr_attn_bwd: dk/dv 16-B alignment");
   const bool rm = mask && mask_sq != 0;
   launch_flash_bwd_q(a, dk, false, rm, (hipStream_t)stream);
   if (int rc = lasr_check_launch("attn_bwd_q")) return rc;
+  if (nsplit > 1) {
+    if (dk == 64) flash_dq_combine_kernel<64><<<combine_blocks(a, dk), 256, 0, (hipStream_t)stream>>>(a);
+    else flash_dq_combine_kernel<32><<<combine_blocks(a, dk), 256, 0, (hipStream_t)stream>>>(a);
+    if (int rc = lasr_check_launch("attn_dq_combine")) return rc;
+  }
   launch_flash_bwd_kv(a, dk, false, rm, (bf16_t*)dk_out, (bf16_t*)dv_out, lddkv, (hipStream_t)stream);
   return lasr_check_launch("attn_bwd_kv");
+}
+
+extern "C" int lasr_attn_bwd(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                             int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                             int64_t mask_sq, float scale, const float* stats, const void* ctx, const void* dctx,
+                             int64_t ldc, float* Dbuf, void* dq, void* dk_out, void* dv_out, int64_t lddkv,
+                             void* stream) {
+  return attn_bwd_impl(q, ldq, k, v, ldkv, B, H, Tq, Tk, dk, mask, mask_sb, mask_sq, scale, stats, ctx, dctx, ldc,
+                       Dbuf, dq, dk_out, dv_out, lddkv, 1, nullptr, 0, stream);
+}
+
+extern "C" int lasr_attn_bwd_split(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, int B,
+                                   int H, int Tq, int Tk, int dk, const uint8_t* mask, int64_t mask_sb,
+                                   int64_t mask_sq, float scale, const float* stats, const void* ctx,
+                                   const void* dctx, int64_t ldc, float* Dbuf, void* dq, void* dk_out, void* dv_out,
+                                   int64_t lddkv, int nsplit, float* work, int64_t work_floats, void* stream) {
+  return attn_bwd_impl(q, ldq, k, v, ldkv, B, H, Tq, Tk, dk, mask, mask_sb, mask_sq, scale, stats, ctx, dctx, ldc,
+                       Dbuf, dq, dk_out, dv_out, lddkv, nsplit, work, work_floats, stream);
 }

@@ -563,20 +563,46 @@ def relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, d
            stream())
 
 
-def attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx):
+def attn_split(B, H, Tq, Tk, nsplit=None):
+    """Key-split count of lasr_attn_fwd_split / _bwd_split for a shape (the library's
+    heuristic unless given; 1 = the one-pass entries)."""
+    ns = N.load().lasr_attn_split_count(B, H, Tq, Tk) if nsplit is None else int(nsplit)
+    return ns
+
+
+def attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx, nsplit=None):
     """Plain attention on the fused kernels (lasr_attn_fwd): q [B*Tq, H*d_k], k / v
-    [B*Tk, H*d_k] row-major views (k and v share a row stride), stats [B*H*Tq*2] fp32."""
+    [B*Tk, H*d_k] row-major views (k and v share a row stride), stats [B*H*Tq*2] fp32.
+    Long key runs over few query blocks (the decoder's source attention at T' 999) split
+    the keys over workgroups (lasr_attn_fwd_split; nsplit overrides the heuristic)."""
     assert v.stride(0) == k.stride(0)
     mask, msb, msq = _fwd_mask(mask, msb, msq, B, Tq, Tk)
-    N.call("lasr_attn_fwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, q.shape[1] // H,
+    dk_ = q.shape[1] // H
+    ns = attn_split(B, H, Tq, Tk, nsplit)
+    if ns > 1:
+        nw = N.load().lasr_attn_split_work(B, H, Tq, dk_, ns)
+        ws = WS.get(nw, q.device)
+        N.call("lasr_attn_fwd_split", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, dk_,
+               ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ctx.stride(0), ns, ptr(ws), ws.numel(), stream())
+        return
+    N.call("lasr_attn_fwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, dk_,
            ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ctx.stride(0), stream())
 
 
-def attn_bwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dq, dk, dv):
+def attn_bwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dq, dk, dv, nsplit=None):
     assert dq.stride(0) == q.stride(0) and v.stride(0) == k.stride(0) and dv.stride(0) == dk.stride(0)
     assert dctx.stride(0) == ctx.stride(0)
     mask, msb, msq = _fwd_mask(mask, msb, msq, B, Tq, Tk)
-    N.call("lasr_attn_bwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, q.shape[1] // H,
+    dk_ = q.shape[1] // H
+    ns = attn_split(B, H, Tq, Tk, nsplit)
+    if ns > 1:
+        nw = N.load().lasr_attn_split_work(B, H, Tq, dk_, ns)
+        ws = WS.get(nw, q.device)
+        N.call("lasr_attn_bwd_split", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, dk_,
+               ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx), ctx.stride(0), ptr(Dbuf), ptr(dq),
+               ptr(dk), ptr(dv), dk.stride(0), ns, ptr(ws), ws.numel(), stream())
+        return
+    N.call("lasr_attn_bwd", ptr(q), q.stride(0), ptr(k), ptr(v), k.stride(0), B, H, Tq, Tk, dk_,
            ptr(mask), msb, msq, scale, ptr(stats), ptr(ctx), ptr(dctx), ctx.stride(0), ptr(Dbuf), ptr(dq),
            ptr(dk), ptr(dv), dk.stride(0), stream())
 

@@ -304,6 +304,61 @@ def test_gemm_dw_group_bit_identical(R, monkeypatch):
             close(db, db0.double() + dy.double().sum(0), 1e-5, "grouped db")
 
 
+@pytest.mark.parametrize("B,H,Tq,Tk,dk,qmask,splits", [(8, 4, 151, 999, 64, False, (2, 3, 4, 5)),
+                                                      (3, 2, 70, 300, 32, True, (2, 5)),
+                                                      (2, 4, 41, 249, 64, False, (4,))])
+def test_attn_key_split(B, H, Tq, Tk, dk, qmask, splits):
+    """lasr_attn_fwd_split / lasr_attn_bwd_split (keys split over workgroups, combined in
+    a second launch) against the one-pass entries on the same inputs: the decoder's source
+    attention at the long config (T' 999, the split the heuristic picks: 4), uneven splits
+    (3, 5 of 16 key blocks), a query-dependent mask with a fully masked utterance, d_k 32 and
+    one key block per split.  Same values up to fp32 summation order: the row maxima
+    exactly, ctx / D / dq / dk / dv within a bf16 ulp of the largest value."""
+    kn = K()
+    g = torch.Generator().manual_seed(Tk + dk)
+    bf = torch.bfloat16
+    D = H * dk
+    q = (torch.randn(B * Tq, D, generator=g) * 0.5).to(DEV, bf)
+    kv = (torch.randn(B * Tk, 2 * D, generator=g) * 0.5).to(DEV, bf)
+    k, v = kv[:, :D], kv[:, D:]
+    if qmask:
+        m = torch.rand(B, Tq, Tk, generator=g) < 0.3
+        m[1] = True  # one utterance fully masked: uniform attention rows
+        mask, msb, msq = kn.pad_mask16(m.to(torch.uint8).to(DEV), B, Tq, Tk)
+    else:
+        lens = torch.randint(Tk // 2, Tk + 1, (B,), generator=g)
+        lens[0] = Tk
+        mask = (torch.arange(Tk)[None, :] >= lens[:, None]).to(torch.uint8).to(DEV)
+        msb, msq = Tk, 0
+    scale = dk ** -0.5
+    dctx = (torch.randn(B * Tq, D, generator=g) * 0.5).to(DEV, bf)
+
+    def run(ns):
+        stats = torch.empty(B * H * Tq * 2, device=DEV)
+        ctx = torch.empty(B * Tq, D, device=DEV, dtype=bf)
+        kn.attn_fwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx, nsplit=ns)
+        Dbuf = torch.empty(B * H * Tq, device=DEV)
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        kn.attn_bwd(q, k, v, B, H, Tq, Tk, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dq, dkv[:, :D], dkv[:, D:],
+                    nsplit=ns)
+        torch.cuda.synchronize()
+        return stats.view(-1, 2), ctx, Dbuf, dq, dkv
+
+    if not qmask and (B, H, Tq, Tk) == (8, 4, 151, 999):
+        assert kn.attn_split(B, H, Tq, Tk) == 4
+    base = run(1)
+    for ns in splits:
+        st, ctx, Db, dq, dkv = run(ns)
+        assert torch.equal(st[:, 0], base[0][:, 0]), f"row maxima differ (nsplit {ns})"
+        close(st[:, 1], base[0][:, 1], 1e-5, f"1/sum nsplit {ns}")
+        close(ctx, base[1], 8e-3, f"ctx nsplit {ns}")
+        close(Db, base[2], 8e-3, f"D nsplit {ns}")  # rowsum(dO * O): O is the (re-rounded) ctx
+        close(dq, base[3], 8e-3, f"dq nsplit {ns}")
+        close(dkv, base[4], 8e-3, f"dk/dv nsplit {ns}")
+        assert torch.isfinite(ctx.float()).all() and torch.isfinite(dq.float()).all()
+
+
 @pytest.mark.parametrize("kind", ["self-masked", "self-nomask", "source"])
 def test_decoder_attention_fused_matches_materialised(kind, monkeypatch):
     """Decoder attention on the fused kernels without the positional term (lasr_attn_fwd /

@@ -99,9 +99,10 @@ def dec_case(name, B, H, L1, dk):
                           "tflops": round(units * unit / sec / 1e12, 1)}), flush=True)
 
 
-def src_case(name, B, H, Tq, Tk, dk):
+def src_case(name, B, H, Tq, Tk, dk, nsplit=None):
     """The decoder's source attention: Tq = L + 1 queries over the encoder output's Tk keys
-    (key padding), plain scaled dot-product (no positional term)."""
+    (key padding), plain scaled dot-product (no positional term); nsplit: the key split
+    (None: the library's choice)."""
     dev = "cuda"
     d = H * dk
     bf = torch.bfloat16
@@ -115,16 +116,17 @@ def src_case(name, B, H, Tq, Tk, dk):
     stats = torch.empty(B * H * Tq * 2, device=dev)
     ctx = torch.empty(B * Tq, d, dtype=bf, device=dev)
     k, v = kv[:, :d], kv[:, d:]
-    fwd = lambda: K.attn_fwd(q, k, v, B, H, Tq, Tk, mask, Tk, 0, scale, stats, ctx)  # noqa: E731
+    fwd = lambda: K.attn_fwd(q, k, v, B, H, Tq, Tk, mask, Tk, 0, scale, stats, ctx, nsplit=nsplit)  # noqa: E731
     Dbuf = torch.empty(B * H * Tq, device=dev)
     dq = torch.empty(B * Tq, d, dtype=bf, device=dev)
     dkv = torch.zeros(B * Tk, 2 * d, dtype=bf, device=dev)
     bwd = lambda: K.attn_bwd(q, k, v, B, H, Tq, Tk, mask, Tk, 0, scale, stats, ctx, dctx, Dbuf,  # noqa: E731
-                             dq, dkv[:, :d], dkv[:, d:])
+                             dq, dkv[:, :d], dkv[:, d:], nsplit=nsplit)
     unit = 2.0 * B * H * Tq * Tk * dk
     for dirn, fn, units in (("fwd", fwd, 2), ("bwd", bwd, 5)):
         sec = graph_time(fn)
         print(json.dumps({"case": name, "dir": dirn, "B": B, "H": H, "Tq": Tq, "Tk": Tk, "dk": dk,
+                          "nsplit": K.attn_split(B, H, Tq, Tk, nsplit),
                           "us": round(sec * 1e6, 2), "tflops": round(units * unit / sec / 1e12, 1)}), flush=True)
 
 
@@ -139,6 +141,11 @@ def main():
         dec_case("dec", 32, 4, 41, 64)
     if not sel or "src" in sel:
         src_case("src", 32, 4, 41, 249, 64)
+    if "srcsplit" in sel:  # the key split of the source attention, swept
+        for ns in (1, 2, 4, 8, 16):
+            src_case("srclong", 8, 4, 151, 999, 64, nsplit=ns)
+        for ns in (1, 2, 4):
+            src_case("src", 32, 4, 41, 249, 64, nsplit=ns)
     if not sel or "srclong" in sel:
         src_case("srclong", 8, 4, 151, 999, 64)
 
