@@ -668,6 +668,10 @@ def main():
                     help="gradient all-reduce path (N>1 or --force-ddp): torch.distributed over RCCL, or "
                          "the C-ABI bucketed reducer libliteasr_comm.so (lasr_reducer_*, its own RCCL "
                          "communicator and stream)")
+    ap.add_argument("--single-rank-collectives", action="store_true",
+                    help="--comm native at world 1: issue the 1-rank RCCL all-reduces anyway (by default "
+                         "world 1 issues none: the average is the identity); measures what RCCL's kernels "
+                         "cost the overlapped backward")
     ap.add_argument("--profile", action="store_true",
                     help="roctx ranges around every fused autograd node (liteasr_amd.utils.markers); "
                          "implies --graph off (ranges are host-side launch spans)")
@@ -744,6 +748,8 @@ def main():
         from liteasr_amd.distributed.ddp import DistributedDataParallel
 
         net = DistributedDataParallel(model, comm=args.comm)
+        if args.single_rank_collectives and net.reducer.native is not None:
+            net.reducer.native.set_single_rank_collectives(True)
     crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=V, smoothing=0.1, ctc_weight=cfgd["w"]))
     opt = Noam(model.parameters(), NoamConfig(model_dim=cfgd["d"]))
     batch = synthetic(cfgd, rank, dev)
@@ -817,6 +823,7 @@ def main():
                        "rank_launcher": launcher,
                        "allreduce": None if not use_ddp else
                        {"backend": dist.get_backend(), "comm": args.comm, "buckets": len(net.reducer.buckets),
+                        "single_rank_collectives": bool(args.single_rank_collectives and args.comm == "native"),
                         "bucket_mb_each": [round((hi - lo) * 4 / 1e6, 2) for lo, hi in net.reducer.native_spans()],
                         "bucket_mb": 25, "overlap": args.overlap == "on" and args.graph == "on" or args.graph == "off",
                         "segments": len(step.segs) if args.graph == "on" and step.segs else None,

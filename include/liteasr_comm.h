@@ -68,9 +68,17 @@ int lasr_reducer_launched(const lasr_reducer* r);
  * Collectives already launched stay in flight on the reducer's stream. */
 int lasr_reducer_reset(lasr_reducer* r);
 
-/* Point the reducer at a new gradient buffer of the same numel (the caller reallocated it,
- * e.g. a device move of the model).  Only between steps. */
+/* Point the reducer at a new gradient buffer of the same numel and the same device (the caller
+ * reallocated it).  Only between steps.  A buffer on another device is refused: the
+ * communicator, stream and events belong to the creation device, so a device move of the
+ * model needs a new reducer. */
 int lasr_reducer_rebind(lasr_reducer* r, float* grad, int64_t numel);
+
+/* At world 1 the average is the identity and the reducer issues nothing (no event, no
+ * collective), as the torch.distributed path does.  on != 0 issues the 1-rank collectives
+ * anyway: the world-1 measurement of what RCCL's kernels cost the overlapped backward.
+ * Only between steps; no effect at world > 1. */
+int lasr_reducer_set_single_rank_collectives(lasr_reducer* r, int on);
 
 /* the gradient buffer the reducer currently averages */
 const float* lasr_reducer_grad(const lasr_reducer* r);

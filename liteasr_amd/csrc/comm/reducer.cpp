@@ -39,6 +39,11 @@ struct lasr_reducer {
   ncclComm_t comm = nullptr;
   bool owns_comm = false;
   int device = 0;
+  int world = 1;
+  // world 1: the average over one rank is the identity, so no collective, no stream wait and
+  // no event is issued (what the torch.distributed path does at world 1); set_single_rank_
+  // collectives(1) issues them anyway (the world-1 measurement of RCCL's cost to the compute)
+  bool single_rank_collectives = false;
   float* grad = nullptr;
   int64_t numel = 0;
   std::vector<int64_t> lo, hi;
@@ -98,7 +103,10 @@ int setup(lasr_reducer* r, int device, float* grad, int64_t numel, const int64_t
   return 0;
 }
 
+bool collectives(const lasr_reducer* r) { return r->world > 1 || r->single_rank_collectives; }
+
 int launch(lasr_reducer* r, int b) {
+  if (!collectives(r)) return 0;
   HIP_TRY(hipStreamWaitEvent(r->stream, r->ready[b], 0));
   float* p = r->grad + r->lo[b];
   NCCL_TRY(ncclAllReduce(p, p, (size_t)(r->hi[b] - r->lo[b]), ncclFloat32, ncclAvg, r->comm, r->stream));
@@ -142,6 +150,7 @@ int lasr_reducer_create(lasr_reducer** out, const void* uid, int world, int rank
     release(r);
     return fail(rc, keep);
   }
+  r->world = world;
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof(id));
   ncclResult_t e = ncclCommInitRank(&r->comm, world, id, rank);
@@ -167,6 +176,9 @@ int lasr_reducer_create_from_comm(lasr_reducer** out, void* comm, int device, fl
     return fail(rc, keep);
   }
   r->comm = (ncclComm_t)comm;
+  int nranks = 0;
+  NCCL_TRY(ncclCommCount(r->comm, &nranks));
+  r->world = nranks;
   *out = r;
   return 0;
 }
@@ -177,7 +189,7 @@ int lasr_reducer_mark_grad_ready(lasr_reducer* r, int bucket, hipStream_t produc
   if (bucket < 0 || bucket >= n) return fail(-1, "bucket index out of range");
   if (r->marked[bucket]) return fail(-1, "bucket " + std::to_string(bucket) + " marked twice in one step");
   r->marked[bucket] = 1;
-  HIP_TRY(hipEventRecord(r->ready[bucket], producer));
+  if (collectives(r)) HIP_TRY(hipEventRecord(r->ready[bucket], producer));
   while (r->next < n && r->marked[r->next]) {
     if (int rc = launch(r, r->next)) return rc;
     ++r->next;
@@ -189,11 +201,13 @@ int lasr_reducer_finalize(lasr_reducer* r, hipStream_t consumer) {
   if (!r) return fail(-1, "null reducer");
   const int n = (int)r->lo.size();
   for (int b = r->next; b < n; ++b) {
-    if (!r->marked[b]) HIP_TRY(hipEventRecord(r->ready[b], consumer));
+    if (!r->marked[b] && collectives(r)) HIP_TRY(hipEventRecord(r->ready[b], consumer));
     if (int rc = launch(r, b)) return rc;
   }
-  HIP_TRY(hipEventRecord(r->done, r->stream));
-  HIP_TRY(hipStreamWaitEvent(consumer, r->done, 0));
+  if (collectives(r)) {
+    HIP_TRY(hipEventRecord(r->done, r->stream));
+    HIP_TRY(hipStreamWaitEvent(consumer, r->done, 0));
+  }
   std::fill(r->marked.begin(), r->marked.end(), 0);
   r->next = 0;
   return 0;
@@ -214,7 +228,25 @@ int lasr_reducer_rebind(lasr_reducer* r, float* grad, int64_t numel) {
     return fail(-1, "rebind: numel " + std::to_string(numel) + " != " + std::to_string(r->numel));
   if (r->next != 0 || std::find(r->marked.begin(), r->marked.end(), 1) != r->marked.end())
     return fail(-1, "rebind inside a step (buckets already marked)");
+  // the communicator, stream and events belong to r->device: a buffer on another device (a
+  // device move of the model) needs a new reducer, not a rebind
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, grad) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(-1, "rebind: the buffer is not device memory");
+  }
+  if (at.type != hipMemoryTypeDevice || at.device != r->device)
+    return fail(-1, "rebind: the buffer is on device " + std::to_string(at.device) + ", the reducer on device " +
+                        std::to_string(r->device) + " (a device move needs a new reducer)");
   r->grad = grad;
+  return 0;
+}
+
+int lasr_reducer_set_single_rank_collectives(lasr_reducer* r, int on) {
+  if (!r) return fail(-1, "null reducer");
+  if (r->next != 0 || std::find(r->marked.begin(), r->marked.end(), 1) != r->marked.end())
+    return fail(-1, "set_single_rank_collectives inside a step");
+  r->single_rank_collectives = on != 0;
   return 0;
 }
 

@@ -137,6 +137,10 @@ class FlatReducer:
         if self.native.grad_ptr() != g.data_ptr():
             if self.native.launched():  # buckets of this step already went out from the old buffer
                 raise RuntimeError("FlatReducer: the flat gradient buffer was replaced inside a step")
+            if not g.is_cuda or g.device.index != self.native.device:
+                raise RuntimeError(f"FlatReducer: the model's gradient moved to {g.device} but the native reducer "
+                                   f"(its RCCL communicator and stream) lives on cuda:{self.native.device}; "
+                                   "rebuild the DistributedDataParallel wrapper after a device move")
             self.native.rebind(g)
 
     def close(self):
@@ -229,20 +233,25 @@ class FlatReducer:
 
     def _verify_native(self):
         """Once, at the first step with world > 1: every bucket the C reducer averaged must equal
-        a torch.distributed average of the same pre-reduction gradient (the two communicators
-        may sum in different orders: fp32 tolerance)."""
+        a torch.distributed average of the same pre-reduction gradient.  The two communicators
+        may sum in different orders, so each element's bar is the fp32 summation bound of its
+        inputs, 4·world·2^-23 · (Σ_ranks |g|) / world, not a fraction of the averaged result
+        (which can be near zero where the ranks' gradients cancel)."""
         self._verify = False
         pre, self._pre = self._pre, None
         for bi, (lo, hi) in enumerate(self.native_spans()):
             ref = pre[bi]
+            mag = ref.abs()
             dist.all_reduce(ref, op=dist.ReduceOp.SUM, group=self.pg)
+            dist.all_reduce(mag, op=dist.ReduceOp.SUM, group=self.pg)
             ref.div_(self.world)
+            tol = mag.mul_(4.0 * 2.0 ** -23).add_(1e-30)  # (4·world·eps) · Σ|g| / world
             got = self.store.grad[lo:hi]
-            tol = 1e-5 * max(1.0, ref.abs().max().item())
-            err = (got - ref).abs().max().item()
-            if err > tol:
-                raise RuntimeError(f"native reducer: bucket {bi} differs from torch.distributed's average "
-                                   f"by {err:.3g} (tolerance {tol:.3g})")
+            bad = (got - ref).abs() > tol
+            if bool(bad.any()):
+                i = int(bad.nonzero()[0, 0])
+                raise RuntimeError(f"native reducer: bucket {bi} element {i} is {got[i].item():.9g}, "
+                                   f"torch.distributed's average {ref[i].item():.9g} (bound {tol[i].item():.3g})")
 
 
 class DistributedDataParallel(nn.Module):

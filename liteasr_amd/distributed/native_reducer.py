@@ -37,6 +37,7 @@ _SIGS = {
     "lasr_reducer_launched": (ctypes.c_int, [ctypes.c_void_p]),
     "lasr_reducer_reset": (ctypes.c_int, [ctypes.c_void_p]),
     "lasr_reducer_rebind": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "lasr_reducer_set_single_rank_collectives": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "lasr_reducer_grad": (ctypes.c_void_p, [ctypes.c_void_p]),
     "lasr_reducer_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "lasr_comm_last_error": (ctypes.c_char_p, []),
@@ -80,6 +81,7 @@ class NativeReducer:
         assert grad.is_cuda and grad.dtype == torch.float32 and grad.is_contiguous()
         L = load()
         self.grad = grad  # keeps the buffer alive as long as the reducer
+        self.device = grad.device.index
         n = len(buckets)
         lo = (ctypes.c_int64 * n)(*[int(b[0]) for b in buckets])
         hi = (ctypes.c_int64 * n)(*[int(b[1]) for b in buckets])
@@ -109,10 +111,21 @@ class NativeReducer:
         return load().lasr_reducer_grad(self._h) or 0
 
     def rebind(self, grad: torch.Tensor):
-        """Average ``grad`` from now on (same numel; between steps only)."""
-        assert grad.is_cuda and grad.dtype == torch.float32 and grad.is_contiguous()
+        """Average ``grad`` from now on (same numel, same device; between steps only).  The
+        communicator, stream and events belong to the creation device: a buffer on another
+        device is refused (here and by the C side)."""
+        assert grad.dtype == torch.float32 and grad.is_contiguous()
+        if not grad.is_cuda or grad.device.index != self.device:
+            raise RuntimeError(f"NativeReducer.rebind: the buffer is on {grad.device}, the reducer on cuda:{self.device} "
+                               "(a device move of the model needs a new DistributedDataParallel wrapper)")
         _check(load().lasr_reducer_rebind(self._h, grad.data_ptr(), grad.numel()), "lasr_reducer_rebind")
         self.grad = grad
+
+    def set_single_rank_collectives(self, on: bool):
+        """World 1 issues no collective by default (the average is the identity); ``on`` issues
+        the 1-rank RCCL all-reduces anyway, to measure their cost beside the backward."""
+        _check(load().lasr_reducer_set_single_rank_collectives(self._h, int(bool(on))),
+               "lasr_reducer_set_single_rank_collectives")
 
     def close(self):
         if self._h:

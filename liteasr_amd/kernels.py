@@ -539,7 +539,10 @@ def _fwd_mask(mask, msb, msq, B, Tq, Tk):
         return mask, msb, msq
     if msq % 16 == 0 and msb % 16 == 0 and mask.data_ptr() % 16 == 0:
         return mask, msb, msq
-    m = mask.reshape(-1).as_strided((B, Tq, Tk), (msb, msq, 1))
+    # element (b, i, j) sits at data_ptr + b*msb + i*msq + j of the caller's storage (the kernels'
+    # addressing): view that storage directly -- a reshape of a non-contiguous mask would copy it
+    # and leave msb / msq describing the original
+    m = torch.as_strided(mask, (B, Tq, Tk), (msb, msq, 1), mask.storage_offset())
     return pad_mask16(m, B, Tq, Tk)
 
 

@@ -134,10 +134,19 @@ def attention(q, k, v, mask, p: Params, name: str, H: int, pos=None, drop=0.0, t
     return linear(out, p, name + ".linear_o")
 
 
-def ffn(x, p: Params, name: str, act: str, drop=0.0, training=True):
-    """PositionwiseFeedForward: liteasr/nets/feed_forward.py:18-19, Swish swish.py:14-16."""
+def ffn(x, p: Params, name: str, act: str, drop=0.0, training=True, gate=None, pre=None):
+    """PositionwiseFeedForward: liteasr/nets/feed_forward.py:18-19, Swish swish.py:14-16.
+    Test hook (ReLU only): ``gate`` (0/1, the shape of the pre-activation) replaces the branch
+    relu takes, h = u * gate -- a parity test feeds the branch the GPU build took so that a
+    pre-activation within rounding of 0 takes the same side on both; ``pre`` collects u."""
     h = linear(x, p, name + ".fc1")
-    h = h * torch.sigmoid(h) if act == "swish" else F.relu(h)
+    if pre is not None:
+        pre.append(h.detach())
+    if gate is not None:
+        assert act == "relu"
+        h = h * gate.to(h.dtype).view_as(h)
+    else:
+        h = h * torch.sigmoid(h) if act == "swish" else F.relu(h)
     return linear(F.dropout(h, drop, training), p, name + ".fc2")
 
 
@@ -217,9 +226,10 @@ def encoder(xs, xlens, p: Params, cfg, bn_state=None, training=True, chunk: int 
     return layer_norm(x, p, "encoder.after_norm"), kmask
 
 
-def decoder(ys_in, dec_mask, memory, mem_mask, p: Params, cfg, training=True):
+def decoder(ys_in, dec_mask, memory, mem_mask, p: Params, cfg, training=True, gates=None, pre=None):
     """TransformerDecoder: liteasr/nets/transformer_decoder.py:70-93, DecoderLayer
-    liteasr/nets/transformer_layer.py:179-221 (pre-norm, ReLU FFN)."""
+    liteasr/nets/transformer_layer.py:179-221 (pre-norm, ReLU FFN).  ``gates`` / ``pre``: the
+    per-layer ReLU test hook of ``ffn``."""
     d = cfg["dec_dim"]
     H = cfg["dec_heads"]
     dr = cfg["dec_dropout"]
@@ -233,18 +243,21 @@ def decoder(ys_in, dec_mask, memory, mem_mask, p: Params, cfg, training=True):
         h = layer_norm(y, p, n + ".src_attn_norm")
         y = y + F.dropout(attention(h, memory, memory, mm, p, n + ".src_attn", H, None, 0.0, training), dr, training)
         h = layer_norm(y, p, n + ".feed_forward_norm")
-        y = y + F.dropout(ffn(h, p, n + ".feed_forward", "relu", cfg["dec_ff_dropout"], training), dr, training)
+        y = y + F.dropout(ffn(h, p, n + ".feed_forward", "relu", cfg["dec_ff_dropout"], training,
+                              gate=None if gates is None else gates[i], pre=pre), dr, training)
     y = layer_norm(y, p, "decoder.after_norm")
     return linear(y, p, "decoder.linear_out")
 
 
-def u2_forward(xs, xlens, ys, ylens, p: Params, cfg, bn_state=None, training=True, chunk=0):
-    """U2.forward: liteasr/models/u2.py:116-159.  Returns (h_attn, h_ctc, h_enc, tgt)."""
+def u2_forward(xs, xlens, ys, ylens, p: Params, cfg, bn_state=None, training=True, chunk=0, dec_gates=None,
+               dec_pre=None):
+    """U2.forward: liteasr/models/u2.py:116-159.  Returns (h_attn, h_ctc, h_enc, tgt).
+    ``dec_gates`` / ``dec_pre``: the decoder's ReLU test hook (``ffn``)."""
     V = cfg["vocab_size"]
     sos = eos = V - 1
     h_enc, kmask = encoder(xs, xlens, p, cfg, bn_state, training, chunk)
     ys_in, dec_mask, tgt = decoder_io(ys, ylens, sos, eos)
-    h_attn = decoder(ys_in, dec_mask, h_enc, kmask, p, cfg, training)
+    h_attn = decoder(ys_in, dec_mask, h_enc, kmask, p, cfg, training, dec_gates, dec_pre)
     h_ctc = linear(F.dropout(h_enc, cfg["dropout"], True), p, "ctc.ctc_lo")  # always on (ctc.py:29)
     return h_attn, h_ctc, h_enc, tgt
 
@@ -274,7 +287,7 @@ def noam_lr(step: int, model_dim: int, factor: float = 1.0, warmup: int = 25000)
 
 
 def train_step(params: Params, buffers: dict, batch, cfg, ctc_weight=0.3, smoothing=0.1,
-               clip=5.0, opt_state=None, model_dim=None, chunk=0, training=True):
+               clip=5.0, opt_state=None, model_dim=None, chunk=0, training=True, dec_gates=None, dec_pre=None):
     """One reference training iteration (accum_grad=1): liteasr/trainer.py:147-171 with
     torch.optim.Adam(betas=(0.9, 0.98), eps=1e-9) under Noam (noam.py:33-39).
     training=False runs the forward in eval mode (BN running statistics, no dropout but
@@ -283,7 +296,7 @@ def train_step(params: Params, buffers: dict, batch, cfg, ctc_weight=0.3, smooth
     xs, xlens, ys, ylens = batch
     names = [k for k in params if params[k].is_floating_point()]
     leaf = {k: params[k].detach().clone().requires_grad_() for k in names}
-    h_attn, h_ctc, _, tgt = u2_forward(xs, xlens, ys, ylens, leaf, cfg, buffers, training, chunk)
+    h_attn, h_ctc, _, tgt = u2_forward(xs, xlens, ys, ylens, leaf, cfg, buffers, training, chunk, dec_gates, dec_pre)
     loss, lc, la = hybrid_loss(h_attn, h_ctc, tgt, ys, xlens, ylens, ctc_weight, smoothing)
     loss.backward()
     grads = {k: (leaf[k].grad if leaf[k].grad is not None else torch.zeros_like(leaf[k])) for k in names}

@@ -38,9 +38,40 @@ def test_reducer_in_order_launch_and_identity(pg):
     torch.cuda.set_device(0)
     g = torch.randn(10000, device="cuda")
     ref = g.clone()
-    r = NativeReducer(g, [(0, 3000), (3000, 7000), (7000, 10000)], unique_id(), 1, 0)
+    uid = unique_id()
+    # world 1 issues nothing by default; with single-rank collectives on, every bucket is a real
+    # 1-rank ncclAllReduce on the reducer's stream (the path world > 1 takes)
+    for forced in (False, True):
+        g.copy_(ref)
+        r = NativeReducer(g, [(0, 3000), (3000, 7000), (7000, 10000)], uid if not forced else unique_id(), 1, 0)
+        try:
+            r.set_single_rank_collectives(forced)
+            _in_order(r, g, ref.clone())
+        finally:
+            r.close()
+
+
+def test_reducer_rebind_refuses_other_device_memory(pg):
+    """rebind accepts only device memory of the reducer's own device (its
+    communicator, stream and events stay there); host memory is refused by the Python check and
+    by the C side itself; a flag change inside a step is refused."""
+    import ctypes
+
+    from liteasr_amd.distributed.native_reducer import NativeReducer, load, unique_id
+
+    g = torch.zeros(4096, device="cuda")
+    r = NativeReducer(g, [(0, 4096)], unique_id(), 1, 0)
     try:
-        _in_order(r, g, ref)
+        host = torch.zeros(4096)
+        with pytest.raises(RuntimeError, match="needs a new DistributedDataParallel"):
+            r.rebind(host)
+        rc = load().lasr_reducer_rebind(r._h, ctypes.c_void_p(host.data_ptr()), 4096)
+        assert rc != 0 and b"not device memory" in load().lasr_comm_last_error()
+        assert r.grad_ptr() == g.data_ptr()
+        r.mark(0)
+        with pytest.raises(RuntimeError, match="inside a step"):
+            r.set_single_rank_collectives(True)
+        r.finalize()
     finally:
         r.close()
 

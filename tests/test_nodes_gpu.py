@@ -57,10 +57,10 @@ def _model(cfg, seed, chunk=0):
     return m.cuda().train(), params
 
 
-def _env(model, seed):
+def _env(model, seed, shape=(B, TX, L)):
     """The kernel env of a step on a config-2 batch (masks, rates, seeds), from one no-grad
     encoder pass; chained norms / batched position projections off for standalone calls."""
-    xs, xlens, ys, ylens = O.synthetic_batch(B, TX, L, model.ctc.ctc_lo.weight.shape[0], seed=seed)
+    xs, xlens, ys, ylens = O.synthetic_batch(*shape, model.ctc.ctc_lo.weight.shape[0], seed=seed)
     xs = xs.bfloat16().float()
     with torch.no_grad():
         _, prep, env = model._run_encoder(xs.cuda(), xlens.cuda(), ys.cuda(), ylens.cuda())
@@ -168,16 +168,22 @@ def test_subsampling_node_config2():
     _check(errs)
 
 
-def test_decoder_layer_node_config2():
+@pytest.mark.parametrize("shape,nsplit", [((B, TX, L), 1), ((8, 4000, 150), 4)], ids=["config2", "long"])
+def test_decoder_layer_node(shape, nsplit):
     """One DecoderLayer (liteasr/nets/transformer_layer.py:179-221: self / source attention,
-    ReLU FFN) + after_norm + linear_out (transformer_decoder.py:91-93) at B 32 x (L+1) 41
-    rows over a T' 249 memory, V 4233; the memory gradient included."""
+    ReLU FFN) + after_norm + linear_out (transformer_decoder.py:91-93), V 4233, the memory
+    gradient included: config 2 (B 32 x (L+1) 41 rows over a T' 249 memory) and the long
+    config (B 8 x (L+1) 151 rows over a T' 999 memory), where the source attention runs with
+    its keys split 4 ways (lasr_attn_split_count) and combined by the second launch."""
+    from liteasr_amd import kernels as K
     from liteasr_amd.nets import functional as FN
 
     cfg = O.default_cfg(enc_layers=1, dec_layers=1)
     model, params = _model(cfg, seed=51)
-    env, prep, _ = _env(model, seed=52)
+    env, prep, _ = _env(model, seed=52, shape=shape)
+    B = shape[0]
     T, d, L1 = prep.T, cfg["dec_dim"], prep.L + 1
+    assert K.attn_split(B, cfg["dec_heads"], L1, T, None) == nsplit, (B, L1, T)
     V = cfg["vocab_size"]
     g = torch.Generator().manual_seed(53)
     y_in = torch.randn(B * L1, d, generator=g)

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-4 GPU pass.  Usage: tools/gpu_r04.sh TAG STEP...; output under gpurun_out/TAG/.
+# GPU pass (round 5).  Usage: tools/gpu_r05.sh TAG STEP...; output under gpurun_out/TAG/.
 # Every step has its own time limit; the script stops at the first failure.
 set -u
-TAG=${1:-r04}; shift
+TAG=${1:-r05}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -31,9 +31,9 @@ for s in "$@"; do
            cp "$(find "$OUT/attn_trace" -name '*kernel_stats.csv' | head -1)" "$OUT/attn_kernel_stats.csv"; rm -rf "$OUT/attn_trace"
            S1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_INSTS_VALU"
            S2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_SCA"
-           i=0; for set in "$S1" "$S2"; do i=$((i+1))
-             run timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/ap$i" -o run -- python3 "$R/tools/attn_bench.py" > "$OUT/ap$i.log" 2>&1
-             run python3 "$R/tools/pmc_kernels.py" "$(find "$OUT/ap$i" -name '*.db' | head -1)" flash_ > "$OUT/attn_pmc_$i.json"; rm -rf "$OUT/ap$i"; done ;;
+           for cs in ${ATTN_CASES:-small long}; do i=0; for set in "$S1" "$S2"; do i=$((i+1))
+             run timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/ap$i" -o run -- python3 "$R/tools/attn_bench.py" $cs > "$OUT/ap$i.log" 2>&1
+             run python3 "$R/tools/pmc_kernels.py" "$(find "$OUT/ap$i" -name '*.db' | head -1)" flash_ > "$OUT/attn_pmc_${cs}_$i.json"; rm -rf "$OUT/ap$i"; done; done ;;
     kgpu) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py tests/test_row_ln_gpu.py > "$OUT/kgpu.log" 2>&1 ;;
     model) run timeout -k 10 900 $PYT tests/test_model_gpu.py tests/test_nodes_gpu.py -s > "$OUT/model.log" 2>&1 ;;
     smoke) run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
@@ -42,6 +42,13 @@ for s in "$@"; do
     long) run timeout -k 10 300 python3 bench.py --config long --no-cpu-baseline > "$OUT/bench_long.json" 2> "$OUT/bench_long.err" ;;
     large) run timeout -k 10 400 python3 bench.py --config large --no-cpu-baseline > "$OUT/bench_large.json" 2> "$OUT/bench_large.err" ;;
     ddp1) run timeout -k 10 300 python3 bench.py --force-ddp --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1.json" 2> "$OUT/bench_ddp1.err" ;;
+    ddpab) # world-1 A/B in one call: plain step, torch DDP, native DDP (no collective at world 1),
+           # native DDP with the 1-rank RCCL all-reduces forced (their cost beside the backward)
+           for rep in 1 2; do for v in plain torch native forced; do
+             case $v in plain) a="";; torch) a="--force-ddp";; native) a="--force-ddp --comm native";;
+               forced) a="--force-ddp --comm native --single-rank-collectives";; esac
+             run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 $a > "$OUT/ddpab_$v.json" 2> "$OUT/ddpab_$v.err"
+             grep "^{" "$OUT/ddpab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); a=d['config']['allreduce'] or {}; t=a.get('timeline_last_step') or {}; print(json.dumps({'arm': '$v', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'segment_ms': t.get('segment_ms'), 'exposed_comm_ms': t.get('exposed_comm_ms')}))" >> "$OUT/ddpab.jsonl"; done; done ;;
     ddp1n) run timeout -k 10 300 python3 bench.py --force-ddp --comm native --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1_native.json" 2> "$OUT/bench_ddp1_native.err" ;;
     tracefam) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_family" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 50 --roofline-case family > "$OUT/trace_family.log" 2>&1
            grep "^{" "$OUT/trace_family.log" | tail -1 > "$OUT/trace_family_meta.json"

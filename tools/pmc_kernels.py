@@ -1,8 +1,10 @@
 """Per-kernel SQ counter summary of a rocprofv3 --pmc pass (counters_collection table of the
 sqlite output): for each kernel name containing one of the given substrings, the mean per
-dispatch of every collected counter.
+dispatch of every collected counter, keyed by the library build (first 16 hex of its sha256).
     python tools/pmc_kernels.py <run_results.db> substr [substr ...]"""
+import hashlib
 import json
+import os
 import sqlite3
 import sys
 from collections import defaultdict
@@ -20,6 +22,9 @@ def main():
             acc[short][cn].append(v)
     out = {k: {cn: sum(v) / len(v) for cn, v in d.items()} | {"dispatches": max(len(v) for v in d.values())}
            for k, d in acc.items()}
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "liteasr_amd", "lib",
+                       "libliteasr_hip.so")
+    out["build"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
     print(json.dumps(out, indent=1))
 
 
