@@ -29,7 +29,29 @@
 namespace {
 
 constexpr int KB = 64;   // keys per block
-constexpr int GLD = 84;  // fp32 row stride of a wave's G' scratch ([16 queries][80 m] + pad)
+// A wave's G' scratch: [16 queries][80 m] fp32, query row `col` starting at float gro(col).
+// The row starts are chosen so that both the parking writes (ds_write_b128 of 4 consecutive m,
+// 8-lane groups) and the diagonal reads (ds_read_b32, lane (g, col) at gro(col) - col + 4g +
+// const) are bank-conflict free: gro(col) = 16-B aligned, gro(col) - col over the 16 rows
+// takes 16 residues mod 32 whose +4 shifts are the other 16, and each 8-row write group
+// starts its rows on 8 distinct 4-bank groups (a stride of 84 was 2-way conflicted on
+// every diagonal read).
+constexpr int GWAVE = 1500;  // floats per wave (gro(15) + 80)
+LASR_DEV int gro(int col) {
+  constexpr int t[16] = {0, 100, 188, 280, 364, 464, 552, 660, 760, 860, 948, 1040, 1124, 1224, 1312, 1420};
+  return t[col];
+}
+// The lane's two G' scratch addresses (bytes), computed once per kernel: the parking writes
+// (+64t) and the diagonal reads (+4(16c + e)).  (Inside the block loop the table lookup would be
+// re-issued as a global load behind every asm memory clobber, and its wait would drain the
+// LDS-DMA ring.)
+struct GAddr {
+  uint32_t wq, diag;
+};
+LASR_DEV GAddr gaddr(uint32_t gq, int lane) {
+  const int g = lane >> 4, col = lane & 15, r = gro(col);
+  return GAddr{gq + 4u * (uint32_t)(r + 4 * g), gq + 4u * (uint32_t)(r - col + 4 * g + 15)};
+}
 
 struct FlashP {
   const bf16_t *qu, *qv, *k, *v, *pos;  // qu/qv [B*T, ldq]; k/v [B*Tk, ldkv]; pos [T, ldp]
@@ -61,11 +83,14 @@ __device__ __attribute__((aligned(16))) bf16_t g_zero_row[64];
 
 // One image layout serves both MFMA operand orientations: row r of DK bf16, its 16-column
 // (32-B) slots XOR-swizzled by hq(r).  A row fragment (8 consecutive columns of one row,
-// ds_read_b128) and the transposed read (4 consecutive rows of one column,
-// ds_read_b64_tr_b16) are both bank-conflict free on it.
+// ds_read_b128: 16 rows per lane group) and the transposed read (4 consecutive rows of one
+// column, ds_read_b64_tr_b16: 8 rows x one 32-B slot per 32-lane group) are both bank-conflict
+// free on it.  d_k 64 (two rows per 256 B): the slot of the 4 same-parity rows of any 8
+// consecutive rows must differ, so hq = (r >> 1) & 3 (the round-4 form, bit 1 | bit 3 << 1,
+// was 2-way conflicted on every transposed read).
 template <int DK>
 LASR_DEV int hq(int r) {
-  if constexpr (DK == 64) return ((r >> 1) & 1) | ((r >> 2) & 2);
+  if constexpr (DK == 64) return (r >> 1) & 3;
   else return (r >> 2) & 1;
 }
 template <int DK>
@@ -268,7 +293,7 @@ LASR_DEV void load_q(const bf16_t* base, int64_t ld, int row, int h, int lane, b
 // read of the block (K and window fragments, mask words) is issued up front; counted waits
 // release the S products while the window reads are still landing.
 template <int DK, int NW, bool RP, bool RM>
-LASR_DEV bool scores_t(const FlashP& a, const char* st, float* gw, const uint8_t* km, const bf16x8 (&qu)[DK / 32],
+LASR_DEV bool scores_t(const FlashP& a, const char* st, GAddr ga, const uint8_t* km, const bf16x8 (&qu)[DK / 32],
                        const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int w, int i0, int j0, float c2,
                        int lane, f32x4 (&s)[4]) {
   using Gm = Geo<DK, NW, RP, RM>;
@@ -312,7 +337,6 @@ LASR_DEV bool scores_t(const FlashP& a, const char* st, float* gw, const uint8_t
   if constexpr (RP) {
     const int T = a.T;
     const int mlo = j0 - i0 + T - Gm::QB + wb;  // m of the wave's first window row
-    const uint32_t gq = ldsa(gw);
     lgkm<4>();  // the window fragments
 #pragma unroll
     for (int t = 0; t < 5; ++t)
@@ -338,11 +362,11 @@ LASR_DEV bool scores_t(const FlashP& a, const char* st, float* gw, const uint8_t
         for (int e = 0; e < 4; ++e) gsel[e] = lo + 4 * g + e <= T - 1 ? g1[e] : g2[e];
       }
       // G'[query col][m - mlo = 16t + 4g + e]
-      asm volatile("ds_write_b128 %0, %1" ::"v"(gq + 4u * (uint32_t)(col * GLD + 16 * t + 4 * g)), "v"(gsel) : "memory");
+      asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(ga.wq), "v"(gsel), "i"(64 * t) : "memory");
     }
     // diagonal: bd(query col, key 16c + 4g + e) = G'[col][16c + 4g + e - col + 15] (the wave's
     // own writes above retire first: LDS operations of a wave complete in order)
-    const uint32_t base = gq + 4u * (uint32_t)(col * (GLD - 1) + 4 * g + 15);
+    const uint32_t base = ga.diag;
     float v[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -425,19 +449,219 @@ LASR_DEV bool block_all_masked(const char* st, int w, int lane) {
 constexpr int KMASK_BYTES = 8192;  // Tk <= 8192 (host-checked)
 template <int DK, int NW, bool RP, bool RM>
 constexpr int fwd_lds() {
-  return 2 * Geo<DK, NW, RP, RM>::STAGE_BYTES + (RP ? NW * 16 * GLD * 4 : 0) + (RM ? 0 : KMASK_BYTES);
+  return 2 * Geo<DK, NW, RP, RM>::STAGE_BYTES + (RP ? NW * GWAVE * 4 : 0) + (RM ? 0 : KMASK_BYTES);
 }
 
+// ---- forward, pipelined -------------------------------------------------------------------
+// Per-lane LDS byte offsets of a block's fragment reads relative to its stage (computed once):
+// every read of a block is base + a compile-time immediate (rows +16 keep the swizzle), so the
+// address arithmetic per block is one add per base for the stage.
+template <int DK, int NW, bool RP, bool RM>
+struct FragOffs {
+  uint32_t k[DK / 32];   // K row fragments: key rows lane%16 (+16c), columns 32ks + 8(lane/16)
+  uint32_t w[DK / 32];   // the wave's window rows wb + lane%16 (+16t)
+  uint32_t v[DK / 16];   // transposed fragments of a [64][DK] image (V^T, K^T): rows 4(lane/16) + (lane/4)%4
+                         // (+32ks +16h), column slot t; relative to the image (region offset as immediate)
+};
+template <int DK, int NW, bool RP, bool RM>
+LASR_DEV FragOffs<DK, NW, RP, RM> frag_offs(int w, int lane) {
+  using Gm = Geo<DK, NW, RP, RM>;
+  FragOffs<DK, NW, RP, RM> o;
+  const int wb = 16 * (NW - 1 - w);
+#pragma unroll
+  for (int ks = 0; ks < DK / 32; ++ks) {
+    o.k[ks] = 2u * (uint32_t)toff<DK>(lane & 15, 32 * ks + 8 * (lane >> 4));
+    o.w[ks] = Gm::W0 * 16u + 2u * (uint32_t)toff<DK>(wb + (lane & 15), 32 * ks + 8 * (lane >> 4));
+  }
+#pragma unroll
+  for (int t = 0; t < DK / 16; ++t)
+    o.v[t] = 2u * (uint32_t)toff<DK>(4 * (lane >> 4) + ((lane >> 2) & 3), 16 * t + (lane & 3) * 4);
+  return o;
+}
+
+// A block's score-side fragments in registers: K (A operand of S^T), the window (A operand of
+// G'^T), the mask words of the lane's 4 keys per 16-key tile.
+template <int DK, bool RP>
+struct KWFrags {
+  v4i rk[4][DK / 32];
+  v4i rw[RP ? 5 : 1][DK / 32];
+  uint32_t mw[4];
+};
+
+// Issue (no wait) every score-side LDS read of the block in stage `sb` (LDS byte address):
+// 4*KS K fragments, then 5*KS window fragments (RP), then the 4 mask words -- in that order, so
+// counted lgkm waits release K first.  km: the key-padding byte image (!RM), row-relative.
+template <int DK, int NW, bool RP, bool RM>
+LASR_DEV void issue_kw(uint32_t sb, const FragOffs<DK, NW, RP, RM>& o, uint32_t kmaddr, int w, int lane,
+                       KWFrags<DK, RP>& f) {
+  using Gm = Geo<DK, NW, RP, RM>;
+  constexpr int KS = DK / 32;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const uint32_t a = sb + o.k[ks];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f.rk[c][ks]) : "v"(a), "i"(c * 16 * DK * 2));
+  }
+  if constexpr (RP) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint32_t a = sb + o.w[ks];
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f.rw[t][ks]) : "v"(a), "i"(t * 16 * DK * 2));
+    }
+  }
+  const int g = lane >> 4, col = lane & 15;
+  const uint32_t mimg = RM ? sb + Gm::M0 * 16u + (uint32_t)((16 * w + col) * KB + 4 * g) : kmaddr + (uint32_t)(4 * g);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(f.mw[c]) : "v"(mimg), "i"(16 * c));
+}
+
+// One relative-position window tile G'^T (16 m x 16 queries) against qv (rows m <= T) or qv1
+// (rows m >= T): the window's row m = T is a zero row, so a tile on one side of it needs one
+// operand; the tile that straddles it takes both and selects per element.
+template <int KS>
+LASR_DEV f32x4 gtile(const v4i (&rw)[KS], const bf16x8 (&qv)[KS], const bf16x8 (&qv1)[KS], int lo, int T, int g) {
+  f32x4 r;
+  if (lo + 15 <= T) {
+    r = mfma(as_frag(rw[0]), qv[0], zero4());
+#pragma unroll
+    for (int ks = 1; ks < KS; ++ks) r = mfma(as_frag(rw[ks]), qv[ks], r);
+  } else if (lo >= T) {
+    r = mfma(as_frag(rw[0]), qv1[0], zero4());
+#pragma unroll
+    for (int ks = 1; ks < KS; ++ks) r = mfma(as_frag(rw[ks]), qv1[ks], r);
+  } else {
+    f32x4 g1 = mfma(as_frag(rw[0]), qv[0], zero4()), g2 = mfma(as_frag(rw[0]), qv1[0], zero4());
+#pragma unroll
+    for (int ks = 1; ks < KS; ++ks) {
+      g1 = mfma(as_frag(rw[ks]), qv[ks], g1);
+      g2 = mfma(as_frag(rw[ks]), qv1[ks], g2);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = lo + 4 * g + e <= T - 1 ? g1[e] : g2[e];
+  }
+  return r;
+}
+
+// Scaled + masked transposed scores (log2 units) of the lane's query against the block's 64
+// keys from fragments already in registers (issue_kw): s[c][e] for key j0 + 16c + 4(lane/16) + e.
+// Same products, sums and roundings as scores_t.  Returns whether a per-element select was
+// needed (masked key or the last block).
+template <int DK, int NW, bool RP, bool RM>
+LASR_DEV bool scores_kw(const FlashP& a, KWFrags<DK, RP>& f, GAddr ga, const bf16x8 (&qu)[DK / 32],
+                        const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int mlo, int j0, float c2,
+                        int lane, f32x4 (&s)[4]) {
+  constexpr int KS = DK / 32, NWT = RP ? 5 : 0;
+  const int g = lane >> 4, col = lane & 15;
+  lgkm<NWT * KS + 4>();  // the K fragments
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) keep(f.rk[c][ks]);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    f32x4 acc = mfma(as_frag(f.rk[c][0]), qu[0], zero4());
+#pragma unroll
+    for (int ks = 1; ks < KS; ++ks) acc = mfma(as_frag(f.rk[c][ks]), qu[ks], acc);
+    s[c] = acc;
+  }
+  float bd[4][4];
+  if constexpr (RP) {
+    const int T = a.T;
+    lgkm<4>();  // the window fragments
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) keep(f.rw[t][ks]);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const f32x4 gt = gtile<KS>(f.rw[t], qv, qv1, mlo + 16 * t, T, g);
+      // G'[query col][m - mlo = 16t + 4g + e]
+      asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(ga.wq), "v"(gt), "i"(64 * t) : "memory");
+    }
+    // diagonal: bd(query col, key 16c + 4g + e) = G'[col][16c + 4g + e - col + 15] (the wave's
+    // own writes above retire first: LDS operations of a wave complete in order)
+    const uint32_t base = ga.diag;
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[4 * c + e]) : "v"(base), "i"(4 * (16 * c + e)));
+    lgkm0();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        keep(v[4 * c + e]);
+        bd[c][e] = v[4 * c + e];
+      }
+  } else {
+    lgkm0();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bd[c][e] = 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) keep(f.mw[c]);
+  const lasr_f2 c2v = {c2, c2};
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      lasr_f2 x = {s[c][e], s[c][e + 1]};
+      const lasr_f2 y = {bd[c][e], bd[c][e + 1]};
+      x = (x + y) * c2v;
+      s[c][e] = x[0];
+      s[c][e + 1] = x[1];
+    }
+  const bool anym = __builtin_amdgcn_ballot_w64((f.mw[0] | f.mw[1] | f.mw[2] | f.mw[3]) != 0u) != 0;
+  if (anym) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[c][e] = (f.mw[c] >> (8 * e)) & 0xffu ? -1e38f : s[c][e];
+  }
+  const bool tail = j0 + KB > a.Tk;
+  if (tail) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j0 + 16 * c + 4 * g + e >= a.Tk) s[c][e] = -INFINITY;
+  }
+  return anym || tail;
+}
+
+// max over the 4 lane groups of a column (lanes l, l^16, l^32, l^48) on the VALU: the gfx950
+// row swaps (v_permlane16_swap: rows 0<->1, 2<->3; v_permlane32_swap: halves), no LDS round trip
+LASR_DEV float xmax_rows(float v) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = fmaxf(__builtin_bit_cast(float, (uint32_t)a[0]), __builtin_bit_cast(float, (uint32_t)a[1]));
+  const uint32_t u2 = __builtin_bit_cast(uint32_t, v);
+  const auto b = __builtin_amdgcn_permlane32_swap(u2, u2, false, false);
+  return fmaxf(__builtin_bit_cast(float, (uint32_t)b[0]), __builtin_bit_cast(float, (uint32_t)b[1]));
+}
+
+// Forward.  A two-stage ring with the block barrier in the middle of a block: once a wave's
+// reads of block j's stage are all issued and landed (the V^T fragments, read during the
+// softmax), the barrier retires that stage, the DMA of block j+2 goes into it, and block j+1's
+// score-side fragments are read into registers while block j's P.V products run -- the next
+// block starts with its K / window / mask fragments landed.  The running max only rescales O
+// and the running sum when some lane's max grew (al = 1 exactly otherwise): bit-identical.
 template <int DK, int NW, bool RP, bool RM>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
   using Gm = Geo<DK, NW, RP, RM>;
   constexpr int KS = DK / 32, NT = Gm::NT;
   __shared__ __attribute__((aligned(16))) char smem[fwd_lds<DK, NW, RP, RM>()];
   char* ring = smem;                                   // 2 stages
-  float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);   // RP: NW x [16][GLD]
-  uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * 16 * GLD : 0));  // !RM: key padding bytes
+  float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);   // RP: NW x GWAVE floats
+  uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * GWAVE : 0));  // !RM: key padding bytes
   // the wave index through readfirstlane: wave-uniform values derived from it stay in SGPRs
-  // (uniform branches and scalar address arithmetic instead of exec-masked vector code)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             col = lane & 15;
   const int h = blockIdx.y, b = blockIdx.z, T = a.T, Tk = a.Tk;
@@ -448,7 +672,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
   const float c2 = a.scale * 1.4426950408889634f;
 
   issue_stage<DK, NW, RP, RM>(a, b, h, i0, jb0 * KB, ring, tid);
-  const uint8_t* km = kmask;
+  if (jb0 + 1 < jb1) issue_stage<DK, NW, RP, RM>(a, b, h, i0, (jb0 + 1) * KB, ring + Gm::STAGE_BYTES, tid);
   if constexpr (!RM) {  // key padding bytes of this utterance (zeros without a mask; keys >= Tk are -inf anyway)
     const uint8_t* mr = a.mask ? a.mask + (int64_t)b * a.msb : nullptr;
     const int kpad = nb * KB;
@@ -460,94 +684,124 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
     load_q<DK>(a.qv, a.ldq, b * T + min(iq, T - 1), h, lane, qv);
     load_q<DK>(a.qv, a.ldq, b * T + min(iq + 1, T - 1), h, lane, qv1);
   }
-  float* gw = gsh + w * 16 * GLD;
+  const FragOffs<DK, NW, RP, RM> fo = frag_offs<DK, NW, RP, RM>(w, lane);
+  const uint32_t ring0 = ldsa(ring), kmaddr = ldsa(kmask);
+  const GAddr ga = gaddr(ldsa(gsh + w * GWAVE), lane);
   float mrun = -INFINITY, lrun = 0.f;
   f32x4 o[DK / 16];
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) o[t] = zero4();
 
+  KWFrags<DK, RP> f;
+  wait_vmcnt<0>();  // both stages' pieces and the Q loads
+  lds_barrier();    // ... of every wave, and the key-padding bytes
+  issue_kw<DK, NW, RP, RM>(ring0, fo, kmaddr + (uint32_t)(jb0 * KB), w, lane, f);
   for (int jb = jb0; jb < jb1; ++jb) {
     const int j0 = jb * KB;
-    char* st = ring + ((jb - jb0) & 1) * Gm::STAGE_BYTES;
-    wait_vmcnt<0>();  // this block's pieces (issued one block ago) and the Q loads
-    lds_barrier();    // ... of every wave; every wave is done with block jb-1's stage
-    if (jb + 1 < jb1)
-      issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb - jb0 + 1) & 1) * Gm::STAGE_BYTES, tid);
+    const int stg = (jb - jb0) & 1;
+    const uint32_t sb = ring0 + (uint32_t)(stg * Gm::STAGE_BYTES);
+    bool skip = false;
     if constexpr (RM) {  // (the streaming chunk mask: the blocks of future chunks)
-      if (__builtin_amdgcn_ballot_w64(mrun <= -1e38f) == 0 && block_all_masked<DK, NW, RP, RM>(st, w, lane)) continue;
+      bool zero_byte = false;
+      lgkm0();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        keep(f.mw[c]);
+        zero_byte |= ((f.mw[c] - 0x01010101u) & ~f.mw[c] & 0x80808080u) != 0u;
+      }
+      skip = __builtin_amdgcn_ballot_w64(mrun <= -1e38f) == 0 && __builtin_amdgcn_ballot_w64(zero_byte) == 0;
     }
     f32x4 s[4];
-    (void)scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
-    // V^T fragments for O^T += V^T P^T, in flight during the softmax (k slots of sub-block ks:
-    // keys 32ks + 4g + e, then 32ks + 16 + 4g + e)
-    const uint32_t vimg = ldsa(st + Gm::V0 * 16);
     v2i lo[2][DK / 16], hi[2][DK / 16];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) {
-        lo[ks][t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 4 * g, 16 * t, lane));
-        hi[ks][t] = lds_tr(frag_tr_addr<DK>(vimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
-      }
-    // online softmax (one query per lane; the 4 lane groups of a query share its max)
-    float bm = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
-                     fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
-    bm = fmaxf(bm, fmaxf(fmaxf(fmaxf(s[2][0], s[2][1]), fmaxf(s[2][2], s[2][3])),
-                         fmaxf(fmaxf(s[3][0], s[3][1]), fmaxf(s[3][2], s[3][3]))));
-    bm = xmax16_32(bm);
-    const float mn = fmaxf(mrun, bm);
-    const float al = __builtin_amdgcn_exp2f(mrun - mn);
-    const lasr_f2 mnv = {mn, mn};
-    lasr_f2 sum2 = {0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        lasr_f2 x = {s[c][e], s[c][e + 1]};
-        x -= mnv;
-        x[0] = __builtin_amdgcn_exp2f(x[0]);
-        x[1] = __builtin_amdgcn_exp2f(x[1]);
-        s[c][e] = x[0];
-        s[c][e + 1] = x[1];
-        sum2 += x;
-      }
-    lrun = lrun * al + (sum2[0] + sum2[1]);
-    mrun = mn;
-#pragma unroll
-    for (int t = 0; t < DK / 16; ++t) o[t] *= al;
-    lgkm0();
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    if (!skip) {
+      (void)scores_kw<DK, NW, RP, RM>(a, f, ga, qu, qv, qv1, j0 - iw + T - 16, j0, c2, lane, s);
+      // V^T fragments for O^T += V^T P^T, in flight during the softmax (k slots of sub-block ks:
+      // keys 32ks + 4g + e, then 32ks + 16 + 4g + e)
 #pragma unroll
       for (int t = 0; t < DK / 16; ++t) {
-        keep(lo[ks][t]);
-        keep(hi[ks][t]);
+        const uint32_t va = sb + fo.v[t];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[ks][t]) : "v"(va), "i"(Gm::V0 * 16 + 32 * ks * DK * 2));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[ks][t])
+                       : "v"(va), "i"(Gm::V0 * 16 + (32 * ks + 16) * DK * 2));
+        }
       }
+      float bm = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                       fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+      bm = fmaxf(bm, fmaxf(fmaxf(fmaxf(s[2][0], s[2][1]), fmaxf(s[2][2], s[2][3])),
+                           fmaxf(fmaxf(s[3][0], s[3][1]), fmaxf(s[3][2], s[3][3]))));
+      bm = xmax_rows(bm);
+      const float mn = fmaxf(mrun, bm);
+      float al = 1.f;
+      if (__builtin_amdgcn_ballot_w64(mn > mrun) != 0) {  // some lane's max grew: rescale (al = 1 elsewhere)
+        al = __builtin_amdgcn_exp2f(mrun - mn);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pb = pack8(s[2 * ks], s[2 * ks + 1]);
+        for (int t = 0; t < DK / 16; ++t) o[t] *= al;
+      }
+      mrun = mn;
+      const lasr_f2 mnv = {mn, mn};
+      lasr_f2 sum2 = {0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < DK / 16; ++t) o[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), pb, o[t]);
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          lasr_f2 x = {s[c][e], s[c][e + 1]};
+          x -= mnv;
+          x[0] = __builtin_amdgcn_exp2f(x[0]);
+          x[1] = __builtin_amdgcn_exp2f(x[1]);
+          s[c][e] = x[0];
+          s[c][e + 1] = x[1];
+          sum2 += x;
+        }
+      lrun = lrun * al + (sum2[0] + sum2[1]);
+    }
+    // mid-block: retire this block's stage, refill it with block jb+2, read block jb+1's
+    // score-side fragments (landed by the next iteration)
+    if (jb + 1 < jb1) {
+      wait_vmcnt<0>();  // block jb+1's pieces (issued a block ago)
+      lds_barrier();    // ... of every wave; every wave is done with this stage (the V^T reads landed)
+      if (jb + 2 < jb1) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + 2 * KB, ring + stg * Gm::STAGE_BYTES, tid);
+      issue_kw<DK, NW, RP, RM>(ring0 + (uint32_t)((stg ^ 1) * Gm::STAGE_BYTES), fo,
+                               kmaddr + (uint32_t)(j0 + KB), w, lane, f);
+    } else if (!skip) {
+      lgkm0();
+    }
+    if (!skip) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int t = 0; t < DK / 16; ++t) {
+          keep(lo[ks][t]);
+          keep(hi[ks][t]);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pb = pack8(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+        for (int t = 0; t < DK / 16; ++t) o[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), pb, o[t]);
+      }
     }
   }
   // statistics in scaled-score units (max * ln 2), 1/sum: P = exp(S - max) / sum
-  const float l = xsum16_32(lrun);
+  const float l = lrun + __shfl_xor(lrun, 16, 64);
+  const float lsum = l + __shfl_xor(l, 32, 64);
   if (ns > 1) {  // a key split: unnormalised O, running max (log2 units) and sum, for the combine
     if (iq < T) {
       const int64_t row = (int64_t)sp * a.B * a.H * T + ((int64_t)b * a.H + h) * T + iq;
-      if (g == 0) *(float2*)(a.mpart + 2 * row) = make_float2(mrun, l);
+      if (g == 0) *(float2*)(a.mpart + 2 * row) = make_float2(mrun, lsum);
       float* op = a.opart + row * DK + 4 * g;
 #pragma unroll
       for (int t = 0; t < DK / 16; ++t) *(f32x4*)(op + 16 * t) = o[t];
     }
     return;
   }
-  const float il = 1.f / l;
+  const float il = 1.f / lsum;
   if (iq < T) {
     if (g == 0) {  // a fully masked row keeps the masked score itself as its max (uniform P)
-      float* sp = a.stats + 2 * (((int64_t)b * a.H + h) * T + iq);
-      sp[0] = mrun <= -1e38f ? -1e38f : mrun * 0.6931471805599453f;
-      sp[1] = il;
+      float* spp = a.stats + 2 * (((int64_t)b * a.H + h) * T + iq);
+      spp[0] = mrun <= -1e38f ? -1e38f : mrun * 0.6931471805599453f;
+      spp[1] = il;
     }
     bf16_t* dst = a.ctx + ((int64_t)b * T + iq) * a.ldc + h * DK + 4 * g;
 #pragma unroll
@@ -572,7 +826,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
   __shared__ __attribute__((aligned(16))) char smem[fwd_lds<DK, NW, RP, RM>()];
   char* ring = smem;
   float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);
-  uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * 16 * GLD : 0));
+  uint8_t* kmask = (uint8_t*)(gsh + (RP ? NW * GWAVE : 0));
   // the wave index through readfirstlane: wave-uniform values derived from it stay in SGPRs
   // (uniform branches and scalar address arithmetic instead of exec-masked vector code)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
@@ -586,7 +840,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
   const int64_t zrow = ((int64_t)b * a.H + h) * T;
 
   issue_stage<DK, NW, RP, RM>(a, b, h, i0, jb0 * KB, ring, tid);
-  const uint8_t* km = kmask;
+  if (jb0 + 1 < jb1) issue_stage<DK, NW, RP, RM>(a, b, h, i0, (jb0 + 1) * KB, ring + Gm::STAGE_BYTES, tid);
   if constexpr (!RM) {  // key padding bytes of this utterance (zeros without a mask; keys >= Tk are -inf anyway)
     const uint8_t* mr = a.mask ? a.mask + (int64_t)b * a.msb : nullptr;
     const int kpad = nb * KB;
@@ -621,58 +875,77 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
     if (g == 0 && iq < T && sp == 0) a.Dbuf[zrow + iq] = D;
   }
   bf16_t* dbd = RP ? a.dbd + (a.dbd_hb ? ((int64_t)h * a.B + b) * T : zrow) * a.ldS : nullptr;
-  float* gw = gsh + w * 16 * GLD;
+  const GAddr ga = gaddr(ldsa(gsh + w * GWAVE), lane);
   f32x4 dq[DK / 16];
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) dq[t] = zero4();
 
+  const FragOffs<DK, NW, RP, RM> fo = frag_offs<DK, NW, RP, RM>(w, lane);
+  const uint32_t ring0 = ldsa(ring), kmaddr = ldsa(kmask);
+  KWFrags<DK, RP> f;
+  wait_vmcnt<0>();  // both stages' pieces and the row loads
+  lds_barrier();    // ... of every wave, and the key-padding bytes
+  // the block barrier sits after the block's last reads of its stage (the K^T fragments,
+  // consumed by the dQ products), where the stage is refilled with block jb+2 while the dBD
+  // stores go out; the next block's score-side fragments are read at its start (prefetched
+  // beside this block's live values they would spill at d_k 64)
   for (int jb = jb0; jb < jb1; ++jb) {
     const int j0 = jb * KB;
-    char* st = ring + ((jb - jb0) & 1) * Gm::STAGE_BYTES;
-    wait_vmcnt<0>();
-    lds_barrier();
-    if (jb + 1 < jb1)
-      issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + KB, ring + ((jb - jb0 + 1) & 1) * Gm::STAGE_BYTES, tid);
+    const int stg = (jb - jb0) & 1;
+    const uint32_t sb = ring0 + (uint32_t)(stg * Gm::STAGE_BYTES);
+    issue_kw<DK, NW, RP, RM>(sb, fo, kmaddr + (uint32_t)j0, w, lane, f);
     f32x4 s[4];
     bool skip = false;
-    if constexpr (RM) skip = rows_live && block_all_masked<DK, NW, RP, RM>(st, w, lane);
+    if constexpr (RM) {
+      bool zero_byte = false;
+      lgkm0();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        keep(f.mw[c]);
+        zero_byte |= ((f.mw[c] - 0x01010101u) & ~f.mw[c] & 0x80808080u) != 0u;
+      }
+      skip = rows_live && __builtin_amdgcn_ballot_w64(zero_byte) == 0;
+    }
+    v2i lo[2][DK / 16], hi[2][DK / 16];
     if (skip) {  // dS = 0 over the block: only its (zero) dBD entries are written
 #pragma unroll
       for (int c = 0; c < 4; ++c) s[c] = zero4();
     } else {
-    const bool msk = scores_t<DK, NW, RP, RM>(a, st, gw, km, qu, qv, qv1, w, i0, j0, c2, lane, s);
-    // V fragments for dP^T = V . dO^T (V rows = keys as the A operand), then the K^T
-    // fragments for dQu^T += K^T dS^T, in flight during dP and dS
-    const uint32_t vimg = ldsa(st + Gm::V0 * 16), kimg = ldsa(st);
-    v4i rv[4][KS];
+      const bool msk = scores_kw<DK, NW, RP, RM>(a, f, ga, qu, qv, qv1, j0 - iw + T - 16, j0, c2, lane, s);
+      // V fragments for dP^T = V . dO^T (V rows = keys as the A operand), then the K^T
+      // fragments for dQu^T += K^T dS^T, in flight during dP and dS
+      v4i rv[4][KS];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint32_t va = sb + fo.k[ks];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) rv[c][ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * c, 32 * ks, lane));
-    v2i lo[2][DK / 16], hi[2][DK / 16];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+        for (int c = 0; c < 4; ++c)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(rv[c][ks]) : "v"(va), "i"(Gm::V0 * 16 + c * 16 * DK * 2));
+      }
 #pragma unroll
       for (int t = 0; t < DK / 16; ++t) {
-        lo[ks][t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 4 * g, 16 * t, lane));
-        hi[ks][t] = lds_tr(frag_tr_addr<DK>(kimg, 32 * ks + 16 + 4 * g, 16 * t, lane));
+        const uint32_t ka = sb + fo.v[t];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo[ks][t]) : "v"(ka), "i"(32 * ks * DK * 2));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[ks][t]) : "v"(ka), "i"((32 * ks + 16) * DK * 2));
+        }
       }
-    lgkm<(4 * DK / 16 > 15 ? 15 : 4 * DK / 16)>();  // the V fragments (older than the K^T reads)
+      lgkm<(4 * DK / 16 > 15 ? 15 : 4 * DK / 16)>();  // the V fragments (older than the K^T reads)
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) keep(rv[c][ks]);
-    f32x4 dp[4];
+        for (int ks = 0; ks < KS; ++ks) keep(rv[c][ks]);
+      f32x4 dp[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      f32x4 acc = zero4();
+      for (int c = 0; c < 4; ++c) {
+        f32x4 acc = mfma(as_frag(rv[c][0]), dof[0], zero4());
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(rv[c][ks]), dof[ks], acc);
-      dp[c] = acc;
-    }
-    // dS = P (dP - D), zero where masked or past Tk (the forward's masked_fill backward), on
-    // packed fp32 pairs (the same roundings per element); the select only in masked blocks
-    {
+        for (int ks = 1; ks < KS; ++ks) acc = mfma(as_frag(rv[c][ks]), dof[ks], acc);
+        dp[c] = acc;
+      }
+      // dS = P (dP - D), zero where masked or past Tk (the forward's masked_fill backward), on
+      // packed fp32 pairs (the same roundings per element); the select only in masked blocks
       const lasr_f2 m2v = {m2, m2}, ilv = {il, il}, Dv = {D, D};
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -682,8 +955,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
           lasr_f2 x = v - m2v;
           x[0] = __builtin_amdgcn_exp2f(x[0]);
           x[1] = __builtin_amdgcn_exp2f(x[1]);
-          const lasr_f2 d = {dp[c][e], dp[c][e + 1]};
-          x = (x * ilv) * (d - Dv);
+          const lasr_f2 dd = {dp[c][e], dp[c][e + 1]};
+          x = (x * ilv) * (dd - Dv);
           s[c][e] = x[0];
           s[c][e + 1] = x[1];
           if (msk) {
@@ -692,21 +965,30 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
           }
         }
     }
-    lgkm0();
+    if (!skip) {
+      lgkm0();  // the K^T fragments
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int t = 0; t < DK / 16; ++t) {
-        keep(lo[ks][t]);
-        keep(hi[ks][t]);
+        for (int t = 0; t < DK / 16; ++t) {
+          keep(lo[ks][t]);
+          keep(hi[ks][t]);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 db = pack8(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+        for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), db, dq[t]);
       }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 db = pack8(s[2 * ks], s[2 * ks + 1]);
-#pragma unroll
-      for (int t = 0; t < DK / 16; ++t) dq[t] = mfma(as_frag(lo[ks][t], hi[ks][t]), db, dq[t]);
     }
-    }  // !skip
+    // this block's reads of its stage are done: retire it, refill it with block jb+2 and read
+    // block jb+1's score-side fragments while the dBD stores go out (placed after the dQ
+    // products, whose K^T fragments would otherwise be live beside the next block's)
+    if (jb + 1 < jb1) {
+      wait_vmcnt<0>();  // block jb+1's pieces (and the previous block's dBD stores)
+      lds_barrier();
+      if (jb + 2 < jb1) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + 2 * KB, ring + stg * Gm::STAGE_BYTES, tid);
+    }
     if constexpr (RP) {
       // inverse rel_shift: the bd entry each score read (none for j == i + 1).  A lane's 4 keys
       // of a tile land on 4 consecutive columns of one dBD row unless they straddle the
@@ -809,7 +1091,14 @@ void launch_flash_bwd_q(const FlashP& a, int dk, bool rp, bool rm, hipStream_t s
 // The positional term: a wave's 16 keys x 16 queries span 31 window rows: two MFMA tiles of
 // G[query][m], parked [m][query] in the wave's scratch and read along the diagonal.
 constexpr int QBK = 64;   // queries per block of the key-side kernel
-constexpr int KLD = 20;   // fp32 row stride of its G scratch ([32 m][16 queries] + pad)
+// Its G scratch: [16 queries][32 m] fp32 per wave, query row q at float kro(q), parked by
+// ds_write_b32 and read along the diagonal by ds_read_b32.  kro(4 + e) - kro(e) = 20 (mod 32)
+// makes every diagonal read conflict free (the round-4 [32 m][16 queries] image, parked by
+// b128 writes, was 4-way conflicted on those reads: 16-B aligned rows put all 32 lanes of a
+// read on the 8 banks of one residue mod 4); the parking writes are at most 2-way, which costs
+// a b32 store nothing.
+constexpr int KWAVE = 564;  // floats per wave (kro(15) + 32)
+LASR_DEV int kro(int q) { return 32 * q + 20 * ((q >> 2) & 1) + 32 * (q >> 3); }
 
 template <int DK, int NW, bool RP, bool RM>
 struct GeoKV {
@@ -827,7 +1116,7 @@ struct GeoKV {
   static_assert(Q_CH % 64 == 0 && QV_CH % 64 == 0 && M_CH % 64 == 0 && W_CH % 64 == 0, "wave-aligned regions");
   static_assert(!RP || W_ROWS >= QBK + KBW - 1, "window rows");
   static_assert(RP || W_CH == 0, "no window without the positional term");
-  static constexpr int LDS = 2 * STAGE_BYTES + (RP ? NW * 32 * KLD * 4 : 0) + 2 * 3 * QBK * 4;
+  static constexpr int LDS = 2 * STAGE_BYTES + (RP ? NW * KWAVE * 4 : 0) + 2 * 3 * QBK * 4;
 };
 
 template <int DK, int NW, bool RP, bool RM>
@@ -903,7 +1192,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
   __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
   char* ring = smem;
   float* gsh = (float*)(smem + 2 * Gm::STAGE_BYTES);
-  float* sst = gsh + (RP ? NW * 32 * KLD : 0);  // [2][3][QBK]: m (log2 units), 1/sum, D
+  float* sst = gsh + (RP ? NW * KWAVE : 0);  // [2][3][QBK]: m (log2 units), 1/sum, D
   // the wave index through readfirstlane: wave-uniform values derived from it stay in SGPRs
   // (uniform branches and scalar address arithmetic instead of exec-masked vector code)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
@@ -932,7 +1221,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
     st_d = a.Dbuf[zrow + ic];
   };
   if (w == 0) load_stats(0);
-  float* gk = gsh + w * 32 * KLD;
+  float* gk = gsh + w * KWAVE;
   f32x4 dkt[DK / 16], dvt[DK / 16];
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) { dkt[t] = zero4(); dvt[t] = zero4(); }
@@ -1048,19 +1337,22 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
 #pragma unroll
               for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(av1[ks]), as_frag(bw[uu][ks]), g2);
             }
-            // lane (g, col) holds G[query 4g + e][m = lo + col]: select by m <= T - 1, park as [m][query]
+            // lane (g, col) holds G[query 4g + e][m = lo + col]: select by m <= T - 1, park as
+            // [query][m] (row 4g + e at kro(4g + e))
             f32x4 gs = n2 ? g2 : g1;
             if (n1 && n2) gs = lo + col <= T - 1 ? g1 : g2;
-            asm volatile("ds_write_b128 %0, %1" ::"v"(gka + 4u * (uint32_t)((16 * uu + col) * KLD + 4 * g)), "v"(gs)
-                         : "memory");
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(gka + 4u * (uint32_t)(kro(4 * g + e) + col)),
+                           "v"(gs[e]), "i"(64 * uu) : "memory");
           }
           // bd(query 4g + e, key col) = G[4g + e][m - mlo = col - 4g - e + 15] (the wave's writes
           // above retire first)
-          const uint32_t ba = gka + 4u * (uint32_t)((col - 4 * g + 12) * KLD + 4 * g + 3);
           float v[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[e]) : "v"(ba), "i"(4 * ((3 - e) * KLD - (3 - e))));
+            asm volatile("ds_read_b32 %0, %1" : "=v"(v[e])
+                         : "v"(gka + 4u * (uint32_t)(kro(4 * g + e) + col - 4 * g - e + 15)));
           lgkm0();
 #pragma unroll
           for (int e = 0; e < 4; ++e) {

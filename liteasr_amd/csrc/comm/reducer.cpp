@@ -235,7 +235,8 @@ int lasr_reducer_rebind(lasr_reducer* r, float* grad, int64_t numel) {
     (void)hipGetLastError();
     return fail(-1, "rebind: the buffer is not device memory");
   }
-  if (at.type != hipMemoryTypeDevice || at.device != r->device)
+  if (at.type != hipMemoryTypeDevice) return fail(-1, "rebind: the buffer is not device memory");
+  if (at.device != r->device)
     return fail(-1, "rebind: the buffer is on device " + std::to_string(at.device) + ", the reducer on device " +
                         std::to_string(r->device) + " (a device move needs a new reducer)");
   r->grad = grad;

@@ -108,8 +108,11 @@ def run_case(cfg_o, B, T, L, dtype, chunk=0, ctc_weight=0.3, seed=0, training=Tr
     h_attn, h_ctc = rec["out"]
     gates = None
     if feed_dec_gates:  # the heads node's saved decoder state (HeadsFn ctx), before backward frees it
-        L1 = h_attn.shape[0] // B
-        gates = [lay.z.double().cpu().view(B, L1, -1) for lay in h_attn.grad_fn.sv.dec.layers]
+        L1 = h_attn.shape[1]  # (B, L+1, V): a view of the heads node's padded rows
+        node = h_attn.grad_fn
+        while not hasattr(node, "sv"):
+            node = node.next_functions[0][0]
+        gates = [lay.z.double().cpu().view(B, L1, -1) for lay in node.sv.dec.layers]
     loss.backward()
     grads = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
     opt.clip_and_step(5.0)

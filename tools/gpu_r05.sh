@@ -16,6 +16,13 @@ for s in "$@"; do
     new) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py tests/test_switches_gpu.py tests/test_nodes_gpu.py \
            "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" "tests/test_model_gpu.py::test_parity_config4_full_model_bf16_emulated" \
            "tests/test_kernels_gpu.py::test_gemm_ksub2_bit_identical" -s > "$OUT/new.log" 2>&1 ;;
+    attncheck) # bitwise A/B of the attention kernels: ab_prev/'s library vs the tree's
+           LITEASR_HIP_LIB=$R/ab_prev/liteasr_amd/lib/libliteasr_hip.so run timeout -k 10 300 python3 tools/attn_check.py dump "$OUT/attn_base.pt" > "$OUT/attn_check.log" 2>&1
+           run timeout -k 10 300 python3 tools/attn_check.py dump "$OUT/attn_new.pt" >> "$OUT/attn_check.log" 2>&1
+           run python3 tools/attn_check.py cmp "$OUT/attn_new.pt" "$OUT/attn_base.pt" > "$OUT/attn_check.jsonl" 2>&1
+           rm -f "$OUT/attn_base.pt" "$OUT/attn_new.pt" ;;
+    new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
+           "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" -s > "$OUT/new5.log" 2>&1 ;;
     attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
     attnbench) run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_bench.jsonl" 2> "$OUT/attn_bench.err" ;;
     attnab) # attention kernels: the library in ab/ (same ABI) vs the tree's, alternating
@@ -57,7 +64,8 @@ for s in "$@"; do
     blaslt) run timeout -k 10 120 python3 tools/blaslt_ref.py > "$OUT/blaslt.jsonl" 2> "$OUT/blaslt.err" ;;
     trace) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace.log" 2>&1
            db=$(find "$OUT/trace" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary.txt" 2>&1
-           python3 "$R/tools/step_summary.py" "$db" 5 --grid > "$OUT/step_summary_grid.txt" 2>&1; rm -f "$db" ;;
+           python3 "$R/tools/step_summary.py" "$db" 5 --grid > "$OUT/step_summary_grid.txt" 2>&1
+           python3 "$R/tools/step_summary.py" "$db" 5 --order > "$OUT/step_order.txt" 2>&1; rm -f "$db" ;;
     tracelong) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_long" -o run -- python3 "$R/bench.py" --config long --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace_long.log" 2>&1
            db=$(find "$OUT/trace_long" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_long.txt" 2>&1; rm -f "$db" ;;
     tracelarge) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_large" -o run -- python3 "$R/bench.py" --config large --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace_large.log" 2>&1

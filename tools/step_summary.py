@@ -2,8 +2,9 @@
 step): the dispatches between the optimizer kernels (adam_kernel) of the last N steps.
 Reports launches per step, summed kernel time (busy) and wall time per step, then per
 kernel name: launches/step, us/step, us/launch.  --grid splits each kernel by its grid size
-(workgroups x, y, z), which tells apart the GEMM shapes sharing one tile instance.
-    python tools/step_summary.py <run_results.db> [N=5] [--grid]"""
+(workgroups x, y, z), which tells apart the GEMM shapes sharing one tile instance; --order
+prints the last step's launches in order (name, grid, us) instead.
+    python tools/step_summary.py <run_results.db> [N=5] [--grid] [--order]"""
 
 import collections
 import re
@@ -12,8 +13,8 @@ import sys
 
 
 def main():
-    argv = [a for a in sys.argv[1:] if a != "--grid"]
-    grid = "--grid" in sys.argv
+    argv = [a for a in sys.argv[1:] if a not in ("--grid", "--order")]
+    grid = "--grid" in sys.argv or "--order" in sys.argv
     db = argv[0]
     n = int(argv[1]) if len(argv) > 1 else 5
     c = sqlite3.connect(db)
@@ -28,6 +29,12 @@ def main():
     wall = (seg[-1][2] - seg[0][1]) / n / 1e6
     print(f"steady state over the last {n} steps: {len(seg) / n:.0f} launches/step, "
           f"busy {busy:.3f} ms/step, wall {wall:.3f} ms/step")
+    if "--order" in sys.argv:
+        last = rows[opt[-2] + 1:opt[-1] + 1]
+        for i, (name, s_, e_) in enumerate(last):
+            k = re.sub(r"\(.*\)", "", name.replace("(anonymous namespace)::", "").replace("void ", ""))
+            print(f"{i:4d} {(e_ - s_) / 1e3:8.1f} {(s_ - last[0][1]) / 1e3:9.1f}  {k[:150]}")
+        return
     tm, cnt = collections.Counter(), collections.Counter()
     for name, s, e in seg:
         k = name.replace("(anonymous namespace)::", "").replace("void ", "")
