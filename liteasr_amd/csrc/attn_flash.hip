@@ -1221,7 +1221,31 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
     st_d = a.Dbuf[zrow + ic];
   };
   if (w == 0) load_stats(0);
-  float* gk = gsh + w * KWAVE;
+  // per-lane LDS offsets, hoisted: row fragments (Q / dO / Qv images, rows lane%16 (+16r), and
+  // Qv shifted one query), the wave's window rows (16w + lane%16, + (48 - 16r + 16uu) as an
+  // immediate), transposed fragments (rows 4g + (lane/4)%4, + 32rs / +16), the G scratch
+  // parking and diagonal addresses, the RM mask byte of (row 4g, the lane's key)
+  struct {
+    uint32_t rq[KS], rq1[KS], w[KS], tr[DK / 16], gw[4], gr[4], mk;
+  } ko;
+  {
+    const uint32_t gka = ldsa(gsh + w * KWAVE);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      ko.rq[ks] = 2u * (uint32_t)toff<DK>(lane & 15, 32 * ks + 8 * g);
+      ko.rq1[ks] = Gm::QV0 * 16u + 2u * (uint32_t)toff<DK>(1 + (lane & 15), 32 * ks + 8 * g);
+      ko.w[ks] = Gm::W0 * 16u + 2u * (uint32_t)toff<DK>(16 * w + (lane & 15), 32 * ks + 8 * g);
+    }
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) ko.tr[t] = 2u * (uint32_t)toff<DK>(4 * g + ((lane >> 2) & 3), 16 * t + (lane & 3) * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      ko.gw[e] = gka + 4u * (uint32_t)(kro(4 * g + e) + col);
+      ko.gr[e] = gka + 4u * (uint32_t)(kro(4 * g + e) + col - 4 * g - e + 15);
+    }
+    ko.mk = (uint32_t)(4 * g * Gm::KBW + 16 * w + col);
+  }
+  const uint32_t ring0 = ldsa(ring);
   f32x4 dkt[DK / 16], dvt[DK / 16];
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) { dkt[t] = zero4(); dvt[t] = zero4(); }
@@ -1243,8 +1267,18 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
       issue_stage_kv<DK, NW, RP, RM>(a, b, h, i0 + QBK, j0, ring + ((qb + 1) & 1) * Gm::STAGE_BYTES, tid);
       if (w == 0) load_stats(i0 + QBK);
     }
-    const uint32_t qimg = ldsa(st), oimg = ldsa(st + Gm::O0 * 16), vimg = ldsa(st + Gm::QV0 * 16);
-    const uint32_t wimg = ldsa(st + Gm::W0 * 16), mimg = ldsa(st + Gm::M0 * 16);
+    const uint32_t sb = ring0 + (uint32_t)((qb & 1) * Gm::STAGE_BYTES);
+    const uint32_t ssa = ldsa(ss) + 16u * (uint32_t)g;  // the lane's 4 query rows' statistics (+16r floats)
+    uint32_t bq[KS], bq1[KS], bw[RP ? KS : 1];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bq[ks] = sb + ko.rq[ks];
+      if constexpr (RP) {
+        bq1[ks] = sb + ko.rq1[ks];
+        bw[ks] = sb + ko.w[ks];
+      }
+    }
+    const uint32_t mrow = sb + Gm::M0 * 16u + ko.mk;
 #pragma unroll 1
     for (int rs = 0; rs < 2; ++rs) {  // query tile pairs (2rs, 2rs + 1)
       f32x4 p2[2], ds2[2];
@@ -1252,35 +1286,39 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
       for (int u = 0; u < 2; ++u) {
         const int r = 2 * rs + u;  // queries i0 + 16r ..; lane rows 4g + e
         // every LDS read of the tile up front: S = Qu . K^T and dP = dO . V^T (query rows as the A
-        // operand), the rows' statistics and mask bytes, then the window products' fragments
+        // operand), the rows' statistics and mask bytes, then the window products' fragments;
+        // addresses are the hoisted per-lane bases plus immediates (rows +16 keep the swizzle)
+        const uint32_t rofs = (uint32_t)(r * 16 * DK * 2);
         v4i aq[KS], ao[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          aq[ks] = lds_b128(frag_row_addr<DK>(qimg, 16 * r, 32 * ks, lane));
-          ao[ks] = lds_b128(frag_row_addr<DK>(oimg, 16 * r, 32 * ks, lane));
+          const uint32_t qa = bq[ks] + rofs;
+          asm volatile("ds_read_b128 %0, %1" : "=v"(aq[ks]) : "v"(qa));
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ao[ks]) : "v"(qa), "i"(Gm::O0 * 16));
         }
         v4i smv, slv, sdv;  // m, 1/sum, D of the lane's 4 query rows
-        asm volatile("ds_read_b128 %0, %1" : "=v"(smv) : "v"(ldsa(ss + 16 * r + 4 * g)));
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(slv) : "v"(ldsa(ss + 16 * r + 4 * g)), "i"(4 * QBK));
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(sdv) : "v"(ldsa(ss + 16 * r + 4 * g)), "i"(8 * QBK));
+        const uint32_t sa = ssa + 64u * (uint32_t)r;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(smv) : "v"(sa));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(slv) : "v"(sa), "i"(4 * QBK));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(sdv) : "v"(sa), "i"(8 * QBK));
         uint32_t mb[4] = {0u, 0u, 0u, 0u};
         if constexpr (RM) {
-          const uint32_t ma = mimg + (uint32_t)((16 * r + 4 * g) * Gm::KBW + 16 * w + col);
+          const uint32_t ma = mrow + (uint32_t)(16 * r * Gm::KBW);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(mb[e]) : "v"(ma), "i"(e * Gm::KBW));
         }
         // window rows of this (query tile, key tile): m0 = jw - (i0 + 16r + 15) + T - 1 at image
         // row 16w - 16r + 48; G1 uses qv rows i, G2 rows i + 1
-        const int wr0 = 16 * w - 16 * r + QBK - 16;
-        v4i av[RP ? KS : 1], av1[RP ? KS : 1], bw[RP ? 2 : 1][RP ? KS : 1];
+        v4i av[RP ? KS : 1], av1[RP ? KS : 1], bwf[RP ? 2 : 1][RP ? KS : 1];
         if constexpr (RP) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
-            av[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r, 32 * ks, lane));
-            av1[ks] = lds_b128(frag_row_addr<DK>(vimg, 16 * r + 1, 32 * ks, lane));
-            bw[0][ks] = lds_b128(frag_row_addr<DK>(wimg, wr0, 32 * ks, lane));
-            bw[1][ks] = lds_b128(frag_row_addr<DK>(wimg, wr0 + 16, 32 * ks, lane));
+            const uint32_t wa = bw[ks] - (uint32_t)(16 * r * DK * 2);
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(av[ks]) : "v"(bq[ks] + rofs), "i"(Gm::QV0 * 16));
+            asm volatile("ds_read_b128 %0, %1" : "=v"(av1[ks]) : "v"(bq1[ks] + rofs));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bwf[0][ks]) : "v"(wa), "i"((QBK - 16) * DK * 2));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bwf[1][ks]) : "v"(wa), "i"(QBK * DK * 2));
           }
           lgkm<4 * KS>();  // all but the window fragments
         } else {
@@ -1303,56 +1341,59 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
             lgkm0();  // the window reads issued above land before their registers are reused
             if constexpr (RP)
 #pragma unroll
-              for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bw[0][ks]); keep(bw[1][ks]); }
+              for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bwf[0][ks]); keep(bwf[1][ks]); }
             p2[u] = zero4();
             ds2[u] = zero4();
             continue;
           }
           anym = __builtin_amdgcn_ballot_w64((mb[0] | mb[1] | mb[2] | mb[3]) != 0u) != 0;
         }
-        f32x4 sc = zero4(), dp = zero4();
+        f32x4 sc = mfma(as_frag(aq[0]), kf[0], zero4()), dp = mfma(as_frag(ao[0]), vf[0], zero4());
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
+        for (int ks = 1; ks < KS; ++ks) {
           sc = mfma(as_frag(aq[ks]), kf[ks], sc);
           dp = mfma(as_frag(ao[ks]), vf[ks], dp);
         }
         float bd[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr (RP) {
           const int mlo = jw - (i0 + 16 * r + 15) + T - 1;
-          const uint32_t gka = ldsa(gk);
           lgkm0();
 #pragma unroll
-          for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bw[0][ks]); keep(bw[1][ks]); }
+          for (int ks = 0; ks < KS; ++ks) { keep(av[ks]); keep(av1[ks]); keep(bwf[0][ks]); keep(bwf[1][ks]); }
 #pragma unroll
           for (int uu = 0; uu < 2; ++uu) {
             const int lo = mlo + 16 * uu;
-            const bool n1 = lo <= T - 1 && lo + 15 >= 0;
-            const bool n2 = lo + 15 >= T + 1 && lo <= 2 * T;
-            f32x4 g1 = zero4(), g2 = zero4();
-            if (n1) {
+            // lane (g, col) holds G[query 4g + e][m = lo + col]: rows m <= T from qv_i (G1), m >= T
+            // from qv_{i+1} (G2; the window's row m = T is zero), the tile across m = T both, selected
+            // per column; parked as [query][m] (row 4g + e at kro(4g + e))
+            f32x4 gs;
+            if (lo + 15 <= T) {
+              gs = mfma(as_frag(av[0]), as_frag(bwf[uu][0]), zero4());
 #pragma unroll
-              for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(av[ks]), as_frag(bw[uu][ks]), g1);
-            }
-            if (n2) {
+              for (int ks = 1; ks < KS; ++ks) gs = mfma(as_frag(av[ks]), as_frag(bwf[uu][ks]), gs);
+            } else if (lo >= T) {
+              gs = mfma(as_frag(av1[0]), as_frag(bwf[uu][0]), zero4());
 #pragma unroll
-              for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(av1[ks]), as_frag(bw[uu][ks]), g2);
+              for (int ks = 1; ks < KS; ++ks) gs = mfma(as_frag(av1[ks]), as_frag(bwf[uu][ks]), gs);
+            } else {
+              f32x4 g1 = mfma(as_frag(av[0]), as_frag(bwf[uu][0]), zero4());
+              f32x4 g2 = mfma(as_frag(av1[0]), as_frag(bwf[uu][0]), zero4());
+#pragma unroll
+              for (int ks = 1; ks < KS; ++ks) {
+                g1 = mfma(as_frag(av[ks]), as_frag(bwf[uu][ks]), g1);
+                g2 = mfma(as_frag(av1[ks]), as_frag(bwf[uu][ks]), g2);
+              }
+              gs = lo + col <= T - 1 ? g1 : g2;
             }
-            // lane (g, col) holds G[query 4g + e][m = lo + col]: select by m <= T - 1, park as
-            // [query][m] (row 4g + e at kro(4g + e))
-            f32x4 gs = n2 ? g2 : g1;
-            if (n1 && n2) gs = lo + col <= T - 1 ? g1 : g2;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(gka + 4u * (uint32_t)(kro(4 * g + e) + col)),
-                           "v"(gs[e]), "i"(64 * uu) : "memory");
+              asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(ko.gw[e]), "v"(gs[e]), "i"(64 * uu) : "memory");
           }
           // bd(query 4g + e, key col) = G[4g + e][m - mlo = col - 4g - e + 15] (the wave's writes
           // above retire first)
           float v[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            asm volatile("ds_read_b32 %0, %1" : "=v"(v[e])
-                         : "v"(gka + 4u * (uint32_t)(kro(4 * g + e) + col - 4 * g - e + 15)));
+          for (int e = 0; e < 4; ++e) asm volatile("ds_read_b32 %0, %1" : "=v"(v[e]) : "v"(ko.gr[e]));
           lgkm0();
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -1387,14 +1428,16 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
         }
       }
       // dV^T += dO^T P, dK^T += Qu^T dS (queries of the pair as k: 32rs + 4g + e, then + 16)
-      const bf16x8 pb = pack8(p2[0], p2[1]), sb = pack8(ds2[0], ds2[1]);
+      const bf16x8 pb = pack8(p2[0], p2[1]), sbf = pack8(ds2[0], ds2[1]);
       v2i olo[DK / 16], ohi[DK / 16], qlo[DK / 16], qhi[DK / 16];
+      const uint32_t pofs = (uint32_t)(32 * rs * DK * 2);
 #pragma unroll
       for (int t = 0; t < DK / 16; ++t) {
-        olo[t] = lds_tr(frag_tr_addr<DK>(oimg, 32 * rs + 4 * g, 16 * t, lane));
-        ohi[t] = lds_tr(frag_tr_addr<DK>(oimg, 32 * rs + 16 + 4 * g, 16 * t, lane));
-        qlo[t] = lds_tr(frag_tr_addr<DK>(qimg, 32 * rs + 4 * g, 16 * t, lane));
-        qhi[t] = lds_tr(frag_tr_addr<DK>(qimg, 32 * rs + 16 + 4 * g, 16 * t, lane));
+        const uint32_t ta = sb + ko.tr[t] + pofs;
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(olo[t]) : "v"(ta), "i"(Gm::O0 * 16));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(ohi[t]) : "v"(ta), "i"(Gm::O0 * 16 + 16 * DK * 2));
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(qlo[t]) : "v"(ta));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(qhi[t]) : "v"(ta), "i"(16 * DK * 2));
       }
       lgkm0();
 #pragma unroll
@@ -1402,7 +1445,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
 #pragma unroll
       for (int t = 0; t < DK / 16; ++t) {
         dvt[t] = mfma(as_frag(olo[t], ohi[t]), pb, dvt[t]);
-        dkt[t] = mfma(as_frag(qlo[t], qhi[t]), sb, dkt[t]);
+        dkt[t] = mfma(as_frag(qlo[t], qhi[t]), sbf, dkt[t]);
       }
     }
   }
