@@ -293,6 +293,15 @@ int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, const void* k,
                      int64_t ldkv, const void* pos, int64_t ldp, int B, int H, int T, int dk,
                      const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, float scale,
                      float* stats, void* ctx, int64_t ldc, void* stream);
+/* lasr_relattn_fwd with lasr_qbias_fwd folded in (one launch fewer per Conformer layer):
+ *   q        [B*T, ldqin] the q slot of the fused qkv projection
+ *   bu, bv   [H*d_k] fp32 pos_bias_u / pos_bias_v (attention.py:93-96), 16-B aligned
+ *   qu, qv   [B*T, ldq]   out: q + u, q + v (bf16, lasr_qbias_fwd's rounding), for the backward
+ * everything else as lasr_relattn_fwd. */
+int lasr_relattn_fwd_qb(const void* q, int64_t ldqin, const float* bu, const float* bv, void* qu, void* qv,
+                        int64_t ldq, const void* k, const void* v, int64_t ldkv, const void* pos, int64_t ldp,
+                        int B, int H, int T, int dk, const uint8_t* mask, int64_t mask_sb, int64_t mask_sq,
+                        float scale, float* stats, void* ctx, int64_t ldc, void* stream);
 /* Backward of lasr_relattn_fwd (recompute; deterministic).  Outputs:
  *   Dbuf [B*H*T]        scratch: rowsum(dctx * ctx)
  *   dqu  [B*T, ldq]     dL/d(q+u)

@@ -110,6 +110,8 @@ SIGNATURES = {
     "lasr_gemm_plan": [C.POINTER(GemmArgs), _p, _p, _p, _p],
     "lasr_gemm_dw_group": [C.POINTER(GemmArgs), _i, _p],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
+    "lasr_relattn_fwd_qb": [_p, _l, _p, _p, _p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p,
+                            _l, _p],
     "lasr_attn_fwd": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_attn_bwd": [_p, _l, _p, _p, _l, _i, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _p, _l, _p, _p, _p, _p,
                       _l, _p],

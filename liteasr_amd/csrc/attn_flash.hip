@@ -76,6 +76,12 @@ struct FlashP {
   // mpart [nsplit][B*H*T][2], combined in split order by a second launch
   int nsplit;
   float *opart, *mpart;
+  // forward with the positional biases folded in (lasr_relattn_fwd_qb): q rows [B*T, ldqin]
+  // (the fused projection's q slot) and pos_bias_u / v [H*d_k] fp32; the kernel forms
+  // qu = q + u and qv = q + v in registers and stores them to qu / qv (ldq) for the backward
+  const bf16_t* qin;
+  int64_t ldqin;
+  const float *bu, *bv;
 };
 
 // bf16 zero row: the relative-position window's rows outside the table (m == T, past 2T)
@@ -286,6 +292,22 @@ LASR_DEV void load_q(const bf16_t* base, int64_t ld, int row, int h, int lane, b
   const bf16_t* p = base + (int64_t)row * ld + h * DK + 8 * (lane >> 4);
 #pragma unroll
   for (int ks = 0; ks < DK / 32; ++ks) f[ks] = *(const bf16x8*)(p + 32 * ks);
+}
+
+// q + bias for one query fragment (8 columns): the fp32 sum rounded to bf16 (RNE), exactly
+// lasr_qbias_fwd's arithmetic
+LASR_DEV bf16x8 qbias_frag(bf16x8 q, const float* bias) {
+  const v4i qi = __builtin_bit_cast(v4i, q);
+  const float4 b0 = *(const float4*)bias, b1 = *(const float4*)(bias + 4);
+  const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  v4i r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = __builtin_bit_cast(float, (uint32_t)qi[i] << 16) + bb[2 * i];
+    const float hi = __builtin_bit_cast(float, (uint32_t)qi[i] & 0xffff0000u) + bb[2 * i + 1];
+    r[i] = (int)pk_bf16(lo, hi);
+  }
+  return __builtin_bit_cast(bf16x8, r);
 }
 
 // Scaled + masked transposed scores of the lane's query against the 64 keys of block j0,
@@ -679,10 +701,32 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_fwd_kernel(FlashP a) {
     for (int j = tid; j < kpad; j += NT) kmask[j] = mr && j < Tk ? mr[j] : 0;
   }
   bf16x8 qu[KS], qv[KS], qv1[KS];
-  load_q<DK>(a.qu, a.ldq, b * T + min(iq, T - 1), h, lane, qu);
-  if constexpr (RP) {
-    load_q<DK>(a.qv, a.ldq, b * T + min(iq, T - 1), h, lane, qv);
-    load_q<DK>(a.qv, a.ldq, b * T + min(iq + 1, T - 1), h, lane, qv1);
+  if (RP && a.qin) {  // the positional biases folded in: qu / qv formed here and stored for the backward
+    bf16x8 q0[KS], q1[KS];
+    load_q<DK>(a.qin, a.ldqin, b * T + min(iq, T - 1), h, lane, q0);
+    load_q<DK>(a.qin, a.ldqin, b * T + min(iq + 1, T - 1), h, lane, q1);
+    const int cb = h * DK + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qu[ks] = qbias_frag(q0[ks], a.bu + cb + 32 * ks);
+      qv[ks] = qbias_frag(q0[ks], a.bv + cb + 32 * ks);
+      qv1[ks] = qbias_frag(q1[ks], a.bv + cb + 32 * ks);
+    }
+    if (iq < T) {
+      bf16_t* du = (bf16_t*)a.qu + ((int64_t)b * T + iq) * a.ldq + cb;
+      bf16_t* dv = (bf16_t*)a.qv + ((int64_t)b * T + iq) * a.ldq + cb;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        *(bf16x8*)(du + 32 * ks) = qu[ks];
+        *(bf16x8*)(dv + 32 * ks) = qv[ks];
+      }
+    }
+  } else {
+    load_q<DK>(a.qu, a.ldq, b * T + min(iq, T - 1), h, lane, qu);
+    if constexpr (RP) {
+      load_q<DK>(a.qv, a.ldq, b * T + min(iq, T - 1), h, lane, qv);
+      load_q<DK>(a.qv, a.ldq, b * T + min(iq + 1, T - 1), h, lane, qv1);
+    }
   }
   const FragOffs<DK, NW, RP, RM> fo = frag_offs<DK, NW, RP, RM>(w, lane);
   const uint32_t ring0 = ldsa(ring), kmaddr = ldsa(kmask);
@@ -1577,6 +1621,37 @@ extern "C" int lasr_relattn_fwd(const void* qu, const void* qv, int64_t ldq, con
   a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
   launch_flash_fwd(a, dk, true, mask && mask_sq != 0, (hipStream_t)stream);
   return lasr_check_launch("relattn_fwd");
+}
+
+// lasr_relattn_fwd with lasr_qbias_fwd folded in: q [B*T, ldqin] (the q slot of the fused
+// projection) and pos_bias_u / v [H*d_k] fp32 in; qu = q + u and qv = q + v are formed in the
+// kernel (the same fp32 sum and bf16 rounding as lasr_qbias_fwd) and written to qu / qv [B*T,
+// ldq] for the backward -- one launch and one re-read of q fewer per layer.
+extern "C" int lasr_relattn_fwd_qb(const void* q, int64_t ldqin, const float* bu, const float* bv, void* qu,
+                                   void* qv, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                                   const void* pos, int64_t ldp, int B, int H, int T, int dk, const uint8_t* mask,
+                                   int64_t mask_sb, int64_t mask_sq, float scale, float* stats, void* ctx,
+                                   int64_t ldc, void* stream) {
+  LASR_CHECK_ARG(dk == 64 || dk == 32, "lasr_relattn_fwd_qb: d_k=%d (32 or 64)", dk);
+  LASR_CHECK_ARG(B >= 0 && H > 0 && T >= 0 && B <= 65535 && H <= 65535, "lasr_relattn_fwd_qb: bad B/H/T");
+  LASR_CHECK_ARG(ldqin % 8 == 0 && ldq % 8 == 0 && ldkv % 8 == 0 && ldp % 8 == 0 && ldc % 8 == 0 && ldc >= H * dk &&
+                     ldq >= H * dk && ldqin >= H * dk,
+                 "lasr_relattn_fwd_qb: row strides must be multiples of 8");
+  LASR_CHECK_ARG(al16(q) && al16(qu) && al16(qv) && al16(k) && al16(v) && al16(pos) && al16(ctx) && al16(bu) &&
+                     al16(bv),
+                 "lasr_relattn_fwd_qb: 16-B alignment");
+  if (B == 0 || T == 0) return LASR_OK;
+  if (int rc = check_mask(mask, mask_sb, mask_sq, T, "lasr_relattn_fwd_qb")) return rc;
+  FlashP a = {};
+  a.qu = (const bf16_t*)qu; a.qv = (const bf16_t*)qv; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.pos = (const bf16_t*)pos;
+  a.ldq = ldq; a.ldkv = ldkv; a.ldp = ldp;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq;
+  a.B = B; a.H = H; a.T = T; a.Tk = T; a.scale = scale;
+  a.stats = stats; a.ctx = (bf16_t*)ctx; a.ldc = ldc;
+  a.qin = (const bf16_t*)q; a.ldqin = ldqin; a.bu = bu; a.bv = bv;
+  launch_flash_fwd(a, dk, true, mask && mask_sq != 0, (hipStream_t)stream);
+  return lasr_check_launch("relattn_fwd_qb");
 }
 
 // Plain scaled dot-product attention (no positional term) with Tk keys per utterance: the

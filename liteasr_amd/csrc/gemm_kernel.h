@@ -9,7 +9,8 @@
 #include <type_traits>
 
 // Ablation hooks for GEMM experiments (tools/gemm_exp.sh); 0 in every product build.
-// bit 1: skip the MFMAs, bit 2: skip the epilogue stores, bit 4: skip the glds loads.
+// bit 1: skip the MFMAs, bit 2: skip the epilogue stores, bit 4: skip the glds loads,
+// bit 8: no dropout draws in the Swish-gate epilogue (keep all), bit 16: no activation math there.
 #ifndef LASR_EXP
 #define LASR_EXP 0
 #endif
@@ -103,13 +104,17 @@ LASR_DEV void epi_core(const GemmP& p, uint32_t dkey, uint64_t dbase, float (&v)
                        bool has_aux, const float (&resv)[N], bool has_res, ZST zst) {
   if constexpr (EPI == EPI_SWISH_GATE_DROP) {
     // zout_mode 1, Swish, dropout on; no aux, residual or beta (FFN fc1 forward)
-    const uint32_t km = drop_keep_mask_even<N>(p.drop, dkey, dbase);
+    const uint32_t km = (LASR_EXP & 8) ? 0xffffffffu : drop_keep_mask_even<N>(p.drop, dkey, dbase);
     float g[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-      const float s = sigmoidf_(v[q]);
-      g[q] = s * (1.f + v[q] * (1.f - s));
-      v[q] *= s;
+      if constexpr ((LASR_EXP & 16) != 0) {
+        g[q] = v[q];
+      } else {
+        const float s = sigmoidf_(v[q]);
+        g[q] = s * (1.f + v[q] * (1.f - s));
+        v[q] *= s;
+      }
     }
 #pragma unroll
     for (int q = 0; q < N; ++q) g[q] *= (km >> q) & 1u ? 1.f : 0.f;

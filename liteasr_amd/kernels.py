@@ -555,6 +555,17 @@ def relattn_fwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx):
            ctx.stride(0), stream())
 
 
+def relattn_fwd_qb(q, bu, bv, qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx):
+    """relattn_fwd with qbias_fwd folded in: q (the qkv projection's q slot) and the fp32
+    pos_bias_u / v in; qu = q + u and qv = q + v are formed by the attention kernel and written
+    to qu / qv (same strides) for the backward (lasr_relattn_fwd_qb)."""
+    assert qv.stride(0) == qu.stride(0) and bu.dtype == torch.float32 and bv.dtype == torch.float32
+    mask, msb, msq = _fwd_mask(mask, msb, msq, B, T, T)
+    N.call("lasr_relattn_fwd_qb", ptr(q), q.stride(0), ptr(bu), ptr(bv), ptr(qu), ptr(qv), qu.stride(0), ptr(k),
+           ptr(v), k.stride(0), ptr(pos), pos.stride(0), B, H, T, qu.shape[1] // H, ptr(mask), msb, msq, scale,
+           ptr(stats), ptr(ctx), ctx.stride(0), stream())
+
+
 def relattn_bwd(qu, qv, k, v, pos, B, H, T, mask, msb, msq, scale, stats, ctx, dctx, Dbuf, dqu,
                 dbd, ldS, dk, dv, dbd_head_major=False):
     assert qv.stride(0) == qu.stride(0) and dqu.stride(0) == qu.stride(0)

@@ -220,15 +220,16 @@ def relmha_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None, po
         K.linear(pos, w.Wpos, p)
     qu = _e((M, d), adt, dev)
     qv = _e((M, d), adt, dev)
-    K.qbias_fwd(qkv, B, T, H, dk, w.u, w.v, qu, qv)
     if fused_relattn(adt, dk, p_att):
-        # scores never materialised (attn_flash.hip); row stats kept for the backward
+        # scores never materialised (attn_flash.hip); row stats kept for the backward; the
+        # kernel forms qu / qv from q and the biases itself (lasr_relattn_fwd_qb)
         stats = _e((B * H * T * 2,), F32, dev)
         ctx = _e((M, d), adt, dev)
-        K.relattn_fwd(qu, qv, qkv[:, d:2 * d], qkv[:, 2 * d:], p, B, H, T, env.mask, env.msb, env.msq,
-                      scale, stats, ctx)
+        K.relattn_fwd_qb(qkv[:, :d], w.u, w.v, qu, qv, qkv[:, d:2 * d], qkv[:, 2 * d:], p, B, H, T, env.mask,
+                         env.msb, env.msq, scale, stats, ctx)
         out = res_proj(ctx, w.Wo, w.bo, x_in, 1.0, p_res, s_res, post)
         return out, SimpleNamespace(qkv=qkv, p=p, qu=qu, qv=qv, ctx=ctx, stats=stats)
+    K.qbias_fwd(qkv, B, T, H, dk, w.u, w.v, qu, qv)
     ldS = ld_scores(T)
     Sac = _e((B, H, T, ldS), F32, dev)
     Sbd = _e((B, H, T, ldS), F32, dev)

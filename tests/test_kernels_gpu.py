@@ -667,6 +667,46 @@ def test_attn_softmax(relpos):
         close(dBD.view(B, H, T, ldS)[..., :T], gref, 1e-6, "relshift bwd")
 
 
+@pytest.mark.parametrize("B,H,T,dk,chunk", [(2, 4, 249, 64, 0), (3, 4, 130, 64, 0), (2, 16, 249, 32, 16),
+                                             (1, 2, 1, 64, 0), (2, 3, 77, 32, 0)])
+def test_relattn_fwd_qb_bit_identical(B, H, T, dk, chunk):
+    """lasr_relattn_fwd_qb (the positional biases folded into the attention forward) equals
+    lasr_qbias_fwd + lasr_relattn_fwd bit for bit: qu, qv, ctx and the row statistics
+    (attention.py:93-96 pos_bias_u / v, :120-154)."""
+    kn = K()
+    torch.manual_seed(T + dk)
+    d = dk * H
+    bf = torch.bfloat16
+    qkv = (torch.randn(B * T, 3 * d, device=DEV) * 0.5).to(bf)
+    pos = (torch.randn(T, d, device=DEV) * 0.5).to(bf)
+    bu, bv = torch.randn(d, device=DEV) * 0.1, torch.randn(d, device=DEV) * 0.1
+    xl = torch.full((B,), T, device=DEV)
+    xl[1::2] = max(T - 17, 1)
+    pad = torch.arange(T, device=DEV)[None, :] >= xl[:, None]
+    if chunk:
+        tri = (torch.arange(T, device=DEV)[None, :] // chunk) > (torch.arange(T, device=DEV)[:, None] // chunk)
+        mask, msb, msq = kn.pad_mask16((pad[:, None, :] | tri[None]).to(torch.uint8), B, T, T)
+    else:
+        mask, msb, msq = pad.to(torch.uint8).contiguous(), T, 0
+    outs = []
+    for fused in (False, True):
+        qu = torch.full((B * T, d), 7.0, dtype=bf, device=DEV)
+        qv = torch.full_like(qu, 7.0)
+        stats = torch.empty(B * H * T * 2, device=DEV)
+        ctx = torch.empty(B * T, d, dtype=bf, device=DEV)
+        if fused:
+            kn.relattn_fwd_qb(qkv[:, :d], bu, bv, qu, qv, qkv[:, d:2 * d], qkv[:, 2 * d:], pos, B, H, T, mask, msb,
+                              msq, dk ** -0.5, stats, ctx)
+        else:
+            kn.qbias_fwd(qkv, B, T, H, dk, bu, bv, qu, qv)
+            kn.relattn_fwd(qu, qv, qkv[:, d:2 * d], qkv[:, 2 * d:], pos, B, H, T, mask, msb, msq, dk ** -0.5, stats,
+                           ctx)
+        torch.cuda.synchronize()
+        outs.append((qu, qv, ctx, stats))
+    for name, a, b in zip(("qu", "qv", "ctx", "stats"), outs[0], outs[1]):
+        assert torch.equal(a, b), name
+
+
 @pytest.mark.parametrize("B,H,T,masking,dk", [(2, 2, 37, "pad", 64), (3, 4, 130, "pad", 64), (2, 4, 249, "pad", 64),
                                                (2, 2, 100, "chunk", 64), (2, 1, 64, "none", 64), (1, 1, 1, "none", 64),
                                                (2, 16, 249, "chunk", 32), (3, 3, 70, "pad", 32),

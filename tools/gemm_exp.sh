@@ -1,7 +1,8 @@
 #!/bin/bash
 # Build GEMM ablation variants of the library (CPU side): liteasr_amd/lib/exp/lib<N>.so with
 # LASR_EXP=N compiled into every GEMM translation unit (gemm.hip, gemm_l0..3.hip).
-# bit 1: skip the MFMAs, bit 2: skip the epilogue stores, bit 4: skip the glds loads.
+# bit 1: skip the MFMAs, bit 2: skip the epilogue stores, bit 4: skip the glds loads, bit 8: no
+# dropout draws in the Swish-gate epilogue, bit 16: no activation math there.
 set -e
 cd "$(dirname "$0")/.."
 make -j8 >/dev/null
