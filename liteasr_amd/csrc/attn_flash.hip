@@ -310,163 +310,6 @@ LASR_DEV bf16x8 qbias_frag(bf16x8 q, const float* bias) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
-// Scaled + masked transposed scores of the lane's query against the 64 keys of block j0,
-// in log2 units (c2 = scale * log2 e): s[c][e] for key j0 + 16c + 4*(lane/16) + e.  Every LDS
-// read of the block (K and window fragments, mask words) is issued up front; counted waits
-// release the S products while the window reads are still landing.
-template <int DK, int NW, bool RP, bool RM>
-LASR_DEV bool scores_t(const FlashP& a, const char* st, GAddr ga, const uint8_t* km, const bf16x8 (&qu)[DK / 32],
-                       const bf16x8 (&qv)[DK / 32], const bf16x8 (&qv1)[DK / 32], int w, int i0, int j0, float c2,
-                       int lane, f32x4 (&s)[4]) {
-  using Gm = Geo<DK, NW, RP, RM>;
-  constexpr int KS = DK / 32, NWT = RP ? 5 : 0;
-  const int g = lane >> 4, col = lane & 15;
-  const uint32_t kimg = ldsa(st), wimg = ldsa(st + Gm::W0 * 16);
-  const int wb = 16 * (NW - 1 - w);  // the wave's first window row
-  v4i rk[4][KS], rw[RP ? 5 : 1][KS];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) rk[c][ks] = lds_b128(frag_row_addr<DK>(kimg, 16 * c, 32 * ks, lane));
-  if constexpr (RP)
-#pragma unroll
-    for (int t = 0; t < 5; ++t)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) rw[t][ks] = lds_b128(frag_row_addr<DK>(wimg, wb + 16 * t, 32 * ks, lane));
-  // mask words: the query-dependent tile, or the key-padding bytes (read unconditionally;
-  // ignored without a mask)
-  uint32_t mw[4];
-  {
-    const uint32_t mimg = RM ? ldsa(st + Gm::M0 * 16) + (uint32_t)((16 * w + col) * KB + 4 * g)
-                             : ldsa(km) + (uint32_t)(j0 + 4 * g);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(mw[c]) : "v"(mimg), "i"(16 * c));
-  }
-  lgkm<NWT * KS + 4>();  // the K fragments
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) keep(rk[c][ks]);
-  // S^T = K . Qu^T
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) acc = mfma(as_frag(rk[c][ks]), qu[ks], acc);
-    s[c] = acc;
-  }
-  float bd[4][4];
-  if constexpr (RP) {
-    const int T = a.T;
-    const int mlo = j0 - i0 + T - Gm::QB + wb;  // m of the wave's first window row
-    lgkm<4>();  // the window fragments
-#pragma unroll
-    for (int t = 0; t < 5; ++t)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) keep(rw[t][ks]);
-#pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      const int lo = mlo + 16 * t;
-      const bool n1 = lo <= T - 1 && lo + 15 >= 0;      // rows with m in [0, T-1]
-      const bool n2 = lo + 15 >= T + 1 && lo <= 2 * T;  // rows with m in [T+1, 2T]
-      f32x4 g1 = zero4(), g2 = zero4();
-      if (n1) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) g1 = mfma(as_frag(rw[t][ks]), qv[ks], g1);
-      }
-      if (n2) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) g2 = mfma(as_frag(rw[t][ks]), qv1[ks], g2);
-      }
-      f32x4 gsel = n2 ? g2 : g1;  // a tile on one side of m = T (zeros elsewhere)
-      if (n1 && n2) {             // the straddle tile (wave-uniform branch)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) gsel[e] = lo + 4 * g + e <= T - 1 ? g1[e] : g2[e];
-      }
-      // G'[query col][m - mlo = 16t + 4g + e]
-      asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(ga.wq), "v"(gsel), "i"(64 * t) : "memory");
-    }
-    // diagonal: bd(query col, key 16c + 4g + e) = G'[col][16c + 4g + e - col + 15] (the wave's
-    // own writes above retire first: LDS operations of a wave complete in order)
-    const uint32_t base = ga.diag;
-    float v[16];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[4 * c + e]) : "v"(base), "i"(4 * (16 * c + e)));
-    lgkm0();
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        keep(v[4 * c + e]);
-        bd[c][e] = v[4 * c + e];
-      }
-  } else {
-    lgkm0();
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bd[c][e] = 0.f;
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) keep(mw[c]);
-  // (s + bd) * c2 on packed fp32 pairs (the same two roundings per element)
-  const lasr_f2 c2v = {c2, c2};
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int e = 0; e < 4; e += 2) {
-      lasr_f2 x = {s[c][e], s[c][e + 1]};
-      const lasr_f2 y = {bd[c][e], bd[c][e + 1]};
-      x = (x + y) * c2v;
-      s[c][e] = x[0];
-      s[c][e + 1] = x[1];
-    }
-  // the per-element mask select only where the wave's block has a masked key (uniform: most
-  // blocks of a key-padding mask have none)
-  const bool anym = __builtin_amdgcn_ballot_w64((mw[0] | mw[1] | mw[2] | mw[3]) != 0u) != 0;
-  if (anym) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[c][e] = (mw[c] >> (8 * e)) & 0xffu ? -1e38f : s[c][e];
-  }
-  const bool tail = j0 + KB > a.Tk;
-  if (tail) {  // the last block: keys past Tk (wave-uniform branch)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (j0 + 16 * c + 4 * g + e >= a.Tk) s[c][e] = -INFINITY;
-  }
-  return anym || tail;
-}
-
-// Query-dependent mask (RM): is every score of the wave's block (its 16 queries x the 64 keys)
-// masked?  (wave-uniform; every mask byte nonzero.)  A block fully masked for rows that do have an
-// unmasked key elsewhere contributes exactly nothing (P = 0 after the rescale, dS = 0): callers
-// skip its arithmetic when every row of the wave is known to have one, which keeps a fully
-// masked row's uniform-P semantics intact.
-template <int DK, int NW, bool RP, bool RM>
-LASR_DEV bool block_all_masked(const char* st, int w, int lane) {
-  using Gm = Geo<DK, NW, RP, RM>;
-  const int g = lane >> 4, col = lane & 15;
-  const uint32_t mimg = ldsa(st + Gm::M0 * 16) + (uint32_t)((16 * w + col) * KB + 4 * g);
-  uint32_t mw[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(mw[c]) : "v"(mimg), "i"(16 * c));
-  lgkm0();
-  bool zero_byte = false;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    keep(mw[c]);
-    zero_byte |= ((mw[c] - 0x01010101u) & ~mw[c] & 0x80808080u) != 0u;
-  }
-  return __builtin_amdgcn_ballot_w64(zero_byte) == 0;
-}
-
 // LDS of the forward: 2 ring stages, the waves' G' scratch (RP), the key-padding bytes (!RM)
 constexpr int KMASK_BYTES = 8192;  // Tk <= 8192 (host-checked)
 template <int DK, int NW, bool RP, bool RM>
@@ -569,7 +412,7 @@ LASR_DEV f32x4 gtile(const v4i (&rw)[KS], const bf16x8 (&qv)[KS], const bf16x8 (
 
 // Scaled + masked transposed scores (log2 units) of the lane's query against the block's 64
 // keys from fragments already in registers (issue_kw): s[c][e] for key j0 + 16c + 4(lane/16) + e.
-// Same products, sums and roundings as scores_t.  Returns whether a per-element select was
+// Returns whether a per-element select was
 // needed (masked key or the last block).
 template <int DK, int NW, bool RP, bool RM>
 LASR_DEV bool scores_kw(const FlashP& a, KWFrags<DK, RP>& f, GAddr ga, const bf16x8 (&qu)[DK / 32],

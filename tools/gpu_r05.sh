@@ -24,6 +24,10 @@ for s in "$@"; do
     epiab) # FFN fc1 epilogue ablation: the tree's library and the LASR_EXP builds in liteasr_amd/lib/exp
            for rep in 1 2; do for v in tree 8 16 24; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 120 python3 tools/epi_ab.py >> "$OUT/epi_ab.jsonl" 2>> "$OUT/epi_ab.err"; done; done ;;
+    envab) # whole step, one tree, two environments alternating (ENV_A / ENV_B: "VAR=val ...")
+           for v in A B A B; do e=$ENV_A; [ $v = B ] && e=$ENV_B
+             env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/envab_$v.json" 2> "$OUT/envab_$v.err" || exit 1
+             grep "^{" "$OUT/envab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median')}))" >> "$OUT/envab.jsonl"; done ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
            "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" -s > "$OUT/new5.log" 2>&1 ;;
     attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
