@@ -366,8 +366,10 @@ def _al16(t):
 
 # The row kernel's main loop ingests the whole weight per 32-row workgroup, one workgroup per CU:
 # measured faster than GEMM + norm up to K = 768 (tools/row_ln_bench.py, profiles/r03), slower at
-# K = 2048, where the 64 x 64 GEMM's 2-3 workgroups per CU keep more of the LDS-DMA in flight.
-ROW_LN_MAX_K = int(os.environ.get("LASR_ROW_LN_MAX_K", "1024"))
+# K = 2048, where the 64 x 64 GEMM's 2-3 workgroups per CU keep more of the LDS-DMA in flight
+# (whole step with the FFN fc2 + norm on the row kernel: 9.83 -> 9.98 ms,
+# profiles/r05/step_ab_row_ln_k2048.jsonl).
+ROW_LN_MAX_K = 1024
 
 
 def row_ln_ok(a, w, D, max_k=None):
