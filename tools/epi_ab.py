@@ -4,6 +4,7 @@ dropout, zout_mode 1), the backward dz (x stored gate, dropout scale), and the p
 same shape.  Run once per library (LITEASR_HIP_LIB: e.g. the LASR_EXP ablation builds of
 tools/gemm_exp.sh) -> one JSON line per case."""
 
+import hashlib
 import json
 import os
 import sys
@@ -37,12 +38,13 @@ def graph_us(fn, iters=50):
 
 def main():
     torch.cuda.set_device(0)
+    torch.manual_seed(0)
     dev = "cuda"
     M, F, D = 7968, 2048, 256
     ln = torch.randn(M, D, device=dev).bfloat16()
     w1 = (torch.randn(F, D, device=dev) * 0.05).bfloat16()
     w2 = (torch.randn(D, F, device=dev) * 0.05).bfloat16()
-    b1 = torch.zeros(F, device=dev)
+    b1 = torch.randn(F, device=dev) * 0.1
     h = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
     g = torch.empty_like(h)
     gb = torch.randn(M, D, device=dev).bfloat16()
@@ -53,8 +55,18 @@ def main():
         "fc1_dz": lambda: K.gemm(gb, w2, dz, alpha=K.dropout_scale(0.1), aux=g, aux_act=ACT_GATE),
         "fc1_plain": lambda: K.linear(ln, w1, h, bias=b1),
     }
+    def hsh(*ts):
+        torch.cuda.synchronize()
+        m = hashlib.sha256()
+        for t in ts:
+            m.update(t.contiguous().view(torch.uint8).cpu().numpy().tobytes())
+        return m.hexdigest()[:16]
+
+    outs = {"fc1_fwd": (h, g), "fc1_dz": (dz,), "fc1_plain": (h,)}
     for name, fn in cases.items():
-        print(json.dumps({"lib": lib, "case": name, "us": round(graph_us(fn), 2)}), flush=True)
+        fn()
+        hv = hsh(*outs[name])
+        print(json.dumps({"lib": lib, "case": name, "us": round(graph_us(fn), 2), "hash": hv}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU pass (round 5).  Usage: tools/gpu_r05.sh TAG STEP...; output under gpurun_out/TAG/.
 # Every step has its own time limit; the script stops at the first failure.
-set -u
+set -u -o pipefail
 TAG=${1:-r05}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
@@ -22,8 +22,11 @@ for s in "$@"; do
            run python3 tools/attn_check.py cmp "$OUT/attn_new.pt" "$OUT/attn_base.pt" > "$OUT/attn_check.jsonl" 2>&1
            rm -f "$OUT/attn_base.pt" "$OUT/attn_new.pt" ;;
     epiab) # FFN fc1 epilogue ablation: the tree's library and the LASR_EXP builds in liteasr_amd/lib/exp
-           for rep in 1 2; do for v in tree 8 16 24; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
+           for rep in 1 2; do for v in tree ${EXP_LIBS:-8 16 24}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 120 python3 tools/epi_ab.py >> "$OUT/epi_ab.jsonl" 2>> "$OUT/epi_ab.err"; done; done ;;
+    conv2ab) # subsampling conv2 GEMMs: the tree's library vs liteasr_amd/lib/exp/lib$N.so (EXP_LIBS="32 ...")
+           for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
+             LITEASR_HIP_LIB=$lib run timeout -k 10 120 python3 tools/conv2_bench.py ${CONV2_SHAPE:-} | sed "s/^{/{\"v\": \"$v\", /" >> "$OUT/conv2_ab.jsonl" || exit 1; done; done ;;
     envab) # whole step, one tree, two environments alternating (ENV_A / ENV_B: "VAR=val ...")
            for v in A B A B; do e=$ENV_A; [ $v = B ] && e=$ENV_B
              env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/envab_$v.json" 2> "$OUT/envab_$v.err" || exit 1
