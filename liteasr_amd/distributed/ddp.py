@@ -55,9 +55,10 @@ class FlatReducer:
         # bucket's current range (the Paraformer's heads sit after its decoder in memory
         # but complete before the encoder) starts a new bucket
         self.buckets: List[List[_Unit]] = []
+        breaks = model.reducer_bucket_breaks() if hasattr(model, "reducer_bucket_breaks") else set()
         cur, size = [], 0
         for u in units:
-            if cur and not (u.lo == max(v.hi for v in cur) or u.hi == min(v.lo for v in cur)):
+            if cur and (u.name in breaks or not (u.lo == max(v.hi for v in cur) or u.hi == min(v.lo for v in cur))):
                 self.buckets.append(cur)
                 cur, size = [], 0
             cur.append(u)

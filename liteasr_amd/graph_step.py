@@ -65,10 +65,12 @@ class GraphedTrainStep:
 
     # ------------------------------------------------------------ schedule
     def _cut_points(self):
-        """Encoder positions j (cut before layer j; n = before the heads) right after whose
-        backward some gradient bucket is complete.  Units finish in the order: ctc,
-        decoder, encoder.after_norm (all in the heads node, position n), encoder layer
-        n-1 ... 0 (layer i at position i), encoder.embed (end of the backward)."""
+        """Encoder positions j (cut before layer j; n = before the heads; -1 = between the
+        subsampling's output projection and its convolutions) right after whose backward some
+        gradient bucket is complete.  Units finish in the order: ctc, decoder,
+        encoder.after_norm (all in the heads node, position n), encoder layer n-1 ... 0
+        (layer i at position i), encoder.embed.out (position -1), encoder.embed.conv (end of
+        the backward)."""
         n = len(self.model.encoder.enc_layers)
         cuts = set()
         for names in self.ddp.reducer.unit_names():
@@ -77,6 +79,8 @@ class GraphedTrainStep:
                 cuts.add(n)
             elif last.startswith("encoder.enc_layers."):
                 cuts.add(int(last.rsplit(".", 1)[1]))
+            elif last == "encoder.embed.out":  # inside the subsampling node (EmbedOutFn | EmbedConvFn)
+                cuts.add(-1)
         return sorted(cuts)
 
     # ------------------------------------------------------------ pieces

@@ -105,7 +105,13 @@ class FusedEncoderModel(LiteasrModel):
         after_norm_ready, or unit_ready)."""
         enc = self.encoder
         return (self._head_units() + ["encoder.after_norm"] + [l._pfx for l in reversed(list(enc.enc_layers))]
-                + ["encoder.embed"])
+                + [enc.embed._n(u) for u in enc.embed.UNITS])
+
+    def reducer_bucket_breaks(self):
+        """Units that always start a new gradient bucket: the subsampling convolutions, so
+        the output projection's bucket is launched before their backward and only the
+        convolutions' gradients (2.4 MB at d 256) remain to reduce after the last segment."""
+        return {self.encoder.embed._n("conv")}
 
     def _head_units(self):
         return ["ctc", "decoder"]
@@ -184,7 +190,7 @@ class FusedEncoderModel(LiteasrModel):
         d = enc.h_dim
         rel = getattr(enc, "use_rel", True)
         env.abs_pe = None if rel else enc.pe.table(T)  # absolute PE: added to x in the embed node
-        x = FN.EmbedFn.apply(xs.float(), enc.embed.out.weight, enc.embed, env)
+        x = FN.EmbedFn.apply(xs.float(), enc.embed.out.weight, enc.embed, env, cut=lambda y: self._cut(y, -1))
         pos, pp = None, None
         if rel:  # relative PE: the dropped-out table feeds every layer's positional projection
             pos = torch.empty(T, d, dtype=self.compute_dtype, device=xs.device)
@@ -215,7 +221,8 @@ class FusedEncoderModel(LiteasrModel):
     @contextlib.contextmanager
     def segmented(self, cuts):
         """Cut the autograd graph of the encoder residual stream before encoder layer j
-        for every j in ``cuts`` (j == enc_layers: between the last layer and the heads).
+        for every j in ``cuts`` (j == enc_layers: between the last layer and the heads;
+        j == -1: inside the subsampling, between its convolutions and its output projection).
         Inside the block each forward appends ``(j, x, x_leaf)`` to the yielded list,
         where ``x_leaf = x.detach().requires_grad_()`` is what the rest of the forward
         consumes, so the backward can run as separate pieces (``torch.autograd.grad`` from

@@ -2,7 +2,8 @@
 
 Granularity (one autograd node each, so torch's engine only chains a handful of
 nodes and never casts/sums tensors itself):
-  EmbedFn          Conv2d subsampling + x*sqrt(d) (+dropout)           subsampling.py, positional_encoding.py:68-75
+  EmbedConvFn      Conv2d subsampling convolutions                      subsampling.py:42-46
+  EmbedOutFn       its output projection + x*sqrt(d) (+dropout)        subsampling.py:47-48, positional_encoding.py:68-75
   ConformerLayerFn one RelativeEncoderLayer (macaron FFN, rel-pos MHSA,  conformer_layer.py:130-147
                    conv module, FFN, final LN)
   HeadsFn          encoder after_norm + CTC head (input dropout always   transformer_encoder.py:126, ctc.py:28-30,
@@ -491,11 +492,12 @@ def _conv2_implicit(adt, C):
 
 # ============================================================ autograd nodes ====
 @ranged
-class EmbedFn(torch.autograd.Function):
-    """Conv2DLayer (liteasr/nets/subsampling.py:42-48) + RelativePositionalEncoding's
-    x*sqrt(d) and dropout (positional_encoding.py:68-75).  Channels-last throughout;
-    the c-major flatten of the reference is folded into a column permutation of
-    embed.out.weight (repacked working copy)."""
+class EmbedConvFn(torch.autograd.Function):
+    """Conv2DLayer's two convolutions (liteasr/nets/subsampling.py:42-46): y2 = relu(conv2(
+    relu(conv1(x)))), channels-last, as [roundup32(M2 + 1), C] rows (the rows past M2 are the
+    zero tail the implicit backward GEMMs read in dy2; EmbedOutFn's backward returns dy2 in
+    that shape).  Its backward finishes conv2's and conv1's weight gradients and reports the
+    data-parallel unit ``<embed>.conv``."""
 
     @staticmethod
     def forward(ctx, xs, anchor, mod, env):
@@ -505,80 +507,117 @@ class EmbedFn(torch.autograd.Function):
         adt, dev = env.adt, xs.device
         T1, F1 = (Tx - 3) // 2 + 1, (Fd - 3) // 2 + 1
         T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        M2 = B * T2 * F2
         xs = xs.contiguous()
         y1 = _e((B, T1, F1, C), adt, dev)
         K.conv1_fwd(xs, w.W1, w.b1, y1)
-        y2 = _e((B * T2 * F2, C), adt, dev)
+        y2_full = _e((K.conv2_dy2_rows(M2), C), adt, dev)
+        y2 = y2_full[:M2]
         implicit = _conv2_implicit(adt, C)
         if implicit:  # conv2 as implicit GEMM: im2col(y1) is never materialised
             col = None
             K.conv2_fwd(y1, w.W2p, w.b2, y2)
         else:  # fp32 parity build: explicit im2col + GEMM
-            col = _e((B * T2 * F2, 9 * C), adt, dev)
+            col = _e((M2, 9 * C), adt, dev)
             K.im2col(y1, col)
             K.linear(col, w.W2p, y2, bias=w.b2, act=ACT_RELU)
-        xl = _e((B * T2, w.d), F32, dev)
-        y2f = y2.view(B * T2, F2 * C)
+        ctx.sv = SimpleNamespace(xs=xs, y1=y1, col=col, dims=(B, T1, F1, T2, F2, C), implicit=implicit)
+        ctx.mod, ctx.env = mod, env
+        return y2_full
+
+    @staticmethod
+    def backward(ctx, dy2_full):
+        sv, mod = ctx.sv, ctx.mod
+        B, T1, F1, T2, F2, C = sv.dims
+        w, g = mod.weights(), mod.grads()
+        M2 = B * T2 * F2
+        dev = dy2_full.device
+        dW2 = _e((C, 9 * C), F32, dev)
+        if sv.implicit and K.conv2_dx_w1_ok(C):
+            # dW2 = dy2^T im2col(y1); dy1 = col2im(dy2 W2p) * relu'(y1) is consumed inside the
+            # data-gradient GEMM's epilogue by conv1's weight gradient (never written or re-read)
+            K.conv2_dw(dy2_full, sv.y1, dW2, rowsum=g.b2)
+            K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
+            K.conv2_dx_w1(dy2_full, w.W2p, sv.y1, sv.xs, g.W1, g.b1)
+        else:
+            dy1 = torch.empty_like(sv.y1)
+            if sv.implicit:
+                K.conv2_dw(dy2_full, sv.y1, dW2, rowsum=g.b2)
+                K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
+                K.conv2_dx(dy2_full, w.W2p, sv.y1, dy1)
+            else:
+                dy2 = dy2_full[:M2]
+                K.gemm(dy2.t(), sv.col, dW2, split_k=0, rowsum=g.b2)
+                K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
+                dcol = _e((M2, 9 * C), dy2.dtype, dev)
+                K.gemm(dy2, w.W2p, dcol)
+                K.col2im(dcol, sv.y1, dy1)
+            K.conv1_bwd(sv.xs, dy1, g.W1, g.b1)
+        mod.unit_ready("conv")
+        return None, None, None, None
+
+
+@ranged
+class EmbedOutFn(torch.autograd.Function):
+    """Conv2DLayer's output projection (subsampling.py:47-48) + RelativePositionalEncoding's
+    x*sqrt(d) and dropout (positional_encoding.py:68-75).  The c-major flatten of the
+    reference is folded into a column permutation of embed.out.weight (repacked working
+    copy).  Its backward returns dy2 = (dx W_out) * relu'(y2) with the zero tail rows and
+    reports the data-parallel unit ``<embed>.out`` before the convolutions' backward runs."""
+
+    @staticmethod
+    def forward(ctx, y2_full, anchor, mod, env):
+        B, Tx, Fd = env.embed_in_shape
+        w = mod.weights()
+        C, d = w.C, w.d
+        T1, F1 = (Tx - 3) // 2 + 1, (Fd - 3) // 2 + 1
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        dev = y2_full.device
+        xl = _e((B * T2, d), F32, dev)
+        y2f = y2_full[:B * T2 * F2].view(B * T2, F2 * C)
         K.linear(y2f, w.Woutp, xl, bias=w.bout)
-        x0 = _e((B * T2, w.d), F32, dev)
+        x0 = _e((B * T2, d), F32, dev)
         # relative PE: x * sqrt(d) (positional_encoding.py:68-75); absolute (use_rel False):
         # x * sqrt(d) + pe[t] (:49-56); dropout either way
-        K.pe_fwd(xl, B * T2, T2, w.d, getattr(env, "abs_pe", None), math.sqrt(w.d), x0, env.p_pos, env.seed + 1)
-        ctx.sv = SimpleNamespace(xs=xs, y1=y1, col=col, y2=y2, dims=(B, T1, F1, T2, F2, C), implicit=implicit)
+        K.pe_fwd(xl, B * T2, T2, d, getattr(env, "abs_pe", None), math.sqrt(d), x0, env.p_pos, env.seed + 1)
+        ctx.sv = SimpleNamespace(y2_full=y2_full, dims=(B, T2, F2, C))
         ctx.mod, ctx.env = mod, env
         return x0
 
     @staticmethod
     def backward(ctx, dx0):
         sv, mod, env = ctx.sv, ctx.mod, ctx.env
-        B, T1, F1, T2, F2, C = sv.dims
+        B, T2, F2, C = sv.dims
         w, g = mod.weights(), mod.grads()
         adt, dev = env.adt, dx0.device
         d = w.d
-        M = B * T2
+        M, M2 = B * T2, B * T2 * F2
         gb = _e((M, d), adt, dev)
         K.branch_grad(dx0.contiguous(), gb, math.sqrt(d), env.p_pos, env.seed + 1)
-        y2f = sv.y2.view(M, F2 * C)
+        y2f = sv.y2_full[:M2].view(M, F2 * C)
         dWo = _e((d, F2 * C), F32, dev)
         K.gemm(gb.t(), y2f, dWo, split_k=0, rowsum=g.bout)
         K.permute_last2(dWo, d, C, F2, g.out_w, reverse=True, accumulate=True)
-        M2 = M * F2
-        dW2 = _e((C, 9 * C), F32, dev)
-        if sv.implicit and K.conv2_dx_w1_ok(C):
-            # as below, with dy1 consumed inside the data-gradient GEMM's epilogue by conv1's
-            # weight gradient (the 2-byte-per-element dy1 is never written or re-read)
-            dy2_full = _e((K.conv2_dy2_rows(M2), C), adt, dev)
-            dy2_full[M2:].zero_()
-            dy2 = dy2_full[:M2].view(M, F2 * C)
-            K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
-            K.conv2_dw(dy2_full, sv.y1, dW2, rowsum=g.b2)
-            K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
-            K.conv2_dx_w1(dy2_full, w.W2p, sv.y1, sv.xs, g.W1, g.b1)
-            mod.on_grads_ready()
-            return None, None, None, None
-        dy1 = torch.empty_like(sv.y1)
-        if sv.implicit:
-            # dy2 with the zero tail rows the implicit backward GEMMs read (k padding, taps
-            # outside dy2); dW2 = dy2^T im2col(y1), dy1 = col2im(dy2 W2p) * relu'(y1)
-            dy2_full = _e((K.conv2_dy2_rows(M2), C), adt, dev)
-            dy2_full[M2:].zero_()
-            dy2 = dy2_full[:M2].view(M, F2 * C)
-            K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
-            K.conv2_dw(dy2_full, sv.y1, dW2, rowsum=g.b2)
-            K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
-            K.conv2_dx(dy2_full, w.W2p, sv.y1, dy1)
-        else:
-            dy2 = _e((M, F2 * C), adt, dev)
-            K.gemm(gb, w.Woutp, dy2, aux=y2f, aux_act=ACT_RELU)
-            dy2 = dy2.view(M2, C)
-            K.gemm(dy2.t(), sv.col, dW2, split_k=0, rowsum=g.b2)
-            K.permute_last2(dW2, C, C, 9, g.conv2_w, reverse=True, accumulate=True)
-            dcol = _e((M2, 9 * C), adt, dev)
-            K.gemm(dy2, w.W2p, dcol)
-            K.col2im(dcol, sv.y1, dy1)
-        K.conv1_bwd(sv.xs, dy1, g.W1, g.b1)
-        mod.on_grads_ready()
-        return None, None, None, None
+        mod.unit_ready("out")
+        dy2_full = _e(sv.y2_full.shape, adt, dev)
+        dy2_full[M2:].zero_()
+        K.gemm(gb, w.Woutp, dy2_full[:M2].view(M, F2 * C), aux=y2f, aux_act=ACT_RELU)
+        return dy2_full, None, None, None
+
+
+class EmbedFn:
+    """The subsampling node (Conv2DLayer, subsampling.py:42-48, + the positional encoding's
+    scale and dropout) as two autograd nodes, EmbedConvFn -> EmbedOutFn, so a segmented
+    backward can launch the output projection's gradient bucket before the convolutions'
+    backward runs (``cut``: the model's segment cut between them)."""
+
+    @staticmethod
+    def apply(xs, anchor, mod, env, cut=None):
+        env.embed_in_shape = tuple(xs.shape)
+        y2 = EmbedConvFn.apply(xs, mod.conv_anchor(), mod, env)
+        if cut is not None:
+            y2 = cut(y2)
+        return EmbedOutFn.apply(y2, anchor, mod, env)
 
 
 def enc_attn_forward(ln, pos, w, env, x_in, p_att, s_att, p_res, s_res, p=None, post=None):

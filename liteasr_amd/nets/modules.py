@@ -209,6 +209,19 @@ class Conv2DLayer(_Bound):
                                conv2_w=self._g("conv.2.weight"), b2=self._g("conv.2.bias"),
                                out_w=self._g("out.weight"), bout=self._g("out.bias"))
 
+    # two data-parallel reducer units (models/_fused.py reducer_units): the output projection's
+    # gradients complete before the convolutions' backward runs (nets/functional.py EmbedOutFn)
+    UNITS = ("out", "conv")
+
+    def conv_anchor(self):
+        """The parameter EmbedConvFn takes as its autograd anchor."""
+        return self.conv[0].weight
+
+    def unit_ready(self, part):
+        """Gradients of ``<prefix>.<part>`` (``out`` / ``conv``) are complete."""
+        if self._ready_hook is not None:
+            self._ready_hook(self._n(part))
+
 
 class _LayerCommon(_Bound):
     def _ln(self, name, grad=False):

@@ -28,7 +28,8 @@ def _tiny():
 
 class _FakeBackward(torch.autograd.Function):
     """Writes grad = (rank+1) * unit_index into each unit's flat range, firing hooks in
-    the fused backward's order (ctc, decoder, encoder.after_norm, layers N-1..0, embed)."""
+    the fused backward's order (ctc, decoder, encoder.after_norm, layers N-1..0, the
+    subsampling's output projection, its convolutions)."""
 
     @staticmethod
     def forward(ctx, x, model, rank):
@@ -40,15 +41,19 @@ class _FakeBackward(torch.autograd.Function):
         m, r = ctx.model, ctx.rank
         st = m.store
         grad = st.ensure_grad()
-        order = [m.ctc, m.decoder, "encoder.after_norm"] + list(reversed(list(m.encoder.enc_layers))) + [m.encoder.embed]
+        emb = m.encoder.embed
+        order = [m.ctc, m.decoder, "encoder.after_norm"] + list(reversed(list(m.encoder.enc_layers))) + \
+            [(emb, u) for u in emb.UNITS]
         for i, mod in enumerate(order):
-            pfx = mod if isinstance(mod, str) else mod._pfx
+            pfx = mod if isinstance(mod, str) else mod[0]._n(mod[1]) if isinstance(mod, tuple) else mod._pfx
             for n in st.names:
                 if n == pfx or n.startswith(pfx + "."):
                     o, k = st.offsets[n], st.shapes[n].numel()
                     grad[o:o + k] += (r + 1) * (i + 1)
             if isinstance(mod, str):
                 m.encoder.after_norm_ready()
+            elif isinstance(mod, tuple):
+                mod[0].unit_ready(mod[1])
             else:
                 mod.on_grads_ready()
         return g, None, None
@@ -148,7 +153,8 @@ def test_flat_ddp_gloo_world2():
     assert a["record"] == list(range(a["nbuckets"]))
     assert torch.equal(b["grad_unreduced"], 2 * a["grad_unreduced"])
     assert torch.equal(a["grad_record"], a["grad_sync"]) and torch.equal(b["grad_record"], a["grad_sync"])
-    # cut points: one per bucket whose last unit completes before the embed's backward
+    # cut points: one per bucket whose last unit completes before the subsampling convolutions'
+    # backward
     n_layers = 3
     ends = [u[-1] for u in a["bucket_units"]]
     expect = set()
@@ -157,7 +163,10 @@ def test_flat_ddp_gloo_world2():
             expect.add(n_layers)
         elif e.startswith("encoder.enc_layers."):
             expect.add(int(e.rsplit(".", 1)[1]))
-    assert a["cuts"] == sorted(expect) and len(a["cuts"]) >= 2, (a["cuts"], ends)
+        elif e == "encoder.embed.out":
+            expect.add(-1)  # inside the subsampling: its convolutions' backward is the last segment
+    assert a["cuts"] == sorted(expect) and len(a["cuts"]) >= 2 and -1 in a["cuts"], (a["cuts"], ends)
+    assert ends[-2:] == ["encoder.embed.out", "encoder.embed.conv"], ends
     del st
 
 
@@ -328,8 +337,11 @@ def test_native_spans_tile_flat_buffer_in_bucket_order():
             assert a1 == b0, (name, a1, b0)
         # launch order walks the flat buffer from the heads' end downwards (encoder layers are
         # laid out 0..n-1, and backward completes n-1..0)
-        assert units[0][0] == "ctc" and units[-1][-1] == "encoder.embed", (name, units)
+        assert units[0][0] == "ctc" and units[-1][-1] == "encoder.embed.conv", (name, units)
     spans, units, numel, _ = out["small"]
-    assert units[-1] == ["encoder.embed"]
-    lo, hi = spans[-1]
-    assert abs((hi - lo) * 4 / 1e6 - 7.35) < 0.05 and len(spans) == 6
+    # the subsampling's output projection and its convolutions are buckets of their own: the
+    # projection's is launched before the convolutions' backward, only 2.37 MB is left after it
+    assert units[-2] == ["encoder.embed.out"] and units[-1] == ["encoder.embed.conv"]
+    (lo0, hi0), (lo1, hi1) = spans[-2], spans[-1]
+    assert abs((hi0 - lo0) * 4 / 1e6 - 4.98) < 0.05 and abs((hi1 - lo1) * 4 / 1e6 - 2.37) < 0.05
+    assert len(spans) == 7

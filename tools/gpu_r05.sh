@@ -24,6 +24,11 @@ for s in "$@"; do
     epiab) # FFN fc1 epilogue ablation: the tree's library and the LASR_EXP builds in liteasr_amd/lib/exp
            for rep in 1 2; do for v in tree ${EXP_LIBS:-8 16 24}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 120 python3 tools/epi_ab.py >> "$OUT/epi_ab.jsonl" 2>> "$OUT/epi_ab.err"; done; done ;;
+    envlist) # whole step, one tree, the environments of ENV_LIST ("VAR=val ...;VAR=val;..."), two passes
+           IFS=';' read -ra ENVS <<< "${ENV_LIST:-}"
+           for rep in 1 2; do for i in "${!ENVS[@]}"; do e=${ENVS[$i]}
+             env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/envlist_$i.json" 2> "$OUT/envlist_$i.err" || exit 1
+             grep "^{" "$OUT/envlist_$i.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); a=(d['config'].get('allreduce') or {}); t=a.get('timeline_last_step') or {}; print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'segment_ms': t.get('segment_ms')}))" >> "$OUT/envlist.jsonl"; done; done ;;
     conv2ab) # subsampling conv2 GEMMs: the tree's library vs liteasr_amd/lib/exp/lib$N.so (EXP_LIBS="32 ...")
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 120 python3 tools/conv2_bench.py ${CONV2_SHAPE:-} | sed "s/^{/{\"v\": \"$v\", /" >> "$OUT/conv2_ab.jsonl" || exit 1; done; done ;;
