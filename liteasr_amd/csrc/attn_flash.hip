@@ -26,6 +26,12 @@
 #include "common.h"
 #include "tile.h"
 
+// compile-time ablation knob (measurement builds only; 0 in the product): bit 1 drops the
+// query-side backward's dBD stores, bit 2 the key-side backward's positional term
+#ifndef LASR_ATTN_EXP
+#define LASR_ATTN_EXP 0
+#endif
+
 namespace {
 
 constexpr int KB = 64;   // keys per block
@@ -876,7 +882,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_q_kernel(FlashP a) 
       lds_barrier();
       if (jb + 2 < jb1) issue_stage<DK, NW, RP, RM>(a, b, h, i0, j0 + 2 * KB, ring + stg * Gm::STAGE_BYTES, tid);
     }
-    if constexpr (RP) {
+    if constexpr (RP && !(LASR_ATTN_EXP & 1)) {
       // inverse rel_shift: the bd entry each score read (none for j == i + 1).  A lane's 4 keys
       // of a tile land on 4 consecutive columns of one dBD row unless they straddle the
       // diagonal or T: 2 or 3 stores (by column parity; ldS is even) instead of 4.
@@ -1104,7 +1110,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
   auto load_stats = [&](int i0) {
     const int i = i0 + lane, ic = min(i, T - 1);
     st_m = a.stats[2 * (zrow + ic)];
-    st_l = i < T ? a.stats[2 * (zrow + ic) + 1] : 0.f;  // queries past T: P = 0
+    // (raw loads: the queries-past-T select happens where the value is written to LDS, after
+    // the block's wait -- a select here made hipcc wait vmcnt(0) right behind the next
+    // stage's LDS-DMA)
+    st_l = a.stats[2 * (zrow + ic) + 1];
     st_d = a.Dbuf[zrow + ic];
   };
   if (w == 0) load_stats(0);
@@ -1133,6 +1142,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
     ko.mk = (uint32_t)(4 * g * Gm::KBW + 16 * w + col);
   }
   const uint32_t ring0 = ldsa(ring);
+  // the lane's K / V rows have landed (with the first stage): passed through asm, so hipcc no
+  // longer tracks their loads -- it waited vmcnt(0) before their first MFMA in every tile loop,
+  // which also drained the next stage's LDS-DMA
+  wait_vmcnt<0>();
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) { keep(kf[ks]); keep(vf[ks]); }
   f32x4 dkt[DK / 16], dvt[DK / 16];
 #pragma unroll
   for (int t = 0; t < DK / 16; ++t) { dkt[t] = zero4(); dvt[t] = zero4(); }
@@ -1145,8 +1160,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
     if (w == 0) {  // this block's statistics into its slot (the other slot may still be read)
       const float m2 = st_m <= -1e38f ? -1e38f : st_m * 1.4426950408889634f;
       const uint32_t sa = ldsa(ss + lane);
+      const float lv = i0 + lane < T ? st_l : 0.f;  // queries past T: P = 0
       asm volatile("ds_write_b32 %0, %1" ::"v"(sa), "v"(m2) : "memory");
-      asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(sa), "v"(st_l), "i"(4 * QBK) : "memory");
+      asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(sa), "v"(lv), "i"(4 * QBK) : "memory");
       asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(sa), "v"(st_d), "i"(8 * QBK) : "memory");
     }
     lds_barrier();
@@ -1242,7 +1258,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
           dp = mfma(as_frag(ao[ks]), vf[ks], dp);
         }
         float bd[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (RP) {
+        if constexpr (RP && !(LASR_ATTN_EXP & 2)) {
           const int mlo = jw - (i0 + 16 * r + 15) + T - 1;
           lgkm0();
 #pragma unroll

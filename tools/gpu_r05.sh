@@ -44,13 +44,19 @@ for s in "$@"; do
            for v in base new base new; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=$R/ab_prev/liteasr_amd/lib/libliteasr_hip.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_ab_$v.tmp" >> "$OUT/attn_ab.jsonl"; rm -f "$OUT/attn_ab_$v.tmp"; done ;;
+    attnexp) # attention kernels: the tree's library vs liteasr_amd/lib/exp/lib$N.so ablation builds (EXP_LIBS), twice
+           for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
+             LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_exp_$v.tmp"
+             sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_exp_$v.tmp" >> "$OUT/attn_exp.jsonl"; rm -f "$OUT/attn_exp_$v.tmp"; done; done ;;
     stepab) # whole step: the previous commit's tree (ab_prev/: `git archive` + its built library) vs this
            # tree, alternating (AB_ARGS: e.g. --config large)
            for v in base new base new; do d=$R; [ $v = base ] && d=$R/ab_prev
              (cd $d && run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-}) > "$OUT/step_ab_$v.json" 2> "$OUT/step_ab_$v.err" || exit 1
              grep "^{" "$OUT/step_ab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'utt_s': d['value']}))" >> "$OUT/step_ab.jsonl"; done ;;
-    attnprof) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/attn_trace" -o run -- python3 "$R/tools/attn_bench.py" > "$OUT/attn_trace.log" 2>&1
-           cp "$(find "$OUT/attn_trace" -name '*kernel_stats.csv' | head -1)" "$OUT/attn_kernel_stats.csv"; rm -rf "$OUT/attn_trace"
+    attnprof) cd /tmp
+           for cs in ${ATTN_CASES:-small long}; do
+             run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/attn_trace" -o run -- python3 "$R/tools/attn_bench.py" $cs > "$OUT/attn_trace.log" 2>&1
+             cp "$(find "$OUT/attn_trace" -name '*kernel_stats.csv' | head -1)" "$OUT/attn_kernel_stats_$cs.csv"; rm -rf "$OUT/attn_trace"; done
            S1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_INSTS_VALU"
            S2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_SCA"
            for cs in ${ATTN_CASES:-small long}; do i=0; for set in "$S1" "$S2"; do i=$((i+1))
