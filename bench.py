@@ -711,11 +711,20 @@ def main():
         else:
             case = {"dw": roofline_case, "hot": hottest_case, "attn": attention_case}[args.roofline_case]
             launch, flops, bytes_, meta = case(CONFIGS[args.config], torch.device("cuda", 0))
-        for _ in range(args.roofline_only):
+        for _ in range(3):
             launch()
         torch.cuda.synchronize()
-        print(json.dumps({**meta, "launches": args.roofline_only, "algorithmic_bytes_per_launch": bytes_,
-                          "algorithmic_flops_per_launch": flops}), flush=True)
+        # (timed on the current stream, which these cases launch on: a quick A/B figure, eager
+        # launches included; the PMC passes read the counters of the same launches)
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(args.roofline_only):
+            launch()
+        t1.record()
+        torch.cuda.synchronize()
+        us = t0.elapsed_time(t1) * 1e3 / max(args.roofline_only, 1)
+        print(json.dumps({**meta, "launches": args.roofline_only + 3, "algorithmic_bytes_per_launch": bytes_,
+                          "algorithmic_flops_per_launch": flops, "us_per_launch_eager": round(us, 2)}), flush=True)
         return
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:

@@ -36,6 +36,7 @@ for s in "$@"; do
            for v in A B A B; do e=$ENV_A; [ $v = B ] && e=$ENV_B
              env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/envab_$v.json" 2> "$OUT/envab_$v.err" || exit 1
              grep "^{" "$OUT/envab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median')}))" >> "$OUT/envab.jsonl"; done ;;
+    switches) run timeout -k 10 900 $PYT tests/test_switches_gpu.py > "$OUT/switches.log" 2>&1 ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
            "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" -s > "$OUT/new5.log" 2>&1 ;;
     attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
@@ -48,6 +49,11 @@ for s in "$@"; do
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_exp_$v.tmp"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_exp_$v.tmp" >> "$OUT/attn_exp.jsonl"; rm -f "$OUT/attn_exp_$v.tmp"; done; done ;;
+    caseab) # bench.py roofline cases (RCASES "small:dw large:dw ..."): the tree's library vs lib/exp/lib$N.so (EXP_LIBS), twice
+           for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
+             for rc in ${RCASES:-small:dw}; do cfg=${rc%%:*}; cs=${rc##*:}
+               LITEASR_HIP_LIB=$lib run timeout -k 10 200 python3 bench.py --config $cfg --roofline-only 20 --roofline-case $cs > "$OUT/caseab.tmp" 2>> "$OUT/caseab.err"
+               grep "^{" "$OUT/caseab.tmp" | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'cfg': '$cfg', 'case': '$cs', 'kernel': d.get('kernel'), 'us': d.get('us_per_launch_eager')}))" >> "$OUT/caseab.jsonl"; done; done; done ;;
     stepab) # whole step: the previous commit's tree (ab_prev/: `git archive` + its built library) vs this
            # tree, alternating (AB_ARGS: e.g. --config large)
            for v in base new base new; do d=$R; [ $v = base ] && d=$R/ab_prev
