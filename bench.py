@@ -841,6 +841,8 @@ def main():
             "step_mfma_frac": round(cfgd["gflop"] * utt / world / 1e3 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(final_loss, 4), "optimizer_state": st,
         }
+        if args.graph == "on":  # launches per step: the node counts of the replayed graphs
+            out["graph_nodes_per_step"] = step.graph_nodes()
         if args.profile:
             out["config"]["profile"] = "roctx ranges per fused node (eager)"
         out["mfma_counter"] = pmc_mfma(args.config)

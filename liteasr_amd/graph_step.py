@@ -42,6 +42,51 @@ from . import kernels as K
 _MODE = "thread_local"
 
 
+def _new_graph():
+    """A graph whose template is kept after capture (``node_counts`` reads it); instantiated
+    explicitly right after its capture (``_done``)."""
+    try:
+        return torch.cuda.CUDAGraph(keep_graph=True)
+    except TypeError:  # an older torch: no template to count
+        return torch.cuda.CUDAGraph()
+
+
+def _done(g):
+    if hasattr(g, "instantiate"):
+        try:
+            g.instantiate()
+        except RuntimeError:  # already instantiated (keep_graph unsupported)
+            pass
+    return g
+
+
+_HIP_NODE_TYPES = {0: "kernel", 1: "memcpy", 2: "memset"}
+
+
+def node_counts(graphs):
+    """Kernel / memcpy / memset / other node counts of captured graphs (hipGraphGetNodes on
+    the kept templates): the launches one replay issues.  None when no template was kept."""
+    import ctypes
+
+    try:
+        lib = ctypes.CDLL("libamdhip64.so")
+        handles = [g.raw_cuda_graph() for g in graphs]
+    except (OSError, RuntimeError, AttributeError):
+        return None
+    out = {"kernel": 0, "memcpy": 0, "memset": 0, "other": 0}
+    for h in handles:
+        n = ctypes.c_size_t(0)
+        if lib.hipGraphGetNodes(ctypes.c_void_p(h), None, ctypes.byref(n)) != 0:
+            return None
+        nodes = (ctypes.c_void_p * n.value)()
+        lib.hipGraphGetNodes(ctypes.c_void_p(h), nodes, ctypes.byref(n))
+        for nd in nodes:
+            t = ctypes.c_int(-1)
+            lib.hipGraphNodeGetType(ctypes.c_void_p(nd), ctypes.byref(t))
+            out[_HIP_NODE_TYPES.get(t.value, "other")] += 1
+    return out
+
+
 class GraphedTrainStep:
     def __init__(self, net, criterion, optimizer, example_batch, clip: float = 5.0, warmup: int = 2,
                  overlap: bool = True, restore: bool = True):
@@ -140,17 +185,20 @@ class GraphedTrainStep:
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
             if self.ddp is None:
-                self.g1 = torch.cuda.CUDAGraph()
+                self.g1 = _new_graph()
                 with torch.cuda.graph(self.g1, capture_error_mode=_MODE):
                     self.loss = self._full()
+                _done(self.g1)
                 self.segs, self.after, self.gupd = None, None, None
             elif not self.overlap:
-                self.g1 = torch.cuda.CUDAGraph()
+                self.g1 = _new_graph()
                 with torch.cuda.graph(self.g1, capture_error_mode=_MODE):
                     self.loss = self._fwd_bwd()
-                self.gupd = torch.cuda.CUDAGraph()
+                _done(self.g1)
+                self.gupd = _new_graph()
                 with torch.cuda.graph(self.gupd, capture_error_mode=_MODE):
                     self._update()
+                _done(self.gupd)
                 self.segs, self.after = None, None
             else:
                 self.segs, self.after = [], []
@@ -159,9 +207,10 @@ class GraphedTrainStep:
                 try:
                     pool = None
                     for i, fn in enumerate(self._segments()):
-                        g = torch.cuda.CUDAGraph()
+                        g = _new_graph()
                         with torch.cuda.graph(g, pool=pool, capture_error_mode=_MODE):
                             out = fn()
+                        _done(g)
                         if i == 0:
                             self.loss = out
                             pool = g.pool()
@@ -173,9 +222,10 @@ class GraphedTrainStep:
                     red._reset()
                 launched = [b for a in self.after for b in a]
                 assert launched == list(range(len(red.buckets))), launched
-                self.gupd = torch.cuda.CUDAGraph()
+                self.gupd = _new_graph()
                 with torch.cuda.graph(self.gupd, pool=pool, capture_error_mode=_MODE):
                     self._update()
+                _done(self.gupd)
             torch.cuda.synchronize()
             # the graphs address this scratch buffer: keep it alive even if a later eager
             # call grows the workspace (kernels._Workspace replaces, never resizes)
@@ -264,6 +314,13 @@ class GraphedTrainStep:
 
     # ------------------------------------------------------------ timing
     _events = None
+
+    def graph_nodes(self):
+        """Launches per replayed step: node counts of every graph the step replays."""
+        gs = [self.g1] if self.segs is None else list(self.segs)
+        if self.gupd is not None:
+            gs.append(self.gupd)
+        return node_counts(gs)
 
     def enable_timing(self):
         """Record HIP events between the replayed segments (eager, outside the graphs) so
