@@ -563,8 +563,8 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
   }
 }
 
-// Channel c's outputs from the combined statistics (shared by both finalisation kernels;
-// explicit fmaf / products so both compile to the same roundings).
+// Channel c's outputs from the combined statistics (explicit fmaf / products: the roundings do
+// not depend on what hipcc contracts).
 LASR_DEV void bn_final_write(int c, double n, double mu, double m2, float eps, float momentum, const float* gamma,
                              const float* beta, float* rmean, float* rvar, float* mean, float* rstd, float* scale,
                              float* shift, int update) {
@@ -644,88 +644,6 @@ __global__ __launch_bounds__(1024) void bn_finalize_par_kernel(
   }
   if (ty != 0 || c >= C) return;
   m2 = sm2[0][tx];
-  bn_final_write(c, n, mu, m2, eps, momentum, gamma, beta, rmean, rvar, mean, rstd, scale, shift, update);
-}
-
-// The same finalisation with one 64-lane wave per channel (4 channels per 256-thread block, 64
-// blocks at C = 256 instead of 16) and no LDS or block barriers: lane l takes the partials
-// l, l + 64, ... in order (bn_finalize_par's group ty = l) and the 64 groups are combined by
-// shuffles in bn_finalize_par's pairwise tree order (lane i += lane i + w, w = 32 .. 1), so the
-// double sums -- and every output -- are bit-identical to it.  A lane keeps up to BNW_KEEP
-// partials in registers between the two passes.
-constexpr int BNW_KEEP = 8;
-LASR_DEV double shfl_down_d(double v, int w) {
-  const int2 u = __builtin_bit_cast(int2, v);
-  return __builtin_bit_cast(double, make_int2(__shfl_down(u.x, w, 64), __shfl_down(u.y, w, 64)));
-}
-LASR_DEV double tree64(double v) {
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) v += shfl_down_d(v, w);
-  return v;  // lane 0
-}
-__global__ __launch_bounds__(256) void bn_finalize_wave_kernel(
-    const float* stats, int nparts, int C, float eps, float momentum, const float* gamma,
-    const float* beta, float* rmean, float* rvar, int64_t* nbt, float* mean, float* rstd,
-    float* scale, float* shift, int update) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && update == 1 && nbt) nbt[0] += 1;
-  if (c >= C) return;  // wave-uniform
-  if (update == 2) {
-    if (lane == 0) {
-      const float rs = rsqrtf(rvar[c] + eps);
-      mean[c] = rmean[c];
-      rstd[c] = rs;
-      const float sc = __fmul_rn(gamma[c], rs);
-      scale[c] = sc;
-      shift[c] = fmaf(-rmean[c], sc, beta[c]);
-    }
-    return;
-  }
-  float kn[BNW_KEEP], km[BNW_KEEP], k2[BNW_KEEP];
-#pragma unroll
-  for (int k = 0; k < BNW_KEEP; ++k) {
-    const int p = lane + 64 * k;
-    const float* st = stats + (int64_t)min(p, nparts - 1) * 3 * C;
-    kn[k] = p < nparts ? st[c] : 0.f;
-    km[k] = st[C + c];
-    k2[k] = st[2 * C + c];
-  }
-  double n = 0.0, s = 0.0;
-#pragma unroll
-  for (int k = 0; k < BNW_KEEP; ++k)
-    if (lane + 64 * k < nparts) {
-      const double nb = kn[k];
-      n += nb;
-      s += nb * (double)km[k];
-    }
-  for (int p = lane + 64 * BNW_KEEP; p < nparts; p += 64) {
-    const float* st = stats + (int64_t)p * 3 * C;
-    const double nb = st[c];
-    n += nb;
-    s += nb * (double)st[C + c];
-  }
-  n = tree64(n);
-  s = tree64(s);
-  n = __builtin_bit_cast(double, make_int2(__shfl(__builtin_bit_cast(int2, n).x, 0, 64),
-                                           __shfl(__builtin_bit_cast(int2, n).y, 0, 64)));
-  s = __builtin_bit_cast(double, make_int2(__shfl(__builtin_bit_cast(int2, s).x, 0, 64),
-                                           __shfl(__builtin_bit_cast(int2, s).y, 0, 64)));
-  const double mu = n > 0.0 ? s / n : 0.0;
-  double m2 = 0.0;
-#pragma unroll
-  for (int k = 0; k < BNW_KEEP; ++k)
-    if (lane + 64 * k < nparts) {
-      const double nb = kn[k], dl = (double)km[k] - mu;
-      m2 += (double)k2[k] + nb * dl * dl;
-    }
-  for (int p = lane + 64 * BNW_KEEP; p < nparts; p += 64) {
-    const float* st = stats + (int64_t)p * 3 * C;
-    const double nb = st[c], dl = (double)st[C + c] - mu;
-    m2 += (double)st[2 * C + c] + nb * dl * dl;
-  }
-  m2 = tree64(m2);
-  if (lane != 0) return;
   bn_final_write(c, n, mu, m2, eps, momentum, gamma, beta, rmean, rvar, mean, rstd, scale, shift, update);
 }
 
@@ -966,15 +884,9 @@ extern "C" int lasr_bn_finalize(const float* stats_ws, int nparts, int C, float 
                                 float* running_mean, float* running_var, int64_t* num_batches,
                                 float* mean, float* rstd, float* scale, float* shift,
                                 int update_running, void* stream) {
-  static const bool wave = [] { const char* e = getenv("LASR_BN_WAVE"); return !(e && e[0] == '0'); }();
-  if (wave)
-    bn_finalize_wave_kernel<<<(unsigned)cdiv(C, 4), 256, 0, (hipStream_t)stream>>>(
-        stats_ws, nparts, C, eps, momentum, gamma, beta, running_mean, running_var, num_batches,
-        mean, rstd, scale, shift, update_running);
-  else
-    bn_finalize_par_kernel<<<(unsigned)cdiv(C, BNF_C), BNF_C * BNF_G, 0, (hipStream_t)stream>>>(
-        stats_ws, nparts, C, eps, momentum, gamma, beta, running_mean, running_var, num_batches,
-        mean, rstd, scale, shift, update_running);
+  bn_finalize_par_kernel<<<(unsigned)cdiv(C, BNF_C), BNF_C * BNF_G, 0, (hipStream_t)stream>>>(
+      stats_ws, nparts, C, eps, momentum, gamma, beta, running_mean, running_var, num_batches,
+      mean, rstd, scale, shift, update_running);
   return lasr_check_launch("bn_finalize");
 }
 

@@ -14,9 +14,7 @@ the parent never touches the GPU.
   LASR_FUSED_LN2       a layer's final norm and the next layer's first norm in one launch
   LASR_BATCH_POS_PROJ  the 12 positional projections as one strided batched GEMM
   LASR_EPI_SPEC        compile-time epilogue instances vs the runtime-branch epilogue
-  LASR_DW_SLICE_XCD    grouped dW K slices tied to XCDs vs the plain block order
-  LASR_BN_WAVE         BatchNorm finalisation with one wave per channel (shuffle tree) vs the
-                       1024-thread LDS-tree kernel"""
+  LASR_DW_SLICE_XCD    grouped dW K slices tied to XCDs vs the plain block order"""
 
 import os
 import subprocess
@@ -29,7 +27,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SWITCHES = ["LASR_ROW_LN", "LASR_DEC_ROW_LN", "LASR_FUSED_LN2", "LASR_BATCH_POS_PROJ", "LASR_EPI_SPEC",
-            "LASR_DW_SLICE_XCD", "LASR_BN_WAVE"]
+            "LASR_DW_SLICE_XCD"]
 
 
 def _step(tmp_path, name, env_extra):
