@@ -601,6 +601,12 @@ def test_graphed_step_matches_eager():
     assert graphed == eager, (graphed, eager)
     assert torch.equal(m1.store.flat, m2.store.flat)
     assert o1.device_state() == o2.device_state()
+    # the launches one replay issues (bench.py's graph_nodes_per_step): every node of the
+    # kept graph templates is a kernel (the product allocates outside the capture, no
+    # memcpy / memset nodes), and a replay issues at least one per fused node
+    nodes = gs.graph_nodes()
+    assert nodes is not None and nodes["memcpy"] == 0 and nodes["other"] == 0, nodes
+    assert nodes["kernel"] > 50, nodes
 
 
 def test_graphed_step_survives_workspace_growth():
