@@ -1182,7 +1182,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
       }
     }
     const uint32_t mrow = sb + Gm::M0 * 16u + ko.mk;
-#pragma unroll 1
+#pragma unroll
     for (int rs = 0; rs < 2; ++rs) {  // query tile pairs (2rs, 2rs + 1)
       f32x4 p2[2], ds2[2];
 #pragma unroll

@@ -419,6 +419,136 @@ LASR_DEV void ctc_lattice_chunked(int b, int T_, int Lmax, const int32_t* __rest
   }
 }
 
+// ---- the lattice in registers, CTC_K steps per barrier ----------------------------------
+// A step's state s needs s, s -/+ 1 and s -/+ 2 of the previous step: neighbouring lanes of
+// one wave, read with DPP wave shifts instead of an LDS round trip and a block barrier per
+// step.  Wave w owns CTC_OWN consecutive states and also computes the 2 CTC_K states beside
+// them (the halo, on the side the recursion reads from): after k in-register steps the 2k
+// outermost halo lanes are stale, so CTC_K steps leave every owned lane exact.  The owned
+// lanes then publish their states to a double-buffered LDS vector and the block syncs once
+// per CTC_K steps (the emission chunks stay staged in LDS as in ctc_lattice_chunked).  Per
+// state the arithmetic is ctc_lattice_chunked's, operand for operand: alpha, beta and nll
+// are unchanged.
+constexpr int CTC_K = 8;
+constexpr int CTC_OWN = 64 - 2 * CTC_K;
+static_assert(CTC_CH % CTC_K == 0, "a step period never straddles an emission chunk");
+LASR_DEV float dpp_shr1(float v) {  // lane l gets lane l - 1 (lane 0: -inf)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+LASR_DEV float dpp_shl1(float v) {  // lane l gets lane l + 1 (lane 63: -inf)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+static int ctc_reg_waves(int Smax) { return (Smax + CTC_OWN - 1) / CTC_OWN; }
+static size_t ctc_reg_lds(int Lmax) { return ((size_t)2 * (2 * Lmax + 1) + (size_t)CTC_CH * (Lmax + 1)) * sizeof(float); }
+
+template <int DIR>
+LASR_DEV void ctc_lattice_regs(int b, int T_, int Lmax, const int32_t* __restrict__ targets, const int32_t* ilen,
+                               const int32_t* tlen, const float* lp, float* out, float* nll) {
+  extern __shared__ float sh[];
+  const int Tb = ilen[b], Lb = tlen[b], S = 2 * Lb + 1, Smax = 2 * Lmax + 1;
+  if (Tb <= 0) {
+    if (DIR > 0 && threadIdx.x == 0) nll[b] = (Lb == 0) ? 0.f : INFINITY;
+    return;
+  }
+  const int32_t* tg = targets + (int64_t)b * Lmax;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nt = blockDim.x;
+  // the lane's state; owned lanes publish it, halo lanes only feed their neighbours
+  const int s = DIR > 0 ? w * CTC_OWN + lane - 2 * CTC_K : w * CTC_OWN + lane;
+  const bool own = (DIR > 0 ? lane >= 2 * CTC_K : lane < CTC_OWN) && s < Smax;
+  const bool act = s >= 0 && s < S;
+  const bool skip = DIR > 0 ? act && s >= 2 && (s & 1) && ext_label(tg, s) != ext_label(tg, s - 2)
+                            : act && s + 2 < S && (s & 1) && ext_label(tg, s) != ext_label(tg, s + 2);
+  const bool near = DIR > 0 ? s >= 1 : s + 1 < S;  // the s -/+ 1 term exists
+  const int eix = (s & 1) ? 1 + (s >> 1) : 0;
+  const int ld = Lmax + 1;
+  const float* lpu = lp + (int64_t)b * T_ * ld;
+  const int64_t last = (int64_t)T_ * ld - 1;
+  float* o = out + (int64_t)b * T_ * Smax;
+  float* vec[2] = {sh, sh + Smax};
+  float* chunk = sh + 2 * Smax;
+  const int CHN = CTC_CH * ld;
+  const int t_first = DIR > 0 ? 0 : Tb - 1;
+  float v = -INFINITY;
+  if (act) {
+    const float e = lpu[(int64_t)t_first * ld + eix];
+    v = DIR > 0 ? (s <= 1 ? e : -INFINITY) : (s >= S - 2 ? e : -INFINITY);
+    if (own) o[(int64_t)t_first * Smax + s] = v;
+  }
+  if (own && act) vec[0][s] = v;
+  const int nsteps = Tb - 1;
+  auto row0 = [&](int c) {
+    const int i_lo = 1 + c * CTC_CH, i_hi = min(i_lo + CTC_CH - 1, nsteps);
+    return DIR > 0 ? t_first + i_lo : t_first - i_hi;
+  };
+  float pre[CTC_CHR];
+  auto load_regs = [&](int c) {
+    const int64_t base = (int64_t)row0(c) * ld;
+#pragma unroll
+    for (int r = 0; r < CTC_CHR; ++r) {
+      const int idx = r * nt + threadIdx.x;
+      pre[r] = idx < CHN ? lpu[min(base + idx, last)] : 0.f;
+    }
+  };
+  auto store_regs = [&]() {
+#pragma unroll
+    for (int r = 0; r < CTC_CHR; ++r) {
+      const int idx = r * nt + threadIdx.x;
+      if (idx < CHN) chunk[idx] = pre[r];
+    }
+  };
+  const int nchunks = (nsteps + CTC_CH - 1) / CTC_CH;
+  if (nchunks > 0) {
+    load_regs(0);
+    store_regs();
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int c = 0; c < nchunks; ++c) {
+    if (c + 1 < nchunks) load_regs(c + 1);  // lands during this chunk's steps
+    const int r0 = row0(c), i_lo = 1 + c * CTC_CH, i_hi = min(i_lo + CTC_CH - 1, nsteps);
+    for (int p0 = i_lo; p0 <= i_hi; p0 += CTC_K) {
+      // the period's start states (owned by this wave or its neighbour) and its emissions
+      v = act ? vec[cur][s] : -INFINITY;
+      float e[CTC_K];
+#pragma unroll
+      for (int k = 0; k < CTC_K; ++k) {
+        const int t = t_first + DIR * (p0 + k);
+        e[k] = act && p0 + k <= i_hi ? chunk[(t - r0) * ld + eix] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < CTC_K; ++k) {
+        if (p0 + k > i_hi) break;  // block-uniform
+        const float n1 = DIR > 0 ? dpp_shr1(v) : dpp_shl1(v);
+        const float n2 = DIR > 0 ? dpp_shr1(n1) : dpp_shl1(n1);
+        const float nv = lse3(v, near ? n1 : -INFINITY, skip ? n2 : -INFINITY) + e[k];
+        v = act ? nv : -INFINITY;
+        if (own && act) o[(int64_t)(t_first + DIR * (p0 + k)) * Smax + s] = v;
+      }
+      cur ^= 1;
+      if (own && act) vec[cur][s] = v;
+      lds_step_sync();
+    }
+    if (c + 1 < nchunks) {  // every wave is past its last read of this chunk (the period barrier)
+      store_regs();
+      lds_step_sync();
+    }
+  }
+  if (DIR > 0 && threadIdx.x == 0) {
+    const float* fin = vec[cur];
+    const float ll = (S >= 2) ? lse2(fin[S - 1], fin[S - 2]) : fin[0];
+    nll[b] = -ll;
+  }
+}
+
+__global__ void ctc_lattice_regs_kernel(int B, int T_, int Lmax, const int32_t* __restrict__ targets,
+                                        const int32_t* ilen, const int32_t* tlen, const float* lp, float* alpha,
+                                        float* nll, float* beta, int beta_only) {
+  if (!beta_only && (int)blockIdx.x < B)
+    ctc_lattice_regs<1>(blockIdx.x, T_, Lmax, targets, ilen, tlen, lp, alpha, nll);
+  else
+    ctc_lattice_regs<-1>(beta_only ? blockIdx.x : blockIdx.x - B, T_, Lmax, targets, ilen, tlen, lp, beta, nullptr);
+}
+
 __global__ void ctc_lattice_chunked_kernel(int B, int T_, int Lmax, const int32_t* __restrict__ targets,
                                            const int32_t* ilen, const int32_t* tlen, const float* lp, float* alpha,
                                            float* nll, float* beta, int beta_only) {
@@ -452,12 +582,24 @@ extern "C" int lasr_ctc_fwd(const void* logits, int ldt, int B, int T, int V, in
   return lasr_ctc_lattice(B, T, Lmax, targets, ilen, tlen, lp, alpha, beta, nll, stream);
 }
 
+// the register-resident lattice when its block fits (64 lanes per CTC_OWN states);
+// LASR_CTC_REGS=0 keeps the one-state-per-thread chunked kernel (same outputs)
+static bool ctc_regs_ok(int Lmax) {
+  static const bool on = [] { const char* e = getenv("LASR_CTC_REGS"); return !(e && e[0] == '0'); }();
+  return on && 64 * ctc_reg_waves(2 * Lmax + 1) <= 1024 && ctc_reg_lds(Lmax) <= 64 * 1024;
+}
+
 extern "C" int lasr_ctc_lattice(int B, int T, int Lmax, const int32_t* targets, const int32_t* ilen,
                                 const int32_t* tlen, const float* lp, float* alpha, float* beta, float* nll,
                                 void* stream) {
   LASR_CHECK_ARG(B > 0 && T > 0 && Lmax >= 0 && 2 * Lmax + 1 <= 1024, "lasr_ctc_lattice: bad sizes");
   LASR_CHECK_ARG(lp && alpha && nll, "lasr_ctc_lattice: lp / alpha / nll");
   const int Smax = 2 * Lmax + 1;
+  if (ctc_regs_ok(Lmax)) {
+    ctc_lattice_regs_kernel<<<beta ? 2 * B : B, 64 * ctc_reg_waves(Smax), ctc_reg_lds(Lmax), (hipStream_t)stream>>>(
+        B, T, Lmax, targets, ilen, tlen, lp, alpha, nll, beta, 0);
+    return lasr_check_launch("ctc_lattice");
+  }
   if (ctc_chunk_lds(Lmax) <= 64 * 1024) {
     ctc_lattice_chunked_kernel<<<beta ? 2 * B : B, ctc_block(Smax), ctc_chunk_lds(Lmax), (hipStream_t)stream>>>(
         B, T, Lmax, targets, ilen, tlen, lp, alpha, nll, beta, 0);
@@ -477,7 +619,12 @@ extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, in
   LASR_CHECK_ARG(2 * Lmax + 1 <= 1024, "lasr_ctc_bwd: Lmax=%d too large", Lmax);
   hipStream_t st = (hipStream_t)stream;
   const int Smax = 2 * Lmax + 1;
-  if (!beta_ready && ctc_chunk_lds(Lmax) <= 64 * 1024) {
+  if (!beta_ready && ctc_regs_ok(Lmax)) {
+    ctc_lattice_regs_kernel<<<B, 64 * ctc_reg_waves(Smax), ctc_reg_lds(Lmax), st>>>(B, T, Lmax, targets, ilen, tlen, lp,
+                                                                                    nullptr, nullptr, beta, 1);
+    const int rc = lasr_check_launch("ctc_beta");
+    if (rc) return rc;
+  } else if (!beta_ready && ctc_chunk_lds(Lmax) <= 64 * 1024) {
     ctc_lattice_chunked_kernel<<<B, ctc_block(Smax), ctc_chunk_lds(Lmax), st>>>(B, T, Lmax, targets, ilen, tlen, lp,
                                                                                 nullptr, nullptr, beta, 1);
     const int rc = lasr_check_launch("ctc_beta");

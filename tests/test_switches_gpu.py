@@ -14,7 +14,9 @@ the parent never touches the GPU.
   LASR_FUSED_LN2       a layer's final norm and the next layer's first norm in one launch
   LASR_BATCH_POS_PROJ  the 12 positional projections as one strided batched GEMM
   LASR_EPI_SPEC        compile-time epilogue instances vs the runtime-branch epilogue
-  LASR_DW_SLICE_XCD    grouped dW K slices tied to XCDs vs the plain block order"""
+  LASR_DW_SLICE_XCD    grouped dW K slices tied to XCDs vs the plain block order
+  LASR_CTC_REGS        the CTC lattice in registers (DPP neighbour reads, one barrier per 8
+                       steps) vs one state per thread with a barrier per step"""
 
 import os
 import subprocess
@@ -27,7 +29,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SWITCHES = ["LASR_ROW_LN", "LASR_DEC_ROW_LN", "LASR_FUSED_LN2", "LASR_BATCH_POS_PROJ", "LASR_EPI_SPEC",
-            "LASR_DW_SLICE_XCD"]
+            "LASR_DW_SLICE_XCD", "LASR_CTC_REGS"]
 
 
 def _step(tmp_path, name, env_extra):

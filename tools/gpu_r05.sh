@@ -94,7 +94,8 @@ for s in "$@"; do
            python3 "$R/tools/step_summary.py" "$db" 5 --grid > "$OUT/step_summary_grid.txt" 2>&1
            python3 "$R/tools/step_summary.py" "$db" 5 --order > "$OUT/step_order.txt" 2>&1; rm -f "$db" ;;
     tracelong) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_long" -o run -- python3 "$R/bench.py" --config long --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace_long.log" 2>&1
-           db=$(find "$OUT/trace_long" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_long.txt" 2>&1; rm -f "$db" ;;
+           db=$(find "$OUT/trace_long" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_long.txt" 2>&1
+           python3 "$R/tools/step_summary.py" "$db" 5 --order > "$OUT/step_order_long.txt" 2>&1; rm -f "$db" ;;
     tracelarge) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_large" -o run -- python3 "$R/bench.py" --config large --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace_large.log" 2>&1
            db=$(find "$OUT/trace_large" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_large.txt" 2>&1; rm -f "$db" ;;
     profile) cd /tmp && run timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d "$OUT/prof_markers" -o run -- python3 "$R/bench.py" --profile --no-cpu-baseline --no-roofline --steps 3 --warmup 1 > "$OUT/profile.log" 2>&1 ;;
