@@ -510,7 +510,7 @@ def ctc_roofline(cfgd, dev, iters=20):
     tg, tl, tr = _time_case(gather, iters), _time_case(lattice, iters), _time_case(gradk, iters)
     tot = tg + tl + tr
     byt = 2.0 * B * Tp * V_ * 2
-    return {"kernels": ["ctc_lse_gather_kernel", "ctc_lattice_chunked_kernel", "ctc_grad_kernel"],
+    return {"kernels": ["ctc_lse_gather_kernel", "ctc_lattice_regs_kernel", "ctc_grad_kernel"],
             "shape": f"B={B} T'={Tp} V={V_} L={L} (S=2L+1={S}), bf16 logits",
             "gather_us": round(tg * 1e6, 2), "lattice_us": round(tl * 1e6, 2), "grad_us": round(tr * 1e6, 2),
             "total_us": round(tot * 1e6, 2), "algorithmic_bytes": byt,

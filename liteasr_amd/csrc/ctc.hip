@@ -210,6 +210,11 @@ __global__ void ctc_beta_kernel(int T_, int Lmax, const int32_t* __restrict__ ta
   ctc_beta(blockIdx.x, T_, Lmax, targets, ilen, tlen, lp, beta);
 }
 
+// timing ablations (tools/gemm_exp.sh with EXP_FILES=ctc; 0 in the product): bit 1 skips the
+// label-gamma scan, bit 2 the whole per-row preamble (blank sum, label posteriors, scan)
+#ifndef LASR_EXP
+#define LASR_EXP 0
+#endif
 template <typename T, typename TG>
 __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ logits, int B, int T_,
                                                        int V, int64_t ld,
@@ -219,14 +224,20 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
                                                        const float* lp, const float* alpha,
                                                        const float* beta, const float* nll,
                                                        TG* grad, float gscale, const float* gdev) {
-  // dynamic LDS: [Lmax] gamma per label position, [Lmax] labels, [(V+31)/32] label bitmap,
-  // [V] gamma per vocabulary entry (read only where the bitmap is set)
+  // dynamic LDS: per label position (Lmax, rounded to 4) its posterior, label, first position
+  // of its label, claim slot and running sum; [(V+31)/32] label bitmap; [V] gamma per
+  // vocabulary entry (read only where the bitmap is set)
   extern __shared__ float sh[];
   __shared__ float red[32];
+  const int L4 = (Lmax + 3) & ~3;
   float* glab = sh;
-  int* lab = (int*)(sh + Lmax);
-  uint32_t* bits = (uint32_t*)(sh + 2 * Lmax);
-  float* gam = sh + 2 * Lmax + (V + 31) / 32;
+  int* lab = (int*)(sh + L4);
+  int* fpos = (int*)(sh + 2 * L4);
+  int* slot = (int*)(sh + 3 * L4);
+  float* lsum = sh + 4 * L4;
+  uint32_t* bits = (uint32_t*)(sh + 5 * L4);
+  float* gam = sh + 5 * L4 + (V + 31) / 32;
+  int* gpos = (int*)gam;  // the vocabulary table holds each label's first position first
   const int row = blockIdx.x;
   const int b = row / T_, t = row - b * T_;
   TG* g = grad + (int64_t)row * ld;
@@ -253,29 +264,53 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const T* __restrict__ log
   const int32_t* tg = targets + (int64_t)b * Lmax;
   // blank posterior: sum over even states
   float gb = 0.f;
+  if (!(LASR_EXP & 2)) {
   for (int s = threadIdx.x * 2; s < S; s += blockDim.x * 2) gb += __expf(a[s] + be[s] + nl - lpt[0]);
   gb = block_sum(gb, red);
+  }
   for (int w = threadIdx.x; w < (V + 31) / 32; w += blockDim.x) bits[w] = 0u;
   __syncthreads();
-  for (int j = threadIdx.x; j < Lb; j += blockDim.x) {
+  for (int j = threadIdx.x; j < Lb && !(LASR_EXP & 2); j += blockDim.x) {
     const int s = 2 * j + 1;
     glab[j] = __expf(a[s] + be[s] + nl - lpt[1 + j]);
     lab[j] = tg[j];
     atomicOr(&bits[tg[j] >> 5], 1u << (tg[j] & 31));
   }
   __syncthreads();
-  // gamma of each distinct label, by the thread of its first position: the positions carrying
-  // it summed in position order from 0 (the per-column loop of r02, done once per label)
-  for (int j = threadIdx.x; j < Lb; j += blockDim.x) {
-    const int c = lab[j];
-    float sub = 0.f;
-    bool first = true;
-    for (int jj = 0; jj < Lb; ++jj) {
-      if (lab[jj] != c) continue;
-      if (jj < j) { first = false; break; }
-      sub += glab[jj];
+  // gamma of each distinct label: the posteriors of the positions carrying it summed in
+  // position order from 0 (the per-column loop of r02, done once per label).  Without a serial
+  // scan of the label list: the first position of each label by an LDS atomicMin (an order-
+  // independent result), then rounds in which every unclaimed position bids for its label's
+  // slot with atomicMin; the round's winner -- the lowest unclaimed position of that label --
+  // adds its posterior to the label's sum.  So the additions happen in position order, and a
+  // label list without repeats takes one round.
+  if (!(LASR_EXP & 3)) {
+    for (int j = threadIdx.x; j < Lb; j += blockDim.x) gpos[lab[j]] = 0x7fffffff;
+    __syncthreads();
+    for (int j = threadIdx.x; j < Lb; j += blockDim.x) atomicMin(&gpos[lab[j]], j);
+    __syncthreads();
+    for (int j = threadIdx.x; j < Lb; j += blockDim.x) {
+      fpos[j] = gpos[lab[j]];
+      slot[j] = 0x7fffffff;
+      lsum[j] = 0.f;
     }
-    if (first) gam[c] = sub;
+    __syncthreads();
+    uint32_t open = 0;  // bit k: position threadIdx.x + k * blockDim.x not yet summed
+    for (int k = 0, j = threadIdx.x; j < Lb && k < 32; ++k, j += blockDim.x) open |= 1u << k;
+    for (;;) {
+      for (int k = 0, j = threadIdx.x; j < Lb && k < 32; ++k, j += blockDim.x)
+        if ((open >> k) & 1u) atomicMin(&slot[fpos[j]], j);
+      __syncthreads();
+      for (int k = 0, j = threadIdx.x; j < Lb && k < 32; ++k, j += blockDim.x) {
+        if (!((open >> k) & 1u) || slot[fpos[j]] != j) continue;
+        lsum[fpos[j]] += glab[j];
+        slot[fpos[j]] = 0x7fffffff;
+        open &= ~(1u << k);
+      }
+      if (!__syncthreads_or(open != 0u)) break;
+    }
+    for (int j = threadIdx.x; j < Lb; j += blockDim.x)
+      if (fpos[j] == j) gam[lab[j]] = lsum[j];
   }
   __syncthreads();
   const float gs = gscale * (gdev ? gdev[0] : 1.f);
@@ -634,8 +669,8 @@ extern "C" int lasr_ctc_bwd(const void* logits, int ldt, int B, int T, int V, in
     const int rc = lasr_check_launch("ctc_beta");
     if (rc) return rc;
   }
-  const size_t shm = ((size_t)2 * (Lmax > 0 ? Lmax : 1) + (V + 31) / 32 + V) * sizeof(float);
-  LASR_CHECK_ARG(shm <= 64 * 1024, "lasr_ctc_bwd: vocab/labels too large for LDS");
+  const size_t shm = ((size_t)5 * (((Lmax > 0 ? Lmax : 1) + 3) & ~3) + (V + 31) / 32 + V) * sizeof(float);
+  LASR_CHECK_ARG(shm <= 64 * 1024 && Lmax <= 32 * 256, "lasr_ctc_bwd: vocab/labels too large for LDS");
 #define CTC_G(TT, TGG)                                                                      \
   ctc_grad_kernel<TT, TGG><<<B * T, 256, shm, st>>>((const TT*)logits, B, T, V, ld, targets, Lmax,\
                                                     ilen, tlen, lse, lp, alpha, beta, nll,     \

@@ -39,6 +39,7 @@ for s in "$@"; do
     switches) run timeout -k 10 900 $PYT tests/test_switches_gpu.py > "$OUT/switches.log" 2>&1 ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
            "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" -s > "$OUT/new5.log" 2>&1 ;;
+    ctc) run timeout -k 10 600 $PYT tests -k "ctc or CTC" > "$OUT/ctc.log" 2>&1 ;;
     attn) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "relattn or decoder_attention or attn" > "$OUT/attn.log" 2>&1 ;;
     attnbench) run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_bench.jsonl" 2> "$OUT/attn_bench.err" ;;
     attnab) # attention kernels: the library in ab/ (same ABI) vs the tree's, alternating
@@ -49,6 +50,10 @@ for s in "$@"; do
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_exp_$v.tmp"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_exp_$v.tmp" >> "$OUT/attn_exp.jsonl"; rm -f "$OUT/attn_exp_$v.tmp"; done; done ;;
+    ctcexp) # CTC kernels at small and long: the tree's library vs lib/exp/lib$N.so (EXP_LIBS), twice
+           for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
+             LITEASR_HIP_LIB=$lib run timeout -k 10 200 python3 tools/ctc_bench.py > "$OUT/ctc.tmp" 2>> "$OUT/ctcexp.err"
+             sed "s/^{/{\"lib\": \"$v\", /" "$OUT/ctc.tmp" >> "$OUT/ctcexp.jsonl"; rm -f "$OUT/ctc.tmp"; done; done ;;
     caseab) # bench.py roofline cases (RCASES "small:dw large:dw ..."): the tree's library vs lib/exp/lib$N.so (EXP_LIBS), twice
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              for rc in ${RCASES:-small:dw}; do cfg=${rc%%:*}; cs=${rc##*:}
