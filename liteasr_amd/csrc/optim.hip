@@ -68,9 +68,36 @@ __global__ __launch_bounds__(256) void opt_finalize_kernel(const float* ws, int 
   }
 }
 
+// The Adam operands are streamed once per step (30 B per parameter, ~1.4 GB), so they are
+// loaded and stored non-temporally: 250 -> 230 us per step at 46.2 M parameters, bit identical
+// (profiles/r05/adam_ab.jsonl).  Timing ablation (tools/gemm_exp.sh with EXP_FILES=optim; 0 in
+// the product): bit 1 goes back to plain loads and stores.
+#ifndef LASR_EXP
+#define LASR_EXP 0
+#endif
+typedef float adam_f4 __attribute__((ext_vector_type(4)));
+LASR_DEV float4 adam_ld(const float4* q) {
+  if constexpr ((LASR_EXP & 1) == 0) {
+    const adam_f4 x = __builtin_nontemporal_load((const adam_f4*)q);
+    return make_float4(x[0], x[1], x[2], x[3]);
+  } else {
+    return *q;
+  }
+}
+LASR_DEV void adam_st(float4* q, float4 x) {
+  if constexpr ((LASR_EXP & 1) == 0) {
+    const adam_f4 y = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(y, (adam_f4*)q);
+  } else {
+    *q = x;
+  }
+}
+
 template <typename TL>
-__global__ __launch_bounds__(256) void adam_kernel(float* p, TL* plp, const float* g, float* m,
-                                                   float* v, int64_t n, const float* state,
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, TL* __restrict__ plp,
+                                                   const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   int64_t n, const float* __restrict__ state,
                                                    float beta1, float beta2, float eps, float wd) {
   if (state[3] != 0.f) return;  // NaN norm: step skipped (reference trainer.py:157)
   const float step = state[0], lr = state[1], coef = state[4];
@@ -78,43 +105,53 @@ __global__ __launch_bounds__(256) void adam_kernel(float* p, TL* plp, const floa
   const float bc2 = 1.f - powf(beta2, step);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
+  // the multiply-adds are spelled out (fmaf / __fmul_rn), so the rounding does not depend on
+  // how the compiler contracts the expression in each copy of it
   auto upd = [&](float gi, float pi, float& mi, float& vi) {
-    gi *= coef;
-    if (wd != 0.f) gi += wd * pi;
-    mi = mi + (1.f - beta1) * (gi - mi);  // lerp, as torch.optim.Adam
-    vi = vi * beta2 + (1.f - beta2) * gi * gi;
-    return pi - step_size * mi / (sqrtf(vi) / bc2s + eps);
+    gi = __fmul_rn(gi, coef);
+    if (wd != 0.f) gi = fmaf(wd, pi, gi);
+    mi = fmaf(1.f - beta1, gi - mi, mi);  // lerp, as torch.optim.Adam
+    vi = fmaf(__fmul_rn(1.f - beta2, gi), gi, __fmul_rn(vi, beta2));
+    return pi - __fmul_rn(step_size, mi) / (sqrtf(vi) / bc2s + eps);
   };
-  // 16-B accesses, 4 parameters per thread and iteration (the same per-element arithmetic)
+  // 16-B accesses, 4 parameters per thread and group; two groups (i, i + stride) per iteration
+  // so eight 16-B loads per thread are in flight (the same per-element arithmetic)
   const bool vec = ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&
                    (((uintptr_t)plp) & (4 * sizeof(TL) - 1)) == 0;
   int64_t done = 0;
   if (vec) {
-    const int64_t n4 = n / 4;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-      const float4 g4 = ((const float4*)g)[i], p4 = ((const float4*)p)[i];
-      float4 m4 = ((float4*)m)[i], v4 = ((float4*)v)[i];
+    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
+    auto group = [&](int64_t i, float4 g4, float4 p4, float4 m4, float4 v4) {
       float o[4];
       o[0] = upd(g4.x, p4.x, m4.x, v4.x);
       o[1] = upd(g4.y, p4.y, m4.y, v4.y);
       o[2] = upd(g4.z, p4.z, m4.z, v4.z);
       o[3] = upd(g4.w, p4.w, m4.w, v4.w);
-      ((float4*)m)[i] = m4;
-      ((float4*)v)[i] = v4;
-      ((float4*)p)[i] = make_float4(o[0], o[1], o[2], o[3]);
+      adam_st((float4*)m + i, m4);
+      adam_st((float4*)v + i, v4);
+      adam_st((float4*)p + i, make_float4(o[0], o[1], o[2], o[3]));
       if (plp) stv<4>(plp + 4 * i, o);
+    };
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + stride < n4; i += 2 * stride) {
+      const int64_t k = i + stride;
+      const float4 ga = adam_ld((const float4*)g + i), pa = adam_ld((const float4*)p + i);
+      const float4 ma = adam_ld((const float4*)m + i), va = adam_ld((const float4*)v + i);
+      const float4 gb = adam_ld((const float4*)g + k), pb = adam_ld((const float4*)p + k);
+      const float4 mb = adam_ld((const float4*)m + k), vb = adam_ld((const float4*)v + k);
+      group(i, ga, pa, ma, va);
+      group(k, gb, pb, mb, vb);
     }
+    for (; i < n4; i += stride)
+      group(i, adam_ld((const float4*)g + i), adam_ld((const float4*)p + i), adam_ld((const float4*)m + i),
+            adam_ld((const float4*)v + i));
     done = n4 * 4;
   }
   for (int64_t i = done + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    float gi = g[i] * coef;
-    float pi = p[i];
-    if (wd != 0.f) gi += wd * pi;
-    const float mi = m[i] + (1.f - beta1) * (gi - m[i]);  // lerp, as torch.optim.Adam
-    const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    float mi = m[i], vi = v[i];
+    const float pi = upd(g[i], p[i], mi, vi);
     m[i] = mi;
     v[i] = vi;
-    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
     p[i] = pi;
     if (plp) plp[i] = from_f<TL>(pi);
   }

@@ -54,6 +54,11 @@ for s in "$@"; do
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              LITEASR_HIP_LIB=$lib run timeout -k 10 200 python3 tools/ctc_bench.py > "$OUT/ctc.tmp" 2>> "$OUT/ctcexp.err"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/ctc.tmp" >> "$OUT/ctcexp.jsonl"; rm -f "$OUT/ctc.tmp"; done; done ;;
+    toolab) # TOOL (a script printing JSON lines) under the tree's library, ab_prev/'s and lib/exp/lib$N.so (EXP_LIBS), twice
+           for rep in 1 2; do for v in tree prev ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so
+             [ $v = prev ] && lib=$R/ab_prev/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && [ $v != prev ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
+             LITEASR_HIP_LIB=$lib run timeout -k 10 200 python3 $TOOL > "$OUT/toolab.tmp" 2>> "$OUT/toolab.err"
+             sed "s/^{/{\"lib\": \"$v\", /" "$OUT/toolab.tmp" >> "$OUT/toolab.jsonl"; rm -f "$OUT/toolab.tmp"; done; done ;;
     caseab) # bench.py roofline cases (RCASES "small:dw large:dw ..."): the tree's library vs lib/exp/lib$N.so (EXP_LIBS), twice
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              for rc in ${RCASES:-small:dw}; do cfg=${rc%%:*}; cs=${rc##*:}
