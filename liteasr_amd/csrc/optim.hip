@@ -9,6 +9,33 @@
 
 constexpr int SQ_CHUNK = 16384;  // elements per partial
 
+// The Adam operands are streamed once per step (30 B per parameter, ~1.4 GB), so they are
+// loaded and stored non-temporally: 250 -> 230 us per step at 46.2 M parameters, bit identical
+// (profiles/r05/adam_ab.jsonl).  Timing ablation (tools/gemm_exp.sh with EXP_FILES=optim; 0 in
+// the product): bit 1 goes back to plain loads and stores; bit 2 reads the gradient
+// non-temporally in the sum of squares too (slower: sum of squares + Adam 262-270 us with plain
+// loads there, 288-297 us with non-temporal ones, 325 us before; profiles/r05/adam_sumsq_ab.jsonl).
+#ifndef LASR_EXP
+#define LASR_EXP 0
+#endif
+typedef float adam_f4 __attribute__((ext_vector_type(4)));
+LASR_DEV float4 adam_ld(const float4* q) {
+  if constexpr ((LASR_EXP & 1) == 0) {
+    const adam_f4 x = __builtin_nontemporal_load((const adam_f4*)q);
+    return make_float4(x[0], x[1], x[2], x[3]);
+  } else {
+    return *q;
+  }
+}
+LASR_DEV void adam_st(float4* q, float4 x) {
+  if constexpr ((LASR_EXP & 1) == 0) {
+    const adam_f4 y = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(y, (adam_f4*)q);
+  } else {
+    *q = x;
+  }
+}
+
 // One partial per SQ_CHUNK elements.  Full chunks: 16-B loads, all 16 per thread issued
 // before the sums (4 accumulators, fixed order); the ragged last chunk: scalar loads.
 __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* g, int64_t n, float* ws) {
@@ -19,7 +46,15 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* g, int6
     constexpr int NV = SQ_CHUNK / (256 * 4);
     float4 v[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = *(const float4*)(g + base + ((int64_t)k * 256 + threadIdx.x) * 4);
+    for (int k = 0; k < NV; ++k) {
+      const float4* q = (const float4*)(g + base + ((int64_t)k * 256 + threadIdx.x) * 4);
+      if constexpr ((LASR_EXP & 2) != 0) {
+        const adam_f4 x = __builtin_nontemporal_load((const adam_f4*)q);
+        v[k] = make_float4(x[0], x[1], x[2], x[3]);
+      } else {
+        v[k] = *q;
+      }
+    }
     float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -65,31 +100,6 @@ __global__ __launch_bounds__(256) void opt_finalize_kernel(const float* ws, int 
     float r = lr;
     if (lr_mode == 1) r = factor * powf(model_dim, -0.5f) * fminf(powf(step, -0.5f), step * powf(warmup, -1.5f));
     state[1] = r;
-  }
-}
-
-// The Adam operands are streamed once per step (30 B per parameter, ~1.4 GB), so they are
-// loaded and stored non-temporally: 250 -> 230 us per step at 46.2 M parameters, bit identical
-// (profiles/r05/adam_ab.jsonl).  Timing ablation (tools/gemm_exp.sh with EXP_FILES=optim; 0 in
-// the product): bit 1 goes back to plain loads and stores.
-#ifndef LASR_EXP
-#define LASR_EXP 0
-#endif
-typedef float adam_f4 __attribute__((ext_vector_type(4)));
-LASR_DEV float4 adam_ld(const float4* q) {
-  if constexpr ((LASR_EXP & 1) == 0) {
-    const adam_f4 x = __builtin_nontemporal_load((const adam_f4*)q);
-    return make_float4(x[0], x[1], x[2], x[3]);
-  } else {
-    return *q;
-  }
-}
-LASR_DEV void adam_st(float4* q, float4 x) {
-  if constexpr ((LASR_EXP & 1) == 0) {
-    const adam_f4 y = {x.x, x.y, x.z, x.w};
-    __builtin_nontemporal_store(y, (adam_f4*)q);
-  } else {
-    *q = x;
   }
 }
 

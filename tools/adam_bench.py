@@ -44,5 +44,14 @@ for rep in range(3):
     e1.record(s)
     torch.cuda.synchronize()
     res.append(e0.elapsed_time(e1) * 1e3 / 20)
+res2 = []
+for rep in range(3):
+    e0.record(s)
+    for _ in range(20):
+        step()
+    e1.record(s)
+    torch.cuda.synchronize()
+    res2.append(e0.elapsed_time(e1) * 1e3 / 20)
 print(json.dumps({"n": n, "adam_step_us": [round(x, 1) for x in res], "min_us": round(min(res), 1),
+                  "sumsq_adam_us": round(min(res2), 1),
                   "GB_s": round(30.0 * n / min(res) / 1e3, 1), "hash": h.hexdigest()[:16]}), flush=True)
