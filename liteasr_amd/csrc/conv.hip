@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) acc += wc[kh * 3 + kw] * xs[kh * F + 2 * f1 + kw];
+      for (int kw = 0; kw < 3; ++kw) acc = fmaf(wc[kh * 3 + kw], xs[kh * F + 2 * f1 + kw], acc);
     out[e] = from_f<T>(fmaxf(acc, 0.f));
   }
 }
@@ -88,10 +88,13 @@ __global__ void conv1_bwd_reduce_kernel(const float* part, int nparts, int C, fl
 // Vectorised conv1 (C % 8 == 0, 256 % (C/8) == 0): a thread owns 8 consecutive channels
 // (their 8x10 weights in registers) and a strided set of output columns f1, so every
 // y1 / dy1 access is one 16-B (bf16) vector and a wave covers whole 512-B channel rows.
-// Same per-output arithmetic order as the scalar kernels above.
+// Same per-output arithmetic as the scalar kernels above: bias, then one fused multiply-add
+// per tap in tap order (spelled fmaf: left to the compiler, the vectorised kernel got a packed
+// multiply and a separate add per tap, 2.7x the VALU of packed FMAs in a VALU-bound kernel).
 constexpr int C1V_ROWS = 32;  // largest (b,t1) row count per vectorised conv1-bwd block (A/B)
 constexpr int C1F_ROWS = 8;   // (b,t1) rows per vectorised conv1-fwd block
 
+typedef float c1_f2 __attribute__((ext_vector_type(2)));
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restrict__ x, int T_, int F,
                                                            int C, int T1, int F1, int nrows, const float* w,
@@ -102,11 +105,30 @@ __global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restri
   extern __shared__ float xs[];  // rpb x 3F
   const int r0 = blockIdx.x * rpb;
   const int nr = min(rpb, nrows - r0);
-  for (int i = threadIdx.x; i < nr * 3 * F; i += 256) {
-    const int rr = i / (3 * F), q = i - rr * 3 * F;
-    const int r = r0 + rr;
-    const int b = r / T1, t1 = r - b * T1;
-    xs[i] = x[((int64_t)b * T_ + 2 * t1) * F + q];
+  // the 3 input rows of output row (b, t1) are input rows 2 t1 .. 2 t1 + 2: 3F contiguous
+  // floats.  With 16-B rows and 8 output rows per block, 32 threads copy a row's 3F/4
+  // vectors, all of a thread's loads in flight before its LDS writes.
+  if (rpb == 8 && (F & 3) == 0 && 3 * F <= 4 * 32 * 4 && (((uintptr_t)x) & 15) == 0) {
+    const int rr = threadIdx.x >> 5, l = threadIdx.x & 31, n4 = 3 * F / 4;
+    if (rr < nr) {
+      const int r = r0 + rr, b = r / T1, t1 = r - b * T1;
+      const float4* src = (const float4*)(x + ((int64_t)b * T_ + 2 * t1) * F);
+      float4* dst = (float4*)(xs + rr * 3 * F);
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (l + 32 * k < n4) v[k] = src[l + 32 * k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (l + 32 * k < n4) dst[l + 32 * k] = v[k];
+    }
+  } else {
+    for (int i = threadIdx.x; i < nr * 3 * F; i += 256) {
+      const int rr = i / (3 * F), q = i - rr * 3 * F;
+      const int r = r0 + rr;
+      const int b = r / T1, t1 = r - b * T1;
+      xs[i] = x[((int64_t)b * T_ + 2 * t1) * F + q];
+    }
   }
   const int CG = C >> 3, cg = threadIdx.x % CG, fg = threadIdx.x / CG, NFG = 256 / CG;
   const int c0 = cg * 8;
@@ -127,13 +149,19 @@ __global__ __launch_bounds__(256) void conv1_fwd_v8_kernel(const float* __restri
       for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xr[kh * F + 2 * f1 + kw];
+      // channel pairs as 2-wide vectors: one v_pk_fma_f32 per tap and pair (the same fused
+      // multiply-add per channel as fmaf)
       float o[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float acc = bv[q];
+      for (int q = 0; q < 8; q += 2) {
+        c1_f2 acc = {bv[q], bv[q + 1]};
 #pragma unroll
-        for (int k = 0; k < 9; ++k) acc += wr[q][k] * xv[k];
-        o[q] = fmaxf(acc, 0.f);
+        for (int k = 0; k < 9; ++k) {
+          const c1_f2 wk = {wr[q][k], wr[q + 1][k]}, xk = {xv[k], xv[k]};
+          acc = __builtin_elementwise_fma(wk, xk, acc);
+        }
+        o[q] = fmaxf(acc[0], 0.f);
+        o[q + 1] = fmaxf(acc[1], 0.f);
       }
       st8(out + (int64_t)f1 * C, o);
     }
