@@ -568,6 +568,50 @@ def test_ctc(B, T, V, L, dtype):
     torch.testing.assert_close(grad2, grad, rtol=0, atol=0, equal_nan=True)  # infeasible rows: nan
 
 
+@pytest.mark.parametrize("B,T,V,L,kind", [(2, 200, 5, 60, "few labels"), (2, 150, 3, 40, "one label"),
+                                          (2, 700, 50, 300, "long list")])
+def test_ctc_label_repeats_and_long_lists(B, T, V, L, kind):
+    """Edge cases of the CTC gradient's per-label gamma (ctc_grad_kernel: first position by an
+    LDS atomicMin, then one claim round per repeat, summed in position order) and of the
+    register lattice: a 4-label vocabulary (every label repeated ~15 times), one label repeated
+    through the whole list (40 rounds), and a 300-label list (positions past the 256-thread
+    block, a 13-wave lattice).  Loss and gradient against fp64 autograd through aten's CTC,
+    the bar of test_ctc (fp32 logits)."""
+    kn = K()
+    g = torch.Generator().manual_seed(11 + L)
+    logits = torch.randn(B, T, V, generator=g) * 2
+    ilen = torch.tensor([T] + [T - 7] * (B - 1))
+    tlen = torch.tensor([L] + [L - 3] * (B - 1))
+    tg = torch.randint(1, V, (B, L), generator=g)
+    if kind == "one label":
+        tg.fill_(1)
+    for b in range(B):
+        tg[b, tlen[b]:] = -1
+    lr = logits.double().requires_grad_()
+    nll_ref = F.ctc_loss(lr.log_softmax(-1).transpose(0, 1), tg.clamp(min=0), ilen, tlen, blank=0,
+                         reduction="none", zero_infinity=False)
+    fin = torch.isfinite(nll_ref)
+    assert fin.all()
+    gref = torch.autograd.grad(nll_ref.sum(), lr)[0]
+    l32 = logits.float().requires_grad_()
+    n32 = F.ctc_loss(l32.log_softmax(-1).transpose(0, 1), tg.clamp(min=0), ilen, tlen, blank=0,
+                     reduction="none", zero_infinity=False)
+    g32 = torch.autograd.grad(n32.sum(), l32)[0].double()
+    err32 = (g32 - gref).abs().max().item()
+    d_log = logits.to(DEV)
+    tg32, il, tl = tg.to(DEV, torch.int32), ilen.to(DEV, torch.int32), tlen.to(DEV, torch.int32)
+    S = 2 * L + 1
+    lse, lpb = torch.empty(B * T, device=DEV), torch.empty(B * T * (L + 1), device=DEV)
+    alpha, beta = torch.empty(B * T * S, device=DEV), torch.empty(B * T * S, device=DEV)
+    nll = torch.empty(B, device=DEV)
+    kn.ctc_fwd(d_log, tg32, il, tl, lse, lpb, alpha, nll)
+    got = nll.cpu().double()
+    assert ((got - nll_ref.detach()).abs() <= 1e-5 * nll_ref.detach().abs().clamp(min=1)).all(), (got, nll_ref)
+    grad = torch.empty(B, T, V, device=DEV, dtype=torch.float32)
+    kn.ctc_bwd(d_log, tg32, il, tl, lse, lpb, alpha, nll, beta, grad, 1.0)
+    close(grad.cpu().double(), gref, max(2e-3, 1.25 * err32), f"ctc grad ({kind})")
+
+
 # ----------------------------------------------------------- label-smoothed KL
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_lsm_kl(dtype):
