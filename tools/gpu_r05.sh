@@ -94,6 +94,12 @@ for s in "$@"; do
              run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 $a > "$OUT/ddpab_$v.json" 2> "$OUT/ddpab_$v.err"
              grep "^{" "$OUT/ddpab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); a=d['config']['allreduce'] or {}; t=a.get('timeline_last_step') or {}; print(json.dumps({'arm': '$v', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'segment_ms': t.get('segment_ms'), 'exposed_comm_ms': t.get('exposed_comm_ms')}))" >> "$OUT/ddpab.jsonl"; done; done ;;
     ddp1n) run timeout -k 10 300 python3 bench.py --force-ddp --comm native --no-cpu-baseline --no-roofline > "$OUT/bench_ddp1_native.json" 2> "$OUT/bench_ddp1_native.err" ;;
+    famsq) cd /tmp  # SQ counter sets over the family roofline case (the stall breakdown)
+           S1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_INSTS_VALU"
+           S2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_SCA"
+           i=0; for set in "$S1" "$S2"; do i=$((i+1))
+             run timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/fs$i" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 10 --roofline-case family > "$OUT/fs$i.log" 2>&1
+             run python3 "$R/tools/pmc_kernels.py" "$(find "$OUT/fs$i" -name '*.db' | head -1)" gemm_bf16_glds_kernel row_res_ln row_dx_ln_bwd > "$OUT/family_sq_${PMC_CONFIG:-small}_$i.json"; rm -rf "$OUT/fs$i"; done ;;
     tracefam) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_family" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 50 --roofline-case family > "$OUT/trace_family.log" 2>&1
            grep "^{" "$OUT/trace_family.log" | tail -1 > "$OUT/trace_family_meta.json"
            run python3 "$R/tools/family_trace.py" "$(find "$OUT/trace_family" -name '*.db' | head -1)" "$OUT/trace_family_meta.json" > "$OUT/family_trace_summary_${PMC_CONFIG:-small}.json"; rm -rf "$OUT/trace_family" ;;
