@@ -536,6 +536,13 @@ int lasr_u2_prep(const int64_t* xlens, const int64_t* ys, const int64_t* ylens, 
                  int L, int Tsub, int sos, int eos, int chunk, int32_t* ys_in, int32_t* tgt,
                  int32_t* tgt_ctc, uint8_t* dec_mask, uint8_t* enc_mask, int32_t* pred_len,
                  int32_t* ylen32, void* stream);
+/* The same with the masks' row strides (bytes): dec_mask [B, L+1, dec_ld], and in chunk mode
+ * enc_mask [B, T', enc_ld]; the columns past L+1 / T' are written 1 (masked), so the masks
+ * come out with the 16-B aligned rows the attention kernels stage by LDS-DMA. */
+int lasr_u2_prep_ld(const int64_t* xlens, const int64_t* ys, const int64_t* ylens, int B, int Tx,
+                    int L, int Tsub, int sos, int eos, int chunk, int32_t* ys_in, int32_t* tgt,
+                    int32_t* tgt_ctc, uint8_t* dec_mask, int dec_ld, uint8_t* enc_mask, int enc_ld,
+                    int32_t* pred_len, int32_t* ylen32, void* stream);
 
 /* ------------------------------------------------------------------------
  * SpecAugment (liteasr/utils/transform/spec_augment.py:14-125; applied per utterance in

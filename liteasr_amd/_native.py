@@ -172,6 +172,7 @@ SIGNATURES = {
     "lasr_embed_bwd": [_p, _i, _i, _p, _i, _f, _f, _u, _p, _p],
     "lasr_pe_fwd": [_p, _i, _l, _i, _i, _p, _f, _f, _u, _p, _i, _p],
     "lasr_u2_prep": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
+    "lasr_u2_prep_ld": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p],
     "lasr_sumsq_nparts": [_l],
     "lasr_sumsq_partial": [_p, _l, _p, _l, _p],
     "lasr_adam_step": [_p, _p, _i, _p, _p, _p, _l, _p, _i, _p, _f, _i, _f, _f, _f, _f, _f, _f,

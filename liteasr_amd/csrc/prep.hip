@@ -15,7 +15,8 @@ LASR_DEV int64_t floordiv(int64_t a, int64_t b) {
 __global__ void u2_prep_kernel(const int64_t* xlens, const int64_t* ys, const int64_t* ylens,
                                int B, int L, int Tsub, int sos, int eos, int chunk,
                                int32_t* ys_in, int32_t* tgt, int32_t* tgt_ctc, uint8_t* dec_mask,
-                               uint8_t* enc_mask, int32_t* pred_len, int32_t* ylen32) {
+                               int dec_ld, uint8_t* enc_mask, int enc_ld, int32_t* pred_len,
+                               int32_t* ylen32) {
   const int b = blockIdx.x;
   const int64_t xl = xlens[b];
   const int64_t yl = ylens[b];
@@ -35,30 +36,41 @@ __global__ void u2_prep_kernel(const int64_t* xlens, const int64_t* ys, const in
     if (j == yl) v = eos;
     tgt[(int64_t)b * L1 + j] = v;
   }
-  for (int e = threadIdx.x; e < L1 * L1; e += blockDim.x) {
-    const int i = e / L1, j = e - i * L1;
-    dec_mask[(int64_t)b * L1 * L1 + e] = (uint8_t)((j >= yl + 1) || (j > i));
+  // rows of dec_ld >= L1 bytes; the columns past L1 (row padding) are 1 = masked
+  for (int e = threadIdx.x; e < L1 * dec_ld; e += blockDim.x) {
+    const int i = e / dec_ld, j = e - i * dec_ld;
+    dec_mask[(int64_t)b * L1 * dec_ld + e] = (uint8_t)((j >= L1) || (j >= yl + 1) || (j > i));
   }
   if (chunk <= 0) {
     for (int t = threadIdx.x; t < Tsub; t += blockDim.x)
       enc_mask[(int64_t)b * Tsub + t] = (uint8_t)((int64_t)4 * t >= xl);
   } else {
-    for (int e = threadIdx.x; e < Tsub * Tsub; e += blockDim.x) {
-      const int i = e / Tsub, j = e - i * Tsub;
-      enc_mask[(int64_t)b * Tsub * Tsub + e] =
-          (uint8_t)(((int64_t)4 * j >= xl) || ((j / chunk) > (i / chunk)));
+    for (int e = threadIdx.x; e < Tsub * enc_ld; e += blockDim.x) {
+      const int i = e / enc_ld, j = e - i * enc_ld;
+      enc_mask[(int64_t)b * Tsub * enc_ld + e] =
+          (uint8_t)((j >= Tsub) || ((int64_t)4 * j >= xl) || ((j / chunk) > (i / chunk)));
     }
   }
+}
+
+extern "C" int lasr_u2_prep_ld(const int64_t* xlens, const int64_t* ys, const int64_t* ylens, int B,
+                               int Tx, int L, int Tsub, int sos, int eos, int chunk, int32_t* ys_in,
+                               int32_t* tgt, int32_t* tgt_ctc, uint8_t* dec_mask, int dec_ld,
+                               uint8_t* enc_mask, int enc_ld, int32_t* pred_len, int32_t* ylen32,
+                               void* stream) {
+  (void)Tx;
+  LASR_CHECK_ARG(dec_ld >= L + 1 && (chunk <= 0 || enc_ld >= Tsub), "lasr_u2_prep: mask row stride too small");
+  if (B <= 0) return LASR_OK;
+  u2_prep_kernel<<<B, 256, 0, (hipStream_t)stream>>>(xlens, ys, ylens, B, L, Tsub, sos, eos, chunk,
+                                                     ys_in, tgt, tgt_ctc, dec_mask, dec_ld, enc_mask,
+                                                     chunk > 0 ? enc_ld : Tsub, pred_len, ylen32);
+  return lasr_check_launch("u2_prep");
 }
 
 extern "C" int lasr_u2_prep(const int64_t* xlens, const int64_t* ys, const int64_t* ylens, int B,
                             int Tx, int L, int Tsub, int sos, int eos, int chunk, int32_t* ys_in,
                             int32_t* tgt, int32_t* tgt_ctc, uint8_t* dec_mask, uint8_t* enc_mask,
                             int32_t* pred_len, int32_t* ylen32, void* stream) {
-  (void)Tx;
-  if (B <= 0) return LASR_OK;
-  u2_prep_kernel<<<B, 256, 0, (hipStream_t)stream>>>(xlens, ys, ylens, B, L, Tsub, sos, eos, chunk,
-                                                     ys_in, tgt, tgt_ctc, dec_mask, enc_mask,
-                                                     pred_len, ylen32);
-  return lasr_check_launch("u2_prep");
+  return lasr_u2_prep_ld(xlens, ys, ylens, B, Tx, L, Tsub, sos, eos, chunk, ys_in, tgt, tgt_ctc, dec_mask,
+                         L + 1, enc_mask, Tsub, pred_len, ylen32, stream);
 }

@@ -801,10 +801,14 @@ def fill(t, value):
 
 
 def u2_prep(xlens, ys, ylens, Tx, Tsub, sos, eos, chunk, out):
+    """out["dec_mask"] [B, L+1, ld] and (chunk > 0) out["enc_mask"] [B, T', ld]: the last
+    dimension is the row stride; columns past L+1 / T' come out 1 (masked)."""
     B, L = ys.shape
-    N.call("lasr_u2_prep", ptr(xlens), ptr(ys), ptr(ylens), B, Tx, L, Tsub, sos, eos, chunk,
-           ptr(out["ys_in"]), ptr(out["tgt"]), ptr(out["tgt_ctc"]), ptr(out["dec_mask"]),
-           ptr(out["enc_mask"]), ptr(out["pred_len"]), ptr(out["ylen"]), stream())
+    dm, em = out["dec_mask"], out["enc_mask"]
+    assert dm.is_contiguous() and dm.shape[-1] >= L + 1 and em.is_contiguous()
+    N.call("lasr_u2_prep_ld", ptr(xlens), ptr(ys), ptr(ylens), B, Tx, L, Tsub, sos, eos, chunk,
+           ptr(out["ys_in"]), ptr(out["tgt"]), ptr(out["tgt_ctc"]), ptr(dm), dm.shape[-1],
+           ptr(em), em.shape[-1] if chunk > 0 else Tsub, ptr(out["pred_len"]), ptr(out["ylen"]), stream())
 
 
 def spec_augment(x, xlens, plan, replace_with_zero=False, out=None):

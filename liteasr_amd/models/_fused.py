@@ -132,11 +132,14 @@ class FusedEncoderModel(LiteasrModel):
         L = ys.shape[1]
         Tsub = ((Tx - 1) // 2 - 1) // 2
         i32, u8 = torch.int32, torch.uint8
+        # query-dependent masks with 16-B aligned rows (the attention kernels stage their tiles
+        # by LDS-DMA): u2_prep writes the padded rows itself (padding columns masked)
+        P16 = lambda n: (n + 15) // 16 * 16  # noqa: E731
         out = {
             "ys_in": torch.empty(B, L + 1, dtype=i32, device=dev),
             "tgt": torch.empty(B * (L + 1), dtype=i32, device=dev),
             "tgt_ctc": torch.empty(B, L, dtype=i32, device=dev),
-            "dec_mask": torch.empty(B, L + 1, L + 1, dtype=u8, device=dev),
+            "dec_mask": torch.empty(B, L + 1, P16(L + 1), dtype=u8, device=dev),
             "enc_mask": torch.empty(B, Tsub, dtype=u8, device=dev),
             "pred_len": torch.empty(B, dtype=i32, device=dev),
             "ylen": torch.empty(B, dtype=i32, device=dev),
@@ -150,12 +153,11 @@ class FusedEncoderModel(LiteasrModel):
             # (u2_prep writes every output: the chunk-mask call gets scratch for the others, so
             # nothing it writes lands in a buffer laid out differently from what it assumes)
             tmp = {k: torch.empty_like(v) for k, v in out.items()}
-            tmp["enc_mask"] = torch.empty(B, Tsub, Tsub, dtype=u8, device=dev)
+            tmp["enc_mask"] = torch.empty(B, Tsub, P16(Tsub), dtype=u8, device=dev)
             K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, self.chunk_size, tmp)
-            chunk = K.pad_mask16(tmp["enc_mask"], B, Tsub, Tsub)[0]
-        # query-dependent masks as views with 16-B aligned rows (the attention kernels stage
-        # their tiles by LDS-DMA); kernels read them through (msb, msq) = the view's strides
-        out["dec_mask"] = K.pad_mask16(out["dec_mask"], B, L + 1, L + 1)[0]
+            chunk = tmp["enc_mask"][:, :, :Tsub]
+        # kernels read the masks through (msb, msq) = the views' strides
+        out["dec_mask"] = out["dec_mask"][:, :, :L + 1]
         p = SimpleNamespace(B=B, Tx=Tx, T=Tsub, L=L, chunk_mask=chunk, **out)
         return p
 

@@ -1176,6 +1176,19 @@ def test_embed_pe_and_prep():
     tri = torch.arange(5)[None, :] > torch.arange(5)[:, None]
     ysm = torch.arange(5)[None, :] >= (ylens.cpu() + 1)[:, None]
     assert torch.equal(out["dec_mask"].cpu().bool(), ysm[:, None, :] | tri[None])
+    # padded rows (lasr_u2_prep_ld, what the model's _prep uses): the same masks in the first
+    # L+1 / T' columns, 1 (masked) in the padding; chunk mode's [B, T', T'] mask likewise
+    pad = dict(out, dec_mask=torch.zeros(3, 5, 16, dtype=torch.uint8, device=DEV))
+    kn.u2_prep(xlens, ys, ylens, Tx, Tsub, 9, 9, 0, pad)
+    assert torch.equal(pad["dec_mask"][:, :, :5], out["dec_mask"]) and bool((pad["dec_mask"][:, :, 5:] == 1).all())
+    ck = 4
+    P = (Tsub + 15) // 16 * 16
+    chk = dict(out, enc_mask=torch.zeros(3, Tsub, P, dtype=torch.uint8, device=DEV))
+    kn.u2_prep(xlens, ys, ylens, Tx, Tsub, 9, 9, ck, chk)
+    t = torch.arange(Tsub)
+    cm = pm[:, :-2:2][:, :-2:2][:, None, :] | ((t[None, :] // ck) > (t[:, None] // ck))[None]
+    assert torch.equal(chk["enc_mask"][:, :, :Tsub].cpu().bool(), cm)
+    assert bool((chk["enc_mask"][:, :, Tsub:] == 1).all())
 
 
 def test_adam_noam_clip():
