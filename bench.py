@@ -30,7 +30,10 @@ sys.path.insert(0, ROOT)
 CONFIGS = {
     # name: model widths, batch shape, hybrid weight; GFLOP/utt fwd+bwd from SURVEY §6
     "small": dict(d=256, H=4, ff=2048, enc=12, dec=6, B=32, T=1000, L=40, w=0.3, gflop=80.14, chunk=0),
-    "large": dict(d=512, H=16, ff=2048, enc=12, dec=6, B=32, T=1000, L=40, w=0.3, gflop=230.77, chunk=16),
+    # config 4: the dynamic-chunk streaming mask (a chunk size drawn per step on the device;
+    # eval / the fixed-c comparison leg use c = 16)
+    "large": dict(d=512, H=16, ff=2048, enc=12, dec=6, B=32, T=1000, L=40, w=0.3, gflop=230.77, chunk=16,
+                  dynamic=True),
     "long": dict(d=256, H=4, ff=2048, enc=12, dec=6, B=8, T=4000, L=150, w=1.0, gflop=364.51, chunk=0),
     "tiny": dict(d=64, H=4, ff=256, enc=2, dec=1, B=16, T=1000, L=20, w=0.3, gflop=1.74, chunk=0),
 }
@@ -48,7 +51,8 @@ def build(cfgd, dtype, dropout, dev):
 
     c = U2Config(input_dim=80, vocab_size=V, enc_dim=cfgd["d"], enc_ff_dim=cfgd["ff"], enc_attn_heads=cfgd["H"],
                  enc_layers=cfgd["enc"], dec_dim=cfgd["d"], dec_ff_dim=cfgd["ff"], dec_attn_heads=cfgd["H"],
-                 dec_layers=cfgd["dec"], dropout_rate=dropout, compute_dtype=dtype, chunk_size=cfgd["chunk"])
+                 dec_layers=cfgd["dec"], dropout_rate=dropout, compute_dtype=dtype, chunk_size=cfgd["chunk"],
+                 dynamic_chunk=bool(cfgd.get("dynamic", False)))
     resolve_self(c)
     # my_U2.yaml: attention dropout 0, everything else model.dropout_rate
     c.enc_attn_dropout_rate = 0.0
@@ -650,6 +654,51 @@ def spawn_ranks(n, argv=None, target=None):
     return rc
 
 
+def chunk_report(model, cfgd, ctr0, steps):
+    """The encoder mask of the timed steps: none, a fixed chunk size, or the dynamic draw --
+    its distribution and the chunk sizes the timed steps used (the device draw is a pure
+    function of the step counter; the host mirror lists it without a sync per step)."""
+    if cfgd.get("dynamic"):
+        T = (((cfgd["T"] - 1) // 2 - 1) // 2)
+        cs = [model.dynamic_chunk_size(model._seed_base + 11, ctr0 + i, T, model.chunk_max) for i in range(steps)]
+        part = [c for c in cs if c < T]
+        return {"mode": "dynamic", "distribution": f"per step on the device: r ~ U{{1..T'-1}} (T' = {T}); "
+                f"r > T'/2 -> full context, else c = r mod {model.chunk_max} + 1 (WeNet add_optional_chunk_mask)",
+                "timed_steps_full_context": len(cs) - len(part),
+                "timed_steps_chunked": len(part), "timed_chunk_sizes": cs,
+                "mean_chunk_of_chunked_steps": round(sum(part) / len(part), 2) if part else None}
+    if cfgd["chunk"]:
+        return {"mode": "fixed", "chunk": cfgd["chunk"]}
+    return {"mode": "none (key padding only)"}
+
+
+def fixed_chunk_leg(model, net, crit, opt, batch, cfgd, args):
+    """The same model and batch with the fixed chunk (chunk_size, c = 16 at large) instead of the
+    dynamic draw: a second captured step timed over the same number of steps, reported beside the
+    dynamic line (the block-skipping attention kernels are cheapest at small c)."""
+    import torch
+
+    from liteasr_amd.graph_step import GraphedTrainStep
+
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    model.dynamic_chunk = False
+    try:
+        step = GraphedTrainStep(net, crit, opt, batch, clip=5.0, warmup=2, overlap=args.overlap == "on")
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    finally:
+        model.dynamic_chunk = True
+    return {"chunk": cfgd["chunk"], "ms_per_step": round(el / args.steps * 1e3, 3),
+            "utt_per_s": round(cfgd["B"] * args.steps / el, 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -658,6 +707,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="small", choices=sorted(CONFIGS))
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--chunk", default="config",
+                    help="encoder streaming chunk mask: 'config' (large: dynamic, others: none), 'dynamic' "
+                         "(a chunk size drawn per step on the device, WeNet's distribution), 'none', or a "
+                         "fixed chunk size")
+    ap.add_argument("--no-chunk-compare", action="store_true",
+                    help="dynamic chunk: skip the second, fixed-c (chunk_size) leg timed after the main one")
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--graph", default="on", choices=["on", "off"],
                     help="replay the step from hipGraphs (liteasr_amd/graph_step.py) or launch eagerly")
@@ -745,7 +800,14 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    cfgd = CONFIGS[args.config]
+    cfgd = dict(CONFIGS[args.config])
+    if args.chunk == "dynamic":
+        cfgd["dynamic"] = True
+        cfgd["chunk"] = cfgd["chunk"] or 16
+    elif args.chunk == "none":
+        cfgd["dynamic"], cfgd["chunk"] = False, 0
+    elif args.chunk != "config":
+        cfgd["dynamic"], cfgd["chunk"] = False, int(args.chunk)
 
     from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
     from liteasr_amd.optims.noam import Noam, NoamConfig
@@ -786,6 +848,7 @@ def main():
     # per-step HIP events on the stream the step runs on (no host sync inside the loop): the
     # median step beside the wall-clock mean the contract's ms_per_step reports
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    ctr0 = int(model._drop_ctr.item())  # the first timed step's counter (dynamic chunk draws)
     t0 = time.perf_counter()
     evs[0].record()
     for i in range(args.steps):
@@ -826,7 +889,8 @@ def main():
                        "model": f"U2 enc {cfgd['enc']}x conformer d{cfgd['d']} H{cfgd['H']} ff{cfgd['ff']}, "
                                 f"dec {cfgd['dec']}x, V {V}", "global_batch": world * cfgd["B"],
                        "per_gpu_batch": cfgd["B"], "seq_len": cfgd["T"], "label_len": cfgd["L"],
-                       "ctc_weight": cfgd["w"], "dropout": args.dropout, "chunk_size": cfgd["chunk"],
+                       "ctc_weight": cfgd["w"], "dropout": args.dropout,
+                       "chunk_size": chunk_report(model, cfgd, ctr0, args.steps),
                        "parallelism": f"dp{world}", "launch": "hipgraph" if args.graph == "on" else "eager",
                        "ranks_seen": dist.get_world_size() if dist.is_initialized() else world,
                        "rank_launcher": launcher,
@@ -858,6 +922,10 @@ def main():
                 out["roofline"] = fam
                 out["roofline"]["attention"] = att
             out["ctc"] = ctc_roofline(cfgd, dev)
+        if cfgd.get("dynamic") and args.graph == "on" and not args.no_chunk_compare:
+            del step
+            out["config"]["chunk_size"]["fixed_chunk_leg"] = fixed_chunk_leg(model, net, crit, opt, batch, cfgd,
+                                                                             args)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.config)
         print(json.dumps(out), flush=True)

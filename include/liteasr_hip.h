@@ -543,6 +543,24 @@ int lasr_u2_prep_ld(const int64_t* xlens, const int64_t* ys, const int64_t* ylen
                     int L, int Tsub, int sos, int eos, int chunk, int32_t* ys_in, int32_t* tgt,
                     int32_t* tgt_ctc, uint8_t* dec_mask, int dec_ld, uint8_t* enc_mask, int enc_ld,
                     int32_t* pred_len, int32_t* ylen32, void* stream);
+/* Every bookkeeping output and the streaming chunk mask in one launch (config 4's
+ * dynamic-chunk mask; the reference composes it as padding_mask | triangle_mask(T', stage=c),
+ * liteasr/utils/mask.py:84-89, applied through the layers' mask argument,
+ * liteasr/nets/transformer_encoder.py:113-120).
+ *   key_mask [B, T'] key padding (NULL: not written),
+ *   chunk_mask [B, T', chunk_ld] (chunk_ld >= T'; columns past T' written 1 = masked):
+ *     mask[b, i, j] = (4 j >= xlen[b]) | (j div c > i div c).
+ *   chunk_mode 0: no chunk mask; 1: c = chunk (> 0); 2: c = *chunk_dev (int32, device: a
+ *     captured graph replays whatever the host wrote there); 3: c drawn on the device from
+ *     (chunk_seed, *ctr) -- ctr the uint64 step counter -- and written to *chunk_dev when
+ *     non-NULL: r uniform in [1, T'-1]; r > T'/2 -> full context, else c = r mod chunk_max + 1
+ *     (WeNet's dynamic chunk distribution).  c <= 0 or c >= T' is full context.  */
+int lasr_u2_prep_chunk(const int64_t* xlens, const int64_t* ys, const int64_t* ylens, int B, int L,
+                       int Tsub, int sos, int eos, int chunk_mode, int chunk, int32_t* chunk_dev,
+                       const uint64_t* ctr, uint64_t chunk_seed, int chunk_max, int32_t* ys_in,
+                       int32_t* tgt, int32_t* tgt_ctc, uint8_t* dec_mask, int dec_ld, uint8_t* key_mask,
+                       uint8_t* chunk_mask, int chunk_ld, int32_t* pred_len, int32_t* ylen32,
+                       void* stream);
 
 /* ------------------------------------------------------------------------
  * SpecAugment (liteasr/utils/transform/spec_augment.py:14-125; applied per utterance in

@@ -10,9 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get(
-    "LITEASR_HIP_LIB", os.path.join(_HERE, "lib", "libliteasr_hip.so")
-)
+LIB_PATH = os.path.join(_HERE, "lib", "libliteasr_hip.so")  # the one product path (A/B tools:
+# tools/with_lib.py points this module at another build before anything loads it)
 
 F32, BF16, I32, I64, U8 = 0, 1, 2, 3, 4
 ACT_NONE, ACT_RELU, ACT_SWISH, ACT_GATE, ACT_TANH = 0, 1, 2, 3, 4
@@ -173,6 +172,8 @@ SIGNATURES = {
     "lasr_pe_fwd": [_p, _i, _l, _i, _i, _p, _f, _f, _u, _p, _i, _p],
     "lasr_u2_prep": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "lasr_u2_prep_ld": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p],
+    "lasr_u2_prep_chunk": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _u, _i,
+                           _p, _p, _p, _p, _i, _p, _p, _i, _p, _p, _p],
     "lasr_sumsq_nparts": [_l],
     "lasr_sumsq_partial": [_p, _l, _p, _l, _p],
     "lasr_adam_step": [_p, _p, _i, _p, _p, _p, _l, _p, _i, _p, _f, _i, _f, _f, _f, _f, _f, _f,

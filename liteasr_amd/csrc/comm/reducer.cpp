@@ -169,6 +169,8 @@ int lasr_reducer_create_from_comm(lasr_reducer** out, void* comm, int device, fl
                                   const int64_t* bucket_hi, int n_buckets) {
   if (!out || !comm) return fail(-1, "null argument");
   *out = nullptr;
+  int nranks = 0;  // queried before anything is allocated: a failure leaks nothing
+  NCCL_TRY(ncclCommCount((ncclComm_t)comm, &nranks));
   auto* r = new lasr_reducer;
   if (int rc = setup(r, device, grad, numel, bucket_lo, bucket_hi, n_buckets)) {
     std::string keep = g_err;
@@ -176,8 +178,6 @@ int lasr_reducer_create_from_comm(lasr_reducer** out, void* comm, int device, fl
     return fail(rc, keep);
   }
   r->comm = (ncclComm_t)comm;
-  int nranks = 0;
-  NCCL_TRY(ncclCommCount(r->comm, &nranks));
   r->world = nranks;
   *out = r;
   return 0;

@@ -800,15 +800,40 @@ def fill(t, value):
     N.call("lasr_fill", ptr(t), dt(t), t.numel(), float(value), stream())
 
 
-def u2_prep(xlens, ys, ylens, Tx, Tsub, sos, eos, chunk, out):
-    """out["dec_mask"] [B, L+1, ld] and (chunk > 0) out["enc_mask"] [B, T', ld]: the last
-    dimension is the row stride; columns past L+1 / T' come out 1 (masked)."""
+CHUNK_NONE, CHUNK_FIXED, CHUNK_DEVICE, CHUNK_SAMPLE = 0, 1, 2, 3
+
+
+def u2_prep(xlens, ys, ylens, Tx, Tsub, sos, eos, chunk, out, chunk_mode=None, chunk_dev=None, ctr=None,
+            chunk_seed=0, chunk_max=25):
+    """One lasr_u2_prep_chunk launch: out["dec_mask"] [B, L+1, ld >= L+1] (the last dimension
+    is the row stride; columns past L+1 come out 1 = masked), out["enc_mask"] [B, T'] (key
+    padding), the targets and lengths, and -- unless chunk_mode is CHUNK_NONE -- the
+    streaming chunk mask out["chunk_mask"] [B, T', ld >= T'] (padding columns masked).
+    chunk_mode defaults to CHUNK_FIXED for chunk > 0, else CHUNK_NONE; CHUNK_DEVICE reads c
+    from the int32 device scalar ``chunk_dev``, CHUNK_SAMPLE draws it from (chunk_seed, the
+    uint64 step counter ``ctr``) and writes it to ``chunk_dev``; c <= 0 or c >= T' is full
+    context."""
     B, L = ys.shape
+    if chunk_mode is None:
+        chunk_mode = CHUNK_FIXED if chunk > 0 else CHUNK_NONE
     dm, em = out["dec_mask"], out["enc_mask"]
-    assert dm.is_contiguous() and dm.shape[-1] >= L + 1 and em.is_contiguous()
-    N.call("lasr_u2_prep_ld", ptr(xlens), ptr(ys), ptr(ylens), B, Tx, L, Tsub, sos, eos, chunk,
+    assert dm.is_contiguous() and dm.dim() == 3 and tuple(dm.shape[:2]) == (B, L + 1) and dm.shape[-1] >= L + 1
+    assert em.is_contiguous() and em.dtype == torch.uint8 and em.numel() == B * Tsub
+    cm, cld = None, 0
+    if chunk_mode != CHUNK_NONE:
+        cm = out["chunk_mask"]
+        assert cm.is_contiguous() and cm.dim() == 3 and tuple(cm.shape[:2]) == (B, Tsub) and cm.shape[-1] >= Tsub
+        cld = cm.shape[-1]
+    if chunk_mode in (CHUNK_DEVICE, CHUNK_SAMPLE):
+        assert chunk_dev is not None and chunk_dev.dtype == torch.int32 and chunk_dev.is_cuda
+    if chunk_mode == CHUNK_SAMPLE:
+        assert ctr is not None and ctr.dtype == torch.int64 and ctr.is_cuda
+    for k, n in (("ys_in", B * (L + 1)), ("tgt", B * (L + 1)), ("tgt_ctc", B * L), ("pred_len", B), ("ylen", B)):
+        assert out[k].dtype == torch.int32 and out[k].numel() == n and out[k].is_contiguous(), k
+    N.call("lasr_u2_prep_chunk", ptr(xlens), ptr(ys), ptr(ylens), B, L, Tsub, sos, eos, chunk_mode,
+           int(chunk) if chunk_mode == CHUNK_FIXED else 0, ptr(chunk_dev), ptr(ctr), int(chunk_seed), int(chunk_max),
            ptr(out["ys_in"]), ptr(out["tgt"]), ptr(out["tgt_ctc"]), ptr(dm), dm.shape[-1],
-           ptr(em), em.shape[-1] if chunk > 0 else Tsub, ptr(out["pred_len"]), ptr(out["ylen"]), stream())
+           ptr(em), ptr(cm), cld, ptr(out["pred_len"]), ptr(out["ylen"]), stream())
 
 
 def spec_augment(x, xlens, plan, replace_with_zero=False, out=None):

@@ -53,6 +53,12 @@ class FusedEncoderModel(LiteasrModel):
             if isinstance(mod, _Bound):
                 mod._store = self.store
         self.register_buffer("_drop_ctr", torch.zeros(1, dtype=torch.int64), persistent=False)
+        # the streaming chunk size of the step (int32, device): written by the prep kernel when
+        # it draws c (dynamic_chunk), read by it when chunk_from_device is set (see chunk_mode)
+        self.register_buffer("_chunk_dev", torch.zeros(1, dtype=torch.int32), persistent=False)
+        self.dynamic_chunk = bool(getattr(self, "dynamic_chunk", False))
+        self.chunk_max = int(getattr(self, "chunk_max", 25))
+        self.chunk_from_device = False
         self._flatten_bn()
         self.last_prep = None
         self._seed_base = 77
@@ -126,6 +132,51 @@ class FusedEncoderModel(LiteasrModel):
         """liteasr/models/u2.py:319-321."""
         return torch.div(torch.div(xlens - 1, 2, rounding_mode="floor") - 1, 2, rounding_mode="floor")
 
+    def chunk_mode(self):
+        """How the encoder's streaming chunk mask is formed this step (lasr_u2_prep_chunk):
+        none (key padding only), a fixed ``chunk_size`` > 0, the device scalar ``_chunk_dev``
+        (``chunk_from_device``: set it with ``set_chunk`` between graph replays), or a per-step
+        draw on the device (``dynamic_chunk``, training mode only: WeNet's distribution, see
+        ``dynamic_chunk_size``; in eval mode a dynamic-chunk model uses ``chunk_size``)."""
+        if self.dynamic_chunk and self.training:
+            return K.CHUNK_SAMPLE
+        if self.chunk_from_device:
+            return K.CHUNK_DEVICE
+        return K.CHUNK_FIXED if self.chunk_size > 0 else K.CHUNK_NONE
+
+    def set_chunk(self, c):
+        """Device-scalar chunk size (stream-ordered write; c <= 0 or c >= T' = full context)
+        for ``chunk_from_device`` mode: a captured step reads it at every replay."""
+        self._chunk_dev.fill_(int(c))
+
+    def last_chunk(self):
+        """The chunk size the last prep used in dynamic / device mode (host sync)."""
+        return int(self._chunk_dev.item())
+
+    @staticmethod
+    def dynamic_chunk_size(seed, ctr, Tsub, cmax=25):
+        """Host mirror of the prep kernel's draw (csrc/prep.hip chunk_draw) for step counter
+        value ``ctr``: r uniform in [1, T'-1]; r > T'/2 -> full context (returns T'), else
+        r mod cmax + 1 (wenet/utils/mask.py add_optional_chunk_mask's distribution)."""
+        M32, M64 = 0xFFFFFFFF, 0xFFFFFFFFFFFFFFFF
+
+        def mix32(x):
+            x &= M32
+            x ^= x >> 16
+            x = (x * 0x7FEB352D) & M32
+            x ^= x >> 15
+            x = (x * 0x846CA68B) & M32
+            x ^= x >> 16
+            return x
+
+        if Tsub <= 1:
+            return max(Tsub, 1)
+        s = (seed + ctr * 0xD1B54A32D192ED03) & M64
+        key = mix32((s & M32) ^ mix32(((s >> 32) + 0x9E3779B9) & M32))
+        h = mix32(key ^ 0x5BD1E995)
+        r = 1 + h % (Tsub - 1)
+        return Tsub if r > Tsub // 2 else r % cmax + 1
+
     def _prep(self, xs, xlens, ys, ylens):
         dev = xs.device
         B, Tx = xs.shape[0], xs.shape[1]
@@ -147,15 +198,13 @@ class FusedEncoderModel(LiteasrModel):
         xl = xlens.to(device=dev, dtype=torch.int64)
         yy = ys.to(device=dev, dtype=torch.int64).contiguous()
         yl = ylens.to(device=dev, dtype=torch.int64)
-        K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, 0, out)
-        chunk = None
-        if self.chunk_size > 0:
-            # (u2_prep writes every output: the chunk-mask call gets scratch for the others, so
-            # nothing it writes lands in a buffer laid out differently from what it assumes)
-            tmp = {k: torch.empty_like(v) for k, v in out.items()}
-            tmp["enc_mask"] = torch.empty(B, Tsub, P16(Tsub), dtype=u8, device=dev)
-            K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, self.chunk_size, tmp)
-            chunk = tmp["enc_mask"][:, :, :Tsub]
+        mode = self.chunk_mode()
+        if mode != K.CHUNK_NONE:
+            out["chunk_mask"] = torch.empty(B, Tsub, P16(Tsub), dtype=u8, device=dev)
+        K.u2_prep(xl, yy, yl, Tx, Tsub, self.sos, self.eos, self.chunk_size, out, chunk_mode=mode,
+                  chunk_dev=self._chunk_dev, ctr=self._drop_ctr, chunk_seed=self._seed_base + 11,
+                  chunk_max=self.chunk_max)
+        chunk = out.pop("chunk_mask")[:, :, :Tsub] if mode != K.CHUNK_NONE else None
         # kernels read the masks through (msb, msq) = the views' strides
         out["dec_mask"] = out["dec_mask"][:, :, :L + 1]
         p = SimpleNamespace(B=B, Tx=Tx, T=Tsub, L=L, chunk_mask=chunk, **out)

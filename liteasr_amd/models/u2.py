@@ -9,6 +9,10 @@ Extensions (default off = reference behaviour):
   compute_dtype  "bf16" (default; fp32 masters/accumulation) or "fp32" (parity build)
   chunk_size     > 0 adds triangle_mask(T', stage=chunk_size) to the encoder
                  self-attention mask (the dynamic-chunk config's oracle-by-composition)
+  dynamic_chunk  True: in training, a chunk size is drawn per step on the device (WeNet's
+                 distribution: full context with probability ~1/2, else c in 1..max_chunk)
+                 and the mask is padding | triangle_mask(T', stage=c) -- BASELINE config 4
+  max_chunk      upper end of the dynamic draw (25)
 """
 
 from __future__ import annotations
@@ -68,6 +72,8 @@ class U2Config(LiteasrDataclass):
     # liteasr_amd extensions
     compute_dtype: str = field(default="bf16")
     chunk_size: int = field(default=0)
+    dynamic_chunk: bool = field(default=False)
+    max_chunk: int = field(default=25)
 
 
 def _arch(v, enum):
@@ -105,6 +111,8 @@ class U2(FusedEncoderModel):
         cd = str(g("compute_dtype", "bf16")).lower()
         self.compute_dtype = torch.float32 if cd in ("fp32", "float32", "float") else torch.bfloat16
         self.chunk_size = int(g("chunk_size", 0) or 0)
+        self.dynamic_chunk = bool(g("dynamic_chunk", False))
+        self.chunk_max = int(g("max_chunk", 25) or 25)
         self.vocab_size = g("vocab_size")
         self._finalize()
 

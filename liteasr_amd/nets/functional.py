@@ -512,6 +512,7 @@ class EmbedConvFn(torch.autograd.Function):
         y1 = _e((B, T1, F1, C), adt, dev)
         K.conv1_fwd(xs, w.W1, w.b1, y1)
         y2_full = _e((K.conv2_dy2_rows(M2), C), adt, dev)
+        y2_full[M2:].zero_()  # the tail rows are part of the autograd output: defined (zero)
         y2 = y2_full[:M2]
         implicit = _conv2_implicit(adt, C)
         if implicit:  # conv2 as implicit GEMM: im2col(y1) is never materialised
@@ -599,8 +600,14 @@ class EmbedOutFn(torch.autograd.Function):
         K.gemm(gb.t(), y2f, dWo, split_k=0, rowsum=g.bout)
         K.permute_last2(dWo, d, C, F2, g.out_w, reverse=True, accumulate=True)
         mod.unit_ready("out")
-        dy2_full = _e(sv.y2_full.shape, adt, dev)
-        dy2_full[M2:].zero_()
+        # dy2 with its zero tail rows (the implicit GEMMs' K padding / out-of-range taps): one
+        # buffer kept per subsampling module, its tail zeroed once when it is allocated (it is
+        # produced here and consumed by EmbedConvFn.backward right after, in the same backward)
+        key = (tuple(sv.y2_full.shape), adt, dev)
+        if getattr(mod, "_dy2_key", None) != key:
+            mod._dy2_buf = torch.zeros(sv.y2_full.shape, dtype=adt, device=dev)
+            mod._dy2_key = key
+        dy2_full = mod._dy2_buf
         K.gemm(gb, w.Woutp, dy2_full[:M2].view(M, F2 * C), aux=y2f, aux_act=ACT_RELU)
         return dy2_full, None, None, None
 

@@ -138,10 +138,14 @@ def ffn(x, p: Params, name: str, act: str, drop=0.0, training=True, gate=None, p
     """PositionwiseFeedForward: liteasr/nets/feed_forward.py:18-19, Swish swish.py:14-16.
     Test hook (ReLU only): ``gate`` (0/1, the shape of the pre-activation) replaces the branch
     relu takes, h = u * gate -- a parity test feeds the branch the GPU build took so that a
-    pre-activation within rounding of 0 takes the same side on both; ``pre`` collects u."""
+    pre-activation within rounding of 0 takes the same side on both; ``pre`` collects
+    (u, bound): bound = K 2^-23 (|x| |W|^T + |b|), the worst-case error of an fp32 K-term dot
+    product (plus bias), per element -- how far from 0 an fp32 build may put u on the other side."""
     h = linear(x, p, name + ".fc1")
     if pre is not None:
-        pre.append(h.detach())
+        w, b = p[name + ".fc1.weight"], p.get(name + ".fc1.bias")
+        mag = F.linear(x.detach().abs(), w.detach().abs(), None if b is None else b.detach().abs())
+        pre.append((h.detach(), w.shape[1] * 2.0 ** -23 * mag))
     if gate is not None:
         assert act == "relu"
         h = h * gate.to(h.dtype).view_as(h)

@@ -41,6 +41,7 @@ def test_group_option_extends_another_and_overrides():
                              "~postprocess.spec_aug", "dataset.batch_size=8"])
     m = cfg.model
     assert (m.enc_dim, m.enc_attn_heads, m.chunk_size, m.enc_layers) == (512, 16, 16, 12)
+    assert m.dynamic_chunk is True and m.max_chunk == 25
     assert m.enc_dropout_rate == 0.2 and m.dec_pos_dropout_rate == 0.2 and m.enc_attn_dropout_rate == 0.0
     assert cfg.criterion.ctc_weight == 1.0 and cfg.criterion.smoothing == 0.1
     assert cfg.common.extra == 3 and "spec_aug" not in cfg.postprocess and cfg.dataset.batch_size == 8

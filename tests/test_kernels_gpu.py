@@ -1183,12 +1183,92 @@ def test_embed_pe_and_prep():
     assert torch.equal(pad["dec_mask"][:, :, :5], out["dec_mask"]) and bool((pad["dec_mask"][:, :, 5:] == 1).all())
     ck = 4
     P = (Tsub + 15) // 16 * 16
-    chk = dict(out, enc_mask=torch.zeros(3, Tsub, P, dtype=torch.uint8, device=DEV))
+    chk = dict(out, chunk_mask=torch.zeros(3, Tsub, P, dtype=torch.uint8, device=DEV),
+               enc_mask=torch.empty_like(out["enc_mask"]))
     kn.u2_prep(xlens, ys, ylens, Tx, Tsub, 9, 9, ck, chk)
     t = torch.arange(Tsub)
     cm = pm[:, :-2:2][:, :-2:2][:, None, :] | ((t[None, :] // ck) > (t[:, None] // ck))[None]
-    assert torch.equal(chk["enc_mask"][:, :, :Tsub].cpu().bool(), cm)
-    assert bool((chk["enc_mask"][:, :, Tsub:] == 1).all())
+    assert torch.equal(chk["chunk_mask"][:, :, :Tsub].cpu().bool(), cm)
+    assert bool((chk["chunk_mask"][:, :, Tsub:] == 1).all())
+    assert torch.equal(chk["enc_mask"], out["enc_mask"])  # the key mask in the same launch
+
+
+def _prep_case(B, Tx, L, seed):
+    g = torch.Generator().manual_seed(seed)
+    xlens = torch.randint(1, Tx + 1, (B,), generator=g)
+    xlens[0] = Tx
+    ylens = torch.randint(0, L + 1, (B,), generator=g)
+    ys = torch.randint(1, 50, (B, L), generator=g)
+    ys[torch.arange(L)[None, :] >= ylens[:, None]] = -1
+    Tsub = ((Tx - 1) // 2 - 1) // 2
+    P = (Tsub + 15) // 16 * 16
+    out = {
+        "ys_in": torch.empty(B, L + 1, dtype=torch.int32, device=DEV),
+        "tgt": torch.empty(B, L + 1, dtype=torch.int32, device=DEV),
+        "tgt_ctc": torch.empty(B, L, dtype=torch.int32, device=DEV),
+        "dec_mask": torch.empty(B, L + 1, (L + 16) // 16 * 16, dtype=torch.uint8, device=DEV),
+        "enc_mask": torch.empty(B, Tsub, dtype=torch.uint8, device=DEV),
+        "chunk_mask": torch.empty(B, Tsub, P, dtype=torch.uint8, device=DEV),
+        "pred_len": torch.empty(B, dtype=torch.int32, device=DEV),
+        "ylen": torch.empty(B, dtype=torch.int32, device=DEV),
+    }
+    return xlens, ys, ylens, Tsub, out
+
+
+def _chunk_ref(xlens, Tx, Tsub, c):
+    """liteasr/utils/mask.py: padding_mask(xlens)[:, :-2:2][:, :-2:2] | triangle_mask(T', stage=c)."""
+    pm = (torch.arange(Tx)[None, :] >= xlens[:, None])[:, :-2:2][:, :-2:2]
+    t = torch.arange(Tsub)
+    return pm[:, None, :] | ((t[None, :] // c) > (t[:, None] // c))[None]
+
+
+@pytest.mark.parametrize("Tx,c", [(1000, 1), (1000, 16), (1000, 25), (1000, 249), (1000, 0), (4000, 7), (61, 3)])
+def test_u2_prep_device_chunk(Tx, c):
+    """Device-scalar chunk mode (lasr_u2_prep_chunk mode 2, what a captured dynamic-chunk step
+    replays): the mask equals padding | triangle_mask(T', stage=c) bit for bit, c <= 0 or
+    c >= T' is full context, and the padding columns are masked; every other output equals
+    the chunk-free call's."""
+    kn = K()
+    xlens, ys, ylens, Tsub, out = _prep_case(5, Tx, 12, seed=Tx + c)
+    ref_out = {k: torch.empty_like(v) for k, v in out.items()}
+    kn.u2_prep(xlens.to(DEV), ys.to(DEV), ylens.to(DEV), Tx, Tsub, 9, 9, 0, ref_out)
+    cd = torch.tensor([c], dtype=torch.int32, device=DEV)
+    kn.u2_prep(xlens.to(DEV), ys.to(DEV), ylens.to(DEV), Tx, Tsub, 9, 9, 0, out, chunk_mode=kn.CHUNK_DEVICE,
+               chunk_dev=cd)
+    ce = c if 0 < c < Tsub else Tsub
+    assert torch.equal(out["chunk_mask"][:, :, :Tsub].cpu().bool(), _chunk_ref(xlens, Tx, Tsub, ce))
+    assert bool((out["chunk_mask"][:, :, Tsub:] == 1).all())
+    for k in ("ys_in", "tgt", "tgt_ctc", "dec_mask", "enc_mask", "pred_len", "ylen"):
+        assert torch.equal(out[k], ref_out[k]), k
+
+
+def test_u2_prep_sampled_chunk_matches_host_draw():
+    """Sampled mode (lasr_u2_prep_chunk mode 3, the dynamic-chunk training step): the device
+    draws c from (seed, step counter), writes it to the device scalar, and builds the mask with
+    it; the host mirror (FusedEncoderModel.dynamic_chunk_size) gives the same c for every
+    counter value, and the draws follow WeNet's distribution (about half full context, the
+    rest spread over 1..25)."""
+    from liteasr_amd.models._fused import FusedEncoderModel as F
+
+    kn = K()
+    Tx = 1000
+    xlens, ys, ylens, Tsub, out = _prep_case(3, Tx, 8, seed=3)
+    xd, yd, ld = xlens.to(DEV), ys.to(DEV), ylens.to(DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    cd = torch.zeros(1, dtype=torch.int32, device=DEV)
+    seen = []
+    for step in list(range(40)) + [2**32 + 5, 2**40 + 77]:
+        ctr.fill_(step)
+        kn.u2_prep(xd, yd, ld, Tx, Tsub, 9, 9, 0, out, chunk_mode=kn.CHUNK_SAMPLE, chunk_dev=cd, ctr=ctr,
+                   chunk_seed=88, chunk_max=25)
+        c = int(cd.item())
+        assert c == F.dynamic_chunk_size(88, step, Tsub, 25), step
+        assert torch.equal(out["chunk_mask"][:, :, :Tsub].cpu().bool(), _chunk_ref(xlens, Tx, Tsub, c)), step
+        seen.append(c)
+    host = [F.dynamic_chunk_size(88, s, Tsub, 25) for s in range(4000)]
+    full = sum(c == Tsub for c in host) / len(host)
+    assert 0.45 < full < 0.55 and set(c for c in host if c != Tsub) == set(range(1, 26)), full
+    assert len(set(seen)) > 5
 
 
 def test_adam_noam_clip():

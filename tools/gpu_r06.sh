@@ -1,8 +1,8 @@
 #!/bin/bash
-# GPU pass (round 5).  Usage: tools/gpu_r05.sh TAG STEP...; output under gpurun_out/TAG/.
+# GPU pass (round 6).  Usage: tools/gpu_r05.sh TAG STEP...; output under gpurun_out/TAG/.
 # Every step has its own time limit; the script stops at the first failure.
 set -u -o pipefail
-TAG=${1:-r05}; shift
+TAG=${1:-r06}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -17,13 +17,13 @@ for s in "$@"; do
            "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" "tests/test_model_gpu.py::test_parity_config4_full_model_bf16_emulated" \
            "tests/test_kernels_gpu.py::test_gemm_ksub2_bit_identical" -s > "$OUT/new.log" 2>&1 ;;
     attncheck) # bitwise A/B of the attention kernels: ab_prev/'s library vs the tree's
-           LITEASR_HIP_LIB=$R/ab_prev/liteasr_amd/lib/libliteasr_hip.so run timeout -k 10 300 python3 tools/attn_check.py dump "$OUT/attn_base.pt" > "$OUT/attn_check.log" 2>&1
+           run timeout -k 10 300 python3 tools/with_lib.py $R/ab_prev/liteasr_amd/lib/libliteasr_hip.so tools/attn_check.py dump "$OUT/attn_base.pt" > "$OUT/attn_check.log" 2>&1
            run timeout -k 10 300 python3 tools/attn_check.py dump "$OUT/attn_new.pt" >> "$OUT/attn_check.log" 2>&1
            run python3 tools/attn_check.py cmp "$OUT/attn_new.pt" "$OUT/attn_base.pt" > "$OUT/attn_check.jsonl" 2>&1
            rm -f "$OUT/attn_base.pt" "$OUT/attn_new.pt" ;;
     epiab) # FFN fc1 epilogue ablation: the tree's library and the LASR_EXP builds in liteasr_amd/lib/exp
            for rep in 1 2; do for v in tree ${EXP_LIBS:-8 16 24}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
-             LITEASR_HIP_LIB=$lib run timeout -k 10 120 python3 tools/epi_ab.py >> "$OUT/epi_ab.jsonl" 2>> "$OUT/epi_ab.err"; done; done ;;
+             run timeout -k 10 120 python3 tools/with_lib.py $lib tools/epi_ab.py >> "$OUT/epi_ab.jsonl" 2>> "$OUT/epi_ab.err"; done; done ;;
     envlist) # whole step, one tree, the environments of ENV_LIST ("VAR=val ...;VAR=val;..."), two passes
            IFS=';' read -ra ENVS <<< "${ENV_LIST:-}"
            for rep in 1 2; do for i in "${!ENVS[@]}"; do e=${ENVS[$i]}
@@ -31,11 +31,14 @@ for s in "$@"; do
              grep "^{" "$OUT/envlist_$i.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); a=(d['config'].get('allreduce') or {}); t=a.get('timeline_last_step') or {}; print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'segment_ms': t.get('segment_ms')}))" >> "$OUT/envlist.jsonl"; done; done ;;
     conv2ab) # subsampling conv2 GEMMs: the tree's library vs liteasr_amd/lib/exp/lib$N.so (EXP_LIBS="32 ...")
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
-             LITEASR_HIP_LIB=$lib run timeout -k 10 120 python3 tools/conv2_bench.py ${CONV2_SHAPE:-} | sed "s/^{/{\"v\": \"$v\", /" >> "$OUT/conv2_ab.jsonl" || exit 1; done; done ;;
+             run timeout -k 10 120 python3 tools/with_lib.py $lib tools/conv2_bench.py ${CONV2_SHAPE:-} | sed "s/^{/{\"v\": \"$v\", /" >> "$OUT/conv2_ab.jsonl" || exit 1; done; done ;;
     envab) # whole step, one tree, two environments alternating (ENV_A / ENV_B: "VAR=val ...")
            for v in A B A B; do e=$ENV_A; [ $v = B ] && e=$ENV_B
              env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/envab_$v.json" 2> "$OUT/envab_$v.err" || exit 1
              grep "^{" "$OUT/envab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median')}))" >> "$OUT/envab.jsonl"; done ;;
+    dyn) run timeout -k 10 900 $PYT tests/test_kernels_gpu.py -k "u2_prep or embed_and_prep or prep" \
+           tests/test_model_gpu.py -k "dynamic or config4 or graphed or chunk" -s > "$OUT/dyn.log" 2>&1 ;;
+    largedyn) run timeout -k 10 500 python3 bench.py --config large --no-cpu-baseline --no-roofline > "$OUT/bench_large_dyn.json" 2> "$OUT/bench_large_dyn.err" ;;
     switches) run timeout -k 10 900 $PYT tests/test_switches_gpu.py > "$OUT/switches.log" 2>&1 ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
            "tests/test_model_gpu.py::test_parity_config4_full_model_fp32" -s > "$OUT/new5.log" 2>&1 ;;
@@ -44,25 +47,25 @@ for s in "$@"; do
     attnbench) run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_bench.jsonl" 2> "$OUT/attn_bench.err" ;;
     attnab) # attention kernels: the library in ab/ (same ABI) vs the tree's, alternating
            for v in base new base new; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v = base ] && lib=$R/ab_prev/liteasr_amd/lib/libliteasr_hip.so
-             LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
+             run timeout -k 10 300 python3 tools/with_lib.py $lib tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_ab_$v.tmp" >> "$OUT/attn_ab.jsonl"; rm -f "$OUT/attn_ab_$v.tmp"; done ;;
     attnexp) # attention kernels: the tree's library vs liteasr_amd/lib/exp/lib$N.so ablation builds (EXP_LIBS), twice
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
-             LITEASR_HIP_LIB=$lib run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_exp_$v.tmp"
+             run timeout -k 10 300 python3 tools/with_lib.py $lib tools/attn_bench.py > "$OUT/attn_exp_$v.tmp"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_exp_$v.tmp" >> "$OUT/attn_exp.jsonl"; rm -f "$OUT/attn_exp_$v.tmp"; done; done ;;
     ctcexp) # CTC kernels at small and long: the tree's library vs lib/exp/lib$N.so (EXP_LIBS), twice
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
-             LITEASR_HIP_LIB=$lib run timeout -k 10 200 python3 tools/ctc_bench.py > "$OUT/ctc.tmp" 2>> "$OUT/ctcexp.err"
+             run timeout -k 10 200 python3 tools/with_lib.py $lib tools/ctc_bench.py > "$OUT/ctc.tmp" 2>> "$OUT/ctcexp.err"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/ctc.tmp" >> "$OUT/ctcexp.jsonl"; rm -f "$OUT/ctc.tmp"; done; done ;;
     toolab) # TOOL (a script printing JSON lines) under the tree's library, ab_prev/'s and lib/exp/lib$N.so (EXP_LIBS), twice
            for rep in 1 2; do for v in tree prev ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so
              [ $v = prev ] && lib=$R/ab_prev/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && [ $v != prev ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
-             LITEASR_HIP_LIB=$lib run timeout -k 10 200 python3 $TOOL > "$OUT/toolab.tmp" 2>> "$OUT/toolab.err"
+             run timeout -k 10 200 python3 tools/with_lib.py $lib $TOOL > "$OUT/toolab.tmp" 2>> "$OUT/toolab.err"
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/toolab.tmp" >> "$OUT/toolab.jsonl"; rm -f "$OUT/toolab.tmp"; done; done ;;
     caseab) # bench.py roofline cases (RCASES "small:dw large:dw ..."): the tree's library vs lib/exp/lib$N.so (EXP_LIBS), twice
            for rep in 1 2; do for v in tree ${EXP_LIBS:-}; do lib=$R/liteasr_amd/lib/libliteasr_hip.so; [ $v != tree ] && lib=$R/liteasr_amd/lib/exp/lib$v.so
              for rc in ${RCASES:-small:dw}; do cfg=${rc%%:*}; cs=${rc##*:}
-               LITEASR_HIP_LIB=$lib run timeout -k 10 200 python3 bench.py --config $cfg --roofline-only 20 --roofline-case $cs > "$OUT/caseab.tmp" 2>> "$OUT/caseab.err"
+               run timeout -k 10 200 python3 tools/with_lib.py $lib bench.py --config $cfg --roofline-only 20 --roofline-case $cs > "$OUT/caseab.tmp" 2>> "$OUT/caseab.err"
                grep "^{" "$OUT/caseab.tmp" | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'cfg': '$cfg', 'case': '$cs', 'kernel': d.get('kernel'), 'us': d.get('us_per_launch_eager')}))" >> "$OUT/caseab.jsonl"; done; done; done ;;
     stepab) # whole step: the previous commit's tree (ab_prev/: `git archive` + its built library) vs this
            # tree, alternating (AB_ARGS: e.g. --config large)
