@@ -98,6 +98,29 @@ typedef struct lasr_gemm_args {
   int ksub;
 } lasr_gemm_args;
 int lasr_gemm(const lasr_gemm_args* args, void* stream);
+/* A GEMM whose rows feed a LayerNorm (the decoder's K = ff GEMMs on B*(L+1) rows; the
+ * reference's layer boundary liteasr/nets/transformer_layer.py:196-221 and the norm
+ * liteasr/nets/layer_norm.py:8-28).  When the plan splits K, the split-K reduction launch also
+ * runs the norm (one launch fewer, bit-identical to lasr_gemm + the norm entry); otherwise the
+ * two launches run.  C must be batch 1 with contiguous rows (ldc == N), no rowsum.
+ *  lasr_gemm_ln_fwd: C fp32 (the epilogue's output, e.g. res + dropout(A B)), then
+ *    y = LN(C) (y_dtype) + mean / rstd per row -- lasr_layernorm_fwd(C, ...).
+ *  lasr_gemm_ln_bwd: C = dln (any epilogue, stored), then lasr_layernorm_bwd(x, dln, ...) with
+ *    dgamma = dbeta = NULL: dx, gb and the dgamma / dbeta partial rows in `part`
+ *    ([cdiv(M, 16)][2N]; the caller reduces them). */
+int lasr_gemm_ln_fwd(const lasr_gemm_args* args, const float* gamma, const float* beta, float eps, void* y,
+                     int y_dtype, float* mean, float* rstd, void* stream);
+int lasr_gemm_ln_bwd(const lasr_gemm_args* args, const void* x, int x_dtype, const float* gamma, const float* mean,
+                     const float* rstd, const void* dres, int dres_dtype, void* dx, int dx_dtype, float* part,
+                     int64_t part_floats, void* gb, int gb_dtype, float bscale, float bp, uint64_t bseed,
+                     void* stream);
+/* The encoder attention's positional-projection gradient GEMM (dp, split over K = B*T') and the
+ * positional-bias gradient of lasr_qbias_bwd (liteasr/nets/attention.py:131-135) with its
+ * partial rows left in ws (du = dv = NULL): when the GEMM's plan splits K, the split-K
+ * reduction and the qbias blocks share one launch (bit-identical to lasr_gemm +
+ * lasr_qbias_bwd); otherwise the two launches run.  C's dtype = dt. */
+int lasr_gemm_qbias_bwd(const lasr_gemm_args* args, const void* dqu, const void* dqv, int dt, int B, int T, int H,
+                        int dk, void* dqkv, int64_t ld, float* ws, int64_t ws_floats, void* stream);
 /* Dropout: one 32-bit counter-hash draw per element pair, 16-bit halves against
  * thr = round(p * 65536); kept values scale by lasr_dropout_scale(p) = 65536 / (65536 - thr)
  * (E[mask * scale] = 1 exactly).  Host helper, no device work. */

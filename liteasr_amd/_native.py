@@ -172,6 +172,9 @@ SIGNATURES = {
     "lasr_pe_fwd": [_p, _i, _l, _i, _i, _p, _f, _f, _u, _p, _i, _p],
     "lasr_u2_prep": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "lasr_u2_prep_ld": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p],
+    "lasr_gemm_qbias_bwd": [C.POINTER(GemmArgs), _p, _p, _i, _i, _i, _i, _i, _p, _l, _p, _l, _p],
+    "lasr_gemm_ln_fwd": [C.POINTER(GemmArgs), _p, _p, _f, _p, _i, _p, _p, _p],
+    "lasr_gemm_ln_bwd": [C.POINTER(GemmArgs), _p, _i, _p, _p, _p, _p, _i, _p, _i, _p, _l, _p, _i, _f, _f, _u, _p],
     "lasr_u2_prep_chunk": [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _u, _i,
                            _p, _p, _p, _p, _i, _p, _p, _i, _p, _p, _p],
     "lasr_sumsq_nparts": [_l],

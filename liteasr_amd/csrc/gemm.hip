@@ -173,7 +173,9 @@ extern "C" int lasr_gemm_plan(const lasr_gemm_args* a, int* tile_m, int* tile_n,
   return LASR_OK;
 }
 
-extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
+extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) { return gemm_run(a, stream, nullptr); }
+
+int gemm_run(const lasr_gemm_args* a, void* stream, GemmRowPost* post) {
   LASR_CHECK_ARG(a != nullptr, "lasr_gemm: null args");
   LASR_CHECK_ARG(a->M >= 0 && a->N >= 0 && a->K >= 0, "lasr_gemm: negative size");
   LASR_CHECK_ARG(a->in_dtype == LASR_F32 || a->in_dtype == LASR_BF16, "lasr_gemm: bad in_dtype");
@@ -270,7 +272,16 @@ extern "C" int lasr_gemm(const lasr_gemm_args* a, void* stream) {
   if (a->c_dtype == LASR_F32) dispatch<float>(p, akc, bkc, bf, BM, BN, ks, nw, glds, grid, st);
   else dispatch<bf16_t>(p, akc, bkc, bf, BM, BN, ks, nw, glds, grid, st);
   int rc = lasr_check_launch("lasr_gemm");
-  if (!rc && split > 1 && a->split_k >= 0) {
+  if (!rc && split > 1 && a->split_k >= 0 && post) {  // a row post-op may take over the reduction
+    const int r = post->launch(p, post->ctx, st);
+    if (r < 0) return r;
+    post->done = r;
+    if (r) {
+      rc = lasr_check_launch("lasr_gemm/splitk_reduce_post");
+      if (rc || !a->rowsum || rs_fused) return rc;
+    }
+  }
+  if (!rc && split > 1 && a->split_k >= 0 && !(post && post->done)) {
     const int64_t total = (int64_t)a->M * a->N * batch;
     const int nblk = (int)std::min<int64_t>(cdiv(p.v4 ? total / 4 : total, 256), 4096);
     if (a->c_dtype == LASR_F32) splitk_reduce_kernel<float><<<nblk, 256, 0, st>>>(p);

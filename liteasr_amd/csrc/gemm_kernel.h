@@ -76,6 +76,17 @@ struct GemmP {
   ConvGeom cv;    // implicit-GEMM instances of the subsampling conv2 only (G != 0)
 };
 
+// A row post-op that may take over a split-K GEMM's reduction launch (gemm_ln.hip: the
+// reduction fused with the next LayerNorm, forward or backward).  launch returns 1 when it
+// launched the fused reduction (done), 0 when lasr_gemm must run the plain one, < 0 on error.
+struct GemmRowPost {
+  int (*launch)(const GemmP& p, const void* ctx, hipStream_t st);
+  const void* ctx;
+  int done;
+};
+struct lasr_gemm_args;
+int gemm_run(const lasr_gemm_args* a, void* stream, GemmRowPost* post);
+
 LASR_DEV float load_any(const void* p, int dt, int64_t i) {
   return dt == LASR_F32 ? ((const float*)p)[i] : bf2f(((const bf16_t*)p)[i]);
 }
@@ -535,9 +546,18 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmP p) {
 
 // Epilogue of 4 consecutive columns n..n+3 of row m (same order as epi_store8); cnt < 4 or
 // !vec -> element-wise tail.
+// The value a TC store keeps, back in fp32 (the bf16 rounding of stv / pk_bf16).
+template <typename TC>
+LASR_DEV float stored_value(float x) {
+  if constexpr (sizeof(TC) == 4) return x;
+  else return __uint_as_float(pk_bf16(x, 0.f) << 16);
+}
+
+// vout (optional): the 4 values as stored in C (the row-LayerNorm post-ops of gemm_ln.hip
+// continue from them in registers)
 template <typename TC, bool VEC>
 LASR_DEV void epi_store4(const GemmP& p, uint32_t dkey, int z1, int z2, int z, int m, int n, int cnt,
-                         const float* acc, float al) {
+                         const float* acc, float al, float* vout = nullptr) {
   float v[4], t[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) v[q] = acc[q] * al;
@@ -581,6 +601,10 @@ LASR_DEV void epi_store4(const GemmP& p, uint32_t dkey, int z1, int z2, int z, i
   }
   if ((LASR_EXP & 2) && v[0] != 1234.5f) return;
   st4(C, v);
+  if (vout) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vout[q] = stored_value<TC>(v[q]);
+  }
 }
 
 // Epilogue straight from the accumulators, no LDS and no barrier.  The main loop issues
@@ -1228,9 +1252,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
       }
 }
 
-// Split-K reduction: sums the split partials in fixed order, then the epilogue.
+// Split-K reduction: sums the split partials in fixed order, then the epilogue.  The body
+// takes its block index and block count, so a fused launch can run it on a block range
+// (gemm_ln.hip: beside the positional-bias reduction).
 template <typename TC>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
+LASR_DEV void splitk_reduce_body(const GemmP& p, int bx, int nbx) {
   const int64_t MN = (int64_t)p.M * p.N;
   const int64_t total = MN * p.batch;
   const float al = alpha_of(p);
@@ -1239,7 +1265,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
     // 4 consecutive columns per thread (N % 4 == 0): 16-B partial loads, 4 slices in
     // flight, summed in slice order
     const int64_t sstride = (int64_t)p.batch * MN;
-    for (int64_t i4 = blockIdx.x * 256 + threadIdx.x; i4 < total / 4; i4 += (int64_t)gridDim.x * 256) {
+    for (int64_t i4 = (int64_t)bx * 256 + threadIdx.x; i4 < total / 4; i4 += (int64_t)nbx * 256) {
       const int64_t i = i4 * 4;
       const int z = (int)(i / MN);
       const int64_t r = i - (int64_t)z * MN;
@@ -1264,7 +1290,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
       epi_store4<TC, true>(p, dkey, z / p.batch_div, z % p.batch_div, z, m, n, 4, acc, al);
     }
   } else {
-    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    for (int64_t i = (int64_t)bx * 256 + threadIdx.x; i < total; i += (int64_t)nbx * 256) {
       const int z = (int)(i / MN);
       const int64_t r = i - (int64_t)z * MN;
       float acc = 0.f;
@@ -1274,12 +1300,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
     }
   }
   if (p.rs_ws) {  // bias-gradient partials (batch == 1)
-    for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < p.M; m += (int64_t)gridDim.x * 256) {
+    for (int64_t m = (int64_t)bx * 256 + threadIdx.x; m < p.M; m += (int64_t)nbx * 256) {
       float acc = 0.f;
       for (int s = 0; s < p.split_k; ++s) acc += p.rs_ws[(int64_t)s * p.M + m];
       p.rowsum[m] += acc;
     }
   }
+}
+template <typename TC>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmP p) {
+  splitk_reduce_body<TC>(p, blockIdx.x, gridDim.x);
 }
 
 

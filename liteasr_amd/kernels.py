@@ -191,6 +191,9 @@ def gemm(
     group: bool = False,
     tile: Optional[tuple] = None,
     ksub: int = 0,
+    ln_fwd: Optional[tuple] = None,
+    ln_bwd: Optional[object] = None,
+    qbias: Optional[tuple] = None,
 ):
     """c = epilogue(alpha * a @ b) for logical views a (..,M,K), b (..,K,N), c (..,M,N).
 
@@ -202,7 +205,14 @@ def gemm(
 
     group=True (a split-K weight gradient inside deferred_reductions): the launch itself may
     be deferred to the end of the block and grouped with the block's other dW GEMMs, so
-    the caller must not modify a or b before the block exits."""
+    the caller must not modify a or b before the block exits.
+
+    ln_fwd=(gamma, beta, eps, y, mean, rstd): the LayerNorm of c's rows follows
+    (lasr_gemm_ln_fwd: in the split-K reduction launch when K is split).  ln_bwd=lnb (an
+    object with x, g, mean, rstd, dx, dgamma, dbeta, dres, gb, bscale, bp, bseed): the
+    LayerNorm backward of c = dln follows (lasr_gemm_ln_bwd), its dgamma / dbeta partials
+    deferred or reduced like layernorm_bwd's.  qbias=(dqu, dqv, B, T, H, dk, dqkv, du, dv):
+    qbias_bwd's work runs beside this GEMM's split-K reduction (lasr_gemm_qbias_bwd)."""
     M, K = a.shape[-2], a.shape[-1]
     K2, Nn = b.shape[-2], b.shape[-1]
     assert K == K2 and c.shape[-2] == M and c.shape[-1] == Nn, (a.shape, b.shape, c.shape)
@@ -297,6 +307,45 @@ def gemm(
             if rowsum is not None and fl.value & 2:  # LASR_PLAN_ROWSUM_FUSED: partials follow C's
                 _defer(part[sp * M * Nn:], sp, M, rowsum)
             return c
+    if ln_fwd is not None:
+        g_, b_, eps, y, mean, rstd = ln_fwd
+        assert c.dtype == torch.float32 and c.is_contiguous() and z1 * z2 == 1 and rowsum is None
+        N.call("lasr_gemm_ln_fwd", C.byref(args), ptr(g_), ptr(b_), float(eps), ptr(y), dt(y), ptr(mean), ptr(rstd),
+               stream())
+        return c
+    if qbias is not None:
+        dqu, dqv, B_, T_, H_, dk_, dqkv, du, dv = qbias
+        assert c.dtype == dqu.dtype == dqv.dtype == dqkv.dtype
+        D_ = H_ * dk_
+        nchunk = (B_ * T_ + 63) // 64  # QB_ROWS (qbias.h)
+        part = torch.empty(nchunk * 2 * D_, dtype=torch.float32, device=c.device)
+        N.call("lasr_gemm_qbias_bwd", C.byref(args), ptr(dqu), ptr(dqv), dt(dqu), B_, T_, H_, dk_, ptr(dqkv),
+               dqkv.stride(0), ptr(part), part.numel(), stream())
+        if _DEFER.depth:
+            _defer(part, nchunk, 2 * D_, du, dv, split=D_)
+        else:
+            arr = (N.ReduceSeg * 1)()
+            arr[0] = N.ReduceSeg(ptr(part), 2 * D_, nchunk, 1, ptr(du), ptr(dv), D_)
+            N.call("lasr_reduce_multi", arr, 1, stream())
+        return c
+    if ln_bwd is not None:
+        q = ln_bwd
+        assert c.is_contiguous() and z1 * z2 == 1 and rowsum is None
+        nblk = (M + 15) // 16  # lasr_layernorm_bwd's 16-row blocks
+        defer = _DEFER.depth and q.dgamma is not None and q.dbeta is not None
+        # (its own buffer: the GEMM's split-K partials live in WS)
+        part = torch.empty(nblk * 2 * Nn, dtype=torch.float32, device=c.device)
+        N.call("lasr_gemm_ln_bwd", C.byref(args), ptr(q.x), dt(q.x), ptr(q.g), ptr(q.mean), ptr(q.rstd),
+               ptr(q.dres), dt(q.dres) if q.dres is not None else 0, ptr(q.dx), dt(q.dx), ptr(part), part.numel(),
+               ptr(q.gb), dt(q.gb) if q.gb is not None else 0, float(q.bscale), float(q.bp), int(q.bseed), stream())
+        if defer:
+            _defer(part, nblk, 2 * Nn, q.dgamma, q.dbeta, split=Nn)
+        elif q.dgamma is not None or q.dbeta is not None:
+            assert q.dgamma is not None and q.dbeta is not None
+            arr = (N.ReduceSeg * 1)()
+            arr[0] = N.ReduceSeg(ptr(part), 2 * Nn, nblk, 1, ptr(q.dgamma), ptr(q.dbeta), Nn)
+            N.call("lasr_reduce_multi", arr, 1, stream())
+        return c
     N.call("lasr_gemm", C.byref(args), stream())
     return c
 

@@ -66,6 +66,13 @@ def ln_forward(x, g, b, adt, y2=False, p2=0.0, seed2=0):
 ROW_LN = os.environ.get("LASR_ROW_LN", "1") != "0"
 # the decoder's norms after / before its attention projections on the row kernel (A/B switch)
 DEC_ROW_LN = os.environ.get("LASR_DEC_ROW_LN", "1") != "0"
+# K >= 1024 GEMMs whose plan splits K (the decoder's FFN on B*(L+1) rows) run the following
+# LayerNorm (forward) / the preceding one's backward in their split-K reduction launch
+# (gemm_ln.hip); False: separate launches (tests/test_fusions_gpu.py pins the two bit for bit)
+SPLITK_LN = True
+# the encoder attention's positional-bias gradient (qbias_bwd) in the positional-projection
+# gradient GEMM's split-K reduction launch (gemm_ln.hip lasr_gemm_qbias_bwd); False: its own launch
+QBIAS_IN_REDUCE = True
 
 
 class PostLN(SimpleNamespace):
@@ -84,6 +91,14 @@ def res_proj(x, W, bias, res, res_scale, p_res, s_res, post=None):
     if post is not None:
         post.y1 = None
     if post is None or not ROW_LN or not K.row_ln_ok(x, W, D):
+        if post is not None and SPLITK_LN and post.nxt is None and x.dtype == torch.bfloat16 and W.shape[1] >= 1024:
+            # the norm in the GEMM's split-K reduction launch (lasr_gemm_ln_fwd; two launches
+            # when the plan does not split K)
+            post.y1 = _e((M, D), F32 if post.f32 else x.dtype, dev)
+            post.m1, post.r1 = _e(M, F32, dev), _e(M, F32, dev)
+            K.linear(x, W, out, bias=bias, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res,
+                     ln_fwd=(post.g, post.b, LN_EPS, post.y1, post.m1, post.r1))
+            return out
         K.linear(x, W, out, bias=bias, res=res, res_scale=res_scale, drop_p=p_res, drop_seed=s_res)
         return out
     post.y1 = _e((M, D), F32 if post.f32 else x.dtype, dev)
@@ -114,6 +129,11 @@ def dx_ln(dy, W, lnb):
                            dres=lnb.dres, gb=lnb.gb, bscale=lnb.bscale, bp=lnb.bp, bseed=lnb.bseed)
         return None
     dln = _e((M, D), dy.dtype, dy.device)
+    if lnb is not None and SPLITK_LN and dy.dtype == torch.bfloat16 and W.shape[0] >= 1024:
+        # the norm backward in the GEMM's split-K reduction launch (lasr_gemm_ln_bwd; two
+        # launches when the plan does not split K)
+        K.gemm(dy, W, dln, ln_bwd=lnb)
+        return None
     K.gemm(dy, W, dln)
     if lnb is None:
         return dln
@@ -274,9 +294,12 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att, lnb=None):
         dqv = _e((M, d), adt, dev)
         K.gemm(dBDh.permute(1, 0, 2, 3)[..., :T], p4, _heads(dqv, B, T, H, dk), alpha=scale)
         dp = _e((T, d), adt, dev)
+        # (qbias_bwd's blocks ride in this GEMM's split-K reduction launch: QBIAS_IN_REDUCE)
+        qb = (dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
         K.gemm(dBDh.view(H, B * T, ldS)[..., :T].transpose(-1, -2), sv.qv.view(M, H, dk).permute(1, 0, 2),
-               dp.view(T, H, dk).permute(1, 0, 2), alpha=scale, split_k=0)
-        K.qbias_bwd(dqu, dqv, B, T, H, dk, dqkv, g.u, g.v)
+               dp.view(T, H, dk).permute(1, 0, 2), alpha=scale, split_k=0, qbias=qb if QBIAS_IN_REDUCE else None)
+        if not QBIAS_IN_REDUCE:
+            K.qbias_bwd(*qb)
         K.gemm(dp.t(), pos, g.Wpos, beta=1.0, split_k=0, group=True)
         K.gemm(dqkv.t(), ln, g.Wqkv, beta=1.0, split_k=0, rowsum=g.bqkv, group=True)
         return dx_ln(dqkv, w.Wqkv, lnb)
@@ -315,6 +338,9 @@ def relmha_backward(gb, ln, pos, sv, w, g, env, p_att, s_att, lnb=None):
 # padding mask) and the source attention over the encoder output (key padding).
 # LASR_FUSED_DEC_ATTN=0 keeps the materialised path.
 FUSED_DEC_ATTN = os.environ.get("LASR_FUSED_DEC_ATTN", "1") != "0"
+# the decoder FFN branch gradients written by the LayerNorm backward that produces each layer's
+# output gradient (False: a branch_grad launch per layer; the test pins the two bit for bit)
+DEC_GB_IN_LN = True
 
 
 def _fused_dec(adt, dk, p_att):
@@ -870,9 +896,13 @@ def decoder_layers_fwd(dec, wd, y, h, B, L1, T, masks, p, adt, seed_shift=0):
         l_, _, m_, r_ = ln_forward(x, ln.g, ln.b, adt)
         return l_, m_, r_
 
+    nxt = None  # (l1, m1, r1) of the next layer, formed in this layer's fc2 launch
     for i, lw in enumerate(wd.layers):
         s = dec.dec_layers[i].seed + seed_shift
-        l1, _, m1, r1 = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
+        if nxt is None:
+            l1, _, m1, r1 = ln_forward(y, lw.ln1.g, lw.ln1.b, adt)
+        else:
+            l1, m1, r1 = nxt
         p2 = post_ln(lw.ln2)
         y1, sa = mha_forward(l1, None, lw.sa, B, L1, L1, wd.H, smask, smsb, smsq, y, pat, _seed(s, 1), pd,
                              _seed(s, 2), post=p2)
@@ -881,12 +911,19 @@ def decoder_layers_fwd(dec, wd, y, h, B, L1, T, masks, p, adt, seed_shift=0):
         y2, ca = mha_forward(l2, h, lw.ca, B, L1, T, wd.H, mmask, T, 0, y1, pca, _seed(s, 3), pd, _seed(s, 4),
                              kv=kvm[:, 2 * wd.d * i: 2 * wd.d * (i + 1)], post=p3)
         l3, m3, r3 = ln_after(y2, p3, lw.ln3)
+        # the next norm (the next layer's first, or after_norm) after the FFN's residual add
+        ln_n = wd.layers[i + 1].ln1 if i + 1 < len(wd.layers) else wd.ln_f
+        p4 = PostLN(g=ln_n.g, b=ln_n.b, f32=False, nxt=None)
         y3, z, hh = ffn_forward(l3, lw.ff.W1, lw.ff.b1, lw.ff.W2, lw.ff.b2, ACT_RELU, pff, _seed(s, 5), y2, 1.0, pd,
-                                _seed(s, 6))
+                                _seed(s, 6), post=p4)
+        nxt = ln_after(y3, p4, ln_n)
         layers_sv.append(SimpleNamespace(y=(y, y1, y2), ln=(l1, l2, l3), st=((m1, r1), (m2, r2), (m3, r3)), sa=sa,
                                          ca=ca, z=z, hh=hh))
         y = y3
-    yf, _, mf, rf = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
+    if nxt is None:
+        yf, _, mf, rf = ln_forward(y, wd.ln_f.g, wd.ln_f.b, adt)
+    else:
+        yf, mf, rf = nxt
     h_attn = K.padded_rows(R, wd.Wout.shape[0], adt, y.device)
     K.linear(yf, wd.Wout, h_attn, bias=wd.bout)
     return h_attn, SimpleNamespace(layers=layers_sv, yL=y, yf=yf, mf=mf, rf=rf, p=p, masks=masks,
@@ -904,23 +941,37 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
     dyf = _e((R, d), adt, dev)
     K.gemm(g_attn, wd.Wout, dyf)
     dy = _e((R, d), F32, dev)
-    K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b)
-    dkvm = _e((B * T, len(wd.layers) * 2 * d), adt, dev)  # the batched memory K/V's gradient
-    for i in range(len(wd.layers) - 1, -1, -1):
+    nl = len(wd.layers)
+    # the FFN branch gradient of each layer (its residual dropout's backward, seed 6 of the
+    # layer) comes out of the LayerNorm backward that produces the layer's output gradient:
+    # the final norm's for the top layer, the next layer's first norm's below (no separate
+    # branch_grad launch; same product per element)
+    ffn_seed = lambda i: _seed(dec.dec_layers[i].seed + sv.seed_shift, 6)  # noqa: E731
+    fused_gb = DEC_GB_IN_LN
+    gb_next = _e((R, d), adt, dev) if fused_gb else None
+    K.layernorm_bwd(sv.yL, dyf, wd.ln_f.g, sv.mf, sv.rf, dy, gd.ln_f.g, gd.ln_f.b, gb=gb_next, bscale=1.0, bp=pd,
+                    bseed=ffn_seed(nl - 1))
+    dkvm = _e((B * T, nl * 2 * d), adt, dev)  # the batched memory K/V's gradient
+    for i in range(nl - 1, -1, -1):
         lw, lg, ls = wd.layers[i], gd.layers[i], sv.layers[i]
         s = dec.dec_layers[i].seed + sv.seed_shift
         y0, y1, y2 = ls.y
         l1, l2, l3 = ls.ln
         (m1, r1), (m2, r2), (m3, r3) = ls.st
         # fresh gb per branch: the grouped dW GEMMs read it at the end of the node
-        gb = _e((R, d), adt, dev)
-        K.branch_grad(dy, gb, 1.0, pd, _seed(s, 6))
-        dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1, lg.ff.W2, lg.ff.b2,
-                           ACT_RELU, pff, _seed(s, 5))
+        gb = gb_next
+        if not fused_gb:  # the separate branch-gradient launch (kept for the bit-identity test)
+            gb = _e((R, d), adt, dev)
+            K.branch_grad(dy, gb, 1.0, pd, ffn_seed(i))
         dy2 = _e((R, d), F32, dev)
-        gb = _e((R, d), adt, dev)
-        K.layernorm_bwd(y2, dln, lw.ln3.g, m3, r3, dy2, lg.ln3.g, lg.ln3.b, dres=dy, gb=gb, bscale=1.0, bp=pd,
-                        bseed=_seed(s, 4))
+        gb3 = _e((R, d), adt, dev)
+        lnb3 = LnBwd(x=y2, g=lw.ln3.g, mean=m3, rstd=r3, dx=dy2, dgamma=lg.ln3.g, dbeta=lg.ln3.b, dres=dy, gb=gb3,
+                     bscale=1.0, bp=pd, bseed=_seed(s, 4))
+        dln = ffn_backward(gb, l3, ls.z, ls.hh, lw.ff.W1, lw.ff.W2, lg.ff.W1, lg.ff.b1, lg.ff.W2, lg.ff.b2,
+                           ACT_RELU, pff, _seed(s, 5), lnb=lnb3)
+        if dln is not None:
+            ln_bwd_of(dln, lnb3)
+        gb = gb3
         # the norms in front of the two attentions run in their input-gradient GEMMs (dx_ln)
         dy1 = _e((R, d), F32, dev)
         gb1 = _e((R, d), adt, dev)
@@ -931,8 +982,10 @@ def decoder_layers_bwd(g_attn, sv, dec, wd, gd, h, B, L1, T, dh, adt):
         if dln is not None:
             ln_bwd_of(dln, lnb2)
         dy0 = _e((R, d), F32, dev)
+        gb_next = _e((R, d), adt, dev) if i > 0 and fused_gb else None
         lnb1 = LnBwd(x=y0, g=lw.ln1.g, mean=m1, rstd=r1, dx=dy0, dgamma=lg.ln1.g, dbeta=lg.ln1.b, dres=dy1,
-                     gb=None, bscale=1.0, bp=0.0, bseed=0)
+                     gb=gb_next, bscale=1.0, bp=pd if gb_next is not None else 0.0,
+                     bseed=ffn_seed(i - 1) if gb_next is not None else 0)
         dln = mha_backward(gb1, l1, None, ls.sa, lw.sa, lg.sa, B, L1, L1, wd.H, smask, smsb, smsq, pat,
                            _seed(s, 1), None, lnb=lnb1 if DEC_ROW_LN else None)
         if dln is not None:

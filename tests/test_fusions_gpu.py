@@ -1,0 +1,87 @@
+"""Round-6 launch fusions, each pinned bit for bit against the path it replaces: one bf16
+training step (dropout 0.1, so the fused dropout-backward draws are exercised) with the fusion
+on and off must give torch.equal losses, flat gradients and BN buffers.  The switches are
+module attributes (not environment variables): the product path is the fused one."""
+
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import u2_oracle as O  # noqa: E402
+
+CFG = O.default_cfg(enc_layers=2, dec_layers=3)  # small-model widths (d 256, ff 2048, V 4233)
+
+
+def _step(cfg, B=3, T=300, L=9, dropout=0.1, seed=4):
+    from liteasr_amd.criterions.hybrid_ctc_attn import HybridCTCLoss, HybridCTCLossConfig
+    from liteasr_amd.models.u2 import U2, U2Config
+    from liteasr_amd.utils.cfg import resolve_self
+
+    c = U2Config(input_dim=cfg["input_dim"], vocab_size=cfg["vocab_size"], enc_dim=cfg["enc_dim"],
+                 enc_ff_dim=cfg["enc_ff"], enc_attn_heads=cfg["enc_heads"], enc_layers=cfg["enc_layers"],
+                 dec_dim=cfg["dec_dim"], dec_ff_dim=cfg["dec_ff"], dec_attn_heads=cfg["dec_heads"],
+                 dec_layers=cfg["dec_layers"], dropout_rate=dropout, compute_dtype="bf16")
+    resolve_self(c)
+    c.enc_attn_dropout_rate = c.dec_self_attn_dropout_rate = c.dec_src_attn_dropout_rate = 0.0
+    m = U2(c)
+    m.load_state_dict({**O.init_params(cfg, seed=seed), **O.init_buffers(cfg)}, strict=False)
+    m = m.cuda().train()
+    crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=cfg["vocab_size"], smoothing=0.1, ctc_weight=0.3))
+    xs, xl, ys, yl = [t.cuda() for t in O.synthetic_batch(B, T, L, cfg["vocab_size"], seed=seed)]
+    loss = crit(m, xs, xl, ys, yl)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.item(), m.store.grad.clone(), [b.clone() for b in m.bn_flat_buffers()]
+
+
+def _same(a, b):
+    assert a[0] == b[0], (a[0], b[0])
+    assert torch.equal(a[1], b[1]), (a[1] - b[1]).abs().max().item()
+    for x, y in zip(a[2], b[2]):
+        assert torch.equal(x, y)
+
+
+def test_decoder_branch_grad_in_layernorm_bwd(monkeypatch):
+    """The decoder FFN branch gradient (its residual dropout's backward) written by the
+    LayerNorm backward that produces the layer output gradient, vs a branch_grad launch."""
+    from liteasr_amd.nets import functional as FN
+
+    on = _step(CFG)
+    monkeypatch.setattr(FN, "DEC_GB_IN_LN", False)
+    off = _step(CFG)
+    _same(on, off)
+
+
+@pytest.mark.parametrize("B,L,d", [(3, 9, 256), (8, 40, 256), (4, 20, 512)])
+def test_splitk_reduce_with_layernorm(monkeypatch, B, L, d):
+    """The decoder's FFN fc2 split-K reduction with the next LayerNorm (lasr_gemm_ln_fwd) and the
+    fc1 input-gradient reduction with the LayerNorm backward in front of the FFN
+    (lasr_gemm_ln_bwd), vs the separate reduction and norm launches; d 512 = config 4's width."""
+    from liteasr_amd.nets import functional as FN
+
+    cfg = CFG if d == 256 else O.default_cfg(enc_dim=512, enc_heads=8, enc_layers=1, dec_dim=512, dec_heads=8,
+                                             dec_layers=2)
+    on = _step(cfg, B=B, L=L)
+    monkeypatch.setattr(FN, "SPLITK_LN", False)
+    off = _step(cfg, B=B, L=L)
+    _same(on, off)
+
+
+@pytest.mark.parametrize("enc_heads,d", [(4, 256), (16, 512)])
+def test_qbias_bwd_in_positional_gemm_reduction(monkeypatch, enc_heads, d):
+    """The encoder attention's positional-bias gradient blocks in the positional-projection
+    gradient GEMM's split-K reduction launch (lasr_gemm_qbias_bwd), vs two launches."""
+    from liteasr_amd.nets import functional as FN
+
+    cfg = O.default_cfg(enc_dim=d, enc_heads=enc_heads, enc_layers=2, dec_dim=d, dec_heads=enc_heads, dec_layers=1)
+    on = _step(cfg, B=4, T=1000, L=12)
+    monkeypatch.setattr(FN, "QBIAS_IN_REDUCE", False)
+    off = _step(cfg, B=4, T=1000, L=12)
+    _same(on, off)

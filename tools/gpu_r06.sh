@@ -38,6 +38,7 @@ for s in "$@"; do
              grep "^{" "$OUT/envab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median')}))" >> "$OUT/envab.jsonl"; done ;;
     dyn) run timeout -k 10 900 $PYT tests/test_kernels_gpu.py -k "u2_prep or embed_and_prep or prep" \
            tests/test_model_gpu.py -k "dynamic or config4 or graphed or chunk" -s > "$OUT/dyn.log" 2>&1 ;;
+    fus) run timeout -k 10 600 $PYT tests/test_fusions_gpu.py -s > "$OUT/fus.log" 2>&1 ;;
     largedyn) run timeout -k 10 500 python3 bench.py --config large --no-cpu-baseline --no-roofline > "$OUT/bench_large_dyn.json" 2> "$OUT/bench_large_dyn.err" ;;
     switches) run timeout -k 10 900 $PYT tests/test_switches_gpu.py > "$OUT/switches.log" 2>&1 ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
