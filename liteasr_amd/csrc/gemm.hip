@@ -317,13 +317,20 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     LASR_CHECK_ARG(a->in_dtype == LASR_BF16 && a->c_dtype == LASR_F32, "lasr_gemm_dw_group: bf16 in, fp32 partials");
     LASR_CHECK_ARG(a->lda_m == 1 && a->lda_k != 1 && a->ldb_n == 1 && a->ldb_k != 1,
                    "lasr_gemm_dw_group: A M-contiguous and B N-contiguous (dW = dY^T X)");
-    LASR_CHECK_ARG(a->split_k < 0 && a->workspace && (a->batch <= 1) && a->M > 0 && a->N > 0 && a->K > 0,
-                   "lasr_gemm_dw_group: partials-only problems with a workspace");
+    const bool direct = a->split_k == 1;  // full-K tiles writing C itself (beta 0 / 1), no slab
+    LASR_CHECK_ARG((direct || (a->split_k < 0 && a->workspace)) && (a->batch <= 1) && a->M > 0 && a->N > 0 &&
+                       a->K > 0,
+                   "lasr_gemm_dw_group: partials-only problems with a workspace, or direct (split_k 1) ones");
+    LASR_CHECK_ARG(!direct || (a->C && a->ldc >= a->N && (a->beta == 0.f || a->beta == 1.f) && a->alpha == 1.f &&
+                               !a->alpha_dev),
+                   "lasr_gemm_dw_group: a direct problem needs C, ldc >= N, beta 0 or 1, alpha 1");
+    LASR_CHECK_ARG(i == 0 || direct == (g.direct[0] != 0), "lasr_gemm_dw_group: direct and split problems mixed");
     LASR_CHECK_ARG(!a->act && !a->zout && !a->aux && !a->res && a->drop_p <= 0.f && !a->bias,
                    "lasr_gemm_dw_group: no epilogue");
     LASR_CHECK_ARG(gemm_uses_glds(a), "lasr_gemm_dw_group: operands not LDS-DMA eligible");
     int BM, BN, split, ks;
     gemm_plan(a, &BM, &BN, &split, &ks);
+    if (direct) split = 2;  // (plan-shape checks below; the launch uses one K slice)
     // the group kernel runs 64-deep ring stages; a lone 32-deep launch gives the same bits
     // (the sub-tiles keep their images and order: test_gemm_ksub2_bit_identical), so a
     // short-K plan (e.g. the decoder's FFN weights, K = B*(L+1)) groups too
@@ -338,7 +345,7 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
       // the whole group): 0.25 fewer LDS-DMA bytes per MFMA than the 4-wave 128 x 128 tile;
       // 11.84 -> 11.63-11.70 ms/step on two boxes (profiles/r03/dw_group_ab.json; 256 x 256
       // with twice the slices, and a 2-stage ring, measured no better).
-      if (a->M >= 256 && a->N >= 256) {
+      if (a->M >= 256 && a->N >= 256 && !direct) {  // (direct groups keep 128 x 128: twice the tiles)
         BM = 256;
         BN = 128;
       }
@@ -346,14 +353,17 @@ extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* strea
     LASR_CHECK_ARG(i == 0 || (BM == BM0 && BN == BN0), "lasr_gemm_dw_group: problems plan different tiles");
     BM0 = BM;
     BN0 = BN;
+    if (direct) split = 1;
     g.M[i] = a->M; g.N[i] = a->N; g.K[i] = a->K;
     g.split[i] = split;
-    g.kchunk[i] = (int)(cdiv(cdiv(a->K, split), 32) * 32);
-    g.v4[i] = a->N % 4 == 0 && aligned16(a->workspace);
+    g.kchunk[i] = direct ? a->K : (int)(cdiv(cdiv(a->K, split), 32) * 32);
+    g.direct[i] = direct;
+    g.C[i] = (float*)a->C; g.ldc[i] = a->ldc; g.beta[i] = a->beta; g.rowsum[i] = a->rowsum;
+    g.v4[i] = a->N % 4 == 0 && aligned16(direct ? a->C : a->workspace);
     g.A[i] = a->A; g.lda[i] = a->lda_k;
     g.B[i] = a->B; g.ldb[i] = a->ldb_k;
     g.ws[i] = (float*)a->workspace;
-    g.rs_ws[i] = a->rowsum ? (float*)a->workspace + (int64_t)split * a->M * a->N : nullptr;
+    g.rs_ws[i] = a->rowsum && !direct ? (float*)a->workspace + (int64_t)split * a->M * a->N : nullptr;
     g.start[i] = blocks;
     const int64_t nb = cdiv(a->M, BM) * cdiv(a->N, BN) * (int64_t)split;
     LASR_CHECK_ARG(blocks + nb + 8 < (1ll << 31), "lasr_gemm_dw_group: too many blocks");

@@ -1134,6 +1134,13 @@ struct DwGroupP {
   float* ws[LASR_DW_GROUP_MAX];
   float* rs_ws[LASR_DW_GROUP_MAX];  // null: no fused bias rowsum
   int slice_xcd;                    // K slices tied to XCDs (gemm_dw_group_kernel)
+  // direct problems (split 1): full-K tiles that write the weight gradient itself (C = beta C +
+  // dY^T X, fp32) and add their bias rowsum into rowsum -- no partial slab, no reduction
+  int direct[LASR_DW_GROUP_MAX];
+  float* C[LASR_DW_GROUP_MAX];
+  int64_t ldc[LASR_DW_GROUP_MAX];
+  float beta[LASR_DW_GROUP_MAX];
+  float* rowsum[LASR_DW_GROUP_MAX];
 };
 
 template <int BM, int BN, int S, int MINB, int NW = 4>
@@ -1153,6 +1160,12 @@ __global__ __launch_bounds__(NW * 64, MINB * NW / 4) void gemm_dw_group_kernel(D
   p.rowsum = g.rs_ws[i];  // only tested for null when split_k > 1: the partials go to rs_ws
   p.rs_ws = g.rs_ws[i];
   p.alpha = 1.f;
+  if (g.direct[i]) {  // the lone split-1 launch's epilogue: beta C + acc, rowsum += (n-tile 0)
+    p.C = g.C[i]; p.ldc = g.ldc[i]; p.beta = g.beta[i];
+    p.rowsum = g.rowsum[i]; p.rs_ws = nullptr; p.ws = nullptr;
+    p.c_vec = ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0;
+    p.epi_mode = p.c_vec && p.beta == 0.f ? 0 : 2;
+  }
   // Block -> (tile, K slice).  The hardware deals blocks to the 8 XCDs round-robin (block % 8;
   // problem ranges start at multiples of 8).  When the split divides 8 and the tiles divide
   // evenly, K slice s lives on XCDs [s * 8/split, (s+1) * 8/split) only, each of them taking

@@ -107,6 +107,13 @@ _GROUP_TILES = {(64, 64): (64, 64), (64, 128): (128, 128), (128, 64): (128, 128)
 # a lone launch (fewer fp32 partial slabs to write and reduce); 128 x 128 groups keep half
 # (the other divisors measured slower)
 DW_GROUP_SPLIT_DIV = {(64, 64): 4, (128, 128): 2}
+# Direct grouped weight gradients: FFN-sized problems with >= this many full-K 128 x 128 tiles
+# (the d 512 FFN weights: 64 each, a group of four = 256 tiles) skip the K split and write the
+# gradient itself (beta = 1), no fp32 partial slab to write and reduce.  Measured at config 4
+# (VERDICT r05 item 3): 20.13 -> 20.74 ms per step, the full-K 128 x 128 tiles are L2-feed bound
+# where the 256 x 128 split-2 tiles are not (profiles/r06/step_ab_dw_direct_large_rejected.jsonl,
+# DESIGN §4); 0 = off.  tests/test_kernels_gpu.py::test_gemm_dw_group_direct pins the path.
+DW_DIRECT_MIN_TILES = 0
 
 
 # GEMMs whose 64 x 64 grid cannot fill half the chip and whose K is long are split over K
@@ -282,6 +289,13 @@ def gemm(
         sp = sp.value
         grouped = (group and DW_GROUP and (tm.value, tn.value) in _GROUP_TILES
                    and (fl.value & 1) and a_m == 1 and b_n == 1 and a.dtype == torch.bfloat16)
+        if (grouped and DW_DIRECT_MIN_TILES > 0 and _GROUP_TILES[(tm.value, tn.value)] == (128, 128)
+                and ((M + 127) // 128) * ((Nn + 127) // 128) >= DW_DIRECT_MIN_TILES):
+            # full-K direct problem of the group: C itself (beta 0 / 1), its bias rowsum direct
+            args.split_k = 1
+            args.workspace, args.workspace_bytes = None, 0
+            _DEFER.gemms.append(((128, 128, "direct"), N.GemmArgs.from_buffer_copy(args), (a, b, c, rowsum)))
+            return c
         div = _group_div(_GROUP_TILES[(tm.value, tn.value)]) if grouped else 1
         if grouped and (div > 1 or sp < 2):
             # short K too (the positional-projection weight, K = T'): two slices join the group

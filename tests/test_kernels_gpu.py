@@ -304,6 +304,44 @@ def test_gemm_dw_group_bit_identical(R, monkeypatch):
             close(db, db0.double() + dy.double().sum(0), 1e-5, "grouped db")
 
 
+@pytest.mark.parametrize("R", [7968, 1312])
+def test_gemm_dw_group_direct(R, monkeypatch):
+    """Direct problems of the grouped weight-gradient launch (the d 512 FFN weights: >=
+    DW_DIRECT_MIN_TILES 128 x 128 tiles each): full-K tiles write the gradient itself (beta 1 or 0)
+    and add the bias rowsum, no partial slab.  dW is bit-identical to one lasr_gemm launch per
+    problem with no K split (a tile's shape never changes an output's k order); the rowsum agrees
+    to fp32 rounding (k rows grouped per thread by tile height) and both match float64."""
+    kn = K()
+    monkeypatch.setattr(kn, "DW_DIRECT_MIN_TILES", 64)  # (off in the product: slower, DESIGN §4)
+    g = torch.Generator().manual_seed(R + 1)
+    probs = [(2048, 512, True, 1.0), (512, 2048, True, 1.0), (2048, 512, False, 0.0), (512, 2048, True, 0.0)]
+    ins = [(torch.randn(R, M, generator=g).to(DEV, torch.bfloat16), torch.randn(R, N, generator=g).to(DEV, torch.bfloat16),
+            torch.randn(M, N, generator=g).to(DEV), torch.randn(M, generator=g).to(DEV) if rs else None, beta)
+           for M, N, rs, beta in probs]
+    outs = {}
+    for grouped in (False, True):
+        res = []
+        with kn.deferred_reductions():
+            for dy, x, dw0, db0, beta in ins:
+                dw = dw0.clone()
+                db = db0.clone() if db0 is not None else None
+                kn.gemm(dy.t(), x, dw, beta=beta, split_k=0 if grouped else 1, rowsum=db, group=grouped)
+                res.append((dw, db))
+            if grouped:
+                keys = {k for k, _, _ in kn._DEFER.gemms}
+                assert keys == {(128, 128, "direct")}, keys
+            assert not kn._DEFER.segs  # no partial slab to reduce
+        torch.cuda.synchronize()
+        outs[grouped] = res
+    for (a, ab), (b, bb), (dy, x, dw0, db0, beta) in zip(outs[False], outs[True], ins):
+        assert torch.equal(a, b)
+        ref = beta * dw0.double() + dy.double().t() @ x.double()
+        close(b, ref, 1e-2, "direct dW")
+        if ab is not None:
+            assert torch.allclose(ab, bb, rtol=1e-6, atol=1e-4)
+            close(bb, db0.double() + dy.double().sum(0), 1e-5, "direct db")
+
+
 @pytest.mark.parametrize("B,H,Tq,Tk,dk,qmask,splits", [(8, 4, 151, 999, 64, False, (2, 3, 4, 5)),
                                                       (3, 2, 70, 300, 32, True, (2, 5)),
                                                       (2, 4, 41, 249, 64, False, (4,))])

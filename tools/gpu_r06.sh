@@ -39,6 +39,13 @@ for s in "$@"; do
     dyn) run timeout -k 10 900 $PYT tests/test_kernels_gpu.py -k "u2_prep or embed_and_prep or prep" \
            tests/test_model_gpu.py -k "dynamic or config4 or graphed or chunk" -s > "$OUT/dyn.log" 2>&1 ;;
     fus) run timeout -k 10 600 $PYT tests/test_fusions_gpu.py -s > "$OUT/fus.log" 2>&1 ;;
+    fc1sweep) run timeout -k 10 300 python3 tools/fc1_tile_sweep.py > "$OUT/fc1_sweep_small.jsonl" 2> "$OUT/fc1_sweep.err"
+           run timeout -k 10 300 python3 tools/fc1_tile_sweep.py 7968 2048 512 > "$OUT/fc1_sweep_large.jsonl" 2>> "$OUT/fc1_sweep.err" ;;
+    flagab) # whole step under FLAG_A / FLAG_B module overrides (tools/flag_ab.py), alternating, AB_ARGS
+           for v in A B A B; do f=$FLAG_A; [ $v = B ] && f=$FLAG_B
+             run timeout -k 10 400 python3 tools/flag_ab.py $f -- bench.py --no-cpu-baseline --no-roofline --no-chunk-compare --steps 40 ${AB_ARGS:-} > "$OUT/flagab_$v.json" 2> "$OUT/flagab_$v.err"
+             grep "^{" "$OUT/flagab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'flags': '$f', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'launches': (d.get('graph_nodes_per_step') or {}).get('kernel')}))" >> "$OUT/flagab.jsonl"; done ;;
+    dwdirect) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "dw_group" > "$OUT/dwdirect.log" 2>&1 ;;
     largedyn) run timeout -k 10 500 python3 bench.py --config large --no-cpu-baseline --no-roofline > "$OUT/bench_large_dyn.json" 2> "$OUT/bench_large_dyn.err" ;;
     switches) run timeout -k 10 900 $PYT tests/test_switches_gpu.py > "$OUT/switches.log" 2>&1 ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
