@@ -1182,6 +1182,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
       }
     }
     const uint32_t mrow = sb + Gm::M0 * 16u + ko.mk;
+    uint32_t tb[DK / 16];  // the transposed fragments' per-lane bases in this stage
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) tb[t] = sb + ko.tr[t];
 #pragma unroll
     for (int rs = 0; rs < 2; ++rs) {  // query tile pairs (2rs, 2rs + 1)
       f32x4 p2[2], ds2[2];
@@ -1191,25 +1194,22 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
         // every LDS read of the tile up front: S = Qu . K^T and dP = dO . V^T (query rows as the A
         // operand), the rows' statistics and mask bytes, then the window products' fragments;
         // addresses are the hoisted per-lane bases plus immediates (rows +16 keep the swizzle)
-        const uint32_t rofs = (uint32_t)(r * 16 * DK * 2);
+        const uint32_t rofs = (uint32_t)(r * 16 * DK * 2);  // (immediates after unrolling: no address adds)
         v4i aq[KS], ao[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          const uint32_t qa = bq[ks] + rofs;
-          asm volatile("ds_read_b128 %0, %1" : "=v"(aq[ks]) : "v"(qa));
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ao[ks]) : "v"(qa), "i"(Gm::O0 * 16));
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(aq[ks]) : "v"(bq[ks]), "i"(rofs));
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ao[ks]) : "v"(bq[ks]), "i"(Gm::O0 * 16 + rofs));
         }
         v4i smv, slv, sdv;  // m, 1/sum, D of the lane's 4 query rows
-        const uint32_t sa = ssa + 64u * (uint32_t)r;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(smv) : "v"(sa));
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(slv) : "v"(sa), "i"(4 * QBK));
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(sdv) : "v"(sa), "i"(8 * QBK));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(smv) : "v"(ssa), "i"(64 * r));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(slv) : "v"(ssa), "i"(64 * r + 4 * QBK));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(sdv) : "v"(ssa), "i"(64 * r + 8 * QBK));
         uint32_t mb[4] = {0u, 0u, 0u, 0u};
         if constexpr (RM) {
-          const uint32_t ma = mrow + (uint32_t)(16 * r * Gm::KBW);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(mb[e]) : "v"(ma), "i"(e * Gm::KBW));
+            asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(mb[e]) : "v"(mrow), "i"(16 * r * Gm::KBW + e * Gm::KBW));
         }
         // window rows of this (query tile, key tile): m0 = jw - (i0 + 16r + 15) + T - 1 at image
         // row 16w - 16r + 48; G1 uses qv rows i, G2 rows i + 1
@@ -1217,11 +1217,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
         if constexpr (RP) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
-            const uint32_t wa = bw[ks] - (uint32_t)(16 * r * DK * 2);
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(av[ks]) : "v"(bq[ks] + rofs), "i"(Gm::QV0 * 16));
-            asm volatile("ds_read_b128 %0, %1" : "=v"(av1[ks]) : "v"(bq1[ks] + rofs));
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bwf[0][ks]) : "v"(wa), "i"((QBK - 16) * DK * 2));
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bwf[1][ks]) : "v"(wa), "i"(QBK * DK * 2));
+            // (window rows 16w - 16r + 48 (+16): r <= 3 keeps the immediates non-negative)
+            static_assert(QBK - 16 - 16 * 3 >= 0, "window immediates");
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(av[ks]) : "v"(bq[ks]), "i"(Gm::QV0 * 16 + rofs));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(av1[ks]) : "v"(bq1[ks]), "i"(rofs));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bwf[0][ks]) : "v"(bw[ks]), "i"((QBK - 16 - 16 * r) * DK * 2));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bwf[1][ks]) : "v"(bw[ks]), "i"((QBK - 16 * r) * DK * 2));
           }
           lgkm<4 * KS>();  // all but the window fragments
         } else {
@@ -1336,11 +1337,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_bwd_kv_kernel(FlashP a,
       const uint32_t pofs = (uint32_t)(32 * rs * DK * 2);
 #pragma unroll
       for (int t = 0; t < DK / 16; ++t) {
-        const uint32_t ta = sb + ko.tr[t] + pofs;
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(olo[t]) : "v"(ta), "i"(Gm::O0 * 16));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(ohi[t]) : "v"(ta), "i"(Gm::O0 * 16 + 16 * DK * 2));
-        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(qlo[t]) : "v"(ta));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(qhi[t]) : "v"(ta), "i"(16 * DK * 2));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(olo[t]) : "v"(tb[t]), "i"(Gm::O0 * 16 + pofs));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(ohi[t]) : "v"(tb[t]), "i"(Gm::O0 * 16 + pofs + 16 * DK * 2));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(qlo[t]) : "v"(tb[t]), "i"(pofs));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(qhi[t]) : "v"(tb[t]), "i"(pofs + 16 * DK * 2));
       }
       lgkm0();
 #pragma unroll

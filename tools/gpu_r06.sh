@@ -46,6 +46,16 @@ for s in "$@"; do
              run timeout -k 10 400 python3 tools/flag_ab.py $f -- bench.py --no-cpu-baseline --no-roofline --no-chunk-compare --steps 40 ${AB_ARGS:-} > "$OUT/flagab_$v.json" 2> "$OUT/flagab_$v.err"
              grep "^{" "$OUT/flagab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'flags': '$f', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'launches': (d.get('graph_nodes_per_step') or {}).get('kernel')}))" >> "$OUT/flagab.jsonl"; done ;;
     dwdirect) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "dw_group" > "$OUT/dwdirect.log" 2>&1 ;;
+    attnab2) # attention kernels: ab_lib/base.so (the library before the change) vs the tree's: bitwise
+           # outputs (attn_check) and graph-replayed times, alternating
+           run timeout -k 10 300 python3 tools/with_lib.py $R/ab_lib/base.so tools/attn_check.py dump "$OUT/attn_base.pt" > "$OUT/attn_check.log" 2>&1
+           run timeout -k 10 300 python3 tools/attn_check.py dump "$OUT/attn_new.pt" >> "$OUT/attn_check.log" 2>&1
+           run python3 tools/attn_check.py cmp "$OUT/attn_new.pt" "$OUT/attn_base.pt" > "$OUT/attn_check.jsonl" 2>&1
+           rm -f "$OUT/attn_base.pt" "$OUT/attn_new.pt"
+           for v in base new base new; do
+             if [ $v = base ]; then run timeout -k 10 300 python3 tools/with_lib.py $R/ab_lib/base.so tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
+             else run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"; fi
+             sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_ab_$v.tmp" >> "$OUT/attn_ab.jsonl"; rm -f "$OUT/attn_ab_$v.tmp"; done ;;
     largedyn) run timeout -k 10 500 python3 bench.py --config large --no-cpu-baseline --no-roofline > "$OUT/bench_large_dyn.json" 2> "$OUT/bench_large_dyn.err" ;;
     switches) run timeout -k 10 900 $PYT tests/test_switches_gpu.py > "$OUT/switches.log" 2>&1 ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
