@@ -90,7 +90,11 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
     for (int c = 0; c < 4; ++c) {
       const int64_t nb = cdiv(a->M, cfg[c][0]) * cdiv(a->N, cfg[c][1]) * (int64_t)batch;
       BM = cfg[c][0]; BN = cfg[c][1];
-      if (nb >= 512) break;
+      // >= 480: the N = 512 GEMMs of config 4 (M 7968) take 128 x 64 at 504 tiles instead of
+      // 64 x 64 at 1000 (2 rounds): fc2 forward 42.4 -> 32.8 us, fc1 dX 38.4 -> 29.3 us in the
+      // graph-replayed sweep, whole large step 19.91 -> 19.38 ms with small unchanged
+      // (profiles/r06/tile_ab_large_n512.jsonl, step_ab_tile_threshold.jsonl)
+      if (nb >= 480) break;
     }
     // very large outputs with long K (subsampling conv2: M 151k, N 256, K 2304): the
     // 128x256 tile halves the A re-reads (tile sweep: 237 vs 266 us)
