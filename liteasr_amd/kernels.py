@@ -433,14 +433,20 @@ def _al16(t):
 # (whole step with the FFN fc2 + norm on the row kernel: 9.83 -> 9.98 ms,
 # profiles/r05/step_ab_row_ln_k2048.jsonl).
 ROW_LN_MAX_K = 1024
+# widest output the product runs on the row kernel: at d 512 (config 4) a 32-row tile streams the
+# whole 512 x K weight per tile and the GEMM + LayerNorm launches are faster (whole large step
+# 19.25 -> 18.95 ms with the row kernels off, profiles/r06/step_ab_row_ln_large.jsonl); the
+# kernels still take D 512 (tests/test_row_ln_gpu.py)
+ROW_LN_MAX_D = 256
 
 
-def row_ln_ok(a, w, D, max_k=None):
+def row_ln_ok(a, w, D, max_k=None, max_d=None):
     """Whether lasr_linear_res_ln / lasr_linear_dx_ln_bwd take a GEMM with A = a [M, K] and the
     D-wide output: bf16, D in (256, 512), K % 64 == 0, unit column strides, 16-B rows; and
-    (the product policy) K <= max_k (default ROW_LN_MAX_K)."""
+    (the product policy) K <= max_k (default ROW_LN_MAX_K), D <= max_d (ROW_LN_MAX_D)."""
     Kd = a.shape[-1]
-    return (a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and D in (256, 512) and a.dim() == 2
+    return (a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and D in (256, 512)
+            and D <= (ROW_LN_MAX_D if max_d is None else max_d) and a.dim() == 2
             and Kd % 64 == 0 and Kd <= (ROW_LN_MAX_K if max_k is None else max_k) and a.stride(1) == 1
             and a.stride(0) % 8 == 0 and w.is_contiguous() and _al16(a) and _al16(w))
 

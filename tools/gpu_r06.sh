@@ -34,7 +34,7 @@ for s in "$@"; do
              run timeout -k 10 120 python3 tools/with_lib.py $lib tools/conv2_bench.py ${CONV2_SHAPE:-} | sed "s/^{/{\"v\": \"$v\", /" >> "$OUT/conv2_ab.jsonl" || exit 1; done; done ;;
     envab) # whole step, one tree, two environments alternating (ENV_A / ENV_B: "VAR=val ...")
            for v in A B A B; do e=$ENV_A; [ $v = B ] && e=$ENV_B
-             env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 ${AB_ARGS:-} > "$OUT/envab_$v.json" 2> "$OUT/envab_$v.err" || exit 1
+             env $e timeout -k 10 400 python3 bench.py --no-cpu-baseline --no-roofline --no-chunk-compare --steps 40 ${AB_ARGS:-} > "$OUT/envab_$v.json" 2> "$OUT/envab_$v.err" || exit 1
              grep "^{" "$OUT/envab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median')}))" >> "$OUT/envab.jsonl"; done ;;
     dyn) run timeout -k 10 900 $PYT tests/test_kernels_gpu.py -k "u2_prep or embed_and_prep or prep" \
            tests/test_model_gpu.py -k "dynamic or config4 or graphed or chunk" -s > "$OUT/dyn.log" 2>&1 ;;
