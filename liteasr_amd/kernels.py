@@ -119,6 +119,7 @@ DW_DIRECT_MIN_TILES = 0
 # GEMMs whose 64 x 64 grid cannot fill half the chip and whose K is long are split over K
 # (lasr_gemm autosplit; the split-K reduction applies the epilogue).
 SMALL_GRID_SPLIT = True
+SMALL_GRID_TILES = 128  # (64 x 64 tiles below which a K >= 1024 GEMM is split)
 
 
 def _group_div(key):
@@ -261,7 +262,7 @@ def gemm(
         args.res, args.res_dtype, args.ldres, args.res_scale = ptr(res), dt(res), res.stride(0), res_scale
     auto_split = (split_k == 1 and SMALL_GRID_SPLIT and rowsum is None and zout is None and not group
                   and a.dtype == torch.bfloat16 and z1 * z2 == 1 and K >= 1024
-                  and ((M + 63) // 64) * ((Nn + 63) // 64) < 128)
+                  and ((M + 63) // 64) * ((Nn + 63) // 64) < SMALL_GRID_TILES)
     if auto_split:  # small grid, long K (the decoder's B*(L+1)-row GEMMs): split K, reduce with the epilogue
         split_k = 0
     args.split_k = split_k

@@ -48,12 +48,12 @@ for s in "$@"; do
     dwdirect) run timeout -k 10 600 $PYT tests/test_kernels_gpu.py -k "dw_group" > "$OUT/dwdirect.log" 2>&1 ;;
     attnab2) # attention kernels: ab_lib/base.so (the library before the change) vs the tree's: bitwise
            # outputs (attn_check) and graph-replayed times, alternating
-           run timeout -k 10 300 python3 tools/with_lib.py $R/ab_lib/base.so tools/attn_check.py dump "$OUT/attn_base.pt" > "$OUT/attn_check.log" 2>&1
+           run timeout -k 10 300 python3 tools/with_lib.py $R/ab_lib/${VARIANT:-base}.so tools/attn_check.py dump "$OUT/attn_base.pt" > "$OUT/attn_check.log" 2>&1
            run timeout -k 10 300 python3 tools/attn_check.py dump "$OUT/attn_new.pt" >> "$OUT/attn_check.log" 2>&1
            run python3 tools/attn_check.py cmp "$OUT/attn_new.pt" "$OUT/attn_base.pt" > "$OUT/attn_check.jsonl" 2>&1
            rm -f "$OUT/attn_base.pt" "$OUT/attn_new.pt"
            for v in base new base new; do
-             if [ $v = base ]; then run timeout -k 10 300 python3 tools/with_lib.py $R/ab_lib/base.so tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
+             if [ $v = base ]; then run timeout -k 10 300 python3 tools/with_lib.py $R/ab_lib/${VARIANT:-base}.so tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"
              else run timeout -k 10 300 python3 tools/attn_bench.py > "$OUT/attn_ab_$v.tmp"; fi
              sed "s/^{/{\"lib\": \"$v\", /" "$OUT/attn_ab_$v.tmp" >> "$OUT/attn_ab.jsonl"; rm -f "$OUT/attn_ab_$v.tmp"; done ;;
     libab) # whole step: the tree's library vs ab_lib/$VARIANT.so (tools/with_lib.py), alternating, AB_ARGS
@@ -61,6 +61,12 @@ for s in "$@"; do
              if [ $v = var ]; then run timeout -k 10 400 python3 tools/with_lib.py $R/ab_lib/$VARIANT.so bench.py --no-cpu-baseline --no-roofline --no-chunk-compare --steps 40 ${AB_ARGS:-} > "$OUT/libab_$v.json" 2> "$OUT/libab_$v.err"
              else run timeout -k 10 400 python3 bench.py --no-cpu-baseline --no-roofline --no-chunk-compare --steps 40 ${AB_ARGS:-} > "$OUT/libab_$v.json" 2> "$OUT/libab_$v.err"; fi
              grep "^{" "$OUT/libab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'variant': '${VARIANT:-}', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'launches': (d.get('graph_nodes_per_step') or {}).get('kernel')}))" >> "$OUT/libab.jsonl"; done ;;
+    flaglist) # whole step under each entry of FLAG_LIST ("mod.attr=v mod.attr=v;...;..."; an empty entry
+           # = the tree as is) and ENV_LIST alike, two passes, AB_ARGS
+           IFS=';' read -ra FL <<< "${FLAG_LIST:-}"
+           for rep in 1 2; do for i in "${!FL[@]}"; do f=${FL[$i]}
+             run timeout -k 10 400 python3 tools/flag_ab.py $f -- bench.py --no-cpu-baseline --no-roofline --no-chunk-compare --steps 40 ${AB_ARGS:-} > "$OUT/flaglist_$i.json" 2> "$OUT/flaglist_$i.err"
+             grep "^{" "$OUT/flaglist_$i.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'flags': '$f', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median'), 'launches': (d.get('graph_nodes_per_step') or {}).get('kernel')}))" >> "$OUT/flaglist.jsonl"; done; done ;;
     largedyn) run timeout -k 10 500 python3 bench.py --config large --no-cpu-baseline --no-roofline > "$OUT/bench_large_dyn.json" 2> "$OUT/bench_large_dyn.err" ;;
     switches) run timeout -k 10 900 $PYT tests/test_switches_gpu.py > "$OUT/switches.log" 2>&1 ;;
     new5) run timeout -k 10 900 $PYT tests/test_native_reducer_gpu.py "tests/test_nodes_gpu.py::test_decoder_layer_node" \
