@@ -145,7 +145,9 @@ for s in "$@"; do
            db=$(find "$OUT/trace_long" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_long.txt" 2>&1
            python3 "$R/tools/step_summary.py" "$db" 5 --order > "$OUT/step_order_long.txt" 2>&1; rm -f "$db" ;;
     tracelarge) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_large" -o run -- python3 "$R/bench.py" --config large --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace_large.log" 2>&1
-           db=$(find "$OUT/trace_large" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_large.txt" 2>&1; rm -f "$db" ;;
+           db=$(find "$OUT/trace_large" -name "*.db" | head -1); python3 "$R/tools/step_summary.py" "$db" > "$OUT/step_summary_large.txt" 2>&1
+           python3 "$R/tools/step_summary.py" "$db" 5 --grid > "$OUT/step_summary_grid_large.txt" 2>&1
+           python3 "$R/tools/step_summary.py" "$db" 5 --order > "$OUT/step_order_large.txt" 2>&1; rm -f "$db" ;;
     profile) cd /tmp && run timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d "$OUT/prof_markers" -o run -- python3 "$R/bench.py" --profile --no-cpu-baseline --no-roofline --steps 3 --warmup 1 > "$OUT/profile.log" 2>&1 ;;
     pmc) for c in ${PMC_CASES:-family dw hot}; do
            cd /tmp && run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$c" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 20 --roofline-case $c > "$OUT/pmc_fetch_$c.log" 2>&1
