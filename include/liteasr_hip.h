@@ -143,6 +143,9 @@ int lasr_gemm_plan(const lasr_gemm_args* args, int* tile_m, int* tile_n, int* sp
  * launch; the partials are bit-identical to separate lasr_gemm calls.  The caller reduces
  * them (lasr_reduce_multi). */
 int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* stream);
+/* Block order of later lasr_gemm_dw_group launches: 1 (default) = the problems with the
+ * longest K slice first, 0 = call order; the partials are the same bits either way. */
+int lasr_gemm_dw_group_order(int longest_first);
 
 /* Batched partial reductions (one launch for a backward node's deferred parameter
  * gradients): out[n] (+)= sum_p part[p*N + n], n < split -> out0[n], else out1[n-split].

@@ -15,6 +15,7 @@
 // attention.py:35-37,58,69,145,149, subsampling.py:34,47, conformer_convolution.py:48,55,
 // ctc.py:29, transformer_decoder.py:91 (and their autograd backward GEMMs).
 #include "gemm_kernel.h"
+#include <algorithm>
 
 // ================================ host launcher ==================================
 // The launcher keeps no process-wide state: tile / stage-depth overrides are per-call fields of
@@ -310,14 +311,38 @@ int gemm_run(const lasr_gemm_args* a, void* stream, GemmRowPost* post) {
 // (dW = dY^T X), and all must share the planned tile; the partials (+ fused rowsum partials)
 // land exactly where lasr_gemm would put them, bit for bit.
 int launch_dw_group(const DwGroupP& g, int BM, int BN, int blocks, hipStream_t st);
+static int dw_group_lpt = 1;  // (lasr_gemm_dw_group_order: tests and A/B runs)
+extern "C" int lasr_gemm_dw_group_order(int longest_first) {
+  dw_group_lpt = longest_first != 0;
+  return LASR_OK;
+}
 
 extern "C" int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* stream) {
   LASR_CHECK_ARG(args && n >= 1 && n <= LASR_DW_GROUP_MAX, "lasr_gemm_dw_group: 1..%d problems", LASR_DW_GROUP_MAX);
   DwGroupP g = {};
   g.n = n;
-  int BM0 = 0, BN0 = 0, blocks = 0;
+  // Problems are laid out longest K slice first.  The hardware deals blocks out in index
+  // order and a CU takes the next block when its current one ends, so a group queued in
+  // backward order (a layer's first FFN last) started its longest blocks in the last round
+  // and they set the launch's tail; longest-first ends the launch about when the chip's
+  // total work does.  Block order does not change any block's k range or destination: the
+  // partials are bit-identical.
+  int ord[LASR_DW_GROUP_MAX];
+  int64_t work[LASR_DW_GROUP_MAX];
   for (int i = 0; i < n; ++i) {
     const lasr_gemm_args* a = args + i;
+    int bm, bn, sp, ks;
+    gemm_plan(a, &bm, &bn, &sp, &ks);
+    // the K slice each block runs (the exact split is settled below; the group's tile is
+    // shared, so the slice length orders the blocks by their work)
+    work[i] = a->split_k == 1 || sp <= 1 ? a->K : cdiv(a->K, sp);
+    ord[i] = i;
+  }
+  if (dw_group_lpt)
+    std::stable_sort(ord, ord + n, [&](int x, int y) { return work[x] > work[y]; });
+  int BM0 = 0, BN0 = 0, blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const lasr_gemm_args* a = args + ord[i];
     LASR_CHECK_ARG(a->in_dtype == LASR_BF16 && a->c_dtype == LASR_F32, "lasr_gemm_dw_group: bf16 in, fp32 partials");
     LASR_CHECK_ARG(a->lda_m == 1 && a->lda_k != 1 && a->ldb_n == 1 && a->ldb_k != 1,
                    "lasr_gemm_dw_group: A M-contiguous and B N-contiguous (dW = dY^T X)");

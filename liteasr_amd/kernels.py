@@ -128,8 +128,16 @@ def _group_div(key):
 _GROUP_MAX = 8
 
 
+# grouped dW blocks laid out longest K slice first (lasr_gemm_dw_group_order; same bits)
+DW_GROUP_LPT = True
+_dw_order_set = [None]
+
+
 def _flush_gemm_group():
     q, _DEFER.gemms = _DEFER.gemms, []
+    if _dw_order_set[0] != DW_GROUP_LPT:
+        N.call("lasr_gemm_dw_group_order", int(DW_GROUP_LPT))
+        _dw_order_set[0] = DW_GROUP_LPT
     byt = {}
     for key, args, refs in q:
         byt.setdefault(key, []).append(args)

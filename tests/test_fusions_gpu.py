@@ -85,3 +85,20 @@ def test_qbias_bwd_in_positional_gemm_reduction(monkeypatch, enc_heads, d):
     monkeypatch.setattr(FN, "QBIAS_IN_REDUCE", False)
     off = _step(cfg, B=4, T=1000, L=12)
     _same(on, off)
+
+
+@pytest.mark.parametrize("d,heads", [(256, 4), (512, 16)])
+def test_dw_group_longest_slice_first(monkeypatch, d, heads):
+    """The grouped weight-gradient blocks laid out longest K slice first
+    (lasr_gemm_dw_group_order) vs call order: only the block order changes, so the step is
+    bit-identical; d 512 = config 4's widths, where the encoder group mixes split-2 FFN blocks
+    with split-4 / split-8 projection blocks."""
+    from liteasr_amd import kernels as K
+
+    cfg = O.default_cfg(enc_dim=d, enc_heads=heads, enc_layers=2, dec_dim=d, dec_heads=heads, dec_layers=1)
+    on = _step(cfg, B=8, T=1000, L=12)
+    monkeypatch.setattr(K, "DW_GROUP_LPT", False)
+    off = _step(cfg, B=8, T=1000, L=12)
+    monkeypatch.setattr(K, "DW_GROUP_LPT", True)
+    K._flush_gemm_group()  # (restores the library's setting for the tests after this one)
+    _same(on, off)
