@@ -146,6 +146,9 @@ int lasr_gemm_dw_group(const lasr_gemm_args* args, int n, void* stream);
 /* Block order of later lasr_gemm_dw_group launches: 1 (default) = the problems with the
  * longest K slice first, 0 = call order; the partials are the same bits either way. */
 int lasr_gemm_dw_group_order(int longest_first);
+/* Planner switch for narrow outputs (N <= 64): 1 (default) = 64 x 64 tiles, 0 = the
+ * fill-the-chip tile order of wider outputs; the results are the same bits. */
+int lasr_gemm_narrow_tiles(int on);
 
 /* Batched partial reductions (one launch for a backward node's deferred parameter
  * gradients): out[n] (+)= sum_p part[p*N + n], n < split -> out0[n], else out1[n-split].

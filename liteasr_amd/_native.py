@@ -109,6 +109,7 @@ SIGNATURES = {
     "lasr_gemm_plan": [C.POINTER(GemmArgs), _p, _p, _p, _p],
     "lasr_gemm_dw_group": [C.POINTER(GemmArgs), _i, _p],
     "lasr_gemm_dw_group_order": [_i],
+    "lasr_gemm_narrow_tiles": [_i],
     "lasr_relattn_fwd": [_p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p, _l, _p],
     "lasr_relattn_fwd_qb": [_p, _l, _p, _p, _p, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _l, _f, _p, _p,
                             _l, _p],

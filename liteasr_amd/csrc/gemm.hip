@@ -49,6 +49,12 @@ static void dispatch(const GemmP& p, bool akc, bool bkc, int bf16in, int BM, int
   }
 }
 
+static int narrow_n_tiles = 1;  // (lasr_gemm_narrow_tiles: A/B runs)
+extern "C" int lasr_gemm_narrow_tiles(int on) {
+  narrow_n_tiles = on != 0;
+  return LASR_OK;
+}
+
 // Tile and split-K choice for one call (shared by lasr_gemm and lasr_gemm_plan).  nwo: 8 for
 // an 8-wave instance (none planned today; see below), else 4.
 static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, int* kso = nullptr,
@@ -88,7 +94,12 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
     while (nb * split < target && split * 2 <= 64 && kt / (split * 2) >= 8) split *= 2;
   } else if (bf) {
     const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
-    for (int c = 0; c < 4; ++c) {
+    // narrow outputs (N <= 64; the per-head d_k-wide attention GEMMs, e.g. dqv = dBD p over
+    // B*H batches, K = T'): 64 x 64 -- a 128-wide tile leaves half or more of its columns
+    // idle, and the short k loops want the most row tiles (dqv at config 4, d_k 32: 34.0 ->
+    // 19.2 us; config 2: 8.8 -> 6.1; long: 20.6 -> 15.9; profiles/r06/attn_gemm_tiles.jsonl)
+    const int c0 = a->N <= 64 && narrow_n_tiles ? 3 : 0;
+    for (int c = c0; c < 4; ++c) {
       const int64_t nb = cdiv(a->M, cfg[c][0]) * cdiv(a->N, cfg[c][1]) * (int64_t)batch;
       BM = cfg[c][0]; BN = cfg[c][1];
       // >= 480: the N = 512 GEMMs of config 4 (M 7968) take 128 x 64 at 504 tiles instead of

@@ -170,6 +170,11 @@ def flush_reductions():
 
 
 # ----------------------------------------------------------------------- GEMM ---
+# the planner's 64 x 64 tiles for outputs at most 64 wide (lasr_gemm_narrow_tiles; same bits)
+GEMM_NARROW_TILES = True
+_narrow_set = [None]
+
+
 def _split(t: torch.Tensor):
     """(batch strides (s1, s2), batch shape (z1, z2), row stride, col stride)."""
     nb = t.dim() - 2
@@ -229,6 +234,9 @@ def gemm(
     LayerNorm backward of c = dln follows (lasr_gemm_ln_bwd), its dgamma / dbeta partials
     deferred or reduced like layernorm_bwd's.  qbias=(dqu, dqv, B, T, H, dk, dqkv, du, dv):
     qbias_bwd's work runs beside this GEMM's split-K reduction (lasr_gemm_qbias_bwd)."""
+    if _narrow_set[0] != GEMM_NARROW_TILES:
+        N.call("lasr_gemm_narrow_tiles", int(GEMM_NARROW_TILES))
+        _narrow_set[0] = GEMM_NARROW_TILES
     M, K = a.shape[-2], a.shape[-1]
     K2, Nn = b.shape[-2], b.shape[-1]
     assert K == K2 and c.shape[-2] == M and c.shape[-1] == Nn, (a.shape, b.shape, c.shape)

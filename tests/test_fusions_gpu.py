@@ -102,3 +102,16 @@ def test_dw_group_longest_slice_first(monkeypatch, d, heads):
     monkeypatch.setattr(K, "DW_GROUP_LPT", True)
     K._flush_gemm_group()  # (restores the library's setting for the tests after this one)
     _same(on, off)
+
+
+@pytest.mark.parametrize("d,heads", [(256, 4), (512, 16)])
+def test_narrow_output_tiles(monkeypatch, d, heads):
+    """The planner's 64 x 64 tiles for outputs at most 64 wide (the per-head d_k GEMMs:
+    lasr_gemm_narrow_tiles) vs the wider tiles it used to pick: one step bit-identical."""
+    from liteasr_amd import kernels as K
+
+    cfg = O.default_cfg(enc_dim=d, enc_heads=heads, enc_layers=2, dec_dim=d, dec_heads=heads, dec_layers=1)
+    on = _step(cfg, B=8, T=1000, L=12)
+    monkeypatch.setattr(K, "GEMM_NARROW_TILES", False)
+    off = _step(cfg, B=8, T=1000, L=12)
+    _same(on, off)
