@@ -967,7 +967,7 @@ void launch_bwd_q_t(const FlashP& a, hipStream_t st) {
 void launch_flash_bwd_q(const FlashP& a, int dk, bool rp, bool rm, hipStream_t st) {
   if (rp) {
     if (dk == 64) rm ? launch_bwd_q_t<64, 8, true, true>(a, st) : launch_bwd_q_t<64, 8, true, false>(a, st);
-    else rm ? launch_bwd_q_t<32, 8, true, true>(a, st) : launch_bwd_q_t<32, 8, true, false>(a, st);
+    else rm ? launch_bwd_q_t<32, 4, true, true>(a, st) : launch_bwd_q_t<32, 4, true, false>(a, st);
     return;
   }
   if (dk == 64) rm ? launch_bwd_q_t<64, 4, false, true>(a, st) : launch_bwd_q_t<64, 4, false, false>(a, st);
@@ -1374,7 +1374,7 @@ void launch_flash_bwd_kv(const FlashP& a, int dk, bool rp, bool rm, bf16_t* dko,
                          hipStream_t st) {
   if (rp) {
     if (dk == 64) rm ? launch_bwd_kv_t<64, 8, true, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<64, 8, true, false>(a, dko, dvo, ld, st);
-    else rm ? launch_bwd_kv_t<32, 8, true, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<32, 8, true, false>(a, dko, dvo, ld, st);
+    else rm ? launch_bwd_kv_t<32, 4, true, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<32, 4, true, false>(a, dko, dvo, ld, st);
     return;
   }
   if (dk == 64) rm ? launch_bwd_kv_t<64, 4, false, true>(a, dko, dvo, ld, st) : launch_bwd_kv_t<64, 4, false, false>(a, dko, dvo, ld, st);
