@@ -491,6 +491,18 @@ int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int dydt, int B,
                         int64_t ws_floats, void* stream);
 /* dw [C][K] and db [C] accumulate; with dw = db = NULL the [nparts][C*K + C] partials
  * (lasr_dwconv_nparts) stay in ws for a deferred lasr_reduce_multi. */
+/* lasr_bn_act_bwd followed by lasr_glu_dwconv_bwd (liteasr/nets/conformer_convolution.py:48-57
+ * backward: BatchNorm + activation, then the depthwise conv and the GLU), with dy never stored:
+ * the depthwise backward computes it while loading its window.  y / dh are [B*T, C] as for
+ * lasr_bn_act_bwd (bn_ws: its workspace, which must not overlap ws), z1 / dz1 / w / dw / db as
+ * for lasr_glu_dwconv_bwd; the same outputs, bit for bit, one launch and 8 B per element of HBM
+ * traffic fewer. */
+int lasr_bn_act_glu_dwconv_bwd(const void* y, int ydt, const void* dh, int hdt, int B, int T, int C,
+                               const float* scale, const float* shift, const float* mean, const float* rstd,
+                               const float* gamma, float* dgamma, float* dbeta, float* bn_ws,
+                               int64_t bn_ws_floats, int batch_stats, int act, const void* z1, int dt, int K,
+                               const float* w, void* dz1, float* dw, float* db, float* ws, int64_t ws_floats,
+                               void* stream);
 
 /* ------------------------------------------------------------------------
  * Elementwise / embedding / positional encoding

@@ -167,6 +167,8 @@ SIGNATURES = {
     "lasr_bn_act_fwd": [_p, _i, _l, _i, _p, _p, _p, _i, _i, _p],
     "lasr_bn_act_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _l, _i, _i, _p],
     "lasr_glu_dwconv_bwd": [_p, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _l, _p],
+    "lasr_bn_act_glu_dwconv_bwd": [_p, _i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _l, _i, _i,
+                                   _p, _i, _i, _p, _p, _p, _p, _p, _l, _p],
     "lasr_cast": [_p, _i, _p, _i, _l, _p],
     "lasr_scale_add": [_p, _i, _p, _i, _f, _f, _p, _i, _l, _p],
     "lasr_embed_pe_fwd": [_p, _i, _i, _i, _p, _p, _f, _f, _u, _p, _i, _p],

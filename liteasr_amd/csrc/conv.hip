@@ -476,17 +476,21 @@ struct DyWin {
     u[0] = u[1] = 0.f;
   }
   LASR_DEV float2 pair(const float* v, const float*) const { return make_float2(v[0], v[1]); }
+  LASR_DEV void finish(int) const {}
 };
 
 // Backward of y = dwconv(GLU(z1)) over the block's DW_TT rows x 128 channels: dW / db partials
 // (dy x the GLU window), dg = the transposed conv of dy, dz1 = GLU'(z1) dg.  The two windows
 // (GLU recomputed, dy) come in with 8-channel loads (dw_window); dg is staged through LDS so
 // the z1 re-read and the dz1 stores are 16-B row vectors (8 channels of a and of the gate).
-template <typename T, typename TD>
+// DYW: how the dy window is read -- DyWin (a stored dy) or BnDyWin (dy computed from the
+// BatchNorm + activation backward's inputs as the window is loaded, no stored dy)
+template <typename T, typename TD, typename DYW = DyWin<TD>>
 __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict__ z1,
                                                              const TD* __restrict__ dy, int T_,
                                                              int C, const float* w, T* dz1,
-                                                             float* part, int vec) {
+                                                             float* part, int vec, DYW fdy = DYW{}) {
+  fdy.finish(C);
   __shared__ float sp[DW_G][DW_K + 1][2 * DW_CP];
   const int cp = threadIdx.x % DW_CP, grp = threadIdx.x / DW_CP;
   const int c = (blockIdx.y * DW_CP + cp) * 2;
@@ -497,7 +501,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
   __shared__ float2 wg[DW_WIN][DW_CP], wd[DW_WIN][DW_CP];
   const int tb = t0 - grp * DW_R;
   dw_window<DW_CP>(z1, 2 * (int64_t)C, 0, b, T_, C, tb, vec != 0, wg, GluWin<T>{C});
-  dw_window<DW_CP>(dy, (int64_t)C, 0, b, T_, C, tb, vec != 0, wd, DyWin<TD>{});
+  dw_window<DW_CP>(dy, (int64_t)C, 0, b, T_, C, tb, vec != 0, wd, fdy);
   __syncthreads();
   float2 g[DW_RW], d[DW_RW];
 #pragma unroll
@@ -688,6 +692,60 @@ LASR_DEV float bn_act_grad(float u) {
   else return swish_grad(u);
 }
 
+// The BatchNorm + activation backward of one element (train mode: the batch-mean terms; eval
+// mode: inv_n = 0): dy from the BN input y, the activation-output gradient dh and the channel's
+// statistics / column totals.  One definition for bn_act_bwd_apply_kernel and BnDyWin.
+template <bool RELU>
+LASR_DEV float bn_dy(float yv, float gv, float sc, float sf, float mu, float rs, float ga, float t1, float t2,
+                     float inv_n) {
+  const float du = gv * bn_act_grad<RELU>(yv * sc + sf);
+  const float xh = (yv - mu) * rs;
+  return ga * rs * (du - t1 * inv_n - xh * t2 * inv_n);
+}
+
+// glu_dwconv_bwd's dy window computed on the fly from y and dh (lasr_bn_act_glu_dwconv_bwd): the
+// values bn_act_bwd_apply_kernel would have stored, without the fp32 dy round trip or its launch
+template <typename TY, typename TH, bool RELU>
+struct BnDyWin {
+  const TY* y;
+  const TH* dh;
+  const float *scale, *shift, *mean, *rstd, *gamma, *tot;
+  float* dgamma;
+  float* dbeta;
+  float inv_n;
+  int C;
+  LASR_DEV float one(float yv, float gv, int c) const {
+    return bn_dy<RELU>(yv, gv, scale[c], shift[c], mean[c], rstd[c], gamma[c], tot[c], tot[C + c], inv_n);
+  }
+  LASR_DEV void load8(const TY* row, int ce, float* v, float* u) const {
+    float yv[8], gv[8];
+    ldv<8>(row + ce, yv);
+    ldv<8>(dh + (row - y) + ce, gv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = one(yv[k], gv[k], ce + k);
+      u[k] = 0.f;
+    }
+  }
+  LASR_DEV void load2(const TY* row, int ce, float* v, float* u) const {
+    float yv[2], gv[2];
+    ldv<2>(row + ce, yv);
+    ldv<2>(dh + (row - y) + ce, gv);
+    v[0] = one(yv[0], gv[0], ce);
+    v[1] = one(yv[1], gv[1], ce + 1);
+    u[0] = u[1] = 0.f;
+  }
+  LASR_DEV float2 pair(const float* v, const float*) const { return make_float2(v[0], v[1]); }
+  // the parameter gradients (bn_act_bwd_apply_kernel's block-0 job: the totals are final here)
+  LASR_DEV void finish(int) const {
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+      for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        dbeta[c] += tot[c];
+        dgamma[c] += tot[C + c];
+      }
+  }
+};
+
 // Elementwise BN + activation, 8 channels per thread (C % 8 == 0; the host checks).
 template <typename TY, typename TH, bool RELU>
 __global__ void bn_act_fwd_kernel(const TY* y, int64_t rows, int C, const float* scale,
@@ -786,9 +844,7 @@ __global__ void bn_act_bwd_apply_kernel(const TY* y, const TH* dh, int64_t rows,
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int c = c0 + q;
-      const float du = gv[q] * bn_act_grad<RELU>(yv[q] * scale[c] + shift[c]);
-      const float xh = (yv[q] - mean[c]) * rstd[c];
-      o[q] = gamma[c] * rstd[c] * (du - tot[c] * inv_n - xh * tot[C + c] * inv_n);
+      o[q] = bn_dy<RELU>(yv[q], gv[q], scale[c], shift[c], mean[c], rstd[c], gamma[c], tot[c], tot[C + c], inv_n);
     }
     stv<8>(dy + e * 8, o);
   }
@@ -1012,5 +1068,87 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
   int rc = lasr_check_launch("glu_dwconv_bwd");
   if (rc || (!dw && !db)) return rc;  // no outputs: partials left in ws (deferred reduction)
   LASR_CHECK_ARG(dw && db, "lasr_glu_dwconv_bwd: dw and db go together");
+  return lasr_reduce_cols(ws, nparts, (int64_t)(DW_K + 1) * C, dw, db, (int64_t)DW_K * C, 1, st);
+}
+
+// lasr_bn_act_bwd + lasr_glu_dwconv_bwd with the BN backward's elementwise pass folded into the
+// depthwise-conv backward's dy window (BnDyWin): one launch and the fp32 dy round trip fewer, the
+// same dz1 / dw / db / dgamma / dbeta bits.
+template <typename TT, typename TY, typename TH, bool RELU>
+static void bn_glu_launch(dim3 g, hipStream_t st, const void* z1, const void* y, const void* dh, int T, int C,
+                          const float* w, void* dz1, float* ws, int vec, const BnDyWin<TY, TH, RELU>& f) {
+  glu_dwconv_bwd_kernel<TT, TY, BnDyWin<TY, TH, RELU>><<<g, 256, 0, st>>>((const TT*)z1, (const TY*)y, T, C, w,
+                                                                          (TT*)dz1, ws, vec, f);
+}
+
+template <typename TT, typename TY, typename TH>
+static void bn_glu_dispatch(bool relu, dim3 g, hipStream_t st, const void* z1, const void* y, const void* dh, int T,
+                            int C, const float* w, void* dz1, float* ws, int vec, const float* scale,
+                            const float* shift, const float* mean, const float* rstd, const float* gamma,
+                            const float* tot, float* dgamma, float* dbeta, float inv_n) {
+  if (relu)
+    bn_glu_launch<TT, TY, TH, true>(g, st, z1, y, dh, T, C, w, dz1, ws, vec,
+                                    BnDyWin<TY, TH, true>{(const TY*)y, (const TH*)dh, scale, shift, mean, rstd,
+                                                          gamma, tot, dgamma, dbeta, inv_n, C});
+  else
+    bn_glu_launch<TT, TY, TH, false>(g, st, z1, y, dh, T, C, w, dz1, ws, vec,
+                                     BnDyWin<TY, TH, false>{(const TY*)y, (const TH*)dh, scale, shift, mean, rstd,
+                                                            gamma, tot, dgamma, dbeta, inv_n, C});
+}
+
+extern "C" int lasr_bn_act_glu_dwconv_bwd(const void* y, int ydt, const void* dh, int hdt, int B, int T, int C,
+                                          const float* scale, const float* shift, const float* mean,
+                                          const float* rstd, const float* gamma, float* dgamma, float* dbeta,
+                                          float* bn_ws, int64_t bn_ws_floats, int batch_stats, int act,
+                                          const void* z1, int dt, int K, const float* w, void* dz1, float* dw,
+                                          float* db, float* ws, int64_t ws_floats, void* stream) {
+  const int64_t rows = (int64_t)B * T;
+  const int64_t nparts_bn = cdiv(rows, BN_ROWS);
+  LASR_CHECK_ARG(bn_ws_floats >= (nparts_bn + 1) * 2 * C, "lasr_bn_act_glu_dwconv_bwd: BN workspace too small");
+  LASR_CHECK_ARG(nparts_bn <= 65535, "lasr_bn_act_glu_dwconv_bwd: too many rows");
+  LASR_CHECK_ARG(act == LASR_ACT_SWISH || act == LASR_ACT_RELU, "lasr_bn_act_glu_dwconv_bwd: act must be SWISH or RELU");
+  LASR_CHECK_ARG(K == DW_K, "lasr_bn_act_glu_dwconv_bwd: only kernel size %d is built", DW_K);
+  LASR_CHECK_ARG(C % 8 == 0 && rows > 0, "lasr_bn_act_glu_dwconv_bwd: C must be a multiple of 8, rows > 0");
+  LASR_CHECK_ARG((ydt == LASR_F32 || ydt == LASR_BF16) && (hdt == LASR_F32 || hdt == LASR_BF16) &&
+                     (dt == LASR_F32 || dt == LASR_BF16), "lasr_bn_act_glu_dwconv_bwd: bad dtype");
+  const int nchunk = (int)cdiv(T, DW_TT);
+  const int nparts = B * nchunk;
+  LASR_CHECK_ARG(ws_floats >= (int64_t)nparts * (DW_K + 1) * C, "lasr_bn_act_glu_dwconv_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  // BN column totals, exactly as lasr_bn_act_bwd computes them
+  float* tot = bn_ws + nparts_bn * 2 * C;
+  {
+    dim3 g((unsigned)cdiv(C, 2 * BN_CP), (unsigned)nparts_bn);
+#define BR(RL, TY, TH) bn_act_bwd_reduce_kernel<TY, TH, RL><<<g, 256, 0, st>>>((const TY*)y, (const TH*)dh, rows, C, scale, shift, mean, rstd, bn_ws)
+    const bool relu = act == LASR_ACT_RELU, yf = ydt == LASR_F32, hf = hdt == LASR_F32;
+    if (relu) {
+      if (yf && hf) BR(true, float, float); else if (yf) BR(true, float, bf16_t);
+      else if (hf) BR(true, bf16_t, float); else BR(true, bf16_t, bf16_t);
+    } else {
+      if (yf && hf) BR(false, float, float); else if (yf) BR(false, float, bf16_t);
+      else if (hf) BR(false, bf16_t, float); else BR(false, bf16_t, bf16_t);
+    }
+#undef BR
+    if (int rc = lasr_check_launch("bn_act_glu_dwconv_bwd/reduce")) return rc;
+    if (int rc = lasr_reduce_cols(bn_ws, (int)nparts_bn, 2 * C, tot, nullptr, 2 * C, 0, st)) return rc;
+  }
+  const float inv_n = batch_stats ? 1.f / (float)rows : 0.f;
+  dim3 g((unsigned)nparts, (unsigned)cdiv(C, 2 * DW_CP));
+  const int vec = ((uintptr_t)z1 & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)dh & 15) == 0 &&
+                  ((uintptr_t)dz1 & 15) == 0;
+  const bool relu = act == LASR_ACT_RELU;
+#define BG(TT, TY, TH) bn_glu_dispatch<TT, TY, TH>(relu, g, st, z1, y, dh, T, C, w, dz1, ws, vec, scale, shift, mean, rstd, gamma, tot, dgamma, dbeta, inv_n)
+  const bool zf = dt == LASR_F32, yf = ydt == LASR_F32, hf = hdt == LASR_F32;
+  if (zf) {
+    if (yf && hf) BG(float, float, float); else if (yf) BG(float, float, bf16_t);
+    else if (hf) BG(float, bf16_t, float); else BG(float, bf16_t, bf16_t);
+  } else {
+    if (yf && hf) BG(bf16_t, float, float); else if (yf) BG(bf16_t, float, bf16_t);
+    else if (hf) BG(bf16_t, bf16_t, float); else BG(bf16_t, bf16_t, bf16_t);
+  }
+#undef BG
+  int rc = lasr_check_launch("bn_act_glu_dwconv_bwd");
+  if (rc || (!dw && !db)) return rc;  // no outputs: partials left in ws (deferred reduction)
+  LASR_CHECK_ARG(dw && db, "lasr_bn_act_glu_dwconv_bwd: dw and db go together");
   return lasr_reduce_cols(ws, nparts, (int64_t)(DW_K + 1) * C, dw, db, (int64_t)DW_K * C, 1, st);
 }

@@ -854,6 +854,27 @@ def glu_dwconv_bwd(z1, dy, B, T, Cc, K, w, dz1, dw, db):
            ptr(dw), ptr(db), ptr(ws), ws.numel(), stream())
 
 
+def bn_act_glu_dwconv_bwd(y, dh, scale, shift, mean, rstd, gamma, dgamma, dbeta, z1, B, T, Cc, K, w, dz1, dw, db,
+                          batch_stats=True, act=N.ACT_SWISH):
+    """bn_act_bwd + glu_dwconv_bwd in one call (lasr_bn_act_glu_dwconv_bwd): the BN backward's dy
+    is computed inside the depthwise backward's window load, never stored.  Same outputs."""
+    rows = y.shape[0]
+    assert rows == B * T and y.shape[1] == Cc and dh.shape == y.shape and z1.shape == (rows, 2 * Cc)
+    # (its own buffer: the depthwise partials below may take WS)
+    bn_ws = torch.empty(((rows + 63) // 64 + 1) * 2 * Cc, dtype=torch.float32, device=y.device)
+    nparts = dwconv_nparts(B, T)
+    head = (ptr(y), dt(y), ptr(dh), dt(dh), B, T, Cc, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), ptr(gamma),
+            ptr(dgamma), ptr(dbeta), ptr(bn_ws), bn_ws.numel(), int(bool(batch_stats)), act, ptr(z1), dt(z1), K,
+            ptr(w), ptr(dz1))
+    if _DEFER.depth:
+        ws = torch.empty(nparts * (K + 1) * Cc, dtype=torch.float32, device=z1.device)
+        N.call("lasr_bn_act_glu_dwconv_bwd", *head, None, None, ptr(ws), ws.numel(), stream())
+        _defer(ws, nparts, (K + 1) * Cc, dw, db, split=K * Cc)
+        return
+    ws = WS.get((nparts + 1) * (K + 1) * Cc, z1.device)
+    N.call("lasr_bn_act_glu_dwconv_bwd", *head, ptr(dw), ptr(db), ptr(ws), ws.numel(), stream())
+
+
 # ---------------------------------------------------------------- elementwise ---
 def cast(src, dst):
     N.call("lasr_cast", ptr(src), dt(src), ptr(dst), dt(dst), src.numel(), stream())

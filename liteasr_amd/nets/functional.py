@@ -73,6 +73,10 @@ SPLITK_LN = True
 # the encoder attention's positional-bias gradient (qbias_bwd) in the positional-projection
 # gradient GEMM's split-K reduction launch (gemm_ln.hip lasr_gemm_qbias_bwd); False: its own launch
 QBIAS_IN_REDUCE = True
+# the conv module's BatchNorm + activation backward folded into the depthwise-conv / GLU
+# backward (lasr_bn_act_glu_dwconv_bwd: dy computed in its window load, never stored); False: the
+# two launches with the fp32 dy between them (tests/test_fusions_gpu.py pins the two bit for bit)
+BN_GLU_FUSED = True
 
 
 class PostLN(SimpleNamespace):
@@ -501,11 +505,17 @@ def conv_backward(gb, ln, sv, w, g, env, lnb=None):
     K.gemm(gb.t(), sv.h3, g.Wpw2, beta=1.0, split_k=0, rowsum=g.bpw2, group=True)
     dh3 = _e((M, d), adt, dev)
     K.gemm(gb, w.Wpw2, dh3)
-    dy = _e((M, d), F32, dev)
-    K.bn_act_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy,
-                 batch_stats=sv.training, act=getattr(w, "act", ACT_SWISH))
     dz1 = _e((M, 2 * d), adt, dev)
-    K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
+    if BN_GLU_FUSED and d % 8 == 0:
+        # the BN backward's dy computed inside the depthwise backward's window load (never stored)
+        K.bn_act_glu_dwconv_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, sv.z1,
+                                B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw, batch_stats=sv.training,
+                                act=getattr(w, "act", ACT_SWISH))
+    else:
+        dy = _e((M, d), F32, dev)
+        K.bn_act_bwd(sv.y, dh3, sv.scale, sv.shift, sv.mean, sv.rstd, w.gamma, g.gamma, g.beta, dy,
+                     batch_stats=sv.training, act=getattr(w, "act", ACT_SWISH))
+        K.glu_dwconv_bwd(sv.z1, dy, B, T, d, w.kernel, w.wdw, dz1, g.wdw, g.bdw)
     K.gemm(dz1.t(), ln, g.Wpw1, beta=1.0, split_k=0, rowsum=g.bpw1, group=True)
     return dx_ln(dz1, w.Wpw1, lnb)
 

@@ -115,3 +115,17 @@ def test_narrow_output_tiles(monkeypatch, d, heads):
     monkeypatch.setattr(K, "GEMM_NARROW_TILES", False)
     off = _step(cfg, B=8, T=1000, L=12)
     _same(on, off)
+
+
+@pytest.mark.parametrize("d,heads", [(256, 4), (512, 16)])
+def test_bn_backward_in_dwconv_window(monkeypatch, d, heads):
+    """The conv module's BatchNorm + Swish backward computed inside the depthwise-conv / GLU
+    backward's window load (lasr_bn_act_glu_dwconv_bwd) vs bn_act_bwd storing an fp32 dy that
+    glu_dwconv_bwd reads: one bf16 step bit-identical, BN running statistics included."""
+    from liteasr_amd.nets import functional as FN
+
+    cfg = O.default_cfg(enc_dim=d, enc_heads=heads, enc_layers=2, dec_dim=d, dec_heads=heads, dec_layers=1)
+    on = _step(cfg, B=4, T=1000, L=12)
+    monkeypatch.setattr(FN, "BN_GLU_FUSED", False)
+    off = _step(cfg, B=4, T=1000, L=12)
+    _same(on, off)
