@@ -192,6 +192,18 @@ int lasr_layernorm_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype,
                        float* dgamma, float* dbeta, float* workspace, int64_t ws_floats,
                        void* gb, int gb_dtype, float bscale, float bp, uint64_t bseed,
                        void* stream);
+/* The two LayerNorm backwards at a Conformer layer boundary in one launch (the reverse of
+ * lasr_layernorm2_fwd; liteasr/nets/conformer_layer.py:130 and :147): the next layer's first
+ * norm, dx1 = dres1 + LN1'(dy1) (x1 fp32, dy1 fp32 / bf16, dres1 fp32; dx1 is not stored),
+ * then this layer's final norm on it, dx2 = LN2'(dx1) (x2 fp32, dx2 fp32) and the branch
+ * gradient gb2 = bscale * drop(dx2) (bf16 / fp32, or NULL).  part1 / part2: each norm's
+ * [ceil(rows/16)][2][D] gamma / beta partial rows, as lasr_layernorm_bwd's workspace holds
+ * them, for the caller's reduction.  Bit-identical to two lasr_layernorm_bwd calls with dx1
+ * stored in fp32 between them. */
+int lasr_layernorm2_bwd(const float* x1, const void* dy1, int dy1_dtype, const float* dres1, int64_t rows, int D,
+                        const float* g1, const float* mean1, const float* rstd1, float* part1, const float* x2,
+                        const float* g2, const float* mean2, const float* rstd2, float* dx2, float* part2, void* gb2,
+                        int gb2_dtype, float bscale, float bp, uint64_t bseed, void* stream);
 /* ------------------------------------------------------------------------
  * Full-row GEMM with the LayerNorm in its epilogue: the residual projections of a
  * Conformer layer and the following sub-block's norm (liteasr/nets/conformer_layer.py:37-78

@@ -132,6 +132,8 @@ SIGNATURES = {
     "lasr_layernorm_fwd": [_p, _i, _l, _i, _p, _p, _f, _p, _i, _p, _p, _p, _i, _f, _u, _p],
     "lasr_layernorm_bwd": [_p, _i, _p, _i, _l, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _l,
                            _p, _i, _f, _f, _u, _p],
+    "lasr_layernorm2_bwd": [_p, _p, _i, _p, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _f, _u,
+                            _p],
     "lasr_branch_grad": [_p, _i, _l, _p, _i, _f, _f, _u, _p],
     "lasr_ctc_fwd": [_p, _i, _i, _i, _i, _l, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "lasr_ctc_lattice": [_i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],

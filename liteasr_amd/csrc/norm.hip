@@ -148,6 +148,70 @@ __global__ __launch_bounds__(1024) void ln_bwd_kernel(const TX* __restrict__ x,
   }
 }
 
+// Two chained LayerNorm backwards per row, across a Conformer layer boundary (the reverse of
+// ln2_fwd_kernel): the next layer's first norm (x1 fp32, dy1 = its GEMM's input gradient, dres1
+// fp32: dx1 = dres1 + LN1'(dy1), kept in registers), then this layer's final norm on dx1 (x2
+// fp32: dx2 = LN2'(dx1) stored, gb2 = bscale2 * drop(dx2)).  Rows, waves, the per-row
+// arithmetic (ln_bwd_row) and the two partial-row layouts are ln_bwd_kernel's: bit-identical
+// to lasr_layernorm_bwd run twice with dx1 stored in fp32 between them.
+template <int NPL, typename TD, typename TGB>
+__global__ __launch_bounds__(1024) void ln2_bwd_kernel(const float* __restrict__ x1, const TD* __restrict__ dy1,
+                                                       const float* __restrict__ dres1, const float* __restrict__ g1,
+                                                       const float* __restrict__ mean1, const float* __restrict__ rstd1,
+                                                       float* __restrict__ part1, const float* __restrict__ x2,
+                                                       const float* __restrict__ g2, const float* __restrict__ mean2,
+                                                       const float* __restrict__ rstd2, float* __restrict__ dx2,
+                                                       float* __restrict__ part2, TGB* __restrict__ gb2,
+                                                       int64_t rows, float bscale, DropCfg bd) {
+  constexpr int D = NPL * 64, WAVES = LnbCfg<NPL>::WAVES, RPW = LnbCfg<NPL>::RPW;
+  __shared__ float sp[WAVES][D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = lane * NPL;
+  float pg1[NPL], pb1[NPL], pg2[NPL], pb2[NPL], gm1[NPL], gm2[NPL];
+  ldv<NPL>(g1 + c0, gm1);
+  ldv<NPL>(g2 + c0, gm2);
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { pg1[i] = 0.f; pb1[i] = 0.f; pg2[i] = 0.f; pb2[i] = 0.f; }
+  const uint32_t key = (gb2 && bd.p > 0.f) ? drop_key(bd) : 0u;
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int64_t row = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK + w * RPW + rr;
+    if (row < rows) {
+      float xv[NPL], d[NPL], r[NPL], o1[NPL], o2[NPL], xw[NPL];
+      ldv<NPL>(x1 + row * D + c0, xv);
+      ldv<NPL>(dy1 + row * D + c0, d);
+      ldv<NPL>(dres1 + row * D + c0, r);
+      ldv<NPL>(x2 + row * D + c0, xw);
+      ln_bwd_row<D, NPL, true>(xv, d, gm1, mean1[row], rstd1[row], r, pg1, pb1, o1);
+      ln_bwd_row<D, NPL, false>(xw, o1, gm2, mean2[row], rstd2[row], r, pg2, pb2, o2);
+      stv<NPL>(dx2 + row * D + c0, o2);
+      if (gb2) {
+        float dm[NPL];
+        if (bd.p > 0.f) drop_mul_n<NPL>(bd, key, (uint64_t)(row * D + c0), dm);
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) o2[i] *= bscale * (bd.p > 0.f ? dm[i] : 1.f);
+        stv<NPL>(gb2 + row * D + c0, o2);
+      }
+    }
+  }
+  // the two norms' partial rows, each combined as ln_bwd_kernel combines its own
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const float* src = pass == 0 ? pg1 : pass == 1 ? pb1 : pass == 2 ? pg2 : pb2;
+    float* part = pass < 2 ? part1 : part2;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) sp[w][c0 + i] = src[i];
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < WAVES; ++k) a += sp[k][c];
+      part[(int64_t)blockIdx.x * 2 * D + (pass & 1) * D + c] = a;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void ln_param_reduce_kernel(const float* part, int nblk, int D, float* dgamma,
                                        float* dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -387,4 +451,44 @@ extern "C" int lasr_colsum(const void* X, int dtype, int64_t M, int64_t N, int64
   int rc = lasr_check_launch("colsum");
   if (rc) return rc;
   return lasr_reduce_cols(workspace, (int)nchunk, N, out, nullptr, N, accumulate, st);
+}
+
+// (liteasr/nets/conformer_layer.py:130 / :147 backward across a layer boundary; see
+// ln2_bwd_kernel.)  dy1 fp32 or bf16, gb2 fp32 / bf16 / none; part1 / part2 [nblk][2][D] each,
+// nblk = ceil(rows / 16), reduced by the caller (lasr_reduce_multi) like lasr_layernorm_bwd's.
+extern "C" int lasr_layernorm2_bwd(const float* x1, const void* dy1, int dy1_dtype, const float* dres1, int64_t rows,
+                                   int D, const float* g1, const float* mean1, const float* rstd1, float* part1,
+                                   const float* x2, const float* g2, const float* mean2, const float* rstd2,
+                                   float* dx2, float* part2, void* gb2, int gb2_dtype, float bscale, float bp,
+                                   uint64_t bseed, void* stream) {
+  LASR_CHECK_ARG(D == 256 || D == 512 || D == 128 || D == 64, "lasr_layernorm2_bwd: D=%d unsupported", D);
+  LASR_CHECK_ARG(x1 && dy1 && dres1 && g1 && mean1 && rstd1 && part1 && x2 && g2 && mean2 && rstd2 && dx2 && part2,
+                 "lasr_layernorm2_bwd: null operand");
+  LASR_CHECK_ARG(dy1_dtype == LASR_F32 || dy1_dtype == LASR_BF16, "lasr_layernorm2_bwd: dy1 dtype");
+  LASR_CHECK_ARG(!gb2 || gb2_dtype == LASR_F32 || gb2_dtype == LASR_BF16, "lasr_layernorm2_bwd: gb2 dtype");
+  LASR_CHECK_ARG(ln_aligned(x1, D, LASR_F32) && ln_aligned(dy1, D, dy1_dtype) && ln_aligned(dres1, D, LASR_F32) &&
+                     ln_aligned(x2, D, LASR_F32) && ln_aligned(dx2, D, LASR_F32) &&
+                     (!gb2 || ln_aligned(gb2, D, gb2_dtype)), "lasr_layernorm2_bwd: misaligned row pointer");
+  if (rows <= 0) return LASR_OK;
+  const unsigned nb = (unsigned)cdiv(rows, LN_ROWS_PER_BLOCK);
+  DropCfg bd = mkdrop(bp, bseed);
+  hipStream_t st = (hipStream_t)stream;
+#define L2B(NPL, TD, TGB)                                                                                        \
+  ln2_bwd_kernel<NPL, TD, TGB><<<nb, LnbCfg<NPL>::WAVES * 64, 0, st>>>(x1, (const TD*)dy1, dres1, g1, mean1, rstd1, \
+                                                                      part1, x2, g2, mean2, rstd2, dx2, part2,     \
+                                                                      (TGB*)gb2, rows, bscale, bd)
+#define L2D(NPL)                                                                    \
+  if (dy1_dtype == LASR_BF16 && gb2_dtype != LASR_F32) L2B(NPL, bf16_t, bf16_t);    \
+  else if (dy1_dtype == LASR_BF16) L2B(NPL, bf16_t, float);                         \
+  else if (gb2_dtype != LASR_F32) L2B(NPL, float, bf16_t);                          \
+  else L2B(NPL, float, float);
+  switch (D / 64) {
+    case 1: { L2D(1) } break;
+    case 2: { L2D(2) } break;
+    case 4: { L2D(4) } break;
+    default: { L2D(8) } break;
+  }
+#undef L2D
+#undef L2B
+  return lasr_check_launch("layernorm2_bwd");
 }

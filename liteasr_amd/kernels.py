@@ -439,6 +439,30 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, gb=Non
         _defer(ws, nblk, 2 * D, dgamma, dbeta, split=D)
 
 
+def layernorm2_bwd(x1, dy1, dres1, g1, mean1, rstd1, dgamma1, dbeta1, x2, g2, mean2, rstd2, dx2, dgamma2, dbeta2,
+                   gb2=None, bscale=1.0, bp=0.0, bseed=0):
+    """Two LayerNorm backwards per row (lasr_layernorm2_bwd): dx1 = dres1 + LN1'(dy1) (not
+    stored), dx2 = LN2'(dx1), gb2 = bscale * drop(dx2); both norms' gamma / beta gradients
+    accumulate (deferred inside deferred_reductions)."""
+    rows, D = x1.shape
+    assert x1.dtype == x2.dtype == dres1.dtype == dx2.dtype == torch.float32
+    assert dy1.shape == x1.shape == x2.shape == dres1.shape == dx2.shape
+    nblk = (rows + 15) // 16  # LN_ROWS_PER_BLOCK (norm.hip)
+    part1 = torch.empty(nblk * 2 * D, dtype=torch.float32, device=x1.device)
+    part2 = torch.empty(nblk * 2 * D, dtype=torch.float32, device=x1.device)
+    N.call("lasr_layernorm2_bwd", ptr(x1), ptr(dy1), dt(dy1), ptr(dres1), rows, D, ptr(g1), ptr(mean1), ptr(rstd1),
+           ptr(part1), ptr(x2), ptr(g2), ptr(mean2), ptr(rstd2), ptr(dx2), ptr(part2), ptr(gb2),
+           dt(gb2) if gb2 is not None else 0, bscale, bp, bseed, stream())
+    if _DEFER.depth:
+        _defer(part1, nblk, 2 * D, dgamma1, dbeta1, split=D)
+        _defer(part2, nblk, 2 * D, dgamma2, dbeta2, split=D)
+        return
+    arr = (N.ReduceSeg * 2)()
+    arr[0] = N.ReduceSeg(ptr(part1), 2 * D, nblk, 1, ptr(dgamma1), ptr(dbeta1), D)
+    arr[1] = N.ReduceSeg(ptr(part2), 2 * D, nblk, 1, ptr(dgamma2), ptr(dbeta2), D)
+    N.call("lasr_reduce_multi", arr, 2, stream())
+
+
 # ------------------------------------------------- full-row GEMM + LayerNorm ---
 def _al16(t):
     return t is None or t.data_ptr() % 16 == 0

@@ -251,7 +251,7 @@ class FusedEncoderModel(LiteasrModel):
         env.pos_proj = {id(layer): p for layer, p in zip(enc.enc_layers, pp)} if pp else None
         layers = list(enc.enc_layers)
         conformer = getattr(enc, "arch", "conformer") == "conformer"
-        env.pre_ln = None
+        env.pre_ln = env.bwd_chain = None
         for j, layer in enumerate(layers):
             x = self._cut(x, j)
             if not conformer:  # Transformer layers: no final norm to chain the next first norm into

@@ -73,6 +73,11 @@ SPLITK_LN = True
 # the encoder attention's positional-bias gradient (qbias_bwd) in the positional-projection
 # gradient GEMM's split-K reduction launch (gemm_ln.hip lasr_gemm_qbias_bwd); False: its own launch
 QBIAS_IN_REDUCE = True
+# a Conformer layer's first-norm backward and the previous layer's final-norm backward in one
+# launch (lasr_layernorm2_bwd, the reverse of FUSED_LN2's chained forward): the previous layer
+# receives its final norm's input gradient instead of computing it; False: two launches with
+# the fp32 gradient between them (tests/test_fusions_gpu.py pins the two bit for bit)
+LN2_BWD_CHAIN = True
 # the conv module's BatchNorm + activation backward folded into the depthwise-conv / GLU
 # backward (lasr_bn_act_glu_dwconv_bwd: dy computed in its window load, never stored); False: the
 # two launches with the fp32 dy between them (tests/test_fusions_gpu.py pins the two bit for bit)
@@ -126,13 +131,26 @@ class LnBwd(SimpleNamespace):
 
 def dx_ln(dy, W, lnb):
     """dln = dy @ W ([M, K] x [K, D]); with `lnb` the LayerNorm backward of dln follows (one
-    launch on the row kernel when it takes the shape) and None is returned, else dln."""
+    launch on the row kernel when it takes the shape) and None is returned, else dln.
+    lnb.chain (an LnBwd on lnb.dx: the previous layer's final norm, ConformerLayerFn) runs
+    right after it -- in the same launch as lnb's (lasr_layernorm2_bwd, lnb.dx never stored)
+    when lnb is not on the row kernel."""
     M, D = dy.shape[0], W.shape[1]
+    ch = getattr(lnb, "chain", None) if lnb is not None else None
     if lnb is not None and ROW_LN and K.row_ln_ok(dy, W, D) and lnb.x.dtype == F32 and lnb.dx.dtype == F32:
         K.linear_dx_ln_bwd(dy, W, lnb.x, lnb.g, lnb.mean, lnb.rstd, lnb.dx, lnb.dgamma, lnb.dbeta,
                            dres=lnb.dres, gb=lnb.gb, bscale=lnb.bscale, bp=lnb.bp, bseed=lnb.bseed)
+        if ch is not None:
+            ln_bwd_of(lnb.dx, ch)
         return None
     dln = _e((M, D), dy.dtype, dy.device)
+    if ch is not None:
+        assert lnb.gb is None and lnb.dres is not None and ch.dres is None and lnb.x.dtype == F32
+        K.gemm(dy, W, dln)
+        K.layernorm2_bwd(lnb.x, dln, lnb.dres, lnb.g, lnb.mean, lnb.rstd, lnb.dgamma, lnb.dbeta, ch.x, ch.g,
+                         ch.mean, ch.rstd, ch.dx, ch.dgamma, ch.dbeta, gb2=ch.gb, bscale=ch.bscale, bp=ch.bp,
+                         bseed=ch.bseed)
+        return None
     if lnb is not None and SPLITK_LN and dy.dtype == torch.bfloat16 and W.shape[0] >= 1024:
         # the norm backward in the GEMM's split-K reduction launch (lasr_gemm_ln_bwd; two
         # launches when the plan does not split K)
@@ -700,8 +718,9 @@ class ConformerLayerFn(torch.autograd.Function):
         x0 = x0.contiguous()
         # (a) macaron FFN, scale 0.5
         pre = getattr(env, "pre_ln", None)  # this layer's first norm, computed by the previous layer
+        prev = None  # the previous layer's final norm, when its forward chained into ours
         if pre is not None and pre[0] == id(layer) and pre[1] == x0.data_ptr():
-            ln_a, ma, ra = pre[2:]
+            ln_a, ma, ra, prev = pre[2:]
             env.pre_ln = None
         else:
             ln_a, _, ma, ra = ln_forward(x0, w.ln_a.g, w.ln_a.b, adt)
@@ -742,7 +761,8 @@ class ConformerLayerFn(torch.autograd.Function):
         if pf_.y1 is not None:
             x5, mf, rf = pf_.y1, pf_.m1, pf_.r1
             if chain:
-                env.pre_ln = (id(nxt[0]), x5.data_ptr(), pf_.y2, pf_.m2, pf_.r2)
+                env.pre_ln = (id(nxt[0]), x5.data_ptr(), pf_.y2, pf_.m2, pf_.r2,
+                              SimpleNamespace(layer=layer, x4=x4, mf=mf, rf=rf))
         else:
             x5 = _e(x4.shape, F32, x4.device)
             mf = _e(x4.shape[0], F32, x4.device)
@@ -752,14 +772,14 @@ class ConformerLayerFn(torch.autograd.Function):
                 m2 = _e(x4.shape[0], F32, x4.device)
                 r2 = _e(x4.shape[0], F32, x4.device)
                 K.layernorm2_fwd(x4, w.ln_f.g, w.ln_f.b, nxt[1], nxt[2], LN_EPS, x5, mf, rf, z, m2, r2)
-                env.pre_ln = (id(nxt[0]), x5.data_ptr(), z, m2, r2)
+                env.pre_ln = (id(nxt[0]), x5.data_ptr(), z, m2, r2, SimpleNamespace(layer=layer, x4=x4, mf=mf, rf=rf))
             else:
                 K.layernorm_fwd(x4, w.ln_f.g, w.ln_f.b, LN_EPS, x5, mf, rf)
         if torch.is_grad_enabled() or anchor.requires_grad:
             ctx.sv = SimpleNamespace(x=(x0, x1, x2, x3, x4), ln=(ln_a, ln_b, ln_c, ln_d),
                                      st=((ma, ra), (mb, rb), (mc, rc), (md, rd), (mf, rf)),
                                      za=za, ha=ha, zd=zd, hd=hd, svb=svb, svc=svc, pos=pos,
-                                     p=(pd, pff, pat))
+                                     p=(pd, pff, pat), prev=prev)
         ctx.layer, ctx.env = layer, env
         return x5
 
@@ -776,12 +796,24 @@ class ConformerLayerFn(torch.autograd.Function):
         M, d = x4.shape
         dx5 = dx5.contiguous()
         # parameter-gradient reductions of the whole layer finish in one launch at the end
+        rx = getattr(env, "bwd_chain", None)
         with K.deferred_reductions():
-            # final LN; emits the (d)-branch gradient 0.5*drop(dx4)
-            dx4 = _e((M, d), F32, dev)
-            gb = _e((M, d), adt, dev)
-            K.layernorm_bwd(x4, dx5, w.ln_f.g, mf, rf, dx4, g.ln_f.g, g.ln_f.b, gb=gb, bscale=0.5,
-                            bp=pd, bseed=_seed(s, 7))
+            if rx is not None and rx[0] == id(layer):
+                # the next layer ran this final norm's backward with its own first norm's
+                # (LN2_BWD_CHAIN): dx5 is already dx4, and gb came with it
+                # (this layer's output has one consumer, the next layer -- directly or through a
+                # backward-segment cut, which may hand over a copy -- so dx5 holds exactly the
+                # dx4 values that layer produced)
+                env.bwd_chain = None
+                if rx[1] != (tuple(dx5.shape), dx5.dtype):
+                    raise RuntimeError("ConformerLayerFn: the chained final-norm gradient did not arrive as produced")
+                dx4, gb = dx5, rx[2]
+            else:
+                # final LN; emits the (d)-branch gradient 0.5*drop(dx4)
+                dx4 = _e((M, d), F32, dev)
+                gb = _e((M, d), adt, dev)
+                K.layernorm_bwd(x4, dx5, w.ln_f.g, mf, rf, dx4, g.ln_f.g, g.ln_f.b, gb=gb, bscale=0.5,
+                                bp=pd, bseed=_seed(s, 7))
             # each sub-block's input-gradient GEMM runs its norm's backward in its epilogue
             # (dx_ln); the branch-gradient buffers are fresh: grouped dW GEMMs read them at the
             # end of the node
@@ -802,10 +834,21 @@ class ConformerLayerFn(torch.autograd.Function):
                               lnb=LnBwd(x=x1, g=w.ln_b.g, mean=mb, rstd=rb, dx=dx1, dgamma=g.ln_b.g, dbeta=g.ln_b.b,
                                         dres=dx2, gb=gb1, bscale=0.5, bp=pd, bseed=_seed(s, 2)))
             dx0 = _e((M, d), F32, dev)
+            lnb_a = LnBwd(x=x0, g=w.ln_a.g, mean=ma, rstd=ra, dx=dx0, dgamma=g.ln_a.g, dbeta=g.ln_a.b,
+                          dres=dx1, gb=None, bscale=1.0, bp=0.0, bseed=0)
+            pv = sv.prev if LN2_BWD_CHAIN else None
+            if pv is not None:
+                # the previous layer's final norm on dx0 in the same launch: it receives dx4 / gb
+                pw, pgr = pv.layer.weights(), pv.layer.grads()
+                dx4p, gbp = _e((M, d), F32, dev), _e((M, d), adt, dev)
+                lnb_a.chain = LnBwd(x=pv.x4, g=pw.ln_f.g, mean=pv.mf, rstd=pv.rf, dx=dx4p, dgamma=pgr.ln_f.g,
+                                    dbeta=pgr.ln_f.b, dres=None, gb=gbp, bscale=0.5, bp=pd,
+                                    bseed=_seed(pv.layer.seed, 7))
             ffn_backward(gb1, ln_a, sv.za, sv.ha, w.ffm.W1, w.ffm.W2, g.ffm.W1, g.ffm.b1, g.ffm.W2, g.ffm.b2,
-                         w.act, pff, _seed(s, 1),
-                         lnb=LnBwd(x=x0, g=w.ln_a.g, mean=ma, rstd=ra, dx=dx0, dgamma=g.ln_a.g, dbeta=g.ln_a.b,
-                                   dres=dx1, gb=None, bscale=1.0, bp=0.0, bseed=0))
+                         w.act, pff, _seed(s, 1), lnb=lnb_a)
+            if pv is not None:
+                env.bwd_chain = (id(pv.layer), (tuple(dx4p.shape), dx4p.dtype), gbp)
+                dx0 = dx4p
         ctx.sv = None
         layer.on_grads_ready()
         return dx0, None, None, None, None

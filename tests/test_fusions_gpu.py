@@ -129,3 +129,18 @@ def test_bn_backward_in_dwconv_window(monkeypatch, d, heads):
     monkeypatch.setattr(FN, "BN_GLU_FUSED", False)
     off = _step(cfg, B=4, T=1000, L=12)
     _same(on, off)
+
+
+@pytest.mark.parametrize("d,heads", [(256, 4), (512, 16)])
+def test_layer_boundary_norm_backwards_chained(monkeypatch, d, heads):
+    """A Conformer layer's first-norm backward and the previous layer's final-norm backward in
+    one launch (lasr_layernorm2_bwd: the previous layer receives dx4 and its branch gradient)
+    vs two lasr_layernorm_bwd launches with the fp32 gradient between them: one bf16 step of
+    three encoder layers bit-identical."""
+    from liteasr_amd.nets import functional as FN
+
+    cfg = O.default_cfg(enc_dim=d, enc_heads=heads, enc_layers=3, dec_dim=d, dec_heads=heads, dec_layers=1)
+    on = _step(cfg, B=4, T=1000, L=12)
+    monkeypatch.setattr(FN, "LN2_BWD_CHAIN", False)
+    off = _step(cfg, B=4, T=1000, L=12)
+    _same(on, off)
