@@ -317,11 +317,12 @@ constexpr int DW_K = 15;
 constexpr int DW_P = (DW_K - 1) / 2;
 constexpr int DW_WIN = DW_TT + 2 * DW_P;
 
-// Thread layout of the GLU/depthwise kernels: 256 threads = DW_G time groups of DW_R rows
+// Thread layout of the GLU/depthwise kernels: DW_NT = 256 threads = DW_G time groups of DW_R rows
 // x 64 channel pairs (128 channels, 2 per thread with 4-B / 8-B loads); a block covers
 // DW_TT = DW_G * DW_R rows, its per-channel partials are combined across the groups in LDS
 // in a fixed order (one partial per block, as lasr_dwconv_nparts counts them).
 constexpr int DW_G = 4, DW_R = DW_TT / DW_G, DW_CP = 64;
+constexpr int DW_NT = DW_G * DW_CP;  // threads per block
 constexpr int DW_RW = DW_R + 2 * DW_P;  // rows a thread reads (window + halo)
 
 
@@ -342,11 +343,11 @@ template <int CP, typename TS, typename F>
 LASR_DEV void dw_window(const TS* src, int64_t ld, int col0, int b, int T_, int C, int tb, bool vec,
                         float2 (*win)[CP], F f) {
   if (vec) {
-    constexpr int CH = CP / 4, NE = DW_WIN * CH, IT = (NE + 255) / 256;
+    constexpr int CH = CP / 4, NE = DW_WIN * CH, IT = (NE + DW_NT - 1) / DW_NT;
     float v[IT][8], u[IT][8];
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
-      const int e = threadIdx.x + 256 * j;
+      const int e = threadIdx.x + DW_NT * j;
       const int rr = e / CH, q = e % CH, t = tb - DW_P + rr, ce = blockIdx.y * 2 * CP + q * 8;
       if (e < NE && ce < C && t >= 0 && t < T_) {
         f.load8(src + ((int64_t)b * T_ + t) * ld + col0, ce, v[j], u[j]);
@@ -357,7 +358,7 @@ LASR_DEV void dw_window(const TS* src, int64_t ld, int col0, int b, int T_, int 
     }
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
-      const int e = threadIdx.x + 256 * j;
+      const int e = threadIdx.x + DW_NT * j;
       if (e >= NE) continue;
       const int rr = e / CH, q = e % CH;
 #pragma unroll
@@ -365,7 +366,7 @@ LASR_DEV void dw_window(const TS* src, int64_t ld, int col0, int b, int T_, int 
     }
     return;
   }
-  for (int e = threadIdx.x; e < DW_WIN * CP; e += 256) {
+  for (int e = threadIdx.x; e < DW_WIN * CP; e += DW_NT) {
     const int rr = e / CP, cq = e % CP, t = tb - DW_P + rr, ce = (blockIdx.y * CP + cq) * 2;
     float2 r = make_float2(0.f, 0.f);
     if (ce < C && t >= 0 && t < T_) {
@@ -389,7 +390,7 @@ struct GluWin {
 };
 
 template <typename T, typename TY>
-__global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const T* __restrict__ z1, int T_,
+__global__ __launch_bounds__(DW_NT) void glu_dwconv_fwd_kernel(const T* __restrict__ z1, int T_,
                                                              int C, const float* w,
                                                              const float* bias, TY* y,
                                                              float* stats, int vec) {
@@ -486,7 +487,7 @@ struct DyWin {
 // DYW: how the dy window is read -- DyWin (a stored dy) or BnDyWin (dy computed from the
 // BatchNorm + activation backward's inputs as the window is loaded, no stored dy)
 template <typename T, typename TD, typename DYW = DyWin<TD>>
-__global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict__ z1,
+__global__ __launch_bounds__(DW_NT) void glu_dwconv_bwd_kernel(const T* __restrict__ z1,
                                                              const TD* __restrict__ dy, int T_,
                                                              int C, const float* w, T* dz1,
                                                              float* part, int vec, DYW fdy = DYW{}) {
@@ -542,7 +543,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
   // dz1 = [dg * s | dg * a * s * (1 - s)], 8 channels per item: DW_TT rows x 16 channel octets
   {
     constexpr int OCT = 2 * DW_CP / 8;
-    for (int e = threadIdx.x; e < DW_TT * OCT; e += 256) {
+    for (int e = threadIdx.x; e < DW_TT * OCT; e += DW_NT) {
       const int rr = e / OCT, q = e % OCT, t = tb + rr, ce = blockIdx.y * 2 * DW_CP + q * 8;
       if (t >= T_ || ce >= C) continue;
       const int64_t r = (int64_t)b * T_ + t;
@@ -584,7 +585,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const T* __restrict
   // partial row of this block in the parameters' own layout: [C][K] weight taps, then [C]
   // bias, so the reduction writes dw / db directly (or is deferred as one segment)
   float* pp = part + (int64_t)blockIdx.x * (DW_K + 1) * C;
-  for (int e = threadIdx.x; e < (DW_K + 1) * 2 * DW_CP; e += 256) {
+  for (int e = threadIdx.x; e < (DW_K + 1) * 2 * DW_CP; e += DW_NT) {
     const int cl = e / (DW_K + 1), k = e % (DW_K + 1);
     const int cg = blockIdx.y * 2 * DW_CP + cl;
     if (cg >= C) continue;
@@ -952,7 +953,7 @@ extern "C" int lasr_glu_dwconv_fwd(const void* z1, int dt, int B, int T, int C, 
   dim3 g((unsigned)(B * nchunk), (unsigned)cdiv(C, 2 * DW_CP));
   hipStream_t st = (hipStream_t)stream;
   const int vec = C % 8 == 0 && ((uintptr_t)z1 & 15) == 0;
-#define GF(TT, TY) glu_dwconv_fwd_kernel<TT, TY><<<g, 256, 0, st>>>((const TT*)z1, T, C, w, bias, (TY*)y, stats_ws, vec)
+#define GF(TT, TY) glu_dwconv_fwd_kernel<TT, TY><<<g, DW_NT, 0, st>>>((const TT*)z1, T, C, w, bias, (TY*)y, stats_ws, vec)
   if (dt == LASR_F32 && ydt == LASR_F32) GF(float, float);
   else if (dt == LASR_F32) GF(float, bf16_t);
   else if (ydt == LASR_F32) GF(bf16_t, float);
@@ -1059,7 +1060,7 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
   dim3 g((unsigned)nparts, (unsigned)cdiv(C, 2 * DW_CP));
   hipStream_t st = (hipStream_t)stream;
   const int vec = C % 8 == 0 && ((uintptr_t)z1 & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dz1 & 15) == 0;
-#define GB(TT, TD) glu_dwconv_bwd_kernel<TT, TD><<<g, 256, 0, st>>>((const TT*)z1, (const TD*)dy, T, C, w, (TT*)dz1, ws, vec)
+#define GB(TT, TD) glu_dwconv_bwd_kernel<TT, TD><<<g, DW_NT, 0, st>>>((const TT*)z1, (const TD*)dy, T, C, w, (TT*)dz1, ws, vec)
   if (dt == LASR_F32 && dydt == LASR_F32) GB(float, float);
   else if (dt == LASR_F32) GB(float, bf16_t);
   else if (dydt == LASR_F32) GB(bf16_t, float);
@@ -1077,7 +1078,7 @@ extern "C" int lasr_glu_dwconv_bwd(const void* z1, int dt, const void* dy, int d
 template <typename TT, typename TY, typename TH, bool RELU>
 static void bn_glu_launch(dim3 g, hipStream_t st, const void* z1, const void* y, const void* dh, int T, int C,
                           const float* w, void* dz1, float* ws, int vec, const BnDyWin<TY, TH, RELU>& f) {
-  glu_dwconv_bwd_kernel<TT, TY, BnDyWin<TY, TH, RELU>><<<g, 256, 0, st>>>((const TT*)z1, (const TY*)y, T, C, w,
+  glu_dwconv_bwd_kernel<TT, TY, BnDyWin<TY, TH, RELU>><<<g, DW_NT, 0, st>>>((const TT*)z1, (const TY*)y, T, C, w,
                                                                           (TT*)dz1, ws, vec, f);
 }
 
