@@ -29,7 +29,7 @@ namespace {
 constexpr int LNF_WAVES = 4;       // ln_fwd_kernel: one row per wave, 4 rows per block
 constexpr int LNB_ROWS = 16;       // ln_bwd_kernel: LN_ROWS_PER_BLOCK
 template <int NPL>
-constexpr int lnb_waves() { return NPL >= 8 ? 8 : 16; }  // LnbCfg<NPL>::WAVES
+constexpr int lnb_waves() { return NPL <= 8 ? 16 : 8; }  // LnbCfg<NPL>::WAVES
 
 struct LnFwdPost {
   const float* gamma;

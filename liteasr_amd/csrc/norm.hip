@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void ln2_fwd_kernel(const float* __restrict__ 
 // block's dgamma/dbeta partials are combined in fixed order through LDS (deterministic).
 template <int NPL>
 struct LnbCfg {
-  static constexpr int WAVES = NPL >= 8 ? 8 : 16;  // d 512: two rows per wave (large step -0.05 ms)
+  static constexpr int WAVES = NPL <= 8 ? 16 : 8;
   static constexpr int RPW = LN_ROWS_PER_BLOCK / WAVES;
 };
 
