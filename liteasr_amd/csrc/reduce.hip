@@ -65,7 +65,9 @@ int lasr_reduce_cols(const float* part, int P, int64_t N, float* out0, float* ou
 //   mode 0 (many partials, P large): reduce_cols' 16 columns x 16 partial groups
 //   mode 1 (few partials, P <= 64): 4 columns per thread, partials summed in order 0..P-1
 //                                   (splitk_reduce_kernel's order)
-constexpr int RM_MAXSEG = 32;
+// 64 segments = 3588 B of kernel arguments (under the 4 KB kernarg budget); a longer list runs
+// in ceil(nseg / 64) launches
+constexpr int RM_MAXSEG = 64;
 constexpr int RM_VEC = 2;  // mode 1: 4-column runs per thread
 struct RSeg {
   const float* part;
@@ -81,10 +83,13 @@ struct RSegs {
 
 __global__ __launch_bounds__(256) void reduce_multi_kernel(RSegs a) {
   __shared__ float sh[RC_GROUPS][RC_COLS + 1];
-  int si = 0;
-  for (int i = 1; i < a.nseg; ++i)
-    if ((int)blockIdx.x >= a.s[i].blk0) si = i;
-  const RSeg& g = a.s[si];
+  // the segment of this block: the last one whose blk0 <= blockIdx.x (blk0 strictly increasing)
+  int lo = 0, hi = a.nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)blockIdx.x >= a.s[mid].blk0) lo = mid; else hi = mid - 1;
+  }
+  const RSeg& g = a.s[lo];
   const int b = blockIdx.x - g.blk0;
   if (g.mode == 1) {
     // RM_VEC runs of 4 columns per thread, 1024 columns apart (coalesced per run); every
@@ -164,7 +169,19 @@ extern "C" int lasr_reduce_multi(const lasr_reduce_seg* segs, int nseg, void* st
   for (int base = 0; base < nseg; base += RM_MAXSEG) {
     RSegs a = {};
     int nblk = 0;
-    for (int i = 0; i < RM_MAXSEG && base + i < nseg; ++i) {
+    const int cnt = nseg - base < RM_MAXSEG ? nseg - base : RM_MAXSEG;
+    // the many-partial (mode 0) segments' blocks first: they are latency-bound chains of loads,
+    // the few-partial slabs' blocks stream around them (blocks are dispatched in index order);
+    // every output is written by one segment, so the order changes no value
+    int ord[RM_MAXSEG], no = 0;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int i = 0; i < cnt; ++i) {
+        const lasr_reduce_seg& q = segs[base + i];
+        const bool v = q.P <= 64 && q.N % 4 == 0 && (q.out1 ? q.split : q.N) % 4 == 0 && ((uintptr_t)q.part & 15) == 0;
+        if (v == (pass == 1)) ord[no++] = i;
+      }
+    for (int oi = 0; oi < cnt; ++oi) {
+      const int i = ord[oi];
       const lasr_reduce_seg& q = segs[base + i];
       LASR_CHECK_ARG(q.part && q.out0 && q.N > 0 && q.P > 0, "lasr_reduce_multi: segment %d invalid", base + i);
       const int64_t split = q.out1 ? q.split : q.N;

@@ -147,12 +147,19 @@ class GraphedTrainStep:
         """Callables of the segmented fwd/bwd, run in order; the first returns the loss."""
         state = {}
 
+        def complete():
+            # every gradient of the piece is reduced by its end (the buckets it completes are
+            # all-reduced next): no encoder layer's reductions may still be queued
+            if K.held_reductions():
+                raise RuntimeError("graph_step: parameter-gradient reductions still queued at a segment end")
+
         def first():
             with self.model.segmented(self.cuts) as pairs:
                 loss = self.crit(self.model, *self.static)
             state["chain"] = sorted(pairs, key=lambda p: p[0], reverse=True)
             top = state["chain"][0][2]
             (state["g"],) = torch.autograd.grad(loss, [top])
+            complete()
             state["k"] = 0
             return loss
 
@@ -161,11 +168,13 @@ class GraphedTrainStep:
             _, x, _ = state["chain"][k]
             nxt = state["chain"][k + 1][2]
             (state["g"],) = torch.autograd.grad(x, [nxt], grad_outputs=state["g"])
+            complete()
             state["k"] = k + 1
 
         def last():
             _, x, _ = state["chain"][state["k"]]
             torch.autograd.backward(x, state["g"])
+            complete()
             state.clear()
 
         return [first] + [middle] * (len(self.cuts) - 1) + [last]

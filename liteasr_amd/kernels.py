@@ -72,23 +72,48 @@ class _Deferred:
         self.depth = 0
         self.segs = []
         self.gemms = []  # queued partials-only dW GEMMs: (tile key, args, operand refs)
+        self.held = []  # reductions of finished `hold` blocks, not yet launched
+        self.done = []  # their on_done callbacks, in block order
 
 
 _DEFER = _Deferred()
 
 
 @contextlib.contextmanager
-def deferred_reductions():
+def deferred_reductions(hold=False, on_done=None):
     """Within the block, gradient outputs of layernorm_bwd / qbias_bwd / split-K weight
     GEMMs (split_k=0, beta 0 or 1, fp32 contiguous C) are only complete after the block
-    exits; nothing inside may read them."""
+    exits; nothing inside may read them.  on_done() runs once they are complete.
+
+    hold=True (the encoder layers' backward nodes): the grouped weight-gradient launches still
+    run at the end of the block, but its reductions wait in a queue (their partial buffers
+    alive) for the next block that does not hold, or flush_reductions(): the reductions of
+    several layers then share lasr_reduce_multi launches, each with its usual summation order,
+    and the held blocks' on_done callbacks run after them, in order."""
     _DEFER.depth += 1
+    ok = False
     try:
         yield
+        ok = True
     finally:
         _DEFER.depth -= 1
         if _DEFER.depth == 0:
-            flush_reductions()
+            if hold and ok:
+                if _DEFER.gemms:
+                    _flush_gemm_group()
+                _DEFER.held.extend(_DEFER.segs)
+                _DEFER.segs = []
+                if on_done is not None:
+                    _DEFER.done.append(on_done)
+            else:
+                if on_done is not None:
+                    _DEFER.done.append(on_done)
+                flush_reductions()
+
+
+def held_reductions():
+    """Number of reductions queued by hold blocks and not yet launched."""
+    return len(_DEFER.held)
 
 
 def _defer(part, P, Ncols, out0, out1=None, split=None, accumulate=True):
@@ -160,10 +185,13 @@ def _flush_node_end(segs):
 
 
 def flush_reductions():
-    segs, _DEFER.segs = _DEFER.segs, []
-    if not segs and not _DEFER.gemms:
-        return
-    _flush_node_end(segs)
+    segs = _DEFER.held + _DEFER.segs
+    _DEFER.held, _DEFER.segs = [], []
+    done, _DEFER.done = _DEFER.done, []
+    if segs or _DEFER.gemms:
+        _flush_node_end(segs)
+    for fn in done:
+        fn()
     # the partial buffers are released here; the caching allocator hands their memory only
     # to work stream-ordered after the reduction
 

@@ -252,6 +252,12 @@ class FusedEncoderModel(LiteasrModel):
         layers = list(enc.enc_layers)
         conformer = getattr(enc, "arch", "conformer") == "conformer"
         env.pre_ln = env.bwd_chain = None
+        # layer nodes that launch the queued parameter-gradient reductions (FN.LAYER_RED_HOLD):
+        # the lowest layer, and the lowest layer of every backward segment (a cut before layer j)
+        seg = self._seg
+        env.red_flush = {id(layers[0])} if layers else set()
+        if seg is not None:
+            env.red_flush |= {id(layers[j]) for j in seg.cuts if 0 <= j < len(layers)}
         for j, layer in enumerate(layers):
             x = self._cut(x, j)
             if not conformer:  # Transformer layers: no final norm to chain the next first norm into

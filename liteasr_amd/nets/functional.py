@@ -82,6 +82,19 @@ LN2_BWD_CHAIN = True
 # backward (lasr_bn_act_glu_dwconv_bwd: dy computed in its window load, never stored); False: the
 # two launches with the fp32 dy between them (tests/test_fusions_gpu.py pins the two bit for bit)
 BN_GLU_FUSED = True
+# the encoder layers' parameter-gradient reductions (LayerNorm gamma / beta, split-K weight
+# slabs, positional biases, depthwise conv) queued across layer nodes and launched together at
+# the lowest layer of each backward segment (kernels.deferred_reductions(hold=True)); the
+# layers' gradient-ready hooks fire after that launch.  False: one reduction launch per layer
+# (tests/test_fusions_gpu.py pins the two bit for bit)
+LAYER_RED_HOLD = True
+
+
+def _red_hold(env, layer):
+    """Whether this encoder layer's backward node may leave its reductions queued: not the
+    last layer node of its backward segment (the model lists those in env.red_flush)."""
+    fl = getattr(env, "red_flush", None)
+    return LAYER_RED_HOLD and fl is not None and id(layer) not in fl
 
 
 class PostLN(SimpleNamespace):
@@ -795,9 +808,10 @@ class ConformerLayerFn(torch.autograd.Function):
         dev, adt = dx5.device, env.adt
         M, d = x4.shape
         dx5 = dx5.contiguous()
-        # parameter-gradient reductions of the whole layer finish in one launch at the end
+        # parameter-gradient reductions of the whole layer finish in one launch at the end (or,
+        # held, with the layers below it in the same backward segment)
         rx = getattr(env, "bwd_chain", None)
-        with K.deferred_reductions():
+        with K.deferred_reductions(hold=_red_hold(env, layer), on_done=layer.on_grads_ready):
             if rx is not None and rx[0] == id(layer):
                 # the next layer ran this final norm's backward with its own first norm's
                 # (LN2_BWD_CHAIN): dx5 is already dx4, and gb came with it
@@ -850,7 +864,6 @@ class ConformerLayerFn(torch.autograd.Function):
                 env.bwd_chain = (id(pv.layer), (tuple(dx4p.shape), dx4p.dtype), gbp)
                 dx0 = dx4p
         ctx.sv = None
-        layer.on_grads_ready()
         return dx0, None, None, None, None
 
 
@@ -900,7 +913,7 @@ class TransformerLayerFn(torch.autograd.Function):
         dev, adt = dx2.device, env.adt
         M, d = x1.shape
         dx2 = dx2.contiguous()
-        with K.deferred_reductions():
+        with K.deferred_reductions(hold=_red_hold(env, layer), on_done=layer.on_grads_ready):
             gb = _e((M, d), adt, dev)
             K.branch_grad(dx2, gb, 1.0, pd, _seed(s, 7))
             dx1 = _e((M, d), F32, dev)
@@ -914,7 +927,6 @@ class TransformerLayerFn(torch.autograd.Function):
                               lnb=LnBwd(x=x0, g=w.ln_b.g, mean=mb, rstd=rb, dx=dx0, dgamma=g.ln_b.g, dbeta=g.ln_b.b,
                                         dres=dx1, gb=None, bscale=1.0, bp=0.0, bseed=0))
         ctx.sv = None
-        layer.on_grads_ready()
         return dx0, None, None, None, None
 
 

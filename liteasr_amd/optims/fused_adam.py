@@ -41,6 +41,8 @@ class FlatAdamState:
 
     def step(self, max_norm, lr_mode, lr, factor, model_dim, warmup, beta1, beta2, eps, wd):
         st = self.store
+        if K.held_reductions():  # an encoder layer's gradient reductions were never launched
+            raise RuntimeError("FusedAdam.step: parameter-gradient reductions still queued")
         if self.m.device != st.flat.device:
             self.to(st.flat.device)
         g = st.ensure_grad()

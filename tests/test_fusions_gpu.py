@@ -144,3 +144,20 @@ def test_layer_boundary_norm_backwards_chained(monkeypatch, d, heads):
     monkeypatch.setattr(FN, "LN2_BWD_CHAIN", False)
     off = _step(cfg, B=4, T=1000, L=12)
     _same(on, off)
+
+
+@pytest.mark.parametrize("d,heads", [(256, 4), (512, 16)])
+def test_layer_reductions_held_across_layers(monkeypatch, d, heads):
+    """The encoder layers' parameter-gradient reductions queued across the layer nodes and
+    launched together at layer 0 (kernels.deferred_reductions(hold=True)) vs one reduction
+    launch per layer node: one bf16 step of four encoder layers bit-identical, nothing left
+    queued after the backward."""
+    from liteasr_amd import kernels as kn
+    from liteasr_amd.nets import functional as FN
+
+    cfg = O.default_cfg(enc_dim=d, enc_heads=heads, enc_layers=4, dec_dim=d, dec_heads=heads, dec_layers=1)
+    on = _step(cfg, B=4, T=1000, L=12)
+    assert kn.held_reductions() == 0
+    monkeypatch.setattr(FN, "LAYER_RED_HOLD", False)
+    off = _step(cfg, B=4, T=1000, L=12)
+    _same(on, off)

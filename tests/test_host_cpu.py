@@ -135,3 +135,30 @@ def test_verify_native_runs_and_catches_a_wrong_average():
         assert out[r]["verified_once"] and out[r]["second_step_unchecked"]
         assert out[r]["caught"] is not None and "bucket 0" in out[r]["caught"], out[r]["caught"]
     assert (out[0]["grad"] == out[1]["grad"]).all()
+
+
+def test_held_reductions_queue_order(monkeypatch):
+    """kernels.deferred_reductions(hold=True): a held block's reductions and on_done wait for
+    the next non-holding block, which launches them first (block order) and then runs every
+    callback in block order; an exception inside a held block flushes instead of holding."""
+    from liteasr_amd import kernels as K
+
+    launched, events = [], []
+    monkeypatch.setattr(K, "_flush_node_end", lambda segs: launched.append([s[0] for s in segs]))
+    monkeypatch.setattr(K, "_DEFER", K._Deferred())
+    for name, hold in (("L3", True), ("L2", True), ("L1", False)):
+        with K.deferred_reductions(hold=hold, on_done=lambda n=name: events.append((n, len(launched)))):
+            K._defer(name + "a", 1, 4, None)
+            K._defer(name + "b", 1, 4, None)
+        if hold:
+            assert launched == [] and events == []
+            assert K.held_reductions() > 0
+    assert launched == [["L3a", "L3b", "L2a", "L2b", "L1a", "L1b"]]
+    assert events == [("L3", 1), ("L2", 1), ("L1", 1)]
+    assert K.held_reductions() == 0
+
+    with pytest.raises(ValueError):
+        with K.deferred_reductions(hold=True, on_done=lambda: events.append(("E", len(launched)))):
+            K._defer("E", 1, 4, None)
+            raise ValueError
+    assert launched[-1] == ["E"] and events[-1] == ("E", 2) and K.held_reductions() == 0

@@ -1434,3 +1434,49 @@ def test_ctc_against_reference_golden_full_size(name):
     err_ours = (gg - g64).abs().max().item() / m
     assert err_ours <= max(2e-3, 1.5 * err_ref), (err_ours, err_ref)
     close(gg, gold, err_ref + err_ours + 1e-6, "ctc grad vs reference golden")
+
+
+def test_reduce_multi_many_segments_bit_identical():
+    """lasr_reduce_multi over 150 segments (three 64-segment launches, the many-partial
+    segments' blocks first in each) gives the bits of one launch per segment: both summation
+    modes (P <= 64 slabs, P > 64 LayerNorm-style partial rows), split outputs, accumulate and
+    overwrite, unaligned column counts; against float64 at the fp32 bar."""
+    from liteasr_amd import _native as N
+
+    kn = K()
+    g = torch.Generator().manual_seed(150)
+    segs = []
+    for i in range(150):
+        P = [2, 3, 4, 8, 64, 65, 498, 31][i % 8]
+        Nc = [4096, 512, 516, 130, 2048 * 3][i % 5]
+        split = Nc // 2 if i % 3 == 0 else None
+        if split is not None and i % 2:
+            split -= split % 4
+        part = torch.randn(P, Nc, generator=g).to(DEV)
+        o0 = torch.randn(split if split else Nc, generator=g).to(DEV)
+        o1 = torch.randn(Nc - split, generator=g).to(DEV) if split else None
+        segs.append((part, P, Nc, o0, o1, split, i % 4 != 1))
+    refs = []
+    for part, P, Nc, o0, o1, split, acc in segs:
+        s = part.double().sum(0)
+        full = (torch.cat([o0, o1]) if o1 is not None else o0).double()
+        refs.append(s + full if acc else s)
+
+    def run(batched):
+        outs = [(o0.clone(), o1.clone() if o1 is not None else None) for _, _, _, o0, o1, _, _ in segs]
+        rows = [N.ReduceSeg(kn.ptr(p), Nc, P, int(acc), kn.ptr(a), kn.ptr(b), sp if sp else Nc)
+                for (p, P, Nc, _, _, sp, acc), (a, b) in zip(segs, outs)]
+        if batched:
+            arr = (N.ReduceSeg * len(rows))(*rows)
+            N.call("lasr_reduce_multi", arr, len(rows), kn.stream())
+        else:
+            for r in rows:
+                arr = (N.ReduceSeg * 1)(r)
+                N.call("lasr_reduce_multi", arr, 1, kn.stream())
+        torch.cuda.synchronize()
+        return [torch.cat([a, b]) if b is not None else a for a, b in outs]
+
+    one, many = run(False), run(True)
+    for i, (a, b, r) in enumerate(zip(one, many, refs)):
+        assert torch.equal(a, b), i
+        close(b, r, 1e-5, f"segment {i}")

@@ -638,16 +638,22 @@ def test_deferred_reductions_bit_exact(monkeypatch):
     params = O.init_params(SMALL, seed=5)
     xs, xlens, ys, ylens = [t.cuda() for t in O.synthetic_batch(2, 300, 9, SMALL["vocab_size"], seed=4)]
     grads = []
+    @contextlib.contextmanager
+    def immediate(hold=False, on_done=None):  # no deferral: every reduction in its own call
+        yield
+        if on_done is not None:
+            on_done()
+
     for defer in (True, False):
         if not defer:
-            monkeypatch.setattr(Kn, "deferred_reductions", contextlib.nullcontext)
+            monkeypatch.setattr(Kn, "deferred_reductions", immediate)
         model = build(SMALL, "bf16")
         model.load_state_dict({**params, **O.init_buffers(SMALL)}, strict=False)
         model = model.cuda().train()
         crit = HybridCTCLoss(HybridCTCLossConfig(vocab_size=SMALL["vocab_size"], smoothing=0.1, ctc_weight=0.3))
         crit(model, xs, xlens, ys, ylens).backward()
         grads.append({n: p.grad.detach().clone() for n, p in model.named_parameters()})
-    assert not Kn._DEFER.segs and Kn._DEFER.depth == 0
+    assert not Kn._DEFER.segs and not Kn._DEFER.held and Kn._DEFER.depth == 0
     for k in grads[0]:
         assert torch.equal(grads[0][k], grads[1][k]), k
 

@@ -38,6 +38,8 @@ for s in "$@"; do
              grep "^{" "$OUT/envab_$v.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'env': '$e', 'args': '${AB_ARGS:-}', 'ms': d['ms_per_step'], 'median': d.get('ms_per_step_median')}))" >> "$OUT/envab.jsonl"; done ;;
     dyn) run timeout -k 10 900 $PYT tests/test_kernels_gpu.py -k "u2_prep or embed_and_prep or prep" \
            tests/test_model_gpu.py -k "dynamic or config4 or graphed or chunk" -s > "$OUT/dyn.log" 2>&1 ;;
+    hold) run timeout -k 10 300 $PYT tests/test_fusions_gpu.py tests/test_kernels_gpu.py -k "held or chained or reduce_multi or dw_group" > "$OUT/hold.log" 2>&1
+          run timeout -k 10 600 $PYT tests/test_native_reducer_gpu.py tests/test_trainer_gpu.py tests/test_model_gpu.py >> "$OUT/hold.log" 2>&1 ;;
     fus) run timeout -k 10 600 $PYT tests/test_fusions_gpu.py -s > "$OUT/fus.log" 2>&1 ;;
     fc1sweep) run timeout -k 10 300 python3 tools/fc1_tile_sweep.py > "$OUT/fc1_sweep_small.jsonl" 2> "$OUT/fc1_sweep.err"
            run timeout -k 10 300 python3 tools/fc1_tile_sweep.py 7968 2048 512 > "$OUT/fc1_sweep_large.jsonl" 2>> "$OUT/fc1_sweep.err" ;;
