@@ -116,6 +116,10 @@ for s in "$@"; do
     model) run timeout -k 10 900 $PYT tests/test_model_gpu.py tests/test_nodes_gpu.py -s > "$OUT/model.log" 2>&1 ;;
     smoke) run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) run timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    benchprof) # rocprofv3 --kernel-trace --stats of the default bench command (the summary kept under profiles/)
+           cd /tmp && run timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/benchprof" -o run -- python3 "$R/bench.py" > "$OUT/rocprofv3_bench.log" 2>&1
+           grep "^{" "$OUT/rocprofv3_bench.log" | tail -1 > "$OUT/rocprofv3_bench.json"
+           cp "$(find "$OUT/benchprof" -name '*kernel_stats.csv' | head -1)" "$OUT/rocprofv3_kernel_stats_bench.csv"; rm -rf "$OUT/benchprof" ;;
     benchq) run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/benchq.json" 2> "$OUT/benchq.err" ;;
     long) run timeout -k 10 300 python3 bench.py --config long --no-cpu-baseline > "$OUT/bench_long.json" 2> "$OUT/bench_long.err" ;;
     large) run timeout -k 10 400 python3 bench.py --config large --no-cpu-baseline > "$OUT/bench_large.json" 2> "$OUT/bench_large.err" ;;
