@@ -133,7 +133,9 @@ static void gemm_plan(const lasr_gemm_args* a, int* BMo, int* BNo, int* splito, 
   }
   if (a->split_k <= -2 && plain && a->workspace) split = -a->split_k;  // explicit partials-only
   const int64_t rs_floats = a->rowsum ? (int64_t)split * a->M : 0;
-  if (split > 1 && ((!plain && !autosplit) || !a->workspace ||
+  // an explicit split (split_k >= 2) may carry any epilogue but the pre-activation copy: the
+  // split-K reduction applies it (tools/splitk_sweep.py)
+  if (split > 1 && ((!plain && !autosplit && (a->split_k < 2 || a->zout)) || !a->workspace ||
                     a->workspace_bytes < ((int64_t)split * batch * a->M * a->N + rs_floats) * 4))
     split = 1;
   // ring depth of the LDS-DMA kernel: 64-deep stages (two 32-deep sub-tiles per counted

@@ -117,7 +117,7 @@ for s in "$@"; do
     smoke) run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) run timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     benchprof) # rocprofv3 --kernel-trace --stats of the default bench command (the summary kept under profiles/)
-           cd /tmp && run timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/benchprof" -o run -- python3 "$R/bench.py" > "$OUT/rocprofv3_bench.log" 2>&1
+           cd /tmp && run timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/benchprof" -o run -- python3 "$R/bench.py" > "$OUT/rocprofv3_bench.log" 2>&1
            grep "^{" "$OUT/rocprofv3_bench.log" | tail -1 > "$OUT/rocprofv3_bench.json"
            cp "$(find "$OUT/benchprof" -name '*kernel_stats.csv' | head -1)" "$OUT/rocprofv3_kernel_stats_bench.csv"; rm -rf "$OUT/benchprof" ;;
     benchq) run timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-roofline --steps 40 > "$OUT/benchq.json" 2> "$OUT/benchq.err" ;;
@@ -141,6 +141,8 @@ for s in "$@"; do
     tracefam) cd /tmp && run timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_family" -o run -- python3 "$R/bench.py" --config ${PMC_CONFIG:-small} --roofline-only 50 --roofline-case family > "$OUT/trace_family.log" 2>&1
            grep "^{" "$OUT/trace_family.log" | tail -1 > "$OUT/trace_family_meta.json"
            run python3 "$R/tools/family_trace.py" "$(find "$OUT/trace_family" -name '*.db' | head -1)" "$OUT/trace_family_meta.json" > "$OUT/family_trace_summary_${PMC_CONFIG:-small}.json"; rm -rf "$OUT/trace_family" ;;
+    splitk) run timeout -k 10 300 python3 tools/splitk_sweep.py > "$OUT/splitk_small.jsonl" 2> "$OUT/splitk.err"
+           run timeout -k 10 300 python3 tools/splitk_sweep.py 7968 512 2048 > "$OUT/splitk_large.jsonl" 2>> "$OUT/splitk.err" ;;
     tileab) run timeout -k 10 200 python3 tools/tile_ab.py > "$OUT/tile_ab.jsonl" 2> "$OUT/tile_ab.err" ;;
     blaslt) run timeout -k 10 120 python3 tools/blaslt_ref.py > "$OUT/blaslt.jsonl" 2> "$OUT/blaslt.err" ;;
     trace) cd /tmp && run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-roofline --steps 10 --warmup 3 > "$OUT/trace.log" 2>&1
