@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size 2, CPU) tests of the FlatParams DDP reducer: initial
+"""Multi-process (gloo, world_size 2 and 4, CPU) tests of the FlatParams DDP reducer: initial
 broadcast, bucket launch order driven by the backward-node hooks, gradient averaging,
 no_sync(), and BN-buffer re-broadcast.  The HIP kernels are not involved: a stand-in
 autograd node writes rank-dependent gradients into the flat grad buffer and fires the
@@ -117,7 +117,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_flat_ddp_gloo_world2():
+def _run_world(world):
     import socket
 
     s = socket.socket()
@@ -126,7 +126,7 @@ def test_flat_ddp_gloo_world2():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = {r: {k: (torch.from_numpy(v) if hasattr(v, "dtype") and hasattr(v, "shape") else v) for k, v in d.items()}
@@ -134,6 +134,34 @@ def test_flat_ddp_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return out
+
+
+def test_flat_ddp_gloo_world4():
+    """The same reducer at world 4 (the N > 1 path rehearsed on more ranks than the GPU tests
+    can use): rank-0 broadcast, the bucket mean over four ranks, rank-local no_sync, record
+    mode and the BN re-broadcast hold on every rank."""
+    world = 4
+    out = _run_world(world)
+    a = out[0]
+    mean = sum(r + 1 for r in range(world)) / world  # 2.5: exact in fp32
+    for r in range(world):
+        o = out[r]
+        assert o["nbuckets"] == a["nbuckets"] > 2
+        assert torch.equal(o["flat"], a["flat"])
+        assert o["bn_after_init"] == 7.0 and o["bn_after_sync"] == 20.0
+        assert torch.equal(o["grad_sync"], a["grad_sync"])
+        assert torch.equal(o["grad_nosync"], (r + 1) * a["grad_nosync"])
+        assert torch.equal(o["grad_unreduced"], (r + 1) * a["grad_unreduced"])
+        assert torch.equal(o["grad_record"], a["grad_sync"])
+        assert o["record"] == list(range(a["nbuckets"]))
+        assert o["cuts"] == a["cuts"]
+    # averaged: mean_r((r + 1) * i) = 2.5 * i, i.e. 2.5 times the rank-0 local gradient
+    assert torch.equal(a["grad_sync"], mean * a["grad_nosync"])
+
+
+def test_flat_ddp_gloo_world2():
+    out = _run_world(2)
     a, b = out[0], out[1]
     assert a["nbuckets"] > 2  # several buckets -> ordered launches were exercised
     assert torch.equal(a["flat"], b["flat"])  # rank-0 parameters broadcast
