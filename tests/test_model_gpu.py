@@ -806,14 +806,14 @@ def _ddp_graph_worker(rank, world, port, q):
         q.put((rank, False, repr(e), None))
 
 
-def _two_ranks(worker):
+def _two_ranks(worker, world=2):
     import multiprocessing as mp
     import random
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    ps = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in ps]
@@ -922,6 +922,16 @@ def test_ddp_grads_equal_single_process_concatenated_batch():
     the segmented graphed path) == one process on the concatenated batch, within 2e-4 of
     each tensor's max; the graphed path bit-equal to the eager DDP path."""
     for rank, ok, info, tb in _two_ranks(_ddp_equiv_worker):
+        assert ok, (rank, info, tb)
+
+
+def test_ddp_grads_equal_single_process_four_ranks():
+    """The same equivalence at world 4 (one utterance per rank, four ranks sharing the GPU over
+    gloo): the bucket mean over four ranks == one process on the concatenated batch, and the
+    segmented graphed path bit-equal to the eager DDP path."""
+    res = _two_ranks(_ddp_equiv_worker, world=4)
+    assert sorted(r[0] for r in res) == [0, 1, 2, 3]
+    for rank, ok, info, tb in res:
         assert ok, (rank, info, tb)
 
 
