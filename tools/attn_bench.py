@@ -3,6 +3,7 @@ launches (HIP events on the capture stream).  One JSON line per (case, direction
   small  : encoder rel-pos MHSA of config 2 (B 32, H 4, T' 249, d_k 64, key padding)
   large  : config 4 (B 32, H 16, T' 249, d_k 32, chunk-16 streaming mask)
   long   : config 5 (B 8, H 4, T' 999, d_k 64, key padding)
+  smallchunk / largepad (only when named): config 2 with the chunk-16 mask, config 4 with key padding
   dec    : the decoder's self attention of config 2 (B 32, H 4, L+1 41, causal + padding)
 Algorithmic flops: forward 3 x 2*B*H*Tq*Tk*d_k (QK^T, the positional product, PV; plain
 attention 2 x), backward 6 x (S recomputed twice: the query- and key-side kernels, dP, dQ, dK,
@@ -136,6 +137,10 @@ def main():
     cases = [("small", 32, 4, 249, 64, 0), ("large", 32, 16, 249, 32, 16), ("long", 8, 4, 999, 64, 0)]
     for c in cases:
         if not sel or c[0] in sel:
+            rel_case(*c)
+    # attribution cases, only when named: d_k 64 with the chunk-mask tile, d_k 32 without it
+    for c in [("smallchunk", 32, 4, 249, 64, 16), ("largepad", 32, 16, 249, 32, 0)]:
+        if c[0] in sel:
             rel_case(*c)
     if not sel or "dec" in sel:
         dec_case("dec", 32, 4, 41, 64)
